@@ -1,0 +1,423 @@
+"""Generate the golden fixtures under tests/golden/ from the *reference* Python modules.
+
+TEST INFRASTRUCTURE ONLY; runs in the build container (needs /root/reference).
+    python oracle/gen_golden.py            # writes tests/golden/*.npz
+
+Each fixture holds seeded inputs (or their seed), the reference's outputs and
+gradients.  Weights come from oracle/fill.py (name-hashed, platform independent), so
+the fixtures hold no state dicts.  The reference runs on CPU in fp32/fp64 exactly as
+its own PyTorch paths do (MSDA: multi_scale_deform_attn.py:341-353 on CPU tensors).
+"""
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+from fill import fill_module, seeded  # noqa: E402
+from ref_import import load_reference  # noqa: E402
+
+OUT = os.path.join(os.path.dirname(HERE), "tests", "golden")
+torch.set_num_threads(8)
+
+
+# Inputs produced by oracle.fill.seeded() are NOT stored (the GPU box regenerates the
+# same bits from the seed); a checksum is stored in their place so a regeneration drift
+# is caught.  Keys listed in REGEN are replaced by "<key>__cs".
+REGEN = set()
+
+
+def checksum(a):
+    a = np.asarray(a, dtype=np.float64)
+    return np.array([a.sum(), np.abs(a).sum(), (a * a).sum(), a.size])
+
+
+def save(name, regen=(), **arrays):
+    os.makedirs(OUT, exist_ok=True)
+    arrs = {}
+    for k, v in arrays.items():
+        v = v.detach().cpu().numpy() if torch.is_tensor(v) else np.asarray(v)
+        if k in regen or any(k.endswith(s) for s in regen):
+            arrs[k + "__cs"] = checksum(v)
+        else:
+            arrs[k] = v
+    path = os.path.join(OUT, name)
+    np.savez_compressed(path, **arrs)
+    print(f"{name}: {os.path.getsize(path) / 1e6:.2f} MB, keys={len(arrs)}")
+
+
+def t(a, dtype=None):
+    x = torch.from_numpy(np.ascontiguousarray(a))
+    return x.to(dtype) if dtype is not None else x
+
+
+# --------------------------------------------------------------------------- MSDA
+def gen_msda(ref):
+    f = ref.msda.multi_scale_deformable_attn_pytorch
+    out = {}
+    # (1) the reference test's exact problem (tests/test_ms_deform_attn.py:34-38), fp64
+    shapes = torch.as_tensor([(6, 4), (3, 2)], dtype=torch.long)
+    S = 6 * 4 + 3 * 2
+    N, M, Lq, L, P = 1, 2, 2, 2, 2
+    for tag, D, seed in [("fwd", 2, 11), ("c30", 30, 12), ("c32", 32, 13), ("c64", 64, 14),
+                         ("c71", 71, 15), ("c1025", 1025, 16)]:
+        value = t(seeded((N, S, M, D), seed, "uniform") * 0.01, torch.float64).requires_grad_()
+        loc = t(seeded((N, Lq, M, L, P, 2), seed + 100, "uniform"), torch.float64).requires_grad_()
+        aw0 = t(seeded((N, Lq, M, L, P), seed + 200, "uniform"), torch.float64) + 1e-5
+        aw0 = aw0 / aw0.sum(-1, keepdim=True).sum(-2, keepdim=True)
+        aw = aw0.clone().requires_grad_()
+        o = f(value, shapes, loc, aw)
+        g = t(seeded(tuple(o.shape), seed + 300), torch.float64)
+        gv, gl, ga = torch.autograd.grad((o * g).sum(), (value, loc, aw))
+        out.update({f"{tag}_value": value, f"{tag}_loc": loc, f"{tag}_aw": aw, f"{tag}_out": o,
+                    f"{tag}_gout": g, f"{tag}_gvalue": gv, f"{tag}_gloc": gl, f"{tag}_gaw": ga})
+    out["shapes"] = shapes
+    out["level_start_index"] = torch.tensor([0, 24], dtype=torch.long)
+    save("msda_ref_test.npz", **out)
+
+    # (2) DINO-like levels, fp32, adversarial locations (exact 1/(2W) multiples, ±1 ulp, <0, >1)
+    lv = [(25, 42), (13, 21), (7, 11), (4, 6)]
+    shapes = torch.as_tensor(lv, dtype=torch.long)
+    lsi = torch.cat([shapes.new_zeros(1), shapes.prod(1).cumsum(0)[:-1]])
+    S = int(shapes.prod(1).sum())
+    bs, M, D, Q, L, P = 1, 4, 32, 300, 4, 4
+    value = t(seeded((bs, S, M, D), 21))
+    refp = seeded((bs, Q, 1, L, 1, 2), 22, "uniform")
+    loc = (refp + 0.02 * seeded((bs, Q, M, L, P, 2), 23)).astype(np.float32)
+    # adversarial block on the first 64 queries
+    rng = np.random.Generator(np.random.PCG64(24))
+    for q in range(64):
+        for m in range(M):
+            for l in range(L):
+                H, W = lv[l]
+                for p in range(P):
+                    for ax, size in ((0, W), (1, H)):
+                        k = rng.integers(-2, 2 * size + 3)
+                        v = np.float32(k) / np.float32(2 * size)
+                        d = rng.integers(-1, 2)
+                        if d:
+                            v = np.nextafter(v, np.float32(d * 10))
+                        loc[0, q, m, l, p, ax] = v
+    loc = t(loc).requires_grad_()
+    logits = t(seeded((bs, Q, M, L * P), 25))
+    aw = logits.softmax(-1).view(bs, Q, M, L, P).contiguous().requires_grad_()
+    value.requires_grad_()
+    o = f(value, shapes, loc, aw)
+    g = t(seeded(tuple(o.shape), 26))
+    gv, gl, ga = torch.autograd.grad((o * g).sum(), (value, loc, aw))
+    save("msda_dino.npz", regen=("value", "gout"), value=value, shapes=shapes, level_start_index=lsi, loc=loc, aw=aw,
+         out=o, gout=g, gvalue=gv, gloc=gl, gaw=ga)
+
+    # (3) the module (multi_scale_deform_attn.py:139-363), 2-d and 4-d reference points
+    torch.manual_seed(0)
+    mod = ref.msda.MultiScaleDeformableAttention(embed_dim=256, num_heads=8, num_levels=4,
+                                                 num_points=4, batch_first=False)
+    fill_module(mod, seed=5)
+    mod.eval()
+    lv = [(16, 20), (8, 10), (4, 5), (2, 3)]
+    shapes = torch.as_tensor(lv, dtype=torch.long)
+    lsi = torch.cat([shapes.new_zeros(1), shapes.prod(1).cumsum(0)[:-1]])
+    S = int(shapes.prod(1).sum())
+    bs, Q = 2, 40
+    res = {"shapes": shapes, "level_start_index": lsi}
+    for tag, rd, seed in (("r2", 2, 31), ("r4", 4, 32)):
+        query = t(seeded((Q, bs, 256), seed)).requires_grad_()
+        value = t(seeded((S, bs, 256), seed + 1)).requires_grad_()
+        qpos = t(seeded((Q, bs, 256), seed + 2))
+        rp = seeded((bs, Q, L, rd), seed + 3, "uniform", lo=0.05, hi=0.95)
+        if rd == 4:
+            rp[..., 2:] *= 0.3
+        rp = t(rp)
+        mask = torch.from_numpy(seeded((bs, S), seed + 4, "uniform") < 0.1)
+        o = mod(query, value=value, query_pos=qpos, key_padding_mask=mask, reference_points=rp,
+                spatial_shapes=shapes, level_start_index=lsi)
+        g = t(seeded(tuple(o.shape), seed + 5))
+        params = [p for _, p in mod.named_parameters()]
+        grads = torch.autograd.grad((o * g).sum(), [query, value] + params)
+        res.update({f"{tag}_query": query, f"{tag}_value": value, f"{tag}_qpos": qpos,
+                    f"{tag}_ref": rp, f"{tag}_mask": mask, f"{tag}_out": o, f"{tag}_gout": g,
+                    f"{tag}_gquery": grads[0], f"{tag}_gvalue": grads[1]})
+        for (n, _), gp in zip(mod.named_parameters(), grads[2:]):
+            res[f"{tag}_g.{n}"] = gp
+    save("msda_module.npz", regen=("_query", "_value", "_qpos", "_gout"), **res)
+
+
+# --------------------------------------------------------------------------- Swin
+def gen_swin_wmsa(ref):
+    res = {}
+    for tag, (B, H, W, shift, C, nH) in {
+        "pad_noshift": (1, 28, 28, 0, 128, 4),
+        "pad_shift": (1, 28, 28, 6, 128, 4),
+        "nopad_noshift": (2, 24, 24, 0, 128, 4),
+        "nopad_shift": (2, 24, 24, 6, 128, 4),
+        "rect_shift": (1, 15, 40, 6, 64, 2),
+    }.items():
+        m = ref.swin.ShiftWindowMSA(embed_dims=C, num_heads=nH, window_size=12, shift_size=shift)
+        fill_module(m, seed=7)
+        m.eval()
+        x = t(seeded((B, H * W, C), 40 + H + shift)).requires_grad_()
+        o = m(x, (H, W))
+        g = t(seeded(tuple(o.shape), 41 + H + shift))
+        names = [n for n, _ in m.named_parameters()]
+        grads = torch.autograd.grad((o * g).sum(), [x] + [p for _, p in m.named_parameters()])
+        res.update({f"{tag}_cfg": np.array([B, H, W, shift, C, nH]), f"{tag}_x": x,
+                    f"{tag}_out": o, f"{tag}_gout": g, f"{tag}_gx": grads[0]})
+        for n, gp in zip(names, grads[1:]):
+            res[f"{tag}_g.{n}"] = gp
+    save("swin_wmsa.npz", regen=("_x", "_gout"), **res)
+
+
+def gen_swin_block(ref):
+    """SwinBlockAdapter (swin.py:505-610) and a full stage with PatchMerging."""
+    res = {}
+    blk = ref.swin.SwinBlockSequence(embed_dims=64, num_heads=2, feedforward_channels=256, depth=2,
+                                     window_size=12,
+                                     downsample=ref.embed.PatchMerging(in_channels=64, out_channels=128,
+                                                                       stride=2, norm_cfg=dict(type="LN")))
+    fill_module(blk, seed=9)
+    blk.eval()
+    H, W = 20, 26
+    for mode in ("rgb", "dte"):
+        x = t(seeded((2, H * W, 64), 50 + len(mode))).requires_grad_()
+        xd, hw_d, xo, hw = blk(x, (H, W), mode)
+        g1 = t(seeded(tuple(xd.shape), 51))
+        g2 = t(seeded(tuple(xo.shape), 52))
+        names = [n for n, _ in blk.named_parameters()]
+        grads = torch.autograd.grad((xd * g1).sum() + (xo * g2).sum(), [x] + [p for _, p in blk.named_parameters()],
+                                    allow_unused=True)
+        res.update({f"{mode}_x": x, f"{mode}_xdown": xd, f"{mode}_xout": xo, f"{mode}_g1": g1,
+                    f"{mode}_g2": g2, f"{mode}_gx": grads[0], f"{mode}_hwdown": np.array(hw_d)})
+        for n, gp in zip(names, grads[1:]):
+            if gp is not None:
+                res[f"{mode}_g.{n}"] = gp
+    res["hw"] = np.array([H, W])
+    save("swin_stage.npz", regen=("_x", "_g1", "_g2"), **res)
+
+
+# --------------------------------------------------------------------------- DAttn
+class _GridRecorder(types.ModuleType):
+    def __init__(self, F):
+        super().__init__("F_rec")
+        self._F = F
+        self.grids = []
+
+    def __getattr__(self, k):
+        return getattr(self._F, k)
+
+    def grid_sample(self, input, grid, **kw):
+        self.grids.append((grid.detach().clone(), tuple(input.shape), kw.get("align_corners")))
+        return self._F.grid_sample(input, grid, **kw)
+
+
+def gen_dattn(ref):
+    import torch.nn.functional as F
+    res = {}
+    # (dims, stride, groups, heads, level, H, W): the four Swin-B DSCF configs at reduced size
+    cfgs = {"s0": (16, 8, 1, 2, 0, 32, 40), "s1": (32, 4, 2, 4, 1, 16, 20),
+            "s2": (64, 2, 4, 8, 2, 16, 12), "s3": (128, 1, 8, 16, 3, 8, 8),
+            "swinl_s0": (24, 8, 1, 2, 0, 24, 32)}
+    rec = _GridRecorder(F)
+    for tag, (dims, stride, g, h, level, H, W) in cfgs.items():
+        m = ref.swin.DAttentionMM(dims=dims, stride=stride, n_groups=g, n_heads=h, dpr=0, level=level)
+        fill_module(m, seed=13)
+        m.eval()
+        B = 2
+        x = t(seeded((B, dims, H, W), 60 + level)).requires_grad_()
+        y = t(seeded((B, dims, H, W), 70 + level, "uniform")).requires_grad_()
+        ref.swin.F = rec
+        rec.grids = []
+        o = m(x, y)
+        ref.swin.F = F
+        gout = t(seeded(tuple(o.shape), 80 + level))
+        names = [n for n, _ in m.named_parameters()]
+        grads = torch.autograd.grad((o * gout).sum(), [x, y] + [p for _, p in m.named_parameters()])
+        res.update({f"{tag}_cfg": np.array([dims, stride, g, h, level, H, W, B]), f"{tag}_x": x,
+                    f"{tag}_y": y, f"{tag}_out": o, f"{tag}_gout": gout, f"{tag}_gx": grads[0],
+                    f"{tag}_gy": grads[1]})
+        for n, gp in zip(names, grads[2:]):
+            res[f"{tag}_g.{n}"] = gp
+        # the 6 feature-sampling grids (pos_x, pos_y; align_corners=True) and the 2 rpe grids
+        assert len(rec.grids) == 8, len(rec.grids)
+        res[f"{tag}_pos_x"] = rec.grids[0][0]
+        res[f"{tag}_pos_y"] = rec.grids[1][0]
+        res[f"{tag}_disp_x"] = rec.grids[6][0]
+        res[f"{tag}_disp_y"] = rec.grids[7][0]
+    save("dattn.npz", regen=("_x", "_y", "_gout"), **res)
+
+
+def gen_fusion_small(ref):
+    res = {}
+    # MPGBlock (swin.py:1045-1068)
+    m = ref.swin.MPGBlock(64, 0.125)
+    fill_module(m, seed=17)
+    xr = t(seeded((2, 6 * 7, 64), 90)).requires_grad_()
+    xd = t(seeded((2, 6 * 7, 64), 91)).requires_grad_()
+    a, b = m(xr, xd, 6, 7)
+    ga, gb = t(seeded(tuple(a.shape), 92)), t(seeded(tuple(b.shape), 93))
+    names = [n for n, _ in m.named_parameters()]
+    grads = torch.autograd.grad((a * ga).sum() + (b * gb).sum(), [xr, xd] + [p for _, p in m.named_parameters()])
+    res.update(mpg_xr=xr, mpg_xd=xd, mpg_a=a, mpg_b=b, mpg_ga=ga, mpg_gb=gb, mpg_gxr=grads[0], mpg_gxd=grads[1])
+    for n, gp in zip(names, grads[2:]):
+        res[f"mpg_g.{n}"] = gp
+    # DeformMPGBlock (swin.py:1071-1091), level 1 config
+    d = ref.swin.DeformMPGBlock(dims=128, stride=4, n_groups=2, n_heads=4, dpr=0, level=1, ratio=0.125)
+    fill_module(d, seed=19)
+    d.eval()
+    H, W = 16, 16
+    xr = t(seeded((2, H * W, 128), 94)).requires_grad_()
+    xd = t(seeded((2, H * W, 128), 95)).requires_grad_()
+    o = d(xr, xd, H, W, 1)
+    go = t(seeded(tuple(o.shape), 96))
+    names = [n for n, _ in d.named_parameters()]
+    grads = torch.autograd.grad((o * go).sum(), [xr, xd] + [p for _, p in d.named_parameters()])
+    res.update(dmpg_xr=xr, dmpg_xd=xd, dmpg_out=o, dmpg_gout=go, dmpg_gxr=grads[0], dmpg_gxd=grads[1])
+    for n, gp in zip(names, grads[2:]):
+        res[f"dmpg_g.{n}"] = gp
+    # Adapter (swin.py:472-502), eval (dropout off)
+    ad = ref.swin.Adapter(128, mlp_ratio=0.0625, skip_connect=False)
+    fill_module(ad, seed=23)
+    ad.eval()
+    x = t(seeded((2, 30, 128), 97)).requires_grad_()
+    o = ad(x)
+    go = t(seeded(tuple(o.shape), 98))
+    gx, = torch.autograd.grad((o * go).sum(), [x])
+    res.update(adapter_x=x, adapter_out=o, adapter_gout=go, adapter_gx=gx)
+    save("fusion_small.npz", regen=("mpg_xr", "mpg_xd", "mpg_ga", "mpg_gb", "dmpg_xr", "dmpg_xd", "dmpg_gout", "adapter_x", "adapter_gout"), **res)
+
+
+# --------------------------------------------------------------------------- CMNeXt
+class _Holder(nn.Module):
+    pass
+
+
+def build_ref_tiny(ref, n_cls=5):
+    """Tiny-Swin CMNeXt (SURVEY §8(c) fixture 5): embed 32, depths (2,2,2,2),
+    heads (1,2,4,8) so head_dim = 32 as in Swin-B/L."""
+    h = _Holder()
+    h.backbone = ref.swin.SwinTransformer(embed_dims=32, depths=(2, 2, 2, 2), num_heads=(1, 2, 4, 8),
+                                          init_cfg=None)
+    dims = [32, 64, 128, 256]
+    h.decode_head = ref.segformer.SegFormerHead(dims, 64, n_cls)
+    h.decode_head_rgb = ref.segformer.SegFormerHead(dims, 32, n_cls)
+    h.decode_head_dte = ref.segformer.SegFormerHead(dims, 32, n_cls)
+    return h
+
+
+def adapter_trainable(name):
+    # optimizers.py:10-20 (TRAIN_TYPE: Adapter)
+    return ("Adapter" in name) or ("extra_patch_embed" in name) or ("head" in name) or ("MPG" in name)
+
+
+def gen_cmnext(ref):
+    res = {}
+    h = build_ref_tiny(ref)
+    fill_module(h, seed=29)
+    h.eval()
+    h.backbone.eval()
+    B, Hi, Wi = 2, 128, 160
+    rgb = t(seeded((B, 3, Hi, Wi), 100))
+    dep = t(seeded((B, 3, Hi, Wi), 101, "uniform"))
+    y, yr, yd = ref.cmnext.CMNeXt.forward(h, [rgb, dep])
+    gy, gr, gd = (t(seeded(tuple(y.shape), 102 + i)) for i in range(3))
+    named = [(n, p) for n, p in h.named_parameters() if adapter_trainable(n)]
+    grads = torch.autograd.grad((y * gy).sum() + (yr * gr).sum() + (yd * gd).sum(), [p for _, p in named])
+    res.update(rgb=rgb, dep=dep, y=y, y_rgb=yr, y_dte=yd, gy=gy, gyr=gr, gyd=gd)
+    for (n, _), gp in zip(named, grads):
+        res[f"g.{n}"] = gp
+    res["state_keys"] = np.array(sorted(h.state_dict().keys()))
+    save("cmnext_tiny.npz", regen=("rgb", "dep", "gy", "gyr", "gyd"), **res)
+
+    # full CMNeXt Swin-B at 512² (config C2 shapes), B=1: checksums only
+    model = ref.cmnext.CMNeXt("SwinTransformer-B", 40, ["img", "depth"])
+    keys = sorted(model.state_dict().keys())
+    shapes = [tuple(model.state_dict()[k].shape) for k in keys]
+    fill_module(model, seed=31)
+    model.eval()
+    model.backbone.eval()
+    rgb = t(seeded((1, 3, 512, 512), 110))
+    dep = t(seeded((1, 3, 512, 512), 111, "uniform"))
+    with torch.no_grad():
+        outs = model.backbone([rgb, dep])
+        y, yr, yd = model([rgb, dep])
+    cs = {}
+    for name, ts in (("fuse", outs[0]), ("rgb", outs[1]), ("dte", outs[2])):
+        for i, f in enumerate(ts):
+            cs[f"feat_{name}{i}"] = np.array([f.double().mean().item(), f.double().abs().mean().item(),
+                                              f.double().pow(2).mean().sqrt().item()])
+    for name, f in (("y", y), ("y_rgb", yr), ("y_dte", yd)):
+        cs[name] = np.array([f.double().mean().item(), f.double().abs().mean().item(),
+                             f.double().pow(2).mean().sqrt().item()])
+        cs[name + "_argmax_hist"] = torch.bincount(f.argmax(1).flatten(), minlength=40).numpy()
+    cs["state_keys"] = np.array(keys)
+    cs["state_shapes"] = np.array([",".join(map(str, s)) for s in shapes])
+    save("cmnext_swinb512_checksums.npz", **cs)
+
+
+# --------------------------------------------------------------------------- LightSB
+def gen_sb(ref):
+    sbm = ref.sb.LightSB(dim=512, n_potentials=10, epsilon=0.1, is_diagonal=True)
+    fill_module(sbm, seed=37)
+    with torch.no_grad():
+        sbm.S_log_diagonal_matrix.copy_(torch.log(torch.tensor(0.1)) +
+                                        0.3 * t(seeded((10, 512), 120, "uniform", lo=-1, hi=1)))
+        sbm.log_alpha_raw.copy_(0.1 * t(seeded((10,), 121)))
+        sbm.r.copy_(t(seeded((10, 512), 122)))
+    rows = 128
+    x = t(seeded((rows, 512), 123))
+    res = {"x": x, "r": sbm.r, "S_log_diag": sbm.S_log_diagonal_matrix, "log_alpha_raw": sbm.log_alpha_raw,
+           "epsilon": sbm.epsilon}
+    for tt in (0.0, 0.3, 0.9):
+        res[f"drift_t{tt}"] = sbm.get_drift(x, torch.full((rows,), tt))
+        res[f"drift64_t{tt}"] = sbm.double().get_drift(x.double(), torch.full((rows,), tt, dtype=torch.float64))
+        sbm.float()
+    res["log_C"] = sbm.get_log_C(x)
+    res["log_potential"] = sbm.get_log_potential(x)
+    # Euler–Maruyama with injected noise (sb.py:163-175 draws torch.randn_like each step)
+    n_steps = 10
+    noise = t(seeded((n_steps, rows, 512), 124))
+    it = iter(noise)
+    orig = torch.randn_like
+    torch.randn_like = lambda a, **k: next(it).to(a.dtype)
+    try:
+        traj = sbm.sample_euler_maruyama(x, n_steps)
+    finally:
+        torch.randn_like = orig
+    res.update(em_noise=noise, em_traj_sel=traj[:, [1, 5, 10]], em_traj_cs=np.stack([np.asarray([traj[:, i].double().sum().item(), traj[:, i].double().abs().sum().item()]) for i in range(n_steps + 1)]), em_steps=np.array(n_steps))
+    save("lightsb.npz", regen=("x", "em_noise", "r"), **res)
+
+
+# --------------------------------------------------------------------------- metrics / MMST
+def gen_metrics_loss(ref):
+    n_cls = 7
+    logits = t(seeded((3, n_cls, 40, 48), 130))
+    gt = torch.from_numpy((seeded((3, 40, 48), 131, "uniform") * n_cls).astype(np.int64))
+    gt[torch.from_numpy(seeded((3, 40, 48), 132, "uniform") < 0.1)] = 255
+    gt[0, :5, :] = 3
+    m = ref.metrics.Metrics(n_cls, 255, "cpu")
+    m.update(logits, gt)
+    m.update(logits.flip(-1), gt)
+    ious, miou = m.compute_iou()
+    # MMST loss (train_mm.py:137-148) with CrossEntropy(ignore_index=255) (losses.py:6-19)
+    lf = nn.CrossEntropyLoss(ignore_index=255)
+    lr_, ld_ = t(seeded((3, n_cls, 40, 48), 133)), t(seeded((3, n_cls, 40, 48), 134))
+    pred = logits.softmax(dim=1).argmax(dim=1)
+    mask_lbl = gt.clone()
+    mask_lbl[pred != gt] = 255
+    loss = lf(logits, gt) + 0.01 * lf(lr_, mask_lbl) + 0.01 * lf(ld_, mask_lbl)
+    save("metrics_loss.npz", logits=logits, gt=gt, ious=np.array(ious), miou=np.array(miou),
+         tp=np.array(m.tp), fp=np.array(m.fp), fn=np.array(m.fn), logits_rgb=lr_, logits_dte=ld_,
+         mmst_loss=loss)
+
+
+if __name__ == "__main__":
+    which = sys.argv[1:] or ["msda", "swin", "block", "dattn", "fusion", "cmnext", "sb", "metrics"]
+    ref = load_reference()
+    torch.manual_seed(0)
+    fns = {"msda": gen_msda, "swin": gen_swin_wmsa, "block": gen_swin_block, "dattn": gen_dattn,
+           "fusion": gen_fusion_small, "cmnext": gen_cmnext, "sb": gen_sb, "metrics": gen_metrics_loss}
+    for w in which:
+        fns[w](ref)

@@ -1,0 +1,191 @@
+"""Container-only loader for the IR-ADS *reference* Python modules.
+
+TEST INFRASTRUCTURE ONLY.  Used solely by ``oracle/gen_golden.py`` to produce the
+golden fixtures under ``tests/golden/``.  ``/root/reference`` never ships to the GPU
+box; nothing in the product, in ``bench.py`` or in the ``-m gpu`` tests imports this.
+
+The reference modules are loaded by file path.  Their missing
+third-party symbols (mmcv 2.0.0rc4, mmengine 0.10.7, mmseg 1.2.2, timm 0.4.12,
+fvcore, geotorch) are registered as small stand-ins whose semantics follow those
+packages as the reference uses them:
+
+* ``build_norm_layer(dict(type='LN'), C)`` -> ``('ln', nn.LayerNorm(C))`` (eps 1e-5)
+* ``build_conv_layer(cfg, ...)`` -> ``nn.Conv2d(...)``
+* mmcv ``FFN``: ``layers = Seq(Seq(Linear, GELU, Dropout), Linear, Dropout)``,
+  ``forward(x, identity) = identity + dropout_layer(layers(x))``
+* ``build_dropout(DropPath)`` -> timm DropPath
+* geotorch.orthogonal -> no-op (only the non-diagonal LightSB path uses it: parity unpinned)
+* ``modeling.sb_modules.MyMixtureSameFamily.MixtureSameFamily`` ->
+  ``torch.distributions.MixtureSameFamily``
+
+The mmcv/mmengine/timm arithmetic is therefore "parity unpinned" (no reference test
+covers it); PyTorch's own LayerNorm / Linear / GELU / grid_sample are the arithmetic.
+"""
+import importlib.util
+import sys
+import types
+
+import torch
+import torch.nn as nn
+
+REF = "/root/reference"
+
+
+def _mod(name, **attrs):
+    m = sys.modules.get(name) or types.ModuleType(name)
+    for k, v in attrs.items():
+        setattr(m, k, v)
+    sys.modules[name] = m
+    return m
+
+
+class _DropPath(nn.Module):
+    def __init__(self, drop_prob=0.0):
+        super().__init__()
+        self.drop_prob = drop_prob
+
+    def forward(self, x):
+        if self.drop_prob == 0.0 or not self.training:
+            return x
+        kp = 1 - self.drop_prob
+        shape = (x.shape[0],) + (1,) * (x.ndim - 1)
+        r = kp + torch.rand(shape, dtype=x.dtype, device=x.device)
+        r.floor_()
+        return x.div(kp) * r
+
+
+def _build_dropout(cfg):
+    cfg = dict(cfg)
+    t = cfg.pop("type")
+    if t == "DropPath":
+        return _DropPath(cfg.get("drop_prob", 0.0))
+    if t == "Dropout":
+        return nn.Dropout(cfg.get("drop_prob", 0.0))
+    raise ValueError(t)
+
+
+class _FFN(nn.Module):
+    def __init__(self, embed_dims=256, feedforward_channels=1024, num_fcs=2,
+                 act_cfg=dict(type="ReLU", inplace=True), ffn_drop=0.0,
+                 dropout_layer=None, add_identity=True, init_cfg=None, **kw):
+        super().__init__()
+        assert num_fcs == 2
+        act = {"GELU": nn.GELU(), "ReLU": nn.ReLU(True)}[act_cfg["type"]]
+        self.layers = nn.Sequential(
+            nn.Sequential(nn.Linear(embed_dims, feedforward_channels), act, nn.Dropout(ffn_drop)),
+            nn.Linear(feedforward_channels, embed_dims),
+            nn.Dropout(ffn_drop),
+        )
+        self.dropout_layer = _build_dropout(dropout_layer) if dropout_layer else nn.Identity()
+        self.add_identity = add_identity
+
+    def forward(self, x, identity=None):
+        out = self.layers(x)
+        if not self.add_identity:
+            return self.dropout_layer(out)
+        if identity is None:
+            identity = x
+        return identity + self.dropout_layer(out)
+
+
+class _BaseModule(nn.Module):
+    def __init__(self, init_cfg=None):
+        super().__init__()
+        self.init_cfg = init_cfg
+
+
+def _build_norm_layer(cfg, num_features):
+    assert cfg["type"] == "LN", cfg
+    return "ln", nn.LayerNorm(num_features)
+
+
+def _to_2tuple(x):
+    return tuple(x) if isinstance(x, (tuple, list)) else (x, x)
+
+
+class _Registry:
+    def register_module(self, *a, **k):
+        return lambda cls: cls
+
+
+def _install_standins():
+    _mod("mmcv")
+    _mod("mmcv.cnn", build_norm_layer=_build_norm_layer,
+         build_conv_layer=lambda cfg, *a, **k: nn.Conv2d(*a, **k))
+    _mod("mmcv.cnn.bricks")
+    _mod("mmcv.cnn.bricks.transformer", FFN=_FFN, build_dropout=_build_dropout)
+    _mod("mmengine")
+    _mod("mmengine.logging", print_log=lambda *a, **k: None)
+    _mod("mmengine.model", BaseModule=_BaseModule, ModuleList=nn.ModuleList)
+    _mod("mmengine.model.weight_init", trunc_normal_=nn.init.trunc_normal_,
+         constant_init=lambda m, val, bias=0: None, trunc_normal_init=lambda m, std, bias=0: None)
+    _mod("mmengine.runner", CheckpointLoader=None)
+    _mod("mmengine.utils", to_2tuple=_to_2tuple)
+    _mod("mmseg")
+    _mod("mmseg.registry", MODELS=_Registry())
+    _mod("timm")
+    _mod("timm.models")
+    _mod("timm.models.layers", DropPath=_DropPath)
+    _mod("fvcore")
+    _mod("fvcore.nn", flop_count_table=None, FlopCountAnalysis=None)
+    _mod("geotorch", orthogonal=lambda *a, **k: None)
+    _mod("modeling")
+    _mod("modeling.sb_modules")
+    _mod("modeling.sb_modules.MyMixtureSameFamily",
+         MixtureSameFamily=torch.distributions.MixtureSameFamily)
+    # placeholder so MultiScaleDeformableAttention is not replaced by the dummy class;
+    # on CPU tensors the module takes its PyTorch path (multi_scale_deform_attn.py:341-353)
+    for p in ("detrex", "detrex.layers"):
+        _mod(p)
+    _mod("detrex._C")
+    for p in ("semseg", "semseg.models", "semseg.models.backbones", "semseg.models.heads",
+              "semseg.models.layers", "modules"):
+        m = _mod(p)
+        m.__path__ = []
+
+
+def _load(name, rel):
+    spec = importlib.util.spec_from_file_location(name, f"{REF}/{rel}")
+    m = importlib.util.module_from_spec(spec)
+    sys.modules[name] = m
+    spec.loader.exec_module(m)
+    return m
+
+
+_LOADED = {}
+
+
+def load_reference():
+    """Return a namespace with the reference's hot-path modules."""
+    if _LOADED:
+        return types.SimpleNamespace(**_LOADED)
+    _install_standins()
+    common = _load("semseg.models.layers.common", "semseg/models/layers/common.py")
+    init = _load("semseg.models.layers.initialize", "semseg/models/layers/initialize.py")
+    layers = sys.modules["semseg.models.layers"]
+    for m in (common, init):
+        for k in dir(m):
+            if not k.startswith("_"):
+                setattr(layers, k, getattr(m, k))
+    embed = _load("semseg.models.backbones.embed", "semseg/models/backbones/embed.py")
+    swin = _load("semseg.models.backbones.swin", "semseg/models/backbones/swin.py")
+    bb = sys.modules["semseg.models.backbones"]
+    bb.SwinTransformer = swin.SwinTransformer
+    seg = _load("semseg.models.heads.segformer", "semseg/models/heads/segformer.py")
+    heads = sys.modules["semseg.models.heads"]
+    heads.SegFormerHead = seg.SegFormerHead
+    heads.LightHamHead = None
+    heads.UPerHead = None
+    base = _load("semseg.models.base", "semseg/models/base.py")
+    cmnext = _load("semseg.models.cmnext", "semseg/models/cmnext.py")
+    msda = _load("detrex.layers.multi_scale_deform_attn", "detrex/layers/multi_scale_deform_attn.py")
+    sb = _load("modules.sb", "modules/sb.py")
+    metrics = _load("semseg.metrics", "semseg/metrics.py")
+    _LOADED.update(swin=swin, embed=embed, segformer=seg, base=base, cmnext=cmnext,
+                   msda=msda, sb=sb, metrics=metrics)
+    return types.SimpleNamespace(**_LOADED)
+
+
+if __name__ == "__main__":
+    r = load_reference()
+    print(sorted(vars(r)))
