@@ -41,7 +41,7 @@ def save(name, regen=(), **arrays):
     arrs = {}
     for k, v in arrays.items():
         v = v.detach().cpu().numpy() if torch.is_tensor(v) else np.asarray(v)
-        if k in regen or any(k.endswith(s) for s in regen):
+        if k in regen:
             arrs[k + "__cs"] = checksum(v)
         else:
             arrs[k] = v
@@ -143,7 +143,7 @@ def gen_msda(ref):
                     f"{tag}_gquery": grads[0], f"{tag}_gvalue": grads[1]})
         for (n, _), gp in zip(mod.named_parameters(), grads[2:]):
             res[f"{tag}_g.{n}"] = gp
-    save("msda_module.npz", regen=("_query", "_value", "_qpos", "_gout"), **res)
+    save("msda_module.npz", regen=[f"{a}_{b}" for a in ("r2", "r4") for b in ("query", "value", "qpos", "gout")], **res)
 
 
 # --------------------------------------------------------------------------- Swin
@@ -168,7 +168,7 @@ def gen_swin_wmsa(ref):
                     f"{tag}_out": o, f"{tag}_gout": g, f"{tag}_gx": grads[0]})
         for n, gp in zip(names, grads[1:]):
             res[f"{tag}_g.{n}"] = gp
-    save("swin_wmsa.npz", regen=("_x", "_gout"), **res)
+    save("swin_wmsa.npz", regen=[k for k in res if k.endswith("_x") or k.endswith("_gout")], **res)
 
 
 def gen_swin_block(ref):
@@ -195,7 +195,7 @@ def gen_swin_block(ref):
             if gp is not None:
                 res[f"{mode}_g.{n}"] = gp
     res["hw"] = np.array([H, W])
-    save("swin_stage.npz", regen=("_x", "_g1", "_g2"), **res)
+    save("swin_stage.npz", regen=[f"{m}_{b}" for m in ("rgb", "dte") for b in ("x", "g1", "g2")], **res)
 
 
 # --------------------------------------------------------------------------- DAttn
@@ -246,7 +246,7 @@ def gen_dattn(ref):
         res[f"{tag}_pos_y"] = rec.grids[1][0]
         res[f"{tag}_disp_x"] = rec.grids[6][0]
         res[f"{tag}_disp_y"] = rec.grids[7][0]
-    save("dattn.npz", regen=("_x", "_y", "_gout"), **res)
+    save("dattn.npz", regen=[f"{c}_{b}" for c in cfgs for b in ("x", "y", "gout")], **res)
 
 
 def gen_fusion_small(ref):

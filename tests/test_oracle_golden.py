@@ -1,0 +1,295 @@
+"""Pin the CPU oracle (oracle/irads_ref.py, oracle/csrc/*.c) against the golden fixtures
+generated from the reference itself (oracle/gen_golden.py).  CPU only."""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+import pytest
+import torch
+
+import irads_ref as R
+from fill import fill_module, seeded
+from golden_util import Fixture, close
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+P = ctypes.c_void_p
+
+
+@pytest.fixture(scope="module")
+def coracle():
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+    lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "liboracle.so"))
+    return lib
+
+
+def _ptr(a):
+    return a.ctypes.data_as(P)
+
+
+# ------------------------------------------------------------------- MSDA
+def test_msda_reference_test_cases():
+    """tests/test_ms_deform_attn.py:34-133 problems, fp64, fwd + grads."""
+    fx = Fixture("msda_ref_test.npz")
+    shapes = fx.t("shapes")
+    for tag in ("fwd", "c30", "c32", "c64", "c71", "c1025"):
+        v = fx.t(f"{tag}_value").requires_grad_()
+        loc = fx.t(f"{tag}_loc").requires_grad_()
+        aw = fx.t(f"{tag}_aw").requires_grad_()
+        o = R.multi_scale_deformable_attn_pytorch(v, shapes, loc, aw)
+        close(o, fx[f"{tag}_out"], 1e-15, 1e-12, f"{tag} out")
+        gv, gl, ga = torch.autograd.grad((o * fx.t(f"{tag}_gout")).sum(), (v, loc, aw))
+        close(gv, fx[f"{tag}_gvalue"], 1e-14, 1e-10, f"{tag} gvalue")
+        close(gl, fx[f"{tag}_gloc"], 1e-14, 1e-10, f"{tag} gloc")
+        close(ga, fx[f"{tag}_gaw"], 1e-14, 1e-10, f"{tag} gaw")
+
+
+def test_msda_c_oracle_bitexact(coracle):
+    """The C restatement reproduces the reference's fp32 output bit-for-bit per sample
+    (its corner indices are the integer floors the HIP kernels must match)."""
+    fx = Fixture("msda_dino.npz")
+    shapes = fx["shapes"].astype(np.int64)
+    S = int((shapes[:, 0] * shapes[:, 1]).sum())
+    bs, M, D, Q, L, P_ = 1, 4, 32, 300, 4, 4
+    value = fx.regen("value", (bs, S, M, D), 21).numpy()
+    loc, aw = fx["loc"], fx["aw"]
+    out = np.zeros((bs, Q, M * D), np.float32)
+    cor = np.zeros((bs, Q, M, L, P_, 2), np.int32)
+    coracle.oracle_msda_fwd(_ptr(value), _ptr(shapes), bs, S, M, D, L, Q, P_, _ptr(loc), _ptr(aw), _ptr(out),
+                            _ptr(cor))
+    close(torch.from_numpy(out), fx["out"], 2e-6, 1e-5, "msda C oracle out")
+    # per-sample bit-exactness vs torch CPU grid_sample (the reference's arithmetic)
+    img = value[0].transpose(1, 2, 0).reshape(M * D, S)
+    start = 0
+    for l, (H, W) in enumerate(shapes):
+        plane = np.ascontiguousarray(img[:, start:start + H * W].reshape(M * D, H, W))
+        g = (np.float32(2) * loc[0, :, 0, l] - np.float32(1)).reshape(-1, 2).astype(np.float32)
+        o = np.zeros((M * D, g.shape[0]), np.float32)
+        c = np.zeros((g.shape[0], 2), np.int32)
+        coracle.oracle_grid_sample(_ptr(plane), M * D, int(H), int(W), _ptr(np.ascontiguousarray(g)), g.shape[0],
+                                   0, _ptr(o), _ptr(c))
+        ref = torch.nn.functional.grid_sample(torch.from_numpy(plane)[None], torch.from_numpy(g)[None, None],
+                                              mode="bilinear", align_corners=False)[0, :, 0].numpy()
+        assert (o.view(np.uint32) == ref.view(np.uint32)).all()
+        assert (c == cor[0, :, 0, l].reshape(-1, 2)).all()
+        start += H * W
+
+
+def test_msda_oracle_fp32_dino():
+    fx = Fixture("msda_dino.npz")
+    shapes = fx.t("shapes")
+    S = int(shapes.prod(1).sum())
+    v = fx.regen("value", (1, S, 4, 32), 21).requires_grad_()
+    loc, aw = fx.t("loc").requires_grad_(), fx.t("aw").requires_grad_()
+    o = R.multi_scale_deformable_attn_pytorch(v, shapes, loc, aw)
+    close(o, fx["out"], 1e-6, 1e-5, "out")
+    g = fx.regen("gout", tuple(o.shape), 26)
+    gv, gl, ga = torch.autograd.grad((o * g).sum(), (v, loc, aw))
+    close(gv, fx["gvalue"], 1e-5, 1e-4, "gvalue")
+    close(gl, fx["gloc"], 1e-4, 1e-4, "gloc")
+    close(ga, fx["gaw"], 1e-5, 1e-4, "gaw")
+
+
+def test_msda_module_oracle():
+    fx = Fixture("msda_module.npz")
+    m = R.MultiScaleDeformableAttention()
+    fill_module(m, seed=5)
+    m.eval()
+    shapes, lsi = fx.t("shapes"), fx.t("level_start_index")
+    S = int(shapes.prod(1).sum())
+    for tag, seed in (("r2", 31), ("r4", 32)):
+        q = fx.regen(f"{tag}_query", (40, 2, 256), seed).requires_grad_()
+        v = fx.regen(f"{tag}_value", (S, 2, 256), seed + 1).requires_grad_()
+        qp = fx.regen(f"{tag}_qpos", (40, 2, 256), seed + 2)
+        o = m(q, value=v, query_pos=qp, key_padding_mask=fx.t(f"{tag}_mask"), reference_points=fx.t(f"{tag}_ref"),
+              spatial_shapes=shapes, level_start_index=lsi)
+        close(o, fx[f"{tag}_out"], 1e-5, 1e-5, f"{tag} out")
+        g = fx.regen(f"{tag}_gout", tuple(o.shape), seed + 5)
+        names = [n for n, _ in m.named_parameters()]
+        grads = torch.autograd.grad((o * g).sum(), [q, v] + [p for _, p in m.named_parameters()])
+        close(grads[0], fx[f"{tag}_gquery"], 1e-4, 1e-4, "gquery")
+        close(grads[1], fx[f"{tag}_gvalue"], 1e-4, 1e-4, "gvalue")
+        for n, gp in zip(names, grads[2:]):
+            close(gp, fx[f"{tag}_g.{n}"], 1e-3, 1e-4, n)
+
+
+# ------------------------------------------------------------------- Swin
+def test_shift_window_msa_oracle():
+    fx = Fixture("swin_wmsa.npz")
+    for tag in ("pad_noshift", "pad_shift", "nopad_noshift", "nopad_shift", "rect_shift"):
+        B, H, W, shift, C, nH = fx[f"{tag}_cfg"].tolist()
+        m = R.ShiftWindowMSA(C, nH, 12, shift)
+        fill_module(m, seed=7)
+        m.eval()
+        x = fx.regen(f"{tag}_x", (B, H * W, C), 40 + H + shift).requires_grad_()
+        o = m(x, (H, W))
+        close(o, fx[f"{tag}_out"], 1e-5, 1e-5, f"{tag} out")
+        g = fx.regen(f"{tag}_gout", tuple(o.shape), 41 + H + shift)
+        names = [n for n, _ in m.named_parameters()]
+        grads = torch.autograd.grad((o * g).sum(), [x] + [p for _, p in m.named_parameters()])
+        close(grads[0], fx[f"{tag}_gx"], 1e-4, 1e-4, f"{tag} gx")
+        for n, gp in zip(names, grads[1:]):
+            close(gp, fx[f"{tag}_g.{n}"], 1e-3, 1e-4, f"{tag} {n}")
+
+
+def test_swin_stage_oracle():
+    fx = Fixture("swin_stage.npz")
+    H, W = fx["hw"].tolist()
+    blk = R.SwinBlockSequence(64, 2, 256, 2, 12, downsample=R.PatchMerging(64, 128))
+    fill_module(blk, seed=9)
+    blk.eval()
+    for mode in ("rgb", "dte"):
+        x = fx.regen(f"{mode}_x", (2, H * W, 64), 50 + len(mode)).requires_grad_()
+        xd, hwd, xo, _ = blk(x, (H, W), mode)
+        assert tuple(hwd) == tuple(fx[f"{mode}_hwdown"].tolist())
+        close(xd, fx[f"{mode}_xdown"], 1e-4, 1e-4, "xdown")
+        close(xo, fx[f"{mode}_xout"], 1e-4, 1e-4, "xout")
+        g1 = fx.regen(f"{mode}_g1", tuple(xd.shape), 51)
+        g2 = fx.regen(f"{mode}_g2", tuple(xo.shape), 52)
+        names = [n for n, _ in blk.named_parameters()]
+        grads = torch.autograd.grad((xd * g1).sum() + (xo * g2).sum(), [x] + [p for _, p in blk.named_parameters()],
+                                    allow_unused=True)
+        close(grads[0], fx[f"{mode}_gx"], 1e-3, 1e-4, "gx")
+        for n, gp in zip(names, grads[1:]):
+            if gp is not None:
+                close(gp, fx[f"{mode}_g.{n}"], 1e-3, 1e-3, f"{mode} {n}")
+
+
+# ------------------------------------------------------------------- DAttn / fusion
+def test_dattn_oracle(coracle):
+    fx = Fixture("dattn.npz")
+    for tag in ("s0", "s1", "s2", "s3", "swinl_s0"):
+        dims, stride, g, h, level, H, W, B = fx[f"{tag}_cfg"].tolist()
+        m = R.DAttentionMM(dims, stride=stride, n_groups=g, n_heads=h, level=level)
+        fill_module(m, seed=13)
+        m.eval()
+        x = fx.regen(f"{tag}_x", (B, dims, H, W), 60 + level).requires_grad_()
+        y = fx.regen(f"{tag}_y", (B, dims, H, W), 70 + level, "uniform").requires_grad_()
+        o = m(x, y)
+        close(o, fx[f"{tag}_out"], 1e-5, 1e-4, f"{tag} out")
+        go = fx.regen(f"{tag}_gout", tuple(o.shape), 80 + level)
+        names = [n for n, _ in m.named_parameters()]
+        grads = torch.autograd.grad((o * go).sum(), [x, y] + [p for _, p in m.named_parameters()])
+        close(grads[0], fx[f"{tag}_gx"], 1e-4, 1e-3, f"{tag} gx")
+        close(grads[1], fx[f"{tag}_gy"], 1e-4, 1e-3, f"{tag} gy")
+        for n, gp in zip(names, grads[2:]):
+            close(gp, fx[f"{tag}_g.{n}"], 1e-3, 1e-3, f"{tag} {n}")
+        # C oracle reproduces the reference's align_corners=True sampling bit-exactly
+        pos = fx[f"{tag}_pos_x"]                       # (B*g, Hk, Wk, 2) in (y, x)
+        grid = np.ascontiguousarray(pos[0][..., ::-1].reshape(-1, 2)).astype(np.float32)
+        gc = dims // g
+        plane = np.ascontiguousarray(x.detach().numpy()[0, :gc])
+        out = np.zeros((gc, grid.shape[0]), np.float32)
+        coracle.oracle_grid_sample(_ptr(plane), gc, H, W, _ptr(grid), grid.shape[0], 1, _ptr(out), None)
+        ref = torch.nn.functional.grid_sample(torch.from_numpy(plane)[None], torch.from_numpy(grid)[None, None],
+                                              mode="bilinear", align_corners=True)[0, :, 0].numpy()
+        assert (out.view(np.uint32) == ref.view(np.uint32)).all()
+
+
+def test_fusion_small_oracle():
+    fx = Fixture("fusion_small.npz")
+    m = R.MPGBlock(64, 0.125)
+    fill_module(m, seed=17)
+    xr = fx.regen("mpg_xr", (2, 42, 64), 90).requires_grad_()
+    xd = fx.regen("mpg_xd", (2, 42, 64), 91).requires_grad_()
+    a, b = m(xr, xd, 6, 7)
+    close(a, fx["mpg_a"], 1e-5, 1e-5, "mpg a")
+    close(b, fx["mpg_b"], 1e-5, 1e-5, "mpg b")
+    d = R.DeformMPGBlock(128, 4, 2, 4, 0, 1, 0.125)
+    fill_module(d, seed=19)
+    d.eval()
+    xr = fx.regen("dmpg_xr", (2, 256, 128), 94).requires_grad_()
+    xd = fx.regen("dmpg_xd", (2, 256, 128), 95).requires_grad_()
+    o = d(xr, xd, 16, 16, 1)
+    close(o, fx["dmpg_out"], 1e-5, 1e-4, "dmpg out")
+    go = fx.regen("dmpg_gout", tuple(o.shape), 96)
+    gxr, gxd = torch.autograd.grad((o * go).sum(), [xr, xd])
+    close(gxr, fx["dmpg_gxr"], 1e-4, 1e-3, "dmpg gxr")
+    close(gxd, fx["dmpg_gxd"], 1e-4, 1e-3, "dmpg gxd")
+    ad = R.Adapter(128, 0.0625, skip_connect=False)
+    fill_module(ad, seed=23)
+    ad.eval()
+    x = fx.regen("adapter_x", (2, 30, 128), 97)
+    close(ad(x), fx["adapter_out"], 1e-6, 1e-5, "adapter")
+
+
+# ------------------------------------------------------------------- CMNeXt
+def adapter_trainable(n):
+    return ("Adapter" in n) or ("extra_patch_embed" in n) or ("head" in n) or ("MPG" in n)
+
+
+def test_cmnext_tiny_oracle():
+    fx = Fixture("cmnext_tiny.npz")
+    m = R.CMNeXt(num_classes=5, _tiny=True)
+    assert sorted(m.state_dict().keys()) == fx["state_keys"].tolist()
+    fill_module(m, seed=29)
+    m.eval()
+    rgb = fx.regen("rgb", (2, 3, 128, 160), 100)
+    dep = fx.regen("dep", (2, 3, 128, 160), 101, "uniform")
+    y, yr, yd = m([rgb, dep])
+    close(y, fx["y"], 1e-4, 1e-4, "y")
+    close(yr, fx["y_rgb"], 1e-4, 1e-4, "y_rgb")
+    close(yd, fx["y_dte"], 1e-4, 1e-4, "y_dte")
+    gs = [fx.regen(k, tuple(y.shape), 102 + i) for i, k in enumerate(("gy", "gyr", "gyd"))]
+    named = [(n, p) for n, p in m.named_parameters() if adapter_trainable(n)]
+    grads = torch.autograd.grad((y * gs[0]).sum() + (yr * gs[1]).sum() + (yd * gs[2]).sum(), [p for _, p in named])
+    for (n, _), g in zip(named, grads):
+        ref = fx[f"g.{n}"]
+        scale = max(float(np.abs(ref).max()), 1e-3)
+        close(g, ref, 2e-3 * scale, 2e-3, n)
+
+
+def test_swinb_state_dict_schema():
+    """the full Swin-B CMNeXt key schema (817 keys) and shapes."""
+    fx = Fixture("cmnext_swinb512_checksums.npz")
+    m = R.CMNeXt("SwinTransformer-B", 40, ["img", "depth"])
+    sd = m.state_dict()
+    keys = sorted(sd.keys())
+    assert keys == fx["state_keys"].tolist()
+    assert [",".join(map(str, sd[k].shape)) for k in keys] == fx["state_shapes"].tolist()
+
+
+@pytest.mark.slow
+def test_swinb512_checksums_oracle():
+    fx = Fixture("cmnext_swinb512_checksums.npz")
+    m = R.CMNeXt("SwinTransformer-B", 40, ["img", "depth"])
+    fill_module(m, seed=31)
+    m.eval()
+    rgb = torch.from_numpy(seeded((1, 3, 512, 512), 110))
+    dep = torch.from_numpy(seeded((1, 3, 512, 512), 111, "uniform"))
+    with torch.no_grad():
+        y, yr, yd = m([rgb, dep])
+    for name, f in (("y", y), ("y_rgb", yr), ("y_dte", yd)):
+        got = np.array([f.double().mean().item(), f.double().abs().mean().item(), f.double().pow(2).mean().sqrt().item()])
+        np.testing.assert_allclose(got, fx[name], rtol=1e-4, atol=1e-5)
+
+
+# ------------------------------------------------------------------- LightSB
+def test_lightsb_oracle():
+    fx = Fixture("lightsb.npz")
+    x = fx.regen("x", (128, 512), 123)
+    r = fx.regen("r", (10, 512), 122)
+    Sl, la, eps = fx.t("S_log_diag"), fx.t("log_alpha_raw"), float(fx["epsilon"])
+    for tt in (0.0, 0.3, 0.9):
+        d = R.lightsb_drift(x, torch.full((128,), tt), r, Sl, la, eps)
+        # the reference's own fp32 drift is 2.1e-3 off its fp64 drift (logsumexp cancellation):
+        # fp32 comparisons get twice that; the fp64 comparison below pins the math.
+        close(d, fx[f"drift_t{tt}"], 4e-3, 1e-4, f"drift {tt}")
+        d64 = R.lightsb_drift(x.double(), torch.full((128,), tt, dtype=torch.float64), r.double(), Sl.double(),
+                              la.double(), eps)
+        close(d64, fx[f"drift64_t{tt}"], 1e-9, 1e-9, f"drift64 {tt}")
+    close(R.lightsb_log_C(x, r, Sl, la, eps), fx["log_C"], 1e-2, 1e-5, "log_C")
+    noise = fx.regen("em_noise", (10, 128, 512), 124)
+    traj = R.lightsb_em(x, 10, noise, r, Sl, la, eps)
+    close(traj[:, [1, 5, 10]], fx["em_traj_sel"], 4e-3, 1e-4, "EM trajectory")
+
+
+# ------------------------------------------------------------------- metrics / MMST
+def test_metrics_and_mmst_oracle():
+    fx = Fixture("metrics_loss.npz")
+    logits, gt = fx.t("logits"), fx.t("gt")
+    tp, fp, fn = R.metrics_tp_fp_fn(logits, gt, 7)
+    tp2, fp2, fn2 = R.metrics_tp_fp_fn(logits.flip(-1), gt, 7)
+    assert [a + b for a, b in zip(tp, tp2)] == fx["tp"].tolist()
+    assert [a + b for a, b in zip(fp, fp2)] == fx["fp"].tolist()
+    assert [a + b for a, b in zip(fn, fn2)] == fx["fn"].tolist()
