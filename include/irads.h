@@ -1,0 +1,141 @@
+/*
+ * irads.h — C ABI of libirads.so, the MI355X (gfx950) hot path of IR-ADS's multimodal
+ * segmentation (Swin window attention, DSCF deformable fusion, multi-scale deformable
+ * attention, LightSB drift / Euler–Maruyama).
+ *
+ * Conventions (every entry point):
+ *   - plain device pointers, explicit sizes, a hipStream_t passed as void*;
+ *   - CALLER ALLOCATES every output and workspace (the reference's _C allocates with
+ *     at::zeros, ms_deform_attn_cuda.cu:55,122-124; here the Python wrapper allocates
+ *     with torch and zero-fills gradient accumulators where noted);
+ *   - asynchronous on `stream`, no host synchronisation, no allocation inside: safe to
+ *     capture into a HIP graph;
+ *   - return 0 on success, a nonzero IRADS_E* code otherwise; irads_last_error() gives
+ *     the thread-local message.  The reference only printf()s kernel launch errors
+ *     (ms_deform_im2col_cuda.cuh:948-952); here they are returned.
+ * dtype codes: IRADS_F32, IRADS_BF16 (storage bf16, fp32 arithmetic), IRADS_F64.
+ */
+#ifndef IRADS_H
+#define IRADS_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define IRADS_F32 0
+#define IRADS_BF16 1
+#define IRADS_F64 2
+
+#define IRADS_OK 0
+#define IRADS_EINVAL 1   /* bad argument / unsupported shape or dtype */
+#define IRADS_ELAUNCH 2  /* kernel launch failed */
+
+const char *irads_last_error(void);
+int irads_version(void);
+
+/* ------------------------------------------------------------------ MSDeformAttn
+ * Replaces detrex._C.ms_deform_attn_forward / _backward
+ * (detrex/layers/csrc/vision.cpp:54-59; ms_deform_attn.h:20-61;
+ *  ms_deform_attn_cuda.cu:21-81, 84-154).  Arithmetic follows the reference's PyTorch
+ * path multi_scale_deformable_attn_pytorch (multi_scale_deform_attn.py:96-136) with
+ * grid = 2*loc-1 and CPU grid_sample's unnormalisation, so the integer corners match it
+ * bit-for-bit.  Layouts (all contiguous):
+ *   value (bs, S, M, D)  shapes (L, 2) int64 (H, W)  level_start (L) int64
+ *   loc (bs, Q, M, L, P, 2) (x, y)  aw (bs, Q, M, L, P)  out (bs, Q, M*D)
+ * dtype: IRADS_F32 or IRADS_F64 (AT_DISPATCH_FLOATING_TYPES, ms_deform_attn_cuda.cu:65).
+ * shapes / level_start are DEVICE pointers (as in the reference). */
+int irads_msda_fwd(int dtype, const void *value, const int64_t *shapes, const int64_t *level_start,
+                   const void *loc, const void *aw, int bs, int S, int M, int D, int L, int Q, int P,
+                   void *out, void *stream);
+/* grad_value MUST be zero-filled by the caller (accumulated with atomics);
+ * grad_loc / grad_aw are fully written. */
+int irads_msda_bwd(int dtype, const void *value, const int64_t *shapes, const int64_t *level_start,
+                   const void *loc, const void *aw, const void *grad_out, int bs, int S, int M, int D,
+                   int L, int Q, int P, void *grad_value, void *grad_loc, void *grad_aw, void *stream);
+/* Debug export: the integer corners (x0, y0) per sample, (bs, Q, M, L, P, 2) int32. */
+int irads_msda_corner_index(int dtype, const void *loc, const int64_t *shapes, int bs, int Q, int M,
+                            int L, int P, int32_t *corners, void *stream);
+
+/* ------------------------------------------------------------------ Swin window attention
+ * Replaces the body of ShiftWindowMSA.forward + WindowMSA.forward between the qkv and
+ * proj Linears (semseg/models/backbones/swin.py:180-254 and :81-119): zero-pad to a
+ * multiple of the window (pad tokens carry q,k,v = qkv bias, :186-190), cyclic roll by
+ * -shift (:193-197), the -100/0 region mask (:199-220), window partition, q*scale·kᵀ +
+ * relative-position bias (:98-105), softmax, ·v, window reverse, roll back, crop.
+ *   qkv   (B, H, W, 3*C) tokens, channel = (3, nH, 32)       dtype F32 or BF16
+ *   qkv_bias (3*C) fp32 or NULL (zeros)    rel_table (529, nH) fp32
+ *   mask  (n_mask, 144, 144) fp32 or NULL: explicit WindowMSA mask (swin.py:107-111);
+ *         NULL => the shift-region mask computed in-kernel when shift > 0
+ *   out   (B, H, W, C) same dtype      lse (B*nW, nH, 144) fp32 workspace for backward
+ * window = 12, head_dim = 32 (every Swin-B/L stage).  scale = qk_scale or 32^-0.5. */
+int irads_winattn_fwd(int dtype, const void *qkv, const float *qkv_bias, const float *rel_table,
+                      const float *mask, int n_mask, int B, int H, int W, int C, int nH, int shift,
+                      float scale, void *out, float *lse, void *stream);
+/* grad_qkv (B, H, W, 3C) fully written.  Optional accumulators (zero-filled by the
+ * caller, fp32, or NULL to skip): grad_table (529, nH); grad_bias_pad (3C) = the qkv-bias
+ * gradient carried by the pad tokens (the real tokens' share flows through the Linear). */
+int irads_winattn_bwd(int dtype, const void *qkv, const float *qkv_bias, const float *rel_table,
+                      const float *mask, int n_mask, int B, int H, int W, int C, int nH, int shift,
+                      float scale, const void *out, const float *lse, const void *grad_out,
+                      void *grad_qkv, float *grad_table, float *grad_bias_pad, void *stream);
+
+/* ------------------------------------------------------------------ DSCF / DAttentionMM
+ * Replaces the grid_sample / einsum / softmax core of DAttentionMM.forward
+ * (swin.py:911-1016).  All fp32.
+ *
+ * Feature sampling (swin.py:911-944): for t in {x, y, q} (each (B, C, H, W)) and the
+ * two position sets pos_x, pos_y ((B*G, n, 2) in (y, x) order, in [-1, 1]), bilinear
+ * align_corners=True zero-padded samples, written as (B, C, 2n) = [at pos_x | at pos_y]. */
+int irads_dattn_sample_fwd(const float *x, const float *y, const float *q, const float *pos_x,
+                           const float *pos_y, int B, int C, int H, int W, int G, int n,
+                           float *xs, float *ys, float *qs, void *stream);
+/* grad_x/grad_y/grad_q zero-filled by caller (atomics); grad_pos_x/_y fully written. */
+int irads_dattn_sample_bwd(const float *x, const float *y, const float *q, const float *pos_x,
+                           const float *pos_y, const float *gxs, const float *gys, const float *gqs,
+                           int B, int C, int H, int W, int G, int n, float *grad_x, float *grad_y,
+                           float *grad_q, float *grad_pos_x, float *grad_pos_y, void *stream);
+/* Fused attention with on-the-fly bilinear rpe bias (swin.py:950-1016):
+ *   q (B*nH, hc, HW)  k, v (B*nH, hc, 2n)  rpe (nH, Ht, Wt)  qgrid_y (H), qgrid_x (W)
+ *   (the reference's _get_q_grid values)  out (B*nH, hc, HW)  lse (B*nH, HW).
+ * hc in {2, 4, 8, 12, 16, 24}. */
+int irads_dattn_attn_fwd(const float *q, const float *k, const float *v, const float *pos_x,
+                         const float *pos_y, const float *rpe, const float *qgrid_y, const float *qgrid_x,
+                         int B, int nH, int G, int hc, int H, int W, int n, int Ht, int Wt, float scale,
+                         float *out, float *lse, void *stream);
+/* grad_q fully written; grad_k, grad_v, grad_rpe, grad_pos_x, grad_pos_y zero-filled by
+ * the caller (per-workgroup partial sums are added atomically). delta (B*nH, HW) fp32
+ * workspace. */
+int irads_dattn_attn_bwd(const float *q, const float *k, const float *v, const float *pos_x,
+                         const float *pos_y, const float *rpe, const float *qgrid_y, const float *qgrid_x,
+                         int B, int nH, int G, int hc, int H, int W, int n, int Ht, int Wt, float scale,
+                         const float *out, const float *lse, const float *grad_out, float *delta,
+                         float *grad_q, float *grad_k, float *grad_v, float *grad_rpe,
+                         float *grad_pos_x, float *grad_pos_y, void *stream);
+/* Debug export: integer corners (x0, y0) of align_corners=True sampling at `grid`
+ * ((N, 2) in (x, y) order, the grid_sample convention) on an H x W map. */
+int irads_dattn_sample_index(const float *grid, int N, int H, int W, int32_t *corners, void *stream);
+
+/* ------------------------------------------------------------------ LightSB (diagonal)
+ * modules/sb.py:19-227, diagonal path.  x (rows, D); r, S_log_diag (K, D);
+ * log_alpha_raw (K); t (rows).  fp32 or fp64 (dtype).
+ * drift (sb.py:106-161) in closed form: (Σ_k softmax_k(arg) c_k/A_k − x) / (1 − t). */
+int irads_sb_drift(int dtype, const void *x, const void *t, const void *r, const void *S_log_diag,
+                   const void *log_alpha_raw, double epsilon, int rows, int D, int K, void *drift,
+                   void *stream);
+/* Euler–Maruyama (sb.py:163-175): traj (rows, n_steps+1, D); noise (n_steps, rows, D)
+ * standard normal draws (the reference's torch.randn_like per step). */
+int irads_sb_em(int dtype, const void *x0, const void *noise, int n_steps, const void *r,
+                const void *S_log_diag, const void *log_alpha_raw, double epsilon, int rows, int D, int K,
+                void *traj, void *stream);
+/* GMM logits of forward()/get_log_C (sb.py:57-104, 206-224):
+ * logits (rows, K) = (xSx + 2 x·r)/(2 eps) + log_alpha_raw/eps; log_C (rows) = logsumexp
+ * (either output may be NULL). */
+int irads_sb_logits(int dtype, const void *x, const void *r, const void *S_log_diag,
+                    const void *log_alpha_raw, double epsilon, int rows, int D, int K, void *logits,
+                    void *log_C, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* IRADS_H */

@@ -1,0 +1,72 @@
+// Shared helpers for the gfx950 kernels of libirads.so.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "../../include/irads.h"
+
+namespace irads {
+
+void set_error(const char *fmt, ...);
+
+#define IRADS_REQUIRE(cond, ...)          \
+    do {                                  \
+        if (!(cond)) {                    \
+            ::irads::set_error(__VA_ARGS__); \
+            return IRADS_EINVAL;          \
+        }                                 \
+    } while (0)
+
+inline int check_launch(const char *what) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        set_error("%s: launch failed: %s", what, hipGetErrorString(e));
+        return IRADS_ELAUNCH;
+    }
+    return IRADS_OK;
+}
+
+typedef __attribute__((ext_vector_type(8))) short bf16x8;
+typedef __attribute__((ext_vector_type(4))) short bf16x4;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+__device__ __forceinline__ float bf2f(unsigned short u) {
+    return __uint_as_float(((unsigned)u) << 16);
+}
+// round-to-nearest-even f32 -> bf16 (finite inputs; NaN kept NaN via the quiet bit)
+__device__ __forceinline__ unsigned short f2bf(float f) {
+    unsigned u = __float_as_uint(f);
+    if ((u & 0x7f800000u) == 0x7f800000u) return (unsigned short)((u >> 16) | ((u & 0xffff) ? 0x40 : 0));
+    u += 0x7fffu + ((u >> 16) & 1u);
+    return (unsigned short)(u >> 16);
+}
+
+template <typename T> struct io;
+template <> struct io<float> {
+    static __device__ __forceinline__ float ld(const float *p, long i) { return p[i]; }
+    static __device__ __forceinline__ void st(float *p, long i, float v) { p[i] = v; }
+};
+template <> struct io<unsigned short> {  // bf16 storage
+    static __device__ __forceinline__ float ld(const unsigned short *p, long i) { return bf2f(p[i]); }
+    static __device__ __forceinline__ void st(unsigned short *p, long i, float v) { p[i] = f2bf(v); }
+};
+
+// XCD-aware, bijective remap of a linear block id (cdna_hip_programming.md §5, T1):
+// consecutive logical ids land on the same XCD (each XCD has its own L2).
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+    const int nx = 8;
+    int q = nwg / nx, r = nwg % nx, x = orig % nx;
+    int base = (x < r) ? x * (q + 1) : r * (q + 1) + (x - r) * q;
+    return base + orig / nx;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+}  // namespace irads

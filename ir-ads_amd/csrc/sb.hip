@@ -1,0 +1,259 @@
+// LightSB (diagonal Schrödinger bridge GMM, modules/sb.py:19-227) kernels for gfx950.
+//
+// get_drift (sb.py:106-161) differentiates a logsumexp with torch.autograd.grad every
+// call.  Its gradient has a closed form: with
+//   A_kd = t/(eps(1-t)) + 1/(eps S_kd),  c_kd = x_d/(eps(1-t)) + r_kd/(eps S_kd),
+//   arg_k = log_alpha_raw_k/eps - ½Σ_d log S_kd - ½Σ_d log A_kd - ½Σ_d r_kd²/(eps S_kd) + ½Σ_d c_kd²/A_kd
+// drift = (Σ_k softmax_k(arg) · c_k/A_k − x) / (1 − t).  One wave owns one row: each lane
+// keeps D/64 coordinates in registers, the K partial sums are wave-reduced with
+// shuffles, and the parameters (1/S, r/S) are staged once per workgroup in LDS.
+// Euler–Maruyama (sb.py:163-175) runs all n_steps inside the kernel with the row
+// resident in registers: HBM traffic is the trajectory itself plus the noise.
+#include "common.h"
+
+namespace irads {
+namespace {
+
+constexpr int kMaxK = 32;
+constexpr int kMaxPerLane = 16;  // D <= 1024
+
+template <typename T>
+__device__ __forceinline__ T wsum(T v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// LDS layout: invS[K*D] (1/S), rS[K*D] (r/S), kc[K] (per-potential constant)
+template <typename T>
+__device__ void stage_params(T *invS, T *rS, T *kc, const T *r, const T *Sl, const T *la, T eps, int D, int K) {
+    for (int i = threadIdx.x; i < K * D; i += blockDim.x) {
+        T is = exp(-Sl[i]);
+        invS[i] = is;
+        rS[i] = r[i] * is;
+    }
+    __syncthreads();
+    const int wave = threadIdx.x / 64, lane = threadIdx.x % 64;
+    for (int k = wave; k < K; k += blockDim.x / 64) {
+        T sls = 0, rsr = 0;
+        for (int d = lane; d < D; d += 64) {
+            sls += Sl[k * D + d];
+            rsr += r[k * D + d] * rS[k * D + d];
+        }
+        sls = wsum(sls);
+        rsr = wsum(rsr);
+        if (lane == 0) kc[k] = la[k] / eps - (T)0.5 * sls - (T)0.5 * rsr / eps;
+    }
+    __syncthreads();
+}
+
+// drift for one row held in registers xv[j] = x[lane + 64 j]
+template <typename T>
+__device__ __forceinline__ void row_drift(const T *xv, T t, const T *invS, const T *rS, const T *kc, T eps, int D,
+                                          int K, T *dv) {
+    const int lane = threadIdx.x % 64;
+    const int nper = (D + 63) / 64;
+    const T a0 = t / (eps * ((T)1 - t));
+    const T cx = (T)1 / (eps * ((T)1 - t));
+    T arg[kMaxK];
+    for (int k = 0; k < K; ++k) {
+        T slog = 0, sc2 = 0;
+        for (int j = 0; j < nper; ++j) {
+            const int d = lane + 64 * j;
+            if (d < D) {
+                const T A = a0 + invS[k * D + d] / eps;
+                const T c = xv[j] * cx + rS[k * D + d] / eps;
+                slog += log(A);
+                sc2 += c * c / A;
+            }
+        }
+        arg[k] = kc[k] - (T)0.5 * wsum(slog) + (T)0.5 * wsum(sc2);
+    }
+    T mx = arg[0];
+    for (int k = 1; k < K; ++k) mx = arg[k] > mx ? arg[k] : mx;
+    T den = 0;
+    for (int k = 0; k < K; ++k) {
+        arg[k] = exp(arg[k] - mx);
+        den += arg[k];
+    }
+    for (int j = 0; j < nper; ++j) {
+        const int d = lane + 64 * j;
+        if (d >= D) continue;
+        T s = 0;
+        for (int k = 0; k < K; ++k) {
+            const T A = a0 + invS[k * D + d] / eps;
+            const T c = xv[j] * cx + rS[k * D + d] / eps;
+            s += arg[k] * (c / A);
+        }
+        dv[j] = (s / den - xv[j]) / ((T)1 - t);
+    }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) sb_drift_kernel(const T *__restrict__ x, const T *__restrict__ tt,
+                                                       const T *__restrict__ r, const T *__restrict__ Sl,
+                                                       const T *__restrict__ la, T eps, int rows, int D, int K,
+                                                       T *__restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    T *invS = (T *)smem, *rS = invS + K * D, *kc = rS + K * D;
+    stage_params(invS, rS, kc, r, Sl, la, eps, D, K);
+    const int lane = threadIdx.x % 64, nper = (D + 63) / 64;
+    for (int row = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64; row < rows; row += gridDim.x * (blockDim.x / 64)) {
+        T xv[kMaxPerLane], dv[kMaxPerLane];
+        for (int j = 0; j < nper; ++j) {
+            const int d = lane + 64 * j;
+            xv[j] = d < D ? x[(long)row * D + d] : (T)0;
+        }
+        row_drift(xv, tt[row], invS, rS, kc, eps, D, K, dv);
+        for (int j = 0; j < nper; ++j) {
+            const int d = lane + 64 * j;
+            if (d < D) out[(long)row * D + d] = dv[j];
+        }
+    }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) sb_em_kernel(const T *__restrict__ x0, const T *__restrict__ noise, int n_steps,
+                                                    const T *__restrict__ r, const T *__restrict__ Sl,
+                                                    const T *__restrict__ la, T eps, int rows, int D, int K,
+                                                    T *__restrict__ traj) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    T *invS = (T *)smem, *rS = invS + K * D, *kc = rS + K * D;
+    stage_params(invS, rS, kc, r, Sl, la, eps, D, K);
+    const int lane = threadIdx.x % 64, nper = (D + 63) / 64;
+    const T dt = (T)1 / (T)n_steps;
+    const T sd = sqrt(dt) * sqrt(eps);  // math.sqrt(dt) * torch.sqrt(epsilon)
+    for (int row = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64; row < rows; row += gridDim.x * (blockDim.x / 64)) {
+        T xv[kMaxPerLane], dv[kMaxPerLane];
+        T *tr = traj + (long)row * (n_steps + 1) * D;
+        for (int j = 0; j < nper; ++j) {
+            const int d = lane + 64 * j;
+            xv[j] = d < D ? x0[(long)row * D + d] : (T)0;
+            if (d < D) tr[d] = xv[j];
+        }
+        T t = 0;
+        for (int i = 0; i < n_steps; ++i) {
+            row_drift(xv, t, invS, rS, kc, eps, D, K, dv);
+            const T *nz = noise + ((long)i * rows + row) * D;
+            for (int j = 0; j < nper; ++j) {
+                const int d = lane + 64 * j;
+                if (d < D) {
+                    xv[j] = xv[j] + dv[j] * dt + sd * nz[d];
+                    tr[(long)(i + 1) * D + d] = xv[j];
+                }
+            }
+            t += dt;
+        }
+    }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) sb_logits_kernel(const T *__restrict__ x, const T *__restrict__ r,
+                                                        const T *__restrict__ Sl, const T *__restrict__ la, T eps,
+                                                        int rows, int D, int K, T *__restrict__ logits,
+                                                        T *__restrict__ logC) {
+    const int lane = threadIdx.x % 64;
+    for (int row = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64; row < rows; row += gridDim.x * (blockDim.x / 64)) {
+        T arg[kMaxK];
+        for (int k = 0; k < K; ++k) {
+            T xsx = 0, xr = 0;
+            for (int d = lane; d < D; d += 64) {
+                const T xd = x[(long)row * D + d];
+                xsx += xd * exp(Sl[k * D + d]) * xd;
+                xr += xd * r[k * D + d];
+            }
+            arg[k] = (wsum(xsx) + (T)2 * wsum(xr)) / ((T)2 * eps) + la[k] / eps;
+        }
+        if (lane == 0) {
+            T mx = arg[0];
+            for (int k = 1; k < K; ++k) mx = arg[k] > mx ? arg[k] : mx;
+            T s = 0;
+            for (int k = 0; k < K; ++k) {
+                if (logits) logits[(long)row * K + k] = arg[k];
+                s += exp(arg[k] - mx);
+            }
+            if (logC) logC[row] = mx + log(s);
+        }
+    }
+}
+
+int check(int dtype, int rows, int D, int K) {
+    IRADS_REQUIRE(dtype == IRADS_F32 || dtype == IRADS_F64, "sb: dtype must be float32 or float64");
+    IRADS_REQUIRE(rows >= 0 && D > 0 && D <= 64 * kMaxPerLane, "sb: dim must be in [1, %d]", 64 * kMaxPerLane);
+    IRADS_REQUIRE(K > 0 && K <= kMaxK, "sb: n_potentials must be in [1, %d]", kMaxK);
+    return IRADS_OK;
+}
+
+unsigned grid_for(int rows) {
+    long g = (rows + 3) / 4;
+    return (unsigned)(g < 2048 ? (g > 0 ? g : 1) : 2048);
+}
+
+}  // namespace
+}  // namespace irads
+
+using namespace irads;
+
+extern "C" int irads_sb_drift(int dtype, const void *x, const void *t, const void *r, const void *S_log_diag,
+                              const void *log_alpha_raw, double epsilon, int rows, int D, int K, void *drift,
+                              void *stream) {
+    if (int e = check(dtype, rows, D, K)) return e;
+    if (rows == 0) return IRADS_OK;
+    hipStream_t st = (hipStream_t)stream;
+    if (dtype == IRADS_F32) {
+        size_t sh = (2 * (size_t)K * D + K) * sizeof(float);
+        sb_drift_kernel<float><<<grid_for(rows), 256, sh, st>>>((const float *)x, (const float *)t, (const float *)r,
+                                                                 (const float *)S_log_diag, (const float *)log_alpha_raw,
+                                                                 (float)epsilon, rows, D, K, (float *)drift);
+    } else {
+        size_t sh = (2 * (size_t)K * D + K) * sizeof(double);
+        IRADS_REQUIRE(sh <= 160 * 1024, "sb: float64 parameters exceed LDS (K*D too large)");
+        sb_drift_kernel<double><<<grid_for(rows), 256, sh, st>>>(
+            (const double *)x, (const double *)t, (const double *)r, (const double *)S_log_diag,
+            (const double *)log_alpha_raw, epsilon, rows, D, K, (double *)drift);
+    }
+    return check_launch("irads_sb_drift");
+}
+
+extern "C" int irads_sb_em(int dtype, const void *x0, const void *noise, int n_steps, const void *r,
+                           const void *S_log_diag, const void *log_alpha_raw, double epsilon, int rows, int D, int K,
+                           void *traj, void *stream) {
+    if (int e = check(dtype, rows, D, K)) return e;
+    IRADS_REQUIRE(n_steps > 0, "sb_em: n_steps must be positive");
+    if (rows == 0) return IRADS_OK;
+    hipStream_t st = (hipStream_t)stream;
+    if (dtype == IRADS_F32) {
+        size_t sh = (2 * (size_t)K * D + K) * sizeof(float);
+        sb_em_kernel<float><<<grid_for(rows), 256, sh, st>>>((const float *)x0, (const float *)noise, n_steps,
+                                                              (const float *)r, (const float *)S_log_diag,
+                                                              (const float *)log_alpha_raw, (float)epsilon, rows, D, K,
+                                                              (float *)traj);
+    } else {
+        size_t sh = (2 * (size_t)K * D + K) * sizeof(double);
+        IRADS_REQUIRE(sh <= 160 * 1024, "sb: float64 parameters exceed LDS (K*D too large)");
+        sb_em_kernel<double><<<grid_for(rows), 256, sh, st>>>((const double *)x0, (const double *)noise, n_steps,
+                                                               (const double *)r, (const double *)S_log_diag,
+                                                               (const double *)log_alpha_raw, epsilon, rows, D, K,
+                                                               (double *)traj);
+    }
+    return check_launch("irads_sb_em");
+}
+
+extern "C" int irads_sb_logits(int dtype, const void *x, const void *r, const void *S_log_diag,
+                               const void *log_alpha_raw, double epsilon, int rows, int D, int K, void *logits,
+                               void *log_C, void *stream) {
+    if (int e = check(dtype, rows, D, K)) return e;
+    if (rows == 0) return IRADS_OK;
+    hipStream_t st = (hipStream_t)stream;
+    if (dtype == IRADS_F32)
+        sb_logits_kernel<float><<<grid_for(rows), 256, 0, st>>>((const float *)x, (const float *)r,
+                                                                 (const float *)S_log_diag, (const float *)log_alpha_raw,
+                                                                 (float)epsilon, rows, D, K, (float *)logits,
+                                                                 (float *)log_C);
+    else
+        sb_logits_kernel<double><<<grid_for(rows), 256, 0, st>>>((const double *)x, (const double *)r,
+                                                                  (const double *)S_log_diag,
+                                                                  (const double *)log_alpha_raw, epsilon, rows, D, K,
+                                                                  (double *)logits, (double *)log_C);
+    return check_launch("irads_sb_logits");
+}

@@ -1,0 +1,96 @@
+"""ctypes binding of libirads.so (C ABI declared in include/irads.h).
+
+The library is built in-tree (``__graft_entry__.build()`` / ``make -C ir-ads_amd/csrc``).
+There is no fallback: if the library or a GPU is missing, every op raises.
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("IRADS_LIB", os.path.join(_HERE, "libirads.so"))
+
+F32, BF16, F64 = 0, 1, 2
+_DT = {torch.float32: F32, torch.bfloat16: BF16, torch.float64: F64}
+
+_vp, _i, _f, _d = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_double
+
+# name -> argtypes (every entry returns int)
+SIGNATURES = {
+    "irads_msda_fwd": [_i, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp, _vp],
+    "irads_msda_bwd": [_i, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp],
+    "irads_msda_corner_index": [_i, _vp, _vp, _i, _i, _i, _i, _i, _vp, _vp],
+    "irads_winattn_fwd": [_i, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _f, _vp, _vp, _vp],
+    "irads_winattn_bwd": [_i, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _f, _vp, _vp, _vp, _vp, _vp, _vp,
+                          _vp],
+    "irads_dattn_sample_fwd": [_vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp],
+    "irads_dattn_sample_bwd": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp,
+                               _vp, _vp],
+    "irads_dattn_attn_fwd": [_vp] * 8 + [_i] * 9 + [_f, _vp, _vp, _vp],
+    "irads_dattn_attn_bwd": [_vp] * 8 + [_i] * 9 + [_f] + [_vp] * 10 + [_vp],
+    "irads_dattn_sample_index": [_vp, _i, _i, _i, _vp, _vp],
+    "irads_sb_drift": [_i, _vp, _vp, _vp, _vp, _vp, _d, _i, _i, _i, _vp, _vp],
+    "irads_sb_em": [_i, _vp, _vp, _i, _vp, _vp, _vp, _d, _i, _i, _i, _vp, _vp],
+    "irads_sb_logits": [_i, _vp, _vp, _vp, _vp, _d, _i, _i, _i, _vp, _vp, _vp],
+}
+
+_lib = None
+
+
+def load(require_gpu=False):
+    """Load libirads.so (raises OSError with the build hint if it is missing)."""
+    global _lib
+    if require_gpu and not torch.cuda.is_available():
+        raise RuntimeError("irads: the HIP hot path needs an MI355X (gfx950) GPU; no GPU is visible. "
+                           "CPU execution is not a product path (the CPU restatement lives in oracle/, "
+                           "test infrastructure only).")
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise OSError(f"irads: {LIB_PATH} not found — build it with `python -c 'import __graft_entry__ as g; "
+                          f"g.build()'` or `make -C ir-ads_amd/csrc`")
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, argt in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.argtypes = argt
+            fn.restype = ctypes.c_int
+        lib.irads_last_error.restype = ctypes.c_char_p
+        lib.irads_last_error.argtypes = []
+        lib.irads_version.restype = ctypes.c_int
+        _lib = lib
+    return _lib
+
+
+def call(name, *args):
+    lib = load(require_gpu=True)
+    rc = getattr(lib, name)(*args)
+    if rc != 0:
+        raise RuntimeError(f"{name} failed (code {rc}): {lib.irads_last_error().decode()}")
+
+
+def ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def dtype_code(t, allowed, what):
+    code = _DT.get(t.dtype)
+    if code is None or code not in allowed:
+        names = {F32: "float32", BF16: "bfloat16", F64: "float64"}
+        raise RuntimeError(f"{what}: dtype {t.dtype} not supported (expected one of "
+                           f"{[names[a] for a in allowed]})")
+    return code
+
+
+def check(t, what, dtype=None):
+    """The reference's AT_ASSERTM checks (ms_deform_attn_cuda.cu:29-39) as RuntimeError."""
+    if not t.is_cuda:
+        raise RuntimeError(f"{what} must be a CUDA tensor")
+    if not t.is_contiguous():
+        raise RuntimeError(f"{what} must be contiguous")
+    if dtype is not None and t.dtype != dtype:
+        raise RuntimeError(f"{what} must be {dtype}, got {t.dtype}")
+    return t

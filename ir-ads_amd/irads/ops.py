@@ -1,0 +1,237 @@
+"""Autograd wrappers around libirads.so (one torch.autograd.Function per hot op).
+
+Ownership: the caller (this module) allocates every output with torch on the current
+device and passes the current HIP stream, so the ops are asynchronous and
+graph-capturable.  Gradient accumulators that the kernels add into atomically are
+zero-filled here.  There is no CPU fallback: CPU tensors raise.
+"""
+import torch
+
+from . import native as N
+
+WINDOW = 12
+HEAD_DIM = 32
+
+
+# ------------------------------------------------------------------ window attention
+class WindowAttentionFn(torch.autograd.Function):
+    """ShiftWindowMSA/WindowMSA core between the qkv and proj Linears
+    (swin.py:180-254 + :95-116).  qkv: (B, H*W, 3C) token order."""
+
+    @staticmethod
+    def forward(ctx, qkv, qkv_bias, table, mask, H, W, num_heads, shift, scale):
+        N.check(qkv, "qkv")
+        B, L, C3 = qkv.shape
+        assert L == H * W, "input feature has wrong size"
+        C = C3 // 3
+        code = N.dtype_code(qkv, (N.F32, N.BF16), "window attention qkv")
+        table_f = N.check(table.detach().float().contiguous(), "relative_position_bias_table")
+        bias_f = None if qkv_bias is None else qkv_bias.detach().float().contiguous()
+        mask_f = None if mask is None else mask.detach().float().contiguous()
+        n_mask = 0 if mask is None else int(mask.shape[0])
+        out = torch.empty((B, L, C), device=qkv.device, dtype=qkv.dtype)
+        Hp, Wp = -(-H // WINDOW) * WINDOW, -(-W // WINDOW) * WINDOW
+        nW = (Hp // WINDOW) * (Wp // WINDOW)
+        lse = torch.empty((B * nW * num_heads * WINDOW * WINDOW,), device=qkv.device, dtype=torch.float32)
+        N.call("irads_winattn_fwd", code, N.ptr(qkv), N.ptr(bias_f), N.ptr(table_f), N.ptr(mask_f), n_mask, B, H, W,
+               C, num_heads, shift, float(scale), N.ptr(out), N.ptr(lse), N.stream())
+        ctx.save_for_backward(qkv, bias_f, table_f, mask_f, out, lse)
+        ctx.cfg = (code, n_mask, B, H, W, C, num_heads, shift, float(scale))
+        ctx.need = (qkv_bias is not None and ctx.needs_input_grad[1], ctx.needs_input_grad[2])
+        ctx.table_dtype = table.dtype
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        qkv, bias_f, table_f, mask_f, out, lse = ctx.saved_tensors
+        code, n_mask, B, H, W, C, nH, shift, scale = ctx.cfg
+        gout = gout.contiguous().to(qkv.dtype)
+        gqkv = torch.empty_like(qkv)
+        gtable = torch.zeros_like(table_f) if ctx.need[1] else None
+        gbias = torch.zeros((3 * C,), device=qkv.device, dtype=torch.float32) if ctx.need[0] else None
+        N.call("irads_winattn_bwd", code, N.ptr(qkv), N.ptr(bias_f), N.ptr(table_f), N.ptr(mask_f), n_mask, B, H, W,
+               C, nH, shift, scale, N.ptr(out), N.ptr(lse), N.ptr(gout), N.ptr(gqkv), N.ptr(gtable), N.ptr(gbias),
+               N.stream())
+        if gtable is not None:
+            gtable = gtable.to(ctx.table_dtype)
+        return gqkv, gbias, gtable, None, None, None, None, None, None
+
+
+def window_attention(qkv, qkv_bias, table, mask, H, W, num_heads, shift, scale):
+    if qkv.dtype not in (torch.float32, torch.bfloat16):
+        raise RuntimeError(f"window attention: dtype {qkv.dtype} not supported (float32 / bfloat16)")
+    return WindowAttentionFn.apply(qkv.contiguous(), qkv_bias, table, mask, H, W, num_heads, shift, scale)
+
+
+# ------------------------------------------------------------------ MSDeformAttn
+class MSDAFn(torch.autograd.Function):
+    """detrex._C.ms_deform_attn_forward/backward replacement
+    (multi_scale_deform_attn.py:44-93)."""
+
+    @staticmethod
+    def forward(ctx, value, spatial_shapes, level_start_index, sampling_locations, attention_weights, im2col_step):
+        for t, n in ((value, "value"), (spatial_shapes, "spatial_shapes"),
+                     (level_start_index, "level_start_index"), (sampling_locations, "sampling_loc"),
+                     (attention_weights, "attn_weight")):
+            N.check(t, n)
+        code = N.dtype_code(value, (N.F32, N.F64), "ms_deform_attn value")
+        if sampling_locations.dtype != value.dtype or attention_weights.dtype != value.dtype:
+            raise RuntimeError("sampling_loc / attn_weight must have value's dtype")
+        bs, S, M, D = value.shape
+        _, Q, _, L, P, _ = sampling_locations.shape
+        step = min(bs, im2col_step) if bs else 1
+        if step <= 0 or bs % step != 0:  # ms_deform_attn_cuda.cu:53
+            raise RuntimeError(f"batch({bs}) must divide im2col_step({im2col_step})")
+        shapes = spatial_shapes.to(torch.int64).contiguous()
+        lsi = level_start_index.to(torch.int64).contiguous()
+        out = torch.empty((bs, Q, M * D), device=value.device, dtype=value.dtype)
+        N.call("irads_msda_fwd", code, N.ptr(value), N.ptr(shapes), N.ptr(lsi), N.ptr(sampling_locations),
+               N.ptr(attention_weights), bs, S, M, D, L, Q, P, N.ptr(out), N.stream())
+        ctx.save_for_backward(value, shapes, lsi, sampling_locations, attention_weights)
+        ctx.im2col_step = im2col_step
+        return out
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, grad_output):
+        value, shapes, lsi, loc, aw = ctx.saved_tensors
+        code = N.dtype_code(value, (N.F32, N.F64), "ms_deform_attn value")
+        bs, S, M, D = value.shape
+        _, Q, _, L, P, _ = loc.shape
+        grad_output = grad_output.contiguous()
+        gv = torch.zeros_like(value)
+        gl = torch.empty_like(loc)
+        ga = torch.empty_like(aw)
+        N.call("irads_msda_bwd", code, N.ptr(value), N.ptr(shapes), N.ptr(lsi), N.ptr(loc), N.ptr(aw),
+               N.ptr(grad_output), bs, S, M, D, L, Q, P, N.ptr(gv), N.ptr(gl), N.ptr(ga), N.stream())
+        return gv, None, None, gl, ga, None
+
+
+def msda_corner_index(sampling_locations, spatial_shapes):
+    """Integer corners (x0, y0) per sample; debug export for the bit-exact test."""
+    N.check(sampling_locations, "sampling_loc")
+    code = N.dtype_code(sampling_locations, (N.F32, N.F64), "sampling_loc")
+    bs, Q, M, L, P, _ = sampling_locations.shape
+    shapes = spatial_shapes.to(torch.int64).contiguous()
+    out = torch.empty((bs, Q, M, L, P, 2), device=sampling_locations.device, dtype=torch.int32)
+    N.call("irads_msda_corner_index", code, N.ptr(sampling_locations), N.ptr(shapes), bs, Q, M, L, P, N.ptr(out),
+           N.stream())
+    return out
+
+
+# ------------------------------------------------------------------ DAttentionMM
+class DAttnSampleFn(torch.autograd.Function):
+    """The six feature grid_samples of DAttentionMM (swin.py:911-944)."""
+
+    @staticmethod
+    def forward(ctx, x, y, q, pos_x, pos_y, groups):
+        B, C, H, W = x.shape
+        n = pos_x.shape[1] * pos_x.shape[2]
+        ts = [N.check(t.contiguous(), nm, torch.float32) for t, nm in
+              ((x, "x"), (y, "y"), (q, "q"), (pos_x, "pos_x"), (pos_y, "pos_y"))]
+        xs, ys, qs = (torch.empty((B, C, 2 * n), device=x.device, dtype=torch.float32) for _ in range(3))
+        N.call("irads_dattn_sample_fwd", *[N.ptr(t) for t in ts], B, C, H, W, groups, n, N.ptr(xs), N.ptr(ys),
+               N.ptr(qs), N.stream())
+        ctx.save_for_backward(*ts)
+        ctx.cfg = (B, C, H, W, groups, n)
+        return xs, ys, qs
+
+    @staticmethod
+    def backward(ctx, gxs, gys, gqs):
+        x, y, q, px, py = ctx.saved_tensors
+        B, C, H, W, G, n = ctx.cfg
+
+        def g(t):
+            return torch.zeros((B, C, 2 * n), device=x.device) if t is None else t.contiguous().float()
+        gxs, gys, gqs = g(gxs), g(gys), g(gqs)
+        gx, gy, gq = torch.zeros_like(x), torch.zeros_like(y), torch.zeros_like(q)
+        gpx, gpy = torch.empty_like(px), torch.empty_like(py)
+        N.call("irads_dattn_sample_bwd", N.ptr(x), N.ptr(y), N.ptr(q), N.ptr(px), N.ptr(py), N.ptr(gxs), N.ptr(gys),
+               N.ptr(gqs), B, C, H, W, G, n, N.ptr(gx), N.ptr(gy), N.ptr(gq), N.ptr(gpx), N.ptr(gpy), N.stream())
+        return gx, gy, gq, gpx, gpy, None
+
+
+class DAttnAttentionFn(torch.autograd.Function):
+    """softmax(scale·qᵀk + bilinear rpe bias)·v of DAttentionMM (swin.py:950-1016)."""
+
+    @staticmethod
+    def forward(ctx, q, k, v, pos_x, pos_y, rpe_table, qgrid_y, qgrid_x, B, n_heads, groups, H, W, scale):
+        hc = q.shape[1]
+        n = pos_x.shape[1] * pos_x.shape[2]
+        ts = [N.check(t.contiguous(), nm, torch.float32) for t, nm in
+              ((q, "q"), (k, "k"), (v, "v"), (pos_x, "pos_x"), (pos_y, "pos_y"), (rpe_table, "rpe_table"),
+               (qgrid_y, "qgrid_y"), (qgrid_x, "qgrid_x"))]
+        Ht, Wt = rpe_table.shape[1], rpe_table.shape[2]
+        out = torch.empty_like(ts[0])
+        lse = torch.empty((B * n_heads, H * W), device=q.device, dtype=torch.float32)
+        N.call("irads_dattn_attn_fwd", *[N.ptr(t) for t in ts], B, n_heads, groups, hc, H, W, n, Ht, Wt,
+               float(scale), N.ptr(out), N.ptr(lse), N.stream())
+        ctx.save_for_backward(*ts, out, lse)
+        ctx.cfg = (B, n_heads, groups, hc, H, W, n, Ht, Wt, float(scale))
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        q, k, v, px, py, rpe, qgy, qgx, out, lse = ctx.saved_tensors
+        B, nH, G, hc, H, W, n, Ht, Wt, scale = ctx.cfg
+        gout = gout.contiguous().float()
+        delta = torch.empty_like(lse)
+        gq = torch.empty_like(q)
+        gk, gv = torch.zeros_like(k), torch.zeros_like(v)
+        grpe = torch.zeros_like(rpe)
+        gpx, gpy = torch.zeros_like(px), torch.zeros_like(py)
+        N.call("irads_dattn_attn_bwd", N.ptr(q), N.ptr(k), N.ptr(v), N.ptr(px), N.ptr(py), N.ptr(rpe), N.ptr(qgy),
+               N.ptr(qgx), B, nH, G, hc, H, W, n, Ht, Wt, scale, N.ptr(out), N.ptr(lse), N.ptr(gout), N.ptr(delta),
+               N.ptr(gq), N.ptr(gk), N.ptr(gv), N.ptr(grpe), N.ptr(gpx), N.ptr(gpy), N.stream())
+        return gq, gk, gv, gpx, gpy, grpe, None, None, None, None, None, None, None, None
+
+
+def dattn_sample_index(grid, H, W):
+    """Integer corners of align_corners=True sampling at grid (N, 2) (x, y)."""
+    grid = N.check(grid.contiguous(), "grid", torch.float32)
+    out = torch.empty((grid.shape[0], 2), device=grid.device, dtype=torch.int32)
+    N.call("irads_dattn_sample_index", N.ptr(grid), grid.shape[0], H, W, N.ptr(out), N.stream())
+    return out
+
+
+# ------------------------------------------------------------------ LightSB
+def _sb_params(x, r, S_log_diag, log_alpha_raw):
+    code = N.dtype_code(x, (N.F32, N.F64), "LightSB x")
+    ts = [N.check(t.detach().to(x.dtype).contiguous(), nm) for t, nm in
+          ((r, "r"), (S_log_diag, "S_log_diagonal_matrix"), (log_alpha_raw, "log_alpha_raw"))]
+    return code, ts
+
+
+def sb_drift(x, t, r, S_log_diag, log_alpha_raw, epsilon):
+    x = N.check(x.detach().contiguous(), "x")
+    code, (r_, s_, a_) = _sb_params(x, r, S_log_diag, log_alpha_raw)
+    t = N.check(t.detach().to(x.dtype).contiguous(), "t")
+    out = torch.empty_like(x)
+    rows, D = x.shape
+    N.call("irads_sb_drift", code, N.ptr(x), N.ptr(t), N.ptr(r_), N.ptr(s_), N.ptr(a_), float(epsilon), rows, D,
+           r_.shape[0], N.ptr(out), N.stream())
+    return out
+
+
+def sb_em(x, noise, r, S_log_diag, log_alpha_raw, epsilon):
+    x = N.check(x.detach().contiguous(), "x")
+    code, (r_, s_, a_) = _sb_params(x, r, S_log_diag, log_alpha_raw)
+    noise = N.check(noise.detach().to(x.dtype).contiguous(), "noise")
+    n_steps = noise.shape[0]
+    rows, D = x.shape
+    traj = torch.empty((rows, n_steps + 1, D), device=x.device, dtype=x.dtype)
+    N.call("irads_sb_em", code, N.ptr(x), N.ptr(noise), n_steps, N.ptr(r_), N.ptr(s_), N.ptr(a_), float(epsilon),
+           rows, D, r_.shape[0], N.ptr(traj), N.stream())
+    return traj
+
+
+def sb_logits(x, r, S_log_diag, log_alpha_raw, epsilon, want_logits=True, want_log_c=True):
+    x = N.check(x.detach().contiguous(), "x")
+    code, (r_, s_, a_) = _sb_params(x, r, S_log_diag, log_alpha_raw)
+    rows, D = x.shape
+    K = r_.shape[0]
+    logits = torch.empty((rows, K), device=x.device, dtype=x.dtype) if want_logits else None
+    log_c = torch.empty((rows,), device=x.device, dtype=x.dtype) if want_log_c else None
+    N.call("irads_sb_logits", code, N.ptr(x), N.ptr(r_), N.ptr(s_), N.ptr(a_), float(epsilon), rows, D, K,
+           N.ptr(logits), N.ptr(log_c), N.stream())
+    return logits, log_c

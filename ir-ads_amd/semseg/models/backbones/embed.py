@@ -1,0 +1,118 @@
+"""Patch embedding / merging of the Swin backbone (reference semseg/models/backbones/embed.py).
+
+Plain PyTorch ops (conv / unfold / LayerNorm / Linear go to MIOpen and hipBLASLt); kept
+here for shape and state-dict parity (keys ``projection``, ``norm``, ``reduction``).
+"""
+import math
+from typing import Sequence
+
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+def _pair(x):
+    return tuple(x) if isinstance(x, (tuple, list)) else (x, x)
+
+
+class AdaptivePadding(nn.Module):
+    """Pad so the filter covers the input: 'corner' pads bottom/right, 'same' both sides."""
+
+    def __init__(self, kernel_size=1, stride=1, dilation=1, padding='corner'):
+        super().__init__()
+        assert padding in ('same', 'corner')
+        self.padding = padding
+        self.kernel_size, self.stride, self.dilation = _pair(kernel_size), _pair(stride), _pair(dilation)
+
+    def get_pad_shape(self, input_shape):
+        pads = []
+        for size, k, s, d in zip(input_shape, self.kernel_size, self.stride, self.dilation):
+            out = math.ceil(size / s)
+            pads.append(max((out - 1) * s + (k - 1) * d + 1 - size, 0))
+        return tuple(pads)
+
+    def forward(self, x):
+        ph, pw = self.get_pad_shape(x.size()[-2:])
+        if ph > 0 or pw > 0:
+            if self.padding == 'corner':
+                x = F.pad(x, [0, pw, 0, ph])
+            else:
+                x = F.pad(x, [pw // 2, pw - pw // 2, ph // 2, ph - ph // 2])
+        return x
+
+
+class PatchEmbed(nn.Module):
+    """Conv patch embedding + LayerNorm; returns (B, h*w, C) and (h, w)."""
+
+    def __init__(self, in_channels=3, embed_dims=768, conv_type='Conv2d', kernel_size=16, stride=None,
+                 padding='corner', dilation=1, bias=True, norm_cfg=None, input_size=None, init_cfg=None):
+        super().__init__()
+        assert conv_type == 'Conv2d'
+        self.embed_dims = embed_dims
+        stride = kernel_size if stride is None else stride
+        kernel_size, stride, dilation = _pair(kernel_size), _pair(stride), _pair(dilation)
+        if isinstance(padding, str):
+            self.adap_padding = AdaptivePadding(kernel_size, stride, dilation, padding)
+            padding = 0
+        else:
+            self.adap_padding = None
+        padding = _pair(padding)
+        self.projection = nn.Conv2d(in_channels, embed_dims, kernel_size, stride, padding, dilation, bias=bias)
+        self.norm = nn.LayerNorm(embed_dims) if norm_cfg is not None else None
+        self.init_input_size = self.init_out_size = None
+        if input_size:
+            input_size = _pair(input_size)
+            self.init_input_size = input_size
+            if self.adap_padding:
+                ph, pw = self.adap_padding.get_pad_shape(input_size)
+                input_size = (input_size[0] + ph, input_size[1] + pw)
+            self.init_out_size = tuple(
+                (input_size[i] + 2 * padding[i] - dilation[i] * (kernel_size[i] - 1) - 1) // stride[i] + 1
+                for i in range(2))
+
+    def forward(self, x):
+        if self.adap_padding:
+            x = self.adap_padding(x)
+        x = self.projection(x)
+        out_size = (x.shape[2], x.shape[3])
+        x = x.flatten(2).transpose(1, 2)
+        if self.norm is not None:
+            x = self.norm(x)
+        return x, out_size
+
+
+class PatchMerging(nn.Module):
+    """2x2 unfold -> LayerNorm(4C) -> Linear(4C, out, bias=False)."""
+
+    def __init__(self, in_channels, out_channels, kernel_size=2, stride=None, padding='corner', dilation=1,
+                 bias=False, norm_cfg=dict(type='LN'), init_cfg=None):
+        super().__init__()
+        self.in_channels, self.out_channels = in_channels, out_channels
+        stride = stride if stride else kernel_size
+        kernel_size, stride, dilation = _pair(kernel_size), _pair(stride), _pair(dilation)
+        if isinstance(padding, str):
+            self.adap_padding = AdaptivePadding(kernel_size, stride, dilation, padding)
+            padding = 0
+        else:
+            self.adap_padding = None
+        padding = _pair(padding)
+        self.sampler = nn.Unfold(kernel_size=kernel_size, dilation=dilation, padding=padding, stride=stride)
+        sample_dim = kernel_size[0] * kernel_size[1] * in_channels
+        self.norm = nn.LayerNorm(sample_dim) if norm_cfg is not None else None
+        self.reduction = nn.Linear(sample_dim, out_channels, bias=bias)
+
+    def forward(self, x, input_size, sub_mode=None):
+        B, L, C = x.shape
+        assert isinstance(input_size, Sequence), f'Expect input_size is `Sequence` but get {input_size}'
+        H, W = input_size
+        assert L == H * W, 'input feature has wrong size'
+        x = x.view(B, H, W, C).permute([0, 3, 1, 2])
+        if self.adap_padding:
+            x = self.adap_padding(x)
+            H, W = x.shape[-2:]
+        x = self.sampler(x)
+        s = self.sampler
+        out_hw = tuple((size + 2 * s.padding[i] - s.dilation[i] * (s.kernel_size[i] - 1) - 1) // s.stride[i] + 1
+                       for i, size in enumerate((H, W)))
+        x = x.transpose(1, 2)
+        x = self.norm(x) if self.norm else x
+        return self.reduction(x), out_hw

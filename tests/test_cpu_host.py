@@ -1,0 +1,116 @@
+"""CPU-side checks: the C-ABI library loads and exports every symbol include/irads.h
+declares; the product modules keep the reference's state-dict schema; the product path
+refuses CPU tensors (no silent fallback)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+import torch
+
+from golden_util import Fixture
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "ir-ads_amd", "irads", "libirads.so")
+
+
+@pytest.fixture(scope="module")
+def lib():
+    if not os.path.exists(LIB):
+        subprocess.run(["make", "-j8", "-C", os.path.join(ROOT, "ir-ads_amd", "csrc")], check=True)
+    return ctypes.CDLL(LIB)
+
+
+def declared_symbols():
+    txt = open(os.path.join(ROOT, "include", "irads.h")).read()
+    return sorted(set(re.findall(r"^(?:int|const char \*)\s*(irads_\w+)\s*\(", txt, re.M)))
+
+
+def test_library_exports_every_declared_symbol(lib):
+    syms = declared_symbols()
+    assert len(syms) >= 15
+    for s in syms:
+        assert hasattr(lib, s), f"libirads.so does not export {s}"
+
+
+def test_native_binding_covers_header():
+    from irads import native
+    syms = set(declared_symbols()) - {"irads_last_error", "irads_version"}
+    assert syms == set(native.SIGNATURES), syms ^ set(native.SIGNATURES)
+
+
+def test_library_is_gfx950(lib):
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readelf", "-n", LIB], capture_output=True, text=True)
+    blob = open(LIB, "rb").read()
+    assert b"gfx950" in blob
+
+
+def test_version_and_error_strings(lib):
+    lib.irads_version.restype = ctypes.c_int
+    assert lib.irads_version() >= 1
+    lib.irads_last_error.restype = ctypes.c_char_p
+    # a bad dtype is rejected before any GPU work
+    f = lib.irads_msda_fwd
+    rc = f(7, None, None, None, None, None, 1, 1, 1, 1, 1, 1, 1, None, None)
+    assert rc != 0 and b"dtype" in lib.irads_last_error()
+    rc = lib.irads_winattn_fwd(0, None, None, None, None, 0, 1, 12, 12, 100, 4, 0, ctypes.c_float(1.0), None, None,
+                               None)
+    assert rc != 0 and b"head_dim" in lib.irads_last_error()
+
+
+def test_product_state_dict_schema_swinb():
+    from semseg.models import CMNeXt
+    fx = Fixture("cmnext_swinb512_checksums.npz")
+    m = CMNeXt("SwinTransformer-B", 40, ["img", "depth"])
+    sd = m.state_dict()
+    keys = sorted(sd.keys())
+    assert keys == fx["state_keys"].tolist()
+    assert [",".join(map(str, sd[k].shape)) for k in keys] == fx["state_shapes"].tolist()
+
+
+def test_product_state_dict_schema_tiny():
+    from semseg.models.backbones import SwinTransformer
+    from semseg.models.heads import SegFormerHead
+    fx = Fixture("cmnext_tiny.npz")
+    h = torch.nn.Module()
+    h.backbone = SwinTransformer(embed_dims=32, depths=(2, 2, 2, 2), num_heads=(1, 2, 4, 8), init_cfg=None)
+    h.decode_head = SegFormerHead([32, 64, 128, 256], 64, 5)
+    h.decode_head_rgb = SegFormerHead([32, 64, 128, 256], 32, 5)
+    h.decode_head_dte = SegFormerHead([32, 64, 128, 256], 32, 5)
+    assert sorted(h.state_dict().keys()) == fx["state_keys"].tolist()
+
+
+def test_product_parameter_order_matches_oracle():
+    """Optimizer state dicts index parameters by registration order: keep it."""
+    import irads_ref as R
+    from semseg.models import CMNeXt
+    a = [n for n, _ in CMNeXt("SwinTransformer-B", 40, ["img", "depth"]).named_parameters()]
+    b = [n for n, _ in R.CMNeXt("SwinTransformer-B", 40, ["img", "depth"]).named_parameters()]
+    assert a == b
+
+
+def test_product_refuses_cpu_tensors():
+    from semseg.models.backbones.swin import DAttentionMM, ShiftWindowMSA
+    from detrex.layers import MultiScaleDeformableAttention
+    with pytest.raises(RuntimeError):
+        ShiftWindowMSA(64, 2, 12, 0)(torch.randn(1, 144, 64), (12, 12))
+    with pytest.raises(RuntimeError):
+        DAttentionMM(16, stride=8, n_groups=1, n_heads=2, level=0)(torch.randn(1, 16, 16, 16), torch.randn(1, 16, 16, 16))
+    m = MultiScaleDeformableAttention()
+    shapes = torch.as_tensor([(4, 4), (2, 2), (1, 1), (1, 1)])
+    with pytest.raises(RuntimeError):
+        m(torch.randn(3, 1, 256), value=torch.randn(22, 1, 256), reference_points=torch.rand(1, 3, 4, 2),
+          spatial_shapes=shapes, level_start_index=torch.tensor([0, 16, 20, 21]))
+
+
+def test_unsupported_configs_raise():
+    from semseg.models.backbones.swin import DAttentionMM, WindowMSA
+    with pytest.raises(NotImplementedError):
+        DAttentionMM(16, n_heads=2, dwc_pe=True, level=0)
+    with pytest.raises(NotImplementedError):
+        from modules.sb import LightSB
+        LightSB(is_diagonal=False)
+    w = WindowMSA(96, 4, (12, 12))  # head_dim 24
+    with pytest.raises((NotImplementedError, RuntimeError)):
+        w(torch.randn(1, 144, 96))

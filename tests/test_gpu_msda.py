@@ -1,0 +1,165 @@
+"""MSDeformAttn HIP kernels vs the reference (golden fixtures) and the C oracle.
+Re-expresses the reference's tests/test_ms_deform_attn.py on the MI355X path."""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+import pytest
+import torch
+
+from golden_util import Fixture, close
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DEV = "cuda"
+
+
+def _ops():
+    from irads import ops
+    return ops
+
+
+def test_forward_equal_with_pytorch_double():
+    """tests/test_ms_deform_attn.py:103-129 (fp64, torch.allclose default tolerances)."""
+    ops = _ops()
+    fx = Fixture("msda_ref_test.npz")
+    shapes = fx.t("shapes", device=DEV)
+    lsi = fx.t("level_start_index", device=DEV)
+    out = ops.MSDAFn.apply(fx.t("fwd_value", device=DEV), shapes, lsi, fx.t("fwd_loc", device=DEV),
+                           fx.t("fwd_aw", device=DEV), 2)
+    assert torch.allclose(out.cpu(), fx.t("fwd_out"))
+    close(out, fx["fwd_out"], 1e-15, 1e-12, "fp64 forward")
+
+
+@pytest.mark.parametrize("tag", ["c30", "c32", "c64", "c71", "c1025"])
+def test_gradients_vs_reference_double(tag):
+    """The channel counts of the reference's gradcheck (hit every backward variant there)."""
+    ops = _ops()
+    fx = Fixture("msda_ref_test.npz")
+    shapes = fx.t("shapes", device=DEV)
+    lsi = fx.t("level_start_index", device=DEV)
+    v = fx.t(f"{tag}_value", device=DEV).requires_grad_()
+    loc = fx.t(f"{tag}_loc", device=DEV).requires_grad_()
+    aw = fx.t(f"{tag}_aw", device=DEV).requires_grad_()
+    o = ops.MSDAFn.apply(v, shapes, lsi, loc, aw, 2)
+    close(o, fx[f"{tag}_out"], 1e-15, 1e-12, f"{tag} out")
+    gv, gl, ga = torch.autograd.grad((o * fx.t(f"{tag}_gout", device=DEV)).sum(), (v, loc, aw))
+    close(gv, fx[f"{tag}_gvalue"], 1e-14, 1e-10, f"{tag} grad_value")
+    close(gl, fx[f"{tag}_gloc"], 1e-14, 1e-10, f"{tag} grad_loc")
+    close(ga, fx[f"{tag}_gaw"], 1e-14, 1e-10, f"{tag} grad_attn_weight")
+
+
+@pytest.mark.parametrize("channels", [30, 32, 64, 71, 1025])
+def test_gradient_numerical(channels):
+    """tests/test_ms_deform_attn.py:131-133: torch gradcheck in fp64."""
+    ops = _ops()
+    g = torch.Generator(device="cpu").manual_seed(channels)
+    shapes = torch.as_tensor([(6, 4), (3, 2)], dtype=torch.long, device=DEV)
+    lsi = torch.cat((shapes.new_zeros((1,)), shapes.prod(1).cumsum(0)[:-1]))
+    S = 30
+    value = (torch.rand(1, S, 2, channels, generator=g) * 0.01).double().to(DEV).requires_grad_()
+    loc = torch.rand(1, 2, 2, 2, 2, 2, generator=g).double().to(DEV).requires_grad_()
+    aw = torch.rand(1, 2, 2, 2, 2, generator=g).double() + 1e-5
+    aw = (aw / aw.sum(-1, keepdim=True).sum(-2, keepdim=True)).to(DEV).requires_grad_()
+    assert torch.autograd.gradcheck(ops.MSDAFn.apply, (value, shapes, lsi, loc, aw, 2))
+
+
+def test_dino_fp32_and_bitexact_corners():
+    """DINO-like levels, adversarial locations: corners bit-exact vs the C oracle (which
+    is bit-exact vs the reference CPU grid_sample); values within fp32 tolerance."""
+    ops = _ops()
+    fx = Fixture("msda_dino.npz")
+    shapes, lsi = fx.t("shapes", device=DEV), fx.t("level_start_index", device=DEV)
+    S = int(fx["shapes"].prod(1).sum())
+    value = fx.regen("value", (1, S, 4, 32), 21).to(DEV).requires_grad_()
+    loc = fx.t("loc", device=DEV).requires_grad_()
+    aw = fx.t("aw", device=DEV).requires_grad_()
+    out = ops.MSDAFn.apply(value, shapes, lsi, loc, aw, 64)
+    close(out, fx["out"], 2e-6, 1e-5, "dino out")
+    g = fx.regen("gout", tuple(out.shape), 26).to(DEV)
+    gv, gl, ga = torch.autograd.grad((out * g).sum(), (value, loc, aw))
+    close(gv, fx["gvalue"], 1e-5, 1e-4, "grad_value")
+    close(gl, fx["gloc"], 1e-4, 1e-4, "grad_loc")
+    close(ga, fx["gaw"], 1e-5, 1e-4, "grad_attn_weight")
+    # integer corners
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+    lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "liboracle.so"))
+    P = ctypes.c_void_p
+    loc_np = np.ascontiguousarray(fx["loc"])
+    shp = fx["shapes"].astype(np.int64)
+    out_np = np.zeros((1, 300, 128), np.float32)
+    cor = np.zeros((1, 300, 4, 4, 4, 2), np.int32)
+    vnp = value.detach().cpu().numpy()
+    lib.oracle_msda_fwd(vnp.ctypes.data_as(P), shp.ctypes.data_as(P), 1, S, 4, 32, 4, 300, 4,
+                        loc_np.ctypes.data_as(P), np.ascontiguousarray(fx["aw"]).ctypes.data_as(P),
+                        out_np.ctypes.data_as(P), cor.ctypes.data_as(P))
+    got = ops.msda_corner_index(loc.detach(), shapes).cpu().numpy()
+    assert (got == cor).all(), f"{int((got != cor).sum())} corner mismatches"
+
+
+def test_module_vs_reference():
+    """MultiScaleDeformableAttention module (2-d and 4-d reference points, padding mask)."""
+    from fill import fill_module
+    from detrex.layers import MultiScaleDeformableAttention
+    fx = Fixture("msda_module.npz")
+    m = MultiScaleDeformableAttention().to(DEV)
+    fill_module(m, seed=5)
+    m.eval()
+    shapes, lsi = fx.t("shapes", device=DEV), fx.t("level_start_index", device=DEV)
+    S = int(fx["shapes"].prod(1).sum())
+    for tag, seed in (("r2", 31), ("r4", 32)):
+        q = fx.regen(f"{tag}_query", (40, 2, 256), seed).to(DEV).requires_grad_()
+        v = fx.regen(f"{tag}_value", (S, 2, 256), seed + 1).to(DEV).requires_grad_()
+        qp = fx.regen(f"{tag}_qpos", (40, 2, 256), seed + 2).to(DEV)
+        o = m(q, value=v, query_pos=qp, key_padding_mask=fx.t(f"{tag}_mask", device=DEV),
+              reference_points=fx.t(f"{tag}_ref", device=DEV), spatial_shapes=shapes, level_start_index=lsi)
+        close(o, fx[f"{tag}_out"], 2e-5, 1e-4, f"{tag} out")
+        g = fx.regen(f"{tag}_gout", tuple(o.shape), seed + 5).to(DEV)
+        names = [n for n, _ in m.named_parameters()]
+        grads = torch.autograd.grad((o * g).sum(), [q, v] + [p for _, p in m.named_parameters()])
+        close(grads[0], fx[f"{tag}_gquery"], 2e-4, 1e-3, "gquery")
+        close(grads[1], fx[f"{tag}_gvalue"], 2e-4, 1e-3, "gvalue")
+        for n, gp in zip(names, grads[2:]):
+            ref = fx[f"{tag}_g.{n}"]
+            close(gp, ref, 1e-3 * max(1.0, float(np.abs(ref).max())), 1e-3, n)
+
+
+def test_errors_like_reference():
+    """RuntimeError on non-contiguous / wrong-device / wrong-dtype input (ms_deform_attn_cuda.cu:29-39)."""
+    ops = _ops()
+    shapes = torch.as_tensor([(6, 4), (3, 2)], dtype=torch.long, device=DEV)
+    lsi = torch.tensor([0, 24], device=DEV)
+    v = torch.rand(1, 30, 2, 8, device=DEV)
+    loc = torch.rand(1, 2, 2, 2, 2, 2, device=DEV)
+    aw = torch.rand(1, 2, 2, 2, 2, device=DEV)
+    with pytest.raises(RuntimeError):
+        ops.MSDAFn.apply(v.transpose(2, 3), shapes, lsi, loc, aw, 2)
+    with pytest.raises(RuntimeError):
+        ops.MSDAFn.apply(v.cpu(), shapes, lsi, loc, aw, 2)
+    with pytest.raises(RuntimeError):
+        ops.MSDAFn.apply(v.half(), shapes, lsi, loc.half(), aw.half(), 2)
+    # empty query set is fine
+    out = ops.MSDAFn.apply(v, shapes, lsi, loc[:, :0].contiguous(), aw[:, :0].contiguous(), 2)
+    assert out.shape == (1, 0, 16)
+
+
+def test_large_dino_encoder_linearity():
+    """Full DINO encoder size (S = Q = 22 223, bs 2): linearity in value and in the
+    attention weights (size-independent properties)."""
+    ops = _ops()
+    torch.manual_seed(0)
+    lv = [(100, 167), (50, 84), (25, 42), (13, 21)]
+    shapes = torch.as_tensor(lv, dtype=torch.long, device=DEV)
+    lsi = torch.cat((shapes.new_zeros((1,)), shapes.prod(1).cumsum(0)[:-1]))
+    S = int(shapes.prod(1).sum())
+    v1, v2 = torch.randn(2, S, 8, 32, device=DEV), torch.randn(2, S, 8, 32, device=DEV)
+    loc = (torch.rand(2, S, 1, 4, 1, 2, device=DEV) + 0.02 * torch.randn(2, S, 8, 4, 4, 2, device=DEV)).contiguous()
+    aw = torch.randn(2, S, 8, 16, device=DEV).softmax(-1).view(2, S, 8, 4, 4).contiguous()
+    o1 = ops.MSDAFn.apply(v1, shapes, lsi, loc, aw, 64)
+    o2 = ops.MSDAFn.apply(v2, shapes, lsi, loc, aw, 64)
+    o12 = ops.MSDAFn.apply((2 * v1 + v2).contiguous(), shapes, lsi, loc, aw, 64)
+    torch.testing.assert_close(o12, 2 * o1 + o2, atol=2e-5, rtol=1e-5)
+    # checksum of checksums against a float64 run of the same kernel
+    o64 = ops.MSDAFn.apply(v1.double(), shapes, lsi, loc.double(), aw.double(), 64)
+    torch.testing.assert_close(o1.double(), o64, atol=1e-5, rtol=1e-5)

@@ -1,0 +1,267 @@
+"""Swin window attention, DSCF fusion and CMNeXt on the HIP path vs the reference
+(golden fixtures) and the CPU oracle.  Tolerances: fp32 paths 1e-4-ish (reference
+CPU fp32 vs GPU fp32 summation order); bf16 paths against the fp32 oracle at the
+bf16 rounding scale, stated per test."""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+import pytest
+import torch
+
+import irads_ref as R
+from fill import fill_module, seeded
+from golden_util import Fixture, close
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DEV = "cuda"
+
+
+def _swin():
+    from semseg.models.backbones import swin
+    return swin
+
+
+# ------------------------------------------------------------------ window attention
+@pytest.mark.parametrize("tag", ["pad_noshift", "pad_shift", "nopad_noshift", "nopad_shift", "rect_shift"])
+def test_shift_window_msa_fp32(tag):
+    swin = _swin()
+    fx = Fixture("swin_wmsa.npz")
+    B, H, W, shift, C, nH = fx[f"{tag}_cfg"].tolist()
+    m = swin.ShiftWindowMSA(C, nH, 12, shift).to(DEV)
+    fill_module(m, seed=7)
+    m.eval()
+    x = fx.regen(f"{tag}_x", (B, H * W, C), 40 + H + shift).to(DEV).requires_grad_()
+    o = m(x, (H, W))
+    close(o, fx[f"{tag}_out"], 2e-5, 1e-4, f"{tag} out")
+    g = fx.regen(f"{tag}_gout", tuple(o.shape), 41 + H + shift).to(DEV)
+    names = [n for n, _ in m.named_parameters()]
+    grads = torch.autograd.grad((o * g).sum(), [x] + [p for _, p in m.named_parameters()])
+    close(grads[0], fx[f"{tag}_gx"], 1e-4, 1e-3, f"{tag} gx")
+    for n, gp in zip(names, grads[1:]):  # includes qkv.bias (pad-token share) and the bias table
+        ref = fx[f"{tag}_g.{n}"]
+        close(gp, ref, 1e-3 * max(1.0, float(np.abs(ref).max())), 1e-3, f"{tag} {n}")
+
+
+@pytest.mark.parametrize("shift", [0, 6])
+def test_window_attention_bf16_vs_fp32(shift):
+    """bf16 MFMA kernels vs the fp32 kernels (themselves pinned above) on the same
+    bf16-representable inputs, at Swin-B stage-0 geometry (128x128 tokens, pad to 132).
+    Tolerance: bf16 P / dS rounding (2^-8 relative) x O(1) magnitudes."""
+    from irads import ops
+    torch.manual_seed(1)
+    B, H, W, C, nH = 2, 128, 128, 128, 4
+    qkv = (torch.randn(B, H * W, 3 * C, device=DEV) * 1.5).bfloat16()
+    bias = (torch.randn(3 * C, device=DEV) * 0.5).bfloat16().float()
+    table = torch.randn(529, nH, device=DEV) * 0.5
+    scale = 32 ** -0.5
+    q32 = qkv.float().requires_grad_()
+    qbf = qkv.clone().requires_grad_()
+    o32 = ops.window_attention(q32, bias, table, None, H, W, nH, shift, scale)
+    obf = ops.window_attention(qbf, bias, table, None, H, W, nH, shift, scale)
+    close(obf.float(), o32, 2e-2, 2e-2, "bf16 forward")
+    g = torch.randn_like(o32).bfloat16()
+    (g32,) = torch.autograd.grad(o32, q32, g.float())
+    (gbf,) = torch.autograd.grad(obf, qbf, g)
+    close(gbf.float(), g32, 5e-2, 5e-2, "bf16 backward")
+    rel = (gbf.float() - g32).norm() / g32.norm()
+    assert rel < 1e-2, f"bf16 grad relative L2 error {rel:.3e}"
+
+
+def test_window_msa_explicit_mask():
+    """WindowMSA.forward(x, mask) (swin.py:81-119) with an explicit (nW, N, N) mask."""
+    swin = _swin()
+    torch.manual_seed(2)
+    C, nH, nW, Bimg = 64, 2, 3, 2
+    m = swin.WindowMSA(C, nH, (12, 12)).to(DEV)
+    ref = R.WindowMSA(C, nH, (12, 12))
+    fill_module(m, seed=3)
+    fill_module(ref, seed=3)
+    x = torch.randn(nW * Bimg, 144, C)
+    mask = torch.where(torch.rand(nW, 144, 144) < 0.3, -100.0, 0.0)
+    close(m(x.to(DEV), mask.to(DEV)), ref(x, mask), 2e-5, 1e-4, "masked WindowMSA")
+
+
+def test_swin_stage_fp32():
+    swin = _swin()
+    from semseg.models.backbones.embed import PatchMerging
+    fx = Fixture("swin_stage.npz")
+    H, W = fx["hw"].tolist()
+    blk = swin.SwinBlockSequence(64, 2, 256, 2, 12, downsample=PatchMerging(64, 128, stride=2)).to(DEV)
+    fill_module(blk, seed=9)
+    blk.eval()
+    for mode in ("rgb", "dte"):
+        x = fx.regen(f"{mode}_x", (2, H * W, 64), 50 + len(mode)).to(DEV).requires_grad_()
+        xd, hwd, xo, _ = blk(x, (H, W), mode)
+        close(xd, fx[f"{mode}_xdown"], 2e-4, 1e-3, "xdown")
+        close(xo, fx[f"{mode}_xout"], 2e-4, 1e-3, "xout")
+        g1 = fx.regen(f"{mode}_g1", tuple(xd.shape), 51).to(DEV)
+        g2 = fx.regen(f"{mode}_g2", tuple(xo.shape), 52).to(DEV)
+        names = [n for n, _ in blk.named_parameters()]
+        grads = torch.autograd.grad((xd * g1).sum() + (xo * g2).sum(), [x] + [p for _, p in blk.named_parameters()],
+                                    allow_unused=True)
+        close(grads[0], fx[f"{mode}_gx"], 2e-3, 2e-3, "gx")
+        for n, gp in zip(names, grads[1:]):
+            if gp is not None:
+                ref = fx[f"{mode}_g.{n}"]
+                close(gp, ref, 2e-3 * max(1.0, float(np.abs(ref).max())), 2e-3, f"{mode} {n}")
+
+
+# ------------------------------------------------------------------ DAttentionMM
+@pytest.mark.parametrize("tag", ["s0", "s1", "s2", "s3", "swinl_s0"])
+def test_dattn_fp32(tag):
+    swin = _swin()
+    fx = Fixture("dattn.npz")
+    dims, stride, g, h, level, H, W, B = fx[f"{tag}_cfg"].tolist()
+    m = swin.DAttentionMM(dims, stride=stride, n_groups=g, n_heads=h, level=level).to(DEV)
+    fill_module(m, seed=13)
+    m.eval()
+    x = fx.regen(f"{tag}_x", (B, dims, H, W), 60 + level).to(DEV).requires_grad_()
+    y = fx.regen(f"{tag}_y", (B, dims, H, W), 70 + level, "uniform").to(DEV).requires_grad_()
+    o = m(x, y)
+    close(o, fx[f"{tag}_out"], 2e-5, 1e-4, f"{tag} out")
+    go = fx.regen(f"{tag}_gout", tuple(o.shape), 80 + level).to(DEV)
+    names = [n for n, _ in m.named_parameters()]
+    grads = torch.autograd.grad((o * go).sum(), [x, y] + [p for _, p in m.named_parameters()])
+    close(grads[0], fx[f"{tag}_gx"], 2e-4, 2e-3, f"{tag} gx")
+    close(grads[1], fx[f"{tag}_gy"], 2e-4, 2e-3, f"{tag} gy")
+    for n, gp in zip(names, grads[2:]):  # rpe_table, conv_offset_* (through pos), fuse_q, ...
+        ref = fx[f"{tag}_g.{n}"]
+        close(gp, ref, 2e-3 * max(1.0, float(np.abs(ref).max())), 2e-3, f"{tag} {n}")
+
+
+@pytest.mark.parametrize("tag", ["s0", "s1", "s2", "s3", "swinl_s0"])
+def test_dattn_sampling_indices_bitexact(tag):
+    """The integer floors of every grid_sample DAttentionMM issues (feature sampling
+    at pos_x / pos_y on H x W, rpe bias at 0.5(q_grid - pos) on 119 x 159), fed the
+    reference's own recorded grids, equal the C oracle's (itself bit-exact vs CPU)."""
+    from irads import ops
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+    lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "liboracle.so"))
+    P = ctypes.c_void_p
+    fx = Fixture("dattn.npz")
+    dims, stride, g, h, level, H, W, B = fx[f"{tag}_cfg"].tolist()
+    for key, (hh, ww) in (("pos_x", (H, W)), ("pos_y", (H, W)), ("disp_x", (119, 159)), ("disp_y", (119, 159))):
+        grid = np.ascontiguousarray(fx[f"{tag}_{key}"][..., ::-1].reshape(-1, 2)).astype(np.float32)
+        n = grid.shape[0]
+        cor = np.zeros((n, 2), np.int32)
+        dummy = np.zeros((1, hh, ww), np.float32)
+        out = np.zeros((1, n), np.float32)
+        lib.oracle_grid_sample(dummy.ctypes.data_as(P), 1, hh, ww, grid.ctypes.data_as(P), n, 1,
+                               out.ctypes.data_as(P), cor.ctypes.data_as(P))
+        got = ops.dattn_sample_index(torch.from_numpy(grid).to(DEV), hh, ww).cpu().numpy()
+        assert (got == cor).all(), f"{tag} {key}: {int((got != cor).any(1).sum())} index mismatches"
+
+
+def test_fusion_blocks_fp32():
+    swin = _swin()
+    fx = Fixture("fusion_small.npz")
+    m = swin.MPGBlock(64, 0.125).to(DEV)
+    fill_module(m, seed=17)
+    xr = fx.regen("mpg_xr", (2, 42, 64), 90).to(DEV)
+    xd = fx.regen("mpg_xd", (2, 42, 64), 91).to(DEV)
+    a, b = m(xr, xd, 6, 7)
+    close(a, fx["mpg_a"], 1e-5, 1e-4, "mpg a")
+    close(b, fx["mpg_b"], 1e-5, 1e-4, "mpg b")
+    d = swin.DeformMPGBlock(128, 4, 2, 4, 0, 1, 0.125).to(DEV)
+    fill_module(d, seed=19)
+    d.eval()
+    xr = fx.regen("dmpg_xr", (2, 256, 128), 94).to(DEV).requires_grad_()
+    xd = fx.regen("dmpg_xd", (2, 256, 128), 95).to(DEV).requires_grad_()
+    o = d(xr, xd, 16, 16, 1)
+    close(o, fx["dmpg_out"], 2e-5, 1e-4, "dmpg out")
+    go = fx.regen("dmpg_gout", tuple(o.shape), 96).to(DEV)
+    gxr, gxd = torch.autograd.grad((o * go).sum(), [xr, xd])
+    close(gxr, fx["dmpg_gxr"], 2e-4, 2e-3, "dmpg gxr")
+    close(gxd, fx["dmpg_gxd"], 2e-4, 2e-3, "dmpg gxd")
+
+
+# ------------------------------------------------------------------ CMNeXt
+class _Tiny(torch.nn.Module):
+    pass
+
+
+def _product_tiny(n_cls=5):
+    swin = _swin()
+    from semseg.models.heads import SegFormerHead
+    from semseg.models.cmnext import CMNeXt
+    h = _Tiny()
+    h.backbone = swin.SwinTransformer(embed_dims=32, depths=(2, 2, 2, 2), num_heads=(1, 2, 4, 8), init_cfg=None)
+    dims = [32, 64, 128, 256]
+    h.decode_head = SegFormerHead(dims, 64, n_cls)
+    h.decode_head_rgb = SegFormerHead(dims, 32, n_cls)
+    h.decode_head_dte = SegFormerHead(dims, 32, n_cls)
+    h.forward = lambda x: CMNeXt.forward(h, x)
+    return h
+
+
+def _adapter_trainable(n):
+    return ("Adapter" in n) or ("extra_patch_embed" in n) or ("head" in n) or ("MPG" in n)
+
+
+def test_cmnext_tiny_fp32():
+    fx = Fixture("cmnext_tiny.npz")
+    m = _product_tiny().to(DEV)
+    assert sorted(m.state_dict().keys()) == fx["state_keys"].tolist()
+    fill_module(m, seed=29)
+    m.eval()
+    m.backbone.eval()
+    rgb = fx.regen("rgb", (2, 3, 128, 160), 100).to(DEV)
+    dep = fx.regen("dep", (2, 3, 128, 160), 101, "uniform").to(DEV)
+    y, yr, yd = m([rgb, dep])
+    for name, t in (("y", y), ("y_rgb", yr), ("y_dte", yd)):
+        ref = fx[name]
+        close(t, ref, 1e-3 * float(np.abs(ref).max()), 1e-3, name)  # "fp32 logits within 1e-3"
+    gs = [fx.regen(k, tuple(y.shape), 102 + i).to(DEV) for i, k in enumerate(("gy", "gyr", "gyd"))]
+    named = [(n, p) for n, p in m.named_parameters() if _adapter_trainable(n)]
+    grads = torch.autograd.grad((y * gs[0]).sum() + (yr * gs[1]).sum() + (yd * gs[2]).sum(), [p for _, p in named])
+    for (n, _), g in zip(named, grads):
+        ref = fx[f"g.{n}"]
+        close(g, ref, 5e-3 * max(float(np.abs(ref).max()), 1e-3), 5e-3, n)
+
+
+def test_cmnext_swinb512_checksums():
+    """Full Swin-B CMNeXt at 512² (config C2 geometry), fp32 eval: checksums of the
+    reference's logits (fixture) and argmax class histograms."""
+    from semseg.models import CMNeXt
+    fx = Fixture("cmnext_swinb512_checksums.npz")
+    m = CMNeXt("SwinTransformer-B", 40, ["img", "depth"]).to(DEV)
+    fill_module(m, seed=31)
+    m.eval()
+    m.backbone.eval()
+    rgb = torch.from_numpy(seeded((1, 3, 512, 512), 110)).to(DEV)
+    dep = torch.from_numpy(seeded((1, 3, 512, 512), 111, "uniform")).to(DEV)
+    with torch.no_grad():
+        y, yr, yd = m([rgb, dep])
+    for name, f in (("y", y), ("y_rgb", yr), ("y_dte", yd)):
+        got = np.array([f.double().mean().item(), f.double().abs().mean().item(), f.double().pow(2).mean().sqrt().item()])
+        np.testing.assert_allclose(got, fx[name], rtol=1e-3, atol=1e-4, err_msg=name)
+
+
+# ------------------------------------------------------------------ LightSB
+def test_lightsb():
+    from modules.sb import LightSB
+    fx = Fixture("lightsb.npz")
+    m = LightSB(dim=512, n_potentials=10, epsilon=0.1).to(DEV)
+    with torch.no_grad():
+        m.r.copy_(fx.regen("r", (10, 512), 122))
+        m.S_log_diagonal_matrix.copy_(fx.t("S_log_diag"))
+        m.log_alpha_raw.copy_(fx.t("log_alpha_raw"))
+    x = fx.regen("x", (128, 512), 123).to(DEV)
+    for tt in (0.0, 0.3, 0.9):
+        d = m.get_drift(x, torch.full((128,), tt, device=DEV))
+        # reference fp32 drift is itself 2.1e-3 off its fp64 drift (logsumexp cancellation)
+        close(d, fx[f"drift_t{tt}"], 4e-3, 1e-4, f"drift {tt}")
+        d64 = m.double().get_drift(x.double(), torch.full((128,), tt, device=DEV, dtype=torch.float64))
+        m.float()
+        close(d64, fx[f"drift64_t{tt}"], 1e-9, 1e-9, f"drift64 {tt}")
+    close(m.get_log_C(x), fx["log_C"], 1e-2, 1e-5, "log_C")
+    close(m.get_log_potential(x), fx["log_potential"], 1e-2, 1e-4, "log_potential")
+    noise = fx.regen("em_noise", (10, 128, 512), 124).to(DEV)
+    traj = m.sample_euler_maruyama(x, 10, noise=noise)
+    assert traj.shape == (128, 11, 512)
+    close(traj[:, [1, 5, 10]], fx["em_traj_sel"], 4e-3, 1e-4, "EM trajectory")
+    s = m(x)
+    assert s.shape == x.shape and torch.isfinite(s).all()
