@@ -1,0 +1,224 @@
+"""Throughput benchmark: IR-ADS CMNeXt Swin-B training step at 512x512 RGB-D on MI355X.
+
+    python bench.py [--gpus N --steps K --warmup W]           # N=1 default
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+One step = one fwd + bwd + AdamW update of CMNeXt('SwinTransformer-B', 40 classes,
+['img', 'depth']) on a per-GPU batch of 8 synthetic 512x512 RGB-D images (config C2 of
+BASELINE.json), bf16 autocast, TRAIN_TYPE Adapter (optimizers.py:7-30), MMST loss
+(train_mm.py:133-150), warmup-poly LR.  Inputs are generated on the device before
+timing (data loading excluded).  Data parallel over RCCL (DDP, one process per GPU),
+weak scaling.  Rank 0 prints one JSON line.
+
+Extra fields: ``roofline`` for the dominant hot-path kernel (Swin window-attention
+forward, bf16), with per-launch durations measured by HIP events on the launch stream
+over the timed region; ``cpu_baseline`` = the CPU restatement (oracle/, the checker)
+timed on this host on a bounded sample of the same workload.
+"""
+import argparse
+import json
+import os
+import random
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "ir-ads_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "train images/sec @512² RGB-D Swin-B, 1/2/4/8 MI355X; mIoU parity"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+N_CLASSES = 40  # NYU-Depth-v2 (nyu.py:20-23)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--batch", type=int, default=8, help="images per GPU (C2: 8)")
+    p.add_argument("--size", type=int, default=512)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-batch", type=int, default=4, help="apply_mask needs >= 4 (swin.py:1098-1103)")
+    p.add_argument("--cpu-steps", type=int, default=1)
+    p.add_argument("--profile-only", action="store_true", help="run warmup + steps, print nothing extra")
+    return p.parse_args()
+
+
+def synthetic_batch(B, size, device, seed):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    rgb = torch.randn(B, 3, size, size, generator=g)                # post-Normalize RGB
+    dep = torch.rand(B, 3, size, size, generator=g)                 # depth / HHA: /255 only
+    lbl = torch.randint(0, N_CLASSES, (B, size, size), generator=g)
+    lbl[torch.rand(B, size, size, generator=g) < 0.1] = 255
+    return rgb.to(device), dep.to(device), lbl.to(device)
+
+
+def build(device, world, local_rank, iters):
+    from semseg.models import CMNeXt
+    from semseg.optimizers import get_optimizer
+    from semseg.schedulers import get_scheduler
+    from semseg.losses import get_loss
+    model = CMNeXt("SwinTransformer-B", N_CLASSES, ["img", "depth"]).to(device)
+    opt = get_optimizer(model, "adamw", 4e-4, "Adapter", 0.01)  # nyu_rgbd.yaml:31-35
+    sched = get_scheduler("warmuppolylr", opt, iters, 0.9, 10, 0.1)
+    if world > 1:
+        from torch.nn.parallel import DistributedDataParallel as DDP
+        # every trainable parameter is used each step: static graph, no unused-param walk
+        model = DDP(model, device_ids=[local_rank], broadcast_buffers=False, gradient_as_bucket_view=True,
+                    static_graph=True)
+    return model, opt, sched, get_loss("CrossEntropy", 255)
+
+
+def train_step(model, opt, sched, loss_fn, batch):
+    from semseg.losses import mmst_loss
+    rgb, dep, lbl = batch
+    opt.zero_grad(set_to_none=True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        logits, logits_rgb, logits_dte = model([rgb, dep])
+        loss = mmst_loss(loss_fn, logits, logits_rgb, logits_dte, lbl)
+    loss.backward()
+    opt.step()
+    sched.step()
+    return loss
+
+
+def cpu_baseline(args):
+    """The oracle's CPU restatement (oracle/irads_ref.py, pinned to the reference's
+    golden fixtures) doing the same training step on a bounded sample."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import irads_ref as R
+    from semseg.losses import get_loss, mmst_loss
+    from semseg.optimizers import adapter_trainable
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    torch.manual_seed(3407)
+    model = R.CMNeXt("SwinTransformer-B", N_CLASSES, ["img", "depth"])
+    params = [p for n, p in model.named_parameters() if adapter_trainable(n)]
+    for n, p in model.named_parameters():
+        p.requires_grad_(adapter_trainable(n))
+    opt = torch.optim.AdamW(params, 4e-4, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01)
+    loss_fn = get_loss("CrossEntropy", 255)
+    model.train()
+    B = args.cpu_batch
+    rgb, dep, lbl = synthetic_batch(B, args.size, "cpu", 3407)
+    batch = (rgb[:B], dep[:B], lbl[:B])
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        y, yr, yd = model([batch[0], batch[1]])
+        mmst_loss(loss_fn, y, yr, yd, batch[2]).backward()
+        opt.step()
+    step()  # warmup
+    t0 = time.perf_counter()
+    for _ in range(args.cpu_steps):
+        step()
+    dt = time.perf_counter() - t0
+    return {"value": round(B * args.cpu_steps / dt, 4), "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"oracle CPU restatement (fp32 PyTorch), same train step at batch {B}, {args.size}x{args.size}, "
+                      f"1 warmup + {args.cpu_steps} timed steps, {dt:.1f} s"}
+
+
+def traffic_from_profile():
+    path = os.path.join(ROOT, "profiles", "pmc_winattn_fwd.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        return json.load(f).get("hbm_bytes_per_launch")
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    device = torch.device("cuda", local_rank)
+    torch.backends.cudnn.benchmark = True
+    random.seed(3407 + rank)
+    np.random.seed(3407 + rank)
+    torch.manual_seed(3407 + rank)
+    total_iters = args.warmup + args.steps
+    model, opt, sched, loss_fn = build(device, world, local_rank, 100000)
+    model.train()
+    batch = synthetic_batch(args.batch, args.size, device, 3407 + rank)
+
+    from irads import ops
+    for _ in range(args.warmup):
+        train_step(model, opt, sched, loss_fn, batch)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    ops.TIMER.enabled = {"winattn_fwd", "winattn_bwd"}
+    ops.TIMER.records.clear()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = train_step(model, opt, sched, loss_fn, batch)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    ops.TIMER.enabled = set()
+    if world > 1:
+        t = torch.tensor([elapsed], device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    loss_val = float(loss.item())
+    fwd = ops.TIMER.summary("winattn_fwd")
+    bwd = ops.TIMER.summary("winattn_bwd")
+    if args.profile_only:
+        if rank == 0:
+            print(json.dumps({"profile_only": True, "ms_per_step": 1e3 * elapsed / args.steps}))
+        if world > 1:
+            dist.destroy_process_group()
+        return
+    images = args.batch * world * args.steps
+    result = {
+        "metric": METRIC, "value": round(images / elapsed, 3), "unit": "images/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+        "data": "synthetic (RGB N(0,1), depth U[0,1), labels U{0..39} with 10% ignore=255; random-init weights)",
+        "config": {"workload": "C2: NYU-Depth-v2 RGB-D CMNeXt(SwinTransformer-B) 512x512 train step "
+                               "(fwd+bwd+AdamW, TRAIN_TYPE Adapter, MMST loss)",
+                   "per_gpu_batch": args.batch, "global_batch": args.batch * world,
+                   "image_size": [args.size, args.size], "parallelism": f"dp{world}"},
+        "loss": round(loss_val, 5),
+    }
+    if fwd:
+        avg_ms = fwd["total_ms"] / fwd["launches"]
+        per_launch_bytes = fwd["bytes"] / fwd["launches"]
+        achieved = fwd["bytes"] / (fwd["total_ms"] * 1e-3) / 1e9
+        traffic = traffic_from_profile()
+        result["roofline"] = {
+            "kernel": "irads_winattn_fwd (bf16, Swin-B shifted-window attention, all 4 stages x 2 streams)",
+            "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "launches": fwd["launches"], "avg_launch_ms": round(avg_ms, 5),
+            "algorithmic_bytes_per_launch": round(per_launch_bytes),
+            "mfma_tflops": round(fwd["flops"] / (fwd["total_ms"] * 1e-3) / 1e12, 2)}
+        if bwd:
+            ab = bwd["bytes"] / (bwd["total_ms"] * 1e-3) / 1e9
+            result["roofline_bwd"] = {"kernel": "irads_winattn_bwd (bf16)", "achieved": round(ab, 1),
+                                      "unit": "GB/s", "frac": round(ab / HBM_PEAK_GBS, 4),
+                                      "avg_launch_ms": round(bwd["total_ms"] / bwd["launches"], 5),
+                                      "share_of_step": round(bwd["total_ms"] / (1e3 * elapsed), 4)}
+            result["roofline"]["share_of_step"] = round(fwd["total_ms"] / (1e3 * elapsed), 4)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            result["cpu_baseline"] = cpu_baseline(args)
+        except Exception as e:  # report, never fake
+            result["cpu_baseline"] = {"value": None, "error": repr(e)[:200]}
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -24,50 +24,51 @@ __device__ __forceinline__ T wsum(T v) {
     return v;
 }
 
-// LDS layout: invS[K*D] (1/S), rS[K*D] (r/S), kc[K] (per-potential constant)
+// LDS layout: ise[K*D] = 1/(eps S), rr[K*D] = r, kc[K] = log_alpha_raw/eps - ½Σ log S.
+// The reference's arg_k carries +½Σc²/A and -½Σr²/(eps S), each O(1e4) at the default
+// S = 0.1, that cancel; here the per-element bracket is rewritten without them:
+//   c²/A - r²/(eps S) = (u²x² + 2u x r/(eps S) - r² a0/(eps S)) / A,
+//   u = 1/(eps(1-t)), a0 = t u, A = a0 + 1/(eps S), c = u x + r/(eps S),
+// which keeps the fp32 drift well inside the reference's own fp32 error.
 template <typename T>
-__device__ void stage_params(T *invS, T *rS, T *kc, const T *r, const T *Sl, const T *la, T eps, int D, int K) {
+__device__ void stage_params(T *ise, T *rr, T *kc, const T *r, const T *Sl, const T *la, T eps, int D, int K) {
     for (int i = threadIdx.x; i < K * D; i += blockDim.x) {
-        T is = exp(-Sl[i]);
-        invS[i] = is;
-        rS[i] = r[i] * is;
+        ise[i] = exp(-Sl[i]) / eps;
+        rr[i] = r[i];
     }
     __syncthreads();
     const int wave = threadIdx.x / 64, lane = threadIdx.x % 64;
     for (int k = wave; k < K; k += blockDim.x / 64) {
-        T sls = 0, rsr = 0;
-        for (int d = lane; d < D; d += 64) {
-            sls += Sl[k * D + d];
-            rsr += r[k * D + d] * rS[k * D + d];
-        }
+        T sls = 0;
+        for (int d = lane; d < D; d += 64) sls += Sl[k * D + d];
         sls = wsum(sls);
-        rsr = wsum(rsr);
-        if (lane == 0) kc[k] = la[k] / eps - (T)0.5 * sls - (T)0.5 * rsr / eps;
+        if (lane == 0) kc[k] = la[k] / eps - (T)0.5 * sls;
     }
     __syncthreads();
 }
 
 // drift for one row held in registers xv[j] = x[lane + 64 j]
 template <typename T>
-__device__ __forceinline__ void row_drift(const T *xv, T t, const T *invS, const T *rS, const T *kc, T eps, int D,
+__device__ __forceinline__ void row_drift(const T *xv, T t, const T *ise, const T *rr, const T *kc, T eps, int D,
                                           int K, T *dv) {
     const int lane = threadIdx.x % 64;
     const int nper = (D + 63) / 64;
-    const T a0 = t / (eps * ((T)1 - t));
-    const T cx = (T)1 / (eps * ((T)1 - t));
+    const T u = (T)1 / (eps * ((T)1 - t));
+    const T a0 = t * u;
     T arg[kMaxK];
     for (int k = 0; k < K; ++k) {
-        T slog = 0, sc2 = 0;
+        T slog = 0, se = 0;
         for (int j = 0; j < nper; ++j) {
             const int d = lane + 64 * j;
             if (d < D) {
-                const T A = a0 + invS[k * D + d] / eps;
-                const T c = xv[j] * cx + rS[k * D + d] / eps;
+                const T is = ise[k * D + d], r = rr[k * D + d], x = xv[j];
+                const T A = a0 + is;
+                const T ux = u * x;
                 slog += log(A);
-                sc2 += c * c / A;
+                se += (ux * ux + (T)2 * ux * r * is - r * r * is * a0) / A;
             }
         }
-        arg[k] = kc[k] - (T)0.5 * wsum(slog) + (T)0.5 * wsum(sc2);
+        arg[k] = kc[k] - (T)0.5 * wsum(slog) + (T)0.5 * wsum(se);
     }
     T mx = arg[0];
     for (int k = 1; k < K; ++k) mx = arg[k] > mx ? arg[k] : mx;
@@ -81,9 +82,8 @@ __device__ __forceinline__ void row_drift(const T *xv, T t, const T *invS, const
         if (d >= D) continue;
         T s = 0;
         for (int k = 0; k < K; ++k) {
-            const T A = a0 + invS[k * D + d] / eps;
-            const T c = xv[j] * cx + rS[k * D + d] / eps;
-            s += arg[k] * (c / A);
+            const T is = ise[k * D + d];
+            s += arg[k] * ((u * xv[j] + rr[k * D + d] * is) / (a0 + is));
         }
         dv[j] = (s / den - xv[j]) / ((T)1 - t);
     }

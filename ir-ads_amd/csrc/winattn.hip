@@ -111,7 +111,7 @@ __global__ void __launch_bounds__(256) winattn_fwd_f32(const float *__restrict__
         float s = 0.f;
         for (int d = 0; d < HD; ++d) s = fmaf(q[d], Ks[ki][d], s);
         s += tb[rel_idx(qi, ki)];
-        s += mask_val(g, mask, w, regS, qi, ki);
+        s += mask_val(g, mask, b * g.nW + w, regS, qi, ki);
         const float mn = fmaxf(m, s);
         const float corr = expf(m - mn), p = expf(s - mn);
         l = l * corr + p;
@@ -181,7 +181,7 @@ __global__ void __launch_bounds__(256) winattn_bwd_f32(const float *__restrict__
                 dp = fmaf(dOs[qi][d], Vs[ki][d], dp);
             }
             const int ri = rel_idx(qi, ki);
-            s += tb[ri] + mask_val(g, mask, w, regS, qi, ki);
+            s += tb[ri] + mask_val(g, mask, b * g.nW + w, regS, qi, ki);
             const float p = expf(s - lseS[qi]);
             const float ds = p * (dp - dlt[qi]);
             for (int d = 0; d < HD; ++d) dq[d] = fmaf(ds, Ks[ki][d], dq[d]);
@@ -205,7 +205,7 @@ __global__ void __launch_bounds__(256) winattn_bwd_f32(const float *__restrict__
                 s = fmaf(Qs[qj][d], Ks[ki][d], s);
                 dp = fmaf(dOs[qj][d], Vs[ki][d], dp);
             }
-            s += tb[rel_idx(qj, ki)] + mask_val(g, mask, w, regS, qj, ki);
+            s += tb[rel_idx(qj, ki)] + mask_val(g, mask, b * g.nW + w, regS, qj, ki);
             const float p = expf(s - lseS[qj]);
             const float ds = p * (dp - dlt[qj]);
             for (int d = 0; d < HD; ++d) {
@@ -314,7 +314,7 @@ __global__ void __launch_bounds__(192, 2) winattn_fwd_bf16(const unsigned short 
                     const int wrg = lastW ? (kw < WS - g.shift ? 1 : 2) : 0;
                     v += (hr * 3 + wrg != qreg) ? -100.0f : 0.0f;
                 }
-                if (MM == 2) v += mask[((long)(w % g.n_mask) * NT + qi) * NT + ki];
+                if (MM == 2) v += mask[((long)((b * g.nW + w) % g.n_mask) * NT + qi) * NT + ki];
                 s[kt][r] = v;
                 mx = fmaxf(mx, v);
             }
@@ -486,7 +486,7 @@ __global__ void __launch_bounds__(192, 2) winattn_bwd_bf16(
                     const int ri = (qinfo & 0xffff) - kpos;
                     float sv = sa[r] * g.scale + tb[ri];
                     if (MM == 1) sv += ((qinfo >> 16) != kreg) ? -100.0f : 0.0f;
-                    if (MM == 2) sv += mask[((long)(w % g.n_mask) * NT + qi) * NT + ki];
+                    if (MM == 2) sv += mask[((long)((b * g.nW + w) % g.n_mask) * NT + qi) * NT + ki];
                     const float p = __expf(sv - lseS[qi]);
                     const float ds = p * (da[r] - dlt[qi]);
                     pb[j][4 * half + r] = (__bf16)p;

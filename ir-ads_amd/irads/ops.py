@@ -13,6 +13,43 @@ WINDOW = 12
 HEAD_DIM = 32
 
 
+class LaunchTimer:
+    """Brackets selected kernel launches with HIP events on the launch stream (the
+    current torch stream, which is where every irads kernel is enqueued).  bench.py
+    enables it over its timed region to report per-launch durations of the dominant
+    kernel; disabled it costs one attribute check per launch."""
+
+    def __init__(self):
+        self.enabled = set()
+        self.records = []  # (name, start_event, end_event, algorithmic_bytes, flops)
+
+    def start(self, name):
+        if name not in self.enabled:
+            return None
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        return ev
+
+    def stop(self, name, ev, nbytes, flops):
+        if ev is None:
+            return
+        end = torch.cuda.Event(enable_timing=True)
+        end.record()
+        self.records.append((name, ev, end, nbytes, flops))
+
+    def summary(self, name):
+        torch.cuda.synchronize()
+        rec = [r for r in self.records if r[0] == name]
+        if not rec:
+            return None
+        ms = [r[1].elapsed_time(r[2]) for r in rec]
+        return {"launches": len(rec), "total_ms": sum(ms), "bytes": sum(r[3] for r in rec),
+                "flops": sum(r[4] for r in rec)}
+
+
+TIMER = LaunchTimer()
+
+
 # ------------------------------------------------------------------ window attention
 class WindowAttentionFn(torch.autograd.Function):
     """ShiftWindowMSA/WindowMSA core between the qkv and proj Linears
@@ -33,8 +70,12 @@ class WindowAttentionFn(torch.autograd.Function):
         Hp, Wp = -(-H // WINDOW) * WINDOW, -(-W // WINDOW) * WINDOW
         nW = (Hp // WINDOW) * (Wp // WINDOW)
         lse = torch.empty((B * nW * num_heads * WINDOW * WINDOW,), device=qkv.device, dtype=torch.float32)
+        ev = TIMER.start("winattn_fwd")
         N.call("irads_winattn_fwd", code, N.ptr(qkv), N.ptr(bias_f), N.ptr(table_f), N.ptr(mask_f), n_mask, B, H, W,
                C, num_heads, shift, float(scale), N.ptr(out), N.ptr(lse), N.stream())
+        # algorithmic work: read q, k, v and write o for every real token; 4·N²·32 flops per (window, head)
+        TIMER.stop("winattn_fwd", ev, B * L * 4 * C * qkv.element_size(),
+                   4 * (WINDOW * WINDOW) ** 2 * HEAD_DIM * B * nW * num_heads)
         ctx.save_for_backward(qkv, bias_f, table_f, mask_f, out, lse)
         ctx.cfg = (code, n_mask, B, H, W, C, num_heads, shift, float(scale))
         ctx.need = (qkv_bias is not None and ctx.needs_input_grad[1], ctx.needs_input_grad[2])
@@ -49,9 +90,15 @@ class WindowAttentionFn(torch.autograd.Function):
         gqkv = torch.empty_like(qkv)
         gtable = torch.zeros_like(table_f) if ctx.need[1] else None
         gbias = torch.zeros((3 * C,), device=qkv.device, dtype=torch.float32) if ctx.need[0] else None
+        ev = TIMER.start("winattn_bwd")
         N.call("irads_winattn_bwd", code, N.ptr(qkv), N.ptr(bias_f), N.ptr(table_f), N.ptr(mask_f), n_mask, B, H, W,
                C, nH, shift, scale, N.ptr(out), N.ptr(lse), N.ptr(gout), N.ptr(gqkv), N.ptr(gtable), N.ptr(gbias),
                N.stream())
+        # algorithmic: read q, k, v, o, dO and write dq, dk, dv per real token; 8·N²·32 flops
+        L = H * W
+        nW = (-(-H // WINDOW)) * (-(-W // WINDOW))
+        TIMER.stop("winattn_bwd", ev, B * L * 9 * C * qkv.element_size(),
+                   8 * (WINDOW * WINDOW) ** 2 * HEAD_DIM * B * nW * nH)
         if gtable is not None:
             gtable = gtable.to(ctx.table_dtype)
         return gqkv, gbias, gtable, None, None, None, None, None, None

@@ -1,0 +1,34 @@
+"""Optimizer factory (reference semseg/optimizers.py:5-49).
+
+TRAIN_TYPE 'Adapter' trains only parameters whose name contains Adapter /
+extra_patch_embed / head / MPG (optimizers.py:7-30) and freezes the rest.  On GPU the
+AdamW update runs as PyTorch's fused multi-tensor kernel (one launch per step)."""
+from torch import nn
+from torch.optim import AdamW, SGD
+
+
+def adapter_trainable(name: str) -> bool:
+    return ("Adapter" in name) or ("extra_patch_embed" in name) or ("head" in name) or ("MPG" in name)
+
+
+def get_optimizer(model: nn.Module, optimizer: str, lr: float, train_type: str, weight_decay: float = 0.01,
+                  verbose: bool = False):
+    fused = {}
+    if 'Adapter' in train_type:
+        params = [p for n, p in model.named_parameters() if adapter_trainable(n) and p.requires_grad]
+        for n, p in model.named_parameters():
+            if "Adap" not in n and "extra_patch_embed" not in n and "head" not in n and "MPG" not in n:
+                p.requires_grad = False
+            elif verbose:
+                print(n)
+        groups = [{"params": params}]
+    else:
+        wd = [p for p in model.parameters() if p.requires_grad and p.dim() != 1]
+        nwd = [p for p in model.parameters() if p.requires_grad and p.dim() == 1]
+        groups = [{"params": wd}, {"params": nwd, "weight_decay": 0}]
+    on_gpu = all(p.is_cuda for g in groups for p in g["params"])
+    if optimizer == 'adamw':
+        if on_gpu:
+            fused = {"fused": True}
+        return AdamW(groups, lr, betas=(0.9, 0.999), eps=1e-8, weight_decay=weight_decay, **fused)
+    return SGD(groups, lr, momentum=0.9, weight_decay=weight_decay)

@@ -391,6 +391,12 @@ class SwinTransformer(nn.Module):
     def forward(self, x):
         xr, hw = self.patch_embed(x[0])
         xd, hwd = self.extra_patch_embed(x[1])
+        if self.training:  # MMST apply_mask (swin.py:1094-1105, 1433-1434)
+            import random
+            idx = random.sample(range(xr.size(0)), xr.size(0) // 2)
+            xr, xd = xr.clone(), xd.clone()
+            xr[idx[0]] = 0
+            xd[idx[1]] = 0
         outs, outs_r, outs_d = [], [], []
         for i, stage in enumerate(self.stages):
             fr, fd = self.MPGBlocks[i](xr, xd, hw[0], hw[1])
