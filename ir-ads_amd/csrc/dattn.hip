@@ -108,24 +108,29 @@ __device__ __forceinline__ void dsample(const Taps &t, const Corner &c, float g,
     diy += g * ((t.sw - t.nw) * (1.0f - c.fx) + (t.se - t.ne) * c.fx);
 }
 
+// thread per (b, group, key, channel-in-group); the GP lanes of one (b, group, key) hold
+// its channels, so d(pos) is a shuffle reduction over GP lanes (no atomics on pos)
+template <int GP>
 __global__ void dattn_sample_bwd_kernel(const float *__restrict__ x, const float *__restrict__ y,
                                         const float *__restrict__ q, const float *__restrict__ px,
                                         const float *__restrict__ py, const float *__restrict__ gxs,
                                         const float *__restrict__ gys, const float *__restrict__ gqs, int B, int C,
                                         int H, int W, int G, int n, float *__restrict__ gx, float *__restrict__ gy,
                                         float *__restrict__ gq, float *__restrict__ gpx, float *__restrict__ gpy) {
-    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;  // (b, gi, j2)
-    const long total = (long)B * G * 2 * n;
-    if (i >= total) return;
-    const int j2 = (int)(i % (2 * n));
-    const int gi = (int)((i / (2 * n)) % G);
-    const int b = (int)(i / (2L * n * G));
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long total = (long)B * G * 2 * n * GP;
+    if (i >= total) return;  // total is a multiple of GP: whole groups exit together
+    const int cc = (int)(i % GP);
+    const long r = i / GP;
+    const int j2 = (int)(r % (2 * n));
+    const int gi = (int)((r / (2 * n)) % G);
+    const int b = (int)(r / (2L * n * G));
     const int gc = C / G, j = j2 % n;
     const long pidx = ((long)(b * G + gi) * n + j) * 2;
     const float *pos = (j2 < n ? px : py) + pidx;
     const Corner cr = corner_ac(pos[1], pos[0], H, W);
     float dix = 0.f, diy = 0.f;
-    for (int cc = 0; cc < gc; ++cc) {
+    if (cc < gc) {
         const int c = gi * gc + cc;
         const long plane = ((long)b * C + c) * H * W;
         const long oi = ((long)b * C + c) * 2 * n + j2;
@@ -137,9 +142,16 @@ __global__ void dattn_sample_bwd_kernel(const float *__restrict__ x, const float
         scatter(gy + plane, H, W, cr, g2);
         scatter(gq + plane, H, W, cr, g3);
     }
-    float *gp = (j2 < n ? gpx : gpy) + pidx;
-    gp[0] = diy * (((float)H - 1.0f) / 2.0f);
-    gp[1] = dix * (((float)W - 1.0f) / 2.0f);
+#pragma unroll
+    for (int o = GP / 2; o > 0; o >>= 1) {
+        dix += __shfl_xor(dix, o, GP);
+        diy += __shfl_xor(diy, o, GP);
+    }
+    if (cc == 0) {
+        float *gp = (j2 < n ? gpx : gpy) + pidx;
+        gp[0] = diy * (((float)H - 1.0f) / 2.0f);
+        gp[1] = dix * (((float)W - 1.0f) / 2.0f);
+    }
 }
 
 // ---------------------------------------------------------------- fused attention
@@ -211,17 +223,35 @@ __global__ void __launch_bounds__(1024) dattn_attn_fwd_kernel(AttnArgs a, float 
     lse[(long)bh * HW + qi] = m + __logf(l);
 }
 
+__device__ __forceinline__ void scatter_lds(float *tg, int Ht, int Wt, const Corner &cr, float ds) {
+    const bool xl = cr.x0 >= 0 && cr.x0 < Wt, xh = cr.x0 + 1 >= 0 && cr.x0 + 1 < Wt;
+    const bool yl = cr.y0 >= 0 && cr.y0 < Ht, yh = cr.y0 + 1 >= 0 && cr.y0 + 1 < Ht;
+    const int o = cr.y0 * Wt + cr.x0;
+    if (yl && xl) atomicAdd(&tg[o], cr.nw * ds);
+    if (yl && xh) atomicAdd(&tg[o + 1], cr.ne * ds);
+    if (yh && xl) atomicAdd(&tg[o + Wt], cr.sw * ds);
+    if (yh && xh) atomicAdd(&tg[o + Wt + 1], cr.se * ds);
+}
+
+// Pass Q (thread per query): dq, delta = dO·O, and the rpe-table gradient.  The 64
+// lanes of a wave are consecutive queries of one row, so for a fixed key their table
+// cells share a row and step ~0.6 cell per lane: the LDS atomics land on consecutive
+// addresses (near conflict-free).  The table itself is read through L1/L2 (a head's
+// 75.7 KB table is shared by every workgroup of that head); LDS holds the gradient.
+// LDS: tgrad[TT] | kv[2n][2*HC] | pos[2n][2]
 template <int HC>
 __global__ void __launch_bounds__(1024) dattn_attn_bwd_q_kernel(AttnArgs a, const float *__restrict__ out,
                                                                 const float *__restrict__ lse,
                                                                 const float *__restrict__ gout,
-                                                                float *__restrict__ delta, float *__restrict__ gq) {
+                                                                float *__restrict__ delta, float *__restrict__ gq,
+                                                                float *__restrict__ grpe) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
     const int n2 = 2 * a.n, HW = a.H * a.W, TT = a.Ht * a.Wt;
-    float *tab = sm, *kv = sm + TT, *pos = kv + n2 * 2 * HC;
+    float *tg = sm, *kv = sm + TT, *pos = kv + n2 * 2 * HC;
     const int bh = blockIdx.y, b = bh / a.nH, h = bh % a.nH;
     const int gi = h / (a.nH / a.G);
-    for (int i = threadIdx.x; i < TT; i += blockDim.x) tab[i] = a.rpe[(long)h * TT + i];
+    const float *tab = a.rpe + (long)h * TT;
+    for (int i = threadIdx.x; i < TT; i += blockDim.x) tg[i] = 0.f;
     for (int i = threadIdx.x; i < n2 * HC; i += blockDim.x) {
         const int c = i / n2, j = i % n2;
         kv[j * 2 * HC + c] = a.k[((long)bh * HC + c) * n2 + j];
@@ -234,70 +264,78 @@ __global__ void __launch_bounds__(1024) dattn_attn_bwd_q_kernel(AttnArgs a, cons
     }
     __syncthreads();
     const int qi = blockIdx.x * blockDim.x + threadIdx.x;
-    if (qi >= HW) return;
-    const float qgy = a.qgy[qi / a.W], qgx = a.qgx[qi % a.W];
-    float qv[HC], dq[HC], dov[HC];
-    float dl = 0.f;
-#pragma unroll
-    for (int c = 0; c < HC; ++c) {
-        const long o = ((long)bh * HC + c) * HW + qi;
-        qv[c] = a.q[o];
-        dov[c] = gout[o];
-        dl = fmaf(dov[c], out[o], dl);
-        dq[c] = 0.f;
-    }
-    const float ls = lse[(long)bh * HW + qi];
-    for (int j = 0; j < n2; ++j) {
-        const float *kr = kv + j * 2 * HC;
-        float s = 0.f, dp = 0.f;
+    if (qi < HW) {
+        const float qgy = a.qgy[qi / a.W], qgx = a.qgx[qi % a.W];
+        float qv[HC], dq[HC], dov[HC];
+        float dl = 0.f;
 #pragma unroll
         for (int c = 0; c < HC; ++c) {
-            s = fmaf(qv[c], kr[c], s);
-            dp = fmaf(dov[c], kr[HC + c], dp);
+            const long o = ((long)bh * HC + c) * HW + qi;
+            qv[c] = a.q[o];
+            dov[c] = gout[o];
+            dl = fmaf(dov[c], out[o], dl);
+            dq[c] = 0.f;
         }
-        Corner cr;
-        Taps tp;
-        s = s * a.scale + rpe_bias(tab, a.Ht, a.Wt, qgy, qgx, pos[2 * j], pos[2 * j + 1], cr, tp);
-        const float p = __expf(s - ls);
-        const float ds = p * (dp - dl) * a.scale;
+        const float ls = lse[(long)bh * HW + qi];
+        for (int j = 0; j < n2; ++j) {
+            const float *kr = kv + j * 2 * HC;
+            float s = 0.f, dp = 0.f;
 #pragma unroll
-        for (int c = 0; c < HC; ++c) dq[c] = fmaf(ds, kr[c], dq[c]);
+            for (int c = 0; c < HC; ++c) {
+                s = fmaf(qv[c], kr[c], s);
+                dp = fmaf(dov[c], kr[HC + c], dp);
+            }
+            Corner cr;
+            Taps tp;
+            s = s * a.scale + rpe_bias(tab, a.Ht, a.Wt, qgy, qgx, pos[2 * j], pos[2 * j + 1], cr, tp);
+            const float p = __expf(s - ls);
+            const float ds = p * (dp - dl);
+            const float dss = ds * a.scale;
+#pragma unroll
+            for (int c = 0; c < HC; ++c) dq[c] = fmaf(dss, kr[c], dq[c]);
+            scatter_lds(tg, a.Ht, a.Wt, cr, ds);
+        }
+#pragma unroll
+        for (int c = 0; c < HC; ++c) gq[((long)bh * HC + c) * HW + qi] = dq[c];
+        delta[(long)bh * HW + qi] = dl;
     }
-#pragma unroll
-    for (int c = 0; c < HC; ++c) gq[((long)bh * HC + c) * HW + qi] = dq[c];
-    delta[(long)bh * HW + qi] = dl;
+    __syncthreads();
+    for (int i = threadIdx.x; i < TT; i += blockDim.x) {
+        const float v = tg[i];
+        if (v != 0.f) atomicAdd(&grpe[(long)h * TT + i], v);
+    }
 }
 
-constexpr int QCH = 32;  // queries staged per LDS round in pass K
+constexpr int QCH = 64;  // queries staged per LDS round in pass K
 
-// LDS: table[TT] | tgrad[TT] | qst[QCH][2*HC + 4] (q, dO, lse, delta, qgy, qgx)
+// Pass K (thread per key): loops over a chunk of queries staged in LDS and keeps dk, dv
+// and d(pos) of its key in registers (no reduction over lanes).  The bias is recomputed
+// from the table through L1/L2; LDS is only the query staging, so several workgroups
+// share a CU.  LDS: qst[QCH][2*HC + 4] (q, dO, lse, delta, qgy, qgx)
 template <int HC>
 __global__ void __launch_bounds__(1024) dattn_attn_bwd_k_kernel(AttnArgs a, const float *__restrict__ lse,
                                                                 const float *__restrict__ delta,
                                                                 const float *__restrict__ gout, int q_per_block,
                                                                 float *__restrict__ gk, float *__restrict__ gv,
-                                                                float *__restrict__ grpe, float *__restrict__ gpx,
-                                                                float *__restrict__ gpy) {
+                                                                float *__restrict__ gpx, float *__restrict__ gpy) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
     const int n2 = 2 * a.n, HW = a.H * a.W, TT = a.Ht * a.Wt;
     constexpr int QS = 2 * HC + 4;
-    float *tab = sm, *tg = sm + TT, *qst = tg + TT;
+    float *qst = sm;
     const int bh = blockIdx.y, b = bh / a.nH, h = bh % a.nH;
     const int gi = h / (a.nH / a.G);
-    for (int i = threadIdx.x; i < TT; i += blockDim.x) {
-        tab[i] = a.rpe[(long)h * TT + i];
-        tg[i] = 0.f;
-    }
+    const float *tab = a.rpe + (long)h * TT;
     const int j = threadIdx.x;
     const bool active = j < n2;
     float kr[HC], vr[HC], dk[HC], dv[HC];
     float pyk = 0.f, pxk = 0.f, dpy = 0.f, dpx = 0.f;
+#pragma unroll
+    for (int c = 0; c < HC; ++c) kr[c] = vr[c] = dk[c] = dv[c] = 0.f;
     if (active) {
 #pragma unroll
         for (int c = 0; c < HC; ++c) {
             kr[c] = a.k[((long)bh * HC + c) * n2 + j];
             vr[c] = a.v[((long)bh * HC + c) * n2 + j];
-            dk[c] = dv[c] = 0.f;
         }
         const float *p = (j < a.n ? a.px : a.py) + ((long)(b * a.G + gi) * a.n + (j % a.n)) * 2;
         pyk = p[0];
@@ -347,18 +385,10 @@ __global__ void __launch_bounds__(1024) dattn_attn_bwd_k_kernel(AttnArgs a, cons
                     dk[c] = fmaf(dss, qs[c], dk[c]);
                     dv[c] = fmaf(p, qs[HC + c], dv[c]);
                 }
-                // bias gradient: table taps and displacement (d disp = -0.5 d pos)
-                float dix = 0.f, diy = 0.f;
+                float dix = 0.f, diy = 0.f;  // d bias / d disp; disp = 0.5 (q_grid - pos)
                 dsample(tp, cr, ds, dix, diy);
                 dpx -= 0.5f * dix * sxt;
                 dpy -= 0.5f * diy * syt;
-                const bool xl = cr.x0 >= 0 && cr.x0 < a.Wt, xh = cr.x0 + 1 >= 0 && cr.x0 + 1 < a.Wt;
-                const bool yl = cr.y0 >= 0 && cr.y0 < a.Ht, yh = cr.y0 + 1 >= 0 && cr.y0 + 1 < a.Ht;
-                const int o = cr.y0 * a.Wt + cr.x0;
-                if (yl && xl) atomicAdd(&tg[o], cr.nw * ds);
-                if (yl && xh) atomicAdd(&tg[o + 1], cr.ne * ds);
-                if (yh && xl) atomicAdd(&tg[o + a.Wt], cr.sw * ds);
-                if (yh && xh) atomicAdd(&tg[o + a.Wt + 1], cr.se * ds);
             }
         }
     }
@@ -371,11 +401,6 @@ __global__ void __launch_bounds__(1024) dattn_attn_bwd_k_kernel(AttnArgs a, cons
         float *gp = (j < a.n ? gpx : gpy) + ((long)(b * a.G + gi) * a.n + (j % a.n)) * 2;
         atomicAdd(gp, dpy);
         atomicAdd(gp + 1, dpx);
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < TT; i += blockDim.x) {
-        const float v = tg[i];
-        if (v != 0.f) atomicAdd(&grpe[(long)h * TT + i], v);
     }
 }
 
@@ -431,10 +456,21 @@ extern "C" int irads_dattn_sample_bwd(const float *x, const float *y, const floa
                                       int C, int H, int W, int G, int n, float *grad_x, float *grad_y, float *grad_q,
                                       float *grad_pos_x, float *grad_pos_y, void *stream) {
     IRADS_REQUIRE(B >= 0 && C > 0 && G > 0 && C % G == 0 && n > 0 && H > 0 && W > 0, "dattn_sample: bad sizes");
-    const long total = (long)B * G * 2 * n;
+    const int gc = C / G;
+    IRADS_REQUIRE(gc <= 64, "dattn_sample: group channels %d > 64", gc);
+    int GP = 1;
+    while (GP < gc) GP <<= 1;
+    const long total = (long)B * G * 2 * n * GP;
     if (total == 0) return IRADS_OK;
-    dattn_sample_bwd_kernel<<<(unsigned)((total + 255) / 256), 256, 0, (hipStream_t)stream>>>(
-        x, y, q, pos_x, pos_y, gxs, gys, gqs, B, C, H, W, G, n, grad_x, grad_y, grad_q, grad_pos_x, grad_pos_y);
+    const unsigned grid = (unsigned)((total + 255) / 256);
+    hipStream_t st = (hipStream_t)stream;
+#define IRADS_SB(P)                                                                                             \
+    case P:                                                                                                     \
+        dattn_sample_bwd_kernel<P><<<grid, 256, 0, st>>>(x, y, q, pos_x, pos_y, gxs, gys, gqs, B, C, H, W, G, n, \
+                                                         grad_x, grad_y, grad_q, grad_pos_x, grad_pos_y);       \
+        break;
+    switch (GP) { IRADS_SB(1) IRADS_SB(2) IRADS_SB(4) IRADS_SB(8) IRADS_SB(16) IRADS_SB(32) IRADS_SB(64) }
+#undef IRADS_SB
     return check_launch("irads_dattn_sample_bwd");
 }
 
@@ -474,24 +510,22 @@ extern "C" int irads_dattn_attn_bwd(const float *q, const float *k, const float 
     if (B == 0) return IRADS_OK;
     hipStream_t st = (hipStream_t)stream;
     const int HW = H * W;
-    const size_t sh_q = fwd_smem(a);
-    const size_t sh_k = ((size_t)2 * Ht * Wt + (size_t)QCH * (2 * hc + 4)) * sizeof(float);
+    const size_t sh_q = ((size_t)Ht * Wt + (size_t)2 * n * 2 * hc + (size_t)2 * n * 2) * sizeof(float);
+    const size_t sh_k = (size_t)QCH * (2 * hc + 4) * sizeof(float);
     IRADS_REQUIRE(sh_q <= 160 * 1024 && sh_k <= 160 * 1024, "dattn_attn_bwd: LDS request exceeds 160 KiB");
     const int bs = attn_block(HW);
     dim3 gq_grid((HW + bs - 1) / bs, B * nH);
     // pass K: one thread per key; enough query chunks per (b, h) to fill the chip
     const int kthreads = ((2 * n + 63) / 64) * 64;
-    int qpb = 512;
-    while (qpb > 64 && (long)((HW + qpb - 1) / qpb) * B * nH < 512) qpb /= 2;
+    int qpb = 1024;
+    while (qpb > QCH && (long)((HW + qpb - 1) / qpb) * B * nH < 1024) qpb /= 2;
     dim3 gk_grid((HW + qpb - 1) / qpb, B * nH);
     IRADS_HC_DISPATCH(hc, {
         (void)hipFuncSetAttribute((const void *)dattn_attn_bwd_q_kernel<HC>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)sh_q);
-        (void)hipFuncSetAttribute((const void *)dattn_attn_bwd_k_kernel<HC>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)sh_k);
-        dattn_attn_bwd_q_kernel<HC><<<gq_grid, bs, sh_q, st>>>(a, out, lse, grad_out, delta, grad_q);
+                                  (int)sh_q);
+        dattn_attn_bwd_q_kernel<HC><<<gq_grid, bs, sh_q, st>>>(a, out, lse, grad_out, delta, grad_q, grad_rpe);
         dattn_attn_bwd_k_kernel<HC><<<gk_grid, kthreads, sh_k, st>>>(a, lse, delta, grad_out, qpb, grad_k, grad_v,
-                                                                     grad_rpe, grad_pos_x, grad_pos_y);
+                                                                     grad_pos_x, grad_pos_y);
     })
     return check_launch("irads_dattn_attn_bwd");
 }

@@ -232,11 +232,30 @@ __global__ void __launch_bounds__(256) winattn_bwd_f32(const float *__restrict__
 }
 
 // ====================================================================== bf16 MFMA path
+// Persistent-chunk design: one workgroup = 9 waves = one head x a contiguous chunk of
+// windows (grid ~ one workgroup per CU).  Per workgroup the 36 relative-position biases
+// each lane needs are gathered ONCE into registers (pre-scaled by log2 e: softmax runs in
+// base 2 with v_exp_f32), so the per-window work is MFMA + a handful of VALU ops per
+// score.  K/V (and Q/dO in backward) rows are staged into LDS row-major with plain 16-B
+// copies; the transposed MFMA operands (Vᵀ, dOᵀ, Qᵀ, Kᵀ) are read with ds_read_b64_tr_b16.
+// The next window's tiles are loaded into registers while the current one computes.
 __device__ __forceinline__ f32x4 mfma16(const bf16x8_t &a, const bf16x8_t &b, const f32x4 &c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
 __device__ __forceinline__ bf16x8_t as_bf(u16x8 v) { return __builtin_bit_cast(bf16x8_t, v); }
+
+typedef __attribute__((ext_vector_type(4))) short i16x4;
+typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
+
+// 4 rows x 16 columns block, column-major per lane (cdna_hip_programming.md T10)
+__device__ __forceinline__ u16x4 tr_read(const unsigned short *p) {
+    return __builtin_bit_cast(u16x4, __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4 *)p));
+}
+
+__device__ __forceinline__ u16x8 cat4(u16x4 a, u16x4 b) {
+    return u16x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+}
 
 __device__ __forceinline__ u16x8 bias_frag(const float *qbias, int c0) {
     u16x8 r;
@@ -250,71 +269,122 @@ __device__ __forceinline__ u16x8 load_frag(const unsigned short *qkv, const floa
     return bias_frag(qbias, c0);
 }
 
-constexpr int KROW = 40;   // Ks row stride (bf16): 80 B, conflict-free 16-B reads
-constexpr int VTROW = 168; // Vt row stride (forward): keys 0..159 (+8 pad)
+// branch-free variant for the staging loops (no divergent load / alloca selects)
+__device__ __forceinline__ u16x8 load_frag_sel(const unsigned short *qkv, const float *qbias, int tok, long C3,
+                                               int c0) {
+    const u16x8 v = *(const u16x8 *)(qkv + (long)(tok >= 0 ? tok : 0) * C3 + c0);
+    return tok >= 0 ? v : bias_frag(qbias, c0);
+}
 
-// MM: 0 = no mask, 1 = shift-region mask computed in-kernel, 2 = explicit mask tensor
+constexpr int RS = 40;    // LDS row stride (bf16) of the row-major tiles: 80 B
+constexpr int NR = 160;   // rows incl. zero padding to 5 k-steps of 32
+constexpr int DSR = 152;  // dS row stride (keys 144..151 stay zero)
+constexpr float LOG2E = 1.4426950408889634f;
+// Relative-position biases live in registers as fp16 pairs (pre-scaled by log2 e): abs
+// error <= 2^-11 |b|, far below the bf16 rounding the reference's AMP applies to the
+// q·kᵀ logits themselves; forward and backward use the same rounded values.
+typedef __attribute__((ext_vector_type(2))) _Float16 h2;
+
+struct Chunk {
+    int h, w_begin, w_end;
+};
+
+__device__ __forceinline__ Chunk decode_chunk(const Geo &g, int cw) {
+    const int lid = xcd_remap(blockIdx.x, gridDim.x);  // heads of one chunk on one XCD
+    Chunk c;
+    c.h = lid % g.nH;
+    c.w_begin = (lid / g.nH) * cw;
+    c.w_end = min(g.B * g.nW, c.w_begin + cw);
+    return c;
+}
+
+__device__ __forceinline__ int token_of(const Geo &g, int bw, int t) {
+    int tok, reg;
+    token_info(g, bw % g.nW, t, bw / g.nW, tok, reg);
+    return tok;
+}
+
+// class bits of token t inside a boundary window: row / column in the second shift region
+__device__ __forceinline__ bool hi_row(const Geo &g, int t) { return t / WS >= WS - g.shift; }
+__device__ __forceinline__ bool hi_col(const Geo &g, int t) { return t % WS >= WS - g.shift; }
+
 template <int MM>
-__global__ void __launch_bounds__(192, 2) winattn_fwd_bf16(const unsigned short *__restrict__ qkv,
+__global__ void __launch_bounds__(576) winattn_fwd_bf16(const unsigned short *__restrict__ qkv,
                                                          const float *__restrict__ qbias,
                                                          const float *__restrict__ table,
-                                                         const float *__restrict__ mask, Geo g,
+                                                         const float *__restrict__ mask, Geo g, int cw,
                                                          unsigned short *__restrict__ out, float *__restrict__ lse) {
-    __shared__ __attribute__((aligned(16))) unsigned short Ks[NT * KROW];
-    __shared__ __attribute__((aligned(16))) unsigned short Vt[HD * VTROW];
-    __shared__ float tb[TBL];
-    __shared__ int tokS[NT], kinf[NT];  // kinf = (row*23 + col) | region << 16
-    int b, w, h;
-    decode_block(g, b, w, h);
+    __shared__ __attribute__((aligned(16))) unsigned short Ks[NT * RS];
+    __shared__ __attribute__((aligned(16))) unsigned short Vs[NR * RS];
+    const Chunk ck = decode_chunk(g, cw);
+    const int h = ck.h;
     const long C3 = 3 * g.C;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    for (int t = tid; t < NT; t += 192) {
-        int tok, reg;
-        token_info(g, w, t, b, tok, reg);
-        tokS[t] = tok;
-        kinf[t] = ((t / WS) * (2 * WS - 1) + t % WS) | (reg << 16);
-    }
-    for (int i = tid; i < TBL; i += 192) tb[i] = table[i * g.nH + h];
-    for (int i = tid; i < HD * (VTROW - NT); i += 192) Vt[(i / (VTROW - NT)) * VTROW + NT + i % (VTROW - NT)] = 0;
-    __syncthreads();
-    // K rows -> Ks, V rows -> Vt (transposed), 16 B per thread-iteration
-    for (int e = tid; e < NT * 4; e += 192) {
-        const int t = e >> 2, ch = e & 3, tok = tokS[t];
-        const u16x8 kf = load_frag(qkv, qbias, tok, C3, g.C + h * HD + ch * 8);
-        const u16x8 vf = load_frag(qkv, qbias, tok, C3, 2 * g.C + h * HD + ch * 8);
-        *(u16x8 *)(Ks + t * KROW + ch * 8) = kf;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) Vt[(ch * 8 + j) * VTROW + t] = vf[j];
-    }
-    __syncthreads();
     const int l16 = lane & 15, grp = lane >> 4;
-    const long rowbase = (((long)b * g.nW + w) * g.nH + h) * NT;
-    const bool lastH = (w / g.nWw) == g.nWh - 1, lastW = (w % g.nWw) == g.nWw - 1;
-#pragma unroll 1
-    for (int qq = 0; qq < 3; ++qq) {
-        const int qt = wave * 3 + qq;
-        const int qi = qt * 16 + l16;  // this lane's query (column of Sᵀ)
-        const int qtok = tokS[qi];
-        const bf16x8_t qf = as_bf(load_frag(qkv, qbias, qtok, C3, h * HD + grp * 8));
-        const int qinfo = kinf[qi];
-        const int qbase = (qinfo & 0xffff) + 264, qreg = qinfo >> 16;
+    for (int i = tid; i < (NR - NT) * RS; i += 576) Vs[NT * RS + i] = 0;
+    // per-lane biases, log2 domain: query qi = 16 wave + l16, key = 16 kt + 4 grp + r
+    const int qi = wave * 16 + l16;
+    unsigned bias[18];  // fp16 pairs
+    unsigned long long hb = 0, wb = 0;  // key class bits (MM == 1)
+#pragma unroll
+    for (int kt = 0; kt < 9; ++kt)
+#pragma unroll
+        for (int r = 0; r < 4; r += 2) {
+            const int ki = kt * 16 + grp * 4 + r;
+            h2 pr;
+            pr[0] = (_Float16)(table[rel_idx(qi, ki) * g.nH + h] * LOG2E);
+            pr[1] = (_Float16)(table[rel_idx(qi, ki + 1) * g.nH + h] * LOG2E);
+            bias[kt * 2 + r / 2] = __builtin_bit_cast(unsigned, pr);
+            if (MM == 1) {
+                hb |= (unsigned long long)hi_row(g, ki) << (kt * 4 + r);
+                wb |= (unsigned long long)hi_col(g, ki) << (kt * 4 + r);
+                hb |= (unsigned long long)hi_row(g, ki + 1) << (kt * 4 + r + 1);
+                wb |= (unsigned long long)hi_col(g, ki + 1) << (kt * 4 + r + 1);
+            }
+        }
+    const bool q_hr = hi_row(g, qi), q_hc = hi_col(g, qi);
+    const float scale2 = g.scale * LOG2E;
+    // staging map: thread -> (token t, 16-B chunk ch) of K and V
+    const int st_t = tid >> 2, st_ch = tid & 3;
+    u16x8 kreg, vreg, qreg;
+    int qtok_next = -1;
+    auto prefetch = [&](int bw) {
+        const int tok = token_of(g, bw, st_t);
+        kreg = load_frag_sel(qkv, qbias, tok, C3, g.C + h * HD + st_ch * 8);
+        vreg = load_frag_sel(qkv, qbias, tok, C3, 2 * g.C + h * HD + st_ch * 8);
+        qtok_next = token_of(g, bw, qi);
+        qreg = load_frag_sel(qkv, qbias, qtok_next, C3, h * HD + grp * 8);
+    };
+    if (ck.w_begin < ck.w_end) prefetch(ck.w_begin);
+    for (int bw = ck.w_begin; bw < ck.w_end; ++bw) {
+        __syncthreads();
+        *(u16x8 *)(Ks + st_t * RS + st_ch * 8) = kreg;
+        *(u16x8 *)(Vs + st_t * RS + st_ch * 8) = vreg;
+        const bf16x8_t qf = as_bf(qreg);
+        const int qtok = qtok_next;
+#pragma unroll
+        for (int i = 0; i < 18; ++i) asm volatile("" : "+v"(bias[i]));  // keep biases packed (no LICM unpack)
+        __syncthreads();
+        if (bw + 1 < ck.w_end) prefetch(bw + 1);
+        unsigned long long mbits = 0;
+        if (MM == 1) {
+            const int wi = bw % g.nW;
+            const bool lastH = wi / g.nWw == g.nWh - 1, lastW = wi % g.nWw == g.nWw - 1;
+            if (lastH) mbits |= q_hr ? ~hb : hb;
+            if (lastW) mbits |= q_hc ? ~wb : wb;
+        }
         f32x4 s[9];
         float mx = -INFINITY;
 #pragma unroll
         for (int kt = 0; kt < 9; ++kt) {
-            const bf16x8_t kf = as_bf(*(const u16x8 *)(Ks + (kt * 16 + l16) * KROW + grp * 8));
+            const bf16x8_t kf = as_bf(*(const u16x8 *)(Ks + (kt * 16 + l16) * RS + grp * 8));
             s[kt] = mfma16(kf, qf, f32x4{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int ki = kt * 16 + grp * 4 + r;
-                const int kh = ki / WS, kw = ki - kh * WS;  // arithmetic, no LDS round trip
-                float v = s[kt][r] * g.scale + tb[qbase - (kh * (2 * WS - 1) + kw)];
-                if (MM == 1) {
-                    const int hr = lastH ? (kh < WS - g.shift ? 1 : 2) : 0;
-                    const int wrg = lastW ? (kw < WS - g.shift ? 1 : 2) : 0;
-                    v += (hr * 3 + wrg != qreg) ? -100.0f : 0.0f;
-                }
-                if (MM == 2) v += mask[((long)((b * g.nW + w) % g.n_mask) * NT + qi) * NT + ki];
+                float v = fmaf(s[kt][r], scale2, (float)__builtin_bit_cast(h2, bias[kt * 2 + r / 2])[r & 1]);
+                if (MM == 1) v += ((mbits >> (kt * 4 + r)) & 1ull) ? -100.0f * LOG2E : 0.0f;
+                if (MM == 2)
+                    v += LOG2E * mask[((long)(bw % g.n_mask) * NT + qi) * NT + kt * 16 + grp * 4 + r];
                 s[kt][r] = v;
                 mx = fmaxf(mx, v);
             }
@@ -326,14 +396,15 @@ __global__ void __launch_bounds__(192, 2) winattn_fwd_bf16(const unsigned short 
         for (int kt = 0; kt < 9; ++kt)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const float p = __expf(s[kt][r] - mx);
+                const float p = exp2f(s[kt][r] - mx);
                 s[kt][r] = p;
                 sum += p;
             }
         sum += __shfl_xor(sum, 16, 64);
         sum += __shfl_xor(sum, 32, 64);
-        // Oᵀ = Vᵀ · Pᵀ over 5 k-steps of 32 keys (keys 144..159 are zero)
+        // Oᵀ = Vᵀ·Pᵀ over 5 k-steps of 32 keys (key order permuted identically in A and B)
         f32x4 o0 = {0.f, 0.f, 0.f, 0.f}, o1 = {0.f, 0.f, 0.f, 0.f};
+        const int tr_row = (l16 >> 2), tr_col = 4 * (l16 & 3);
 #pragma unroll
         for (int ks = 0; ks < 5; ++ks) {
             bf16x8_t pb;
@@ -342,19 +413,10 @@ __global__ void __launch_bounds__(192, 2) winattn_fwd_bf16(const unsigned short 
                 pb[r] = (__bf16)s[2 * ks][r];
                 pb[4 + r] = (2 * ks + 1 < 9) ? (__bf16)s[2 * ks + 1][r] : (__bf16)0.f;
             }
-            const int k0 = 32 * ks + 4 * grp, k1 = k0 + 16;
-            u16x8 a0, a1;
-            const u16x4 x00 = *(const u16x4 *)(Vt + l16 * VTROW + k0);
-            const u16x4 x01 = *(const u16x4 *)(Vt + l16 * VTROW + k1);
-            const u16x4 x10 = *(const u16x4 *)(Vt + (16 + l16) * VTROW + k0);
-            const u16x4 x11 = *(const u16x4 *)(Vt + (16 + l16) * VTROW + k1);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                a0[j] = x00[j];
-                a0[4 + j] = x01[j];
-                a1[j] = x10[j];
-                a1[4 + j] = x11[j];
-            }
+            const unsigned short *v0 = Vs + (32 * ks + 4 * grp + tr_row) * RS + tr_col;
+            const unsigned short *v1 = v0 + 16 * RS;
+            const u16x8 a0 = cat4(tr_read(v0), tr_read(v1));
+            const u16x8 a1 = cat4(tr_read(v0 + 16), tr_read(v1 + 16));
             o0 = mfma16(as_bf(a0), pb, o0);
             o1 = mfma16(as_bf(a1), pb, o1);
         }
@@ -370,225 +432,227 @@ __global__ void __launch_bounds__(192, 2) winattn_fwd_bf16(const unsigned short 
             *(u16x4 *)(op + grp * 4) = w0;
             *(u16x4 *)(op + 16 + grp * 4) = w1;
         }
-        if (grp == 0) lse[rowbase + qi] = mx + __logf(sum);
+        if (grp == 0) lse[((long)bw * g.nH + h) * NT + qi] = mx + __log2f(sum);  // base-2 LSE
     }
 }
 
-constexpr int TROW = 152;  // Qt / dOt / Kt / dS row stride (bf16): 304 B, conflict-free
-
-template <int MM>
-__global__ void __launch_bounds__(192, 2) winattn_bwd_bf16(
+// EX: support the optional rel-table / pad-bias gradient accumulators (frozen in IR-ADS's
+// Adapter training, so the default instantiation compiles them out)
+template <int MM, bool EX>
+__global__ void __launch_bounds__(576) winattn_bwd_bf16(
     const unsigned short *__restrict__ qkv, const float *__restrict__ qbias, const float *__restrict__ table,
-    const float *__restrict__ mask, Geo g, const unsigned short *__restrict__ out, const float *__restrict__ lse,
+    const float *__restrict__ mask, Geo g, int cw, const unsigned short *__restrict__ out, const float *__restrict__ lse,
     const unsigned short *__restrict__ gout, unsigned short *__restrict__ gqkv, float *__restrict__ gtable,
     float *__restrict__ gbias) {
-    __shared__ __attribute__((aligned(16))) unsigned short Qt[HD * TROW];
-    __shared__ __attribute__((aligned(16))) unsigned short dOt[HD * TROW];
-    __shared__ __attribute__((aligned(16))) unsigned short Kt[HD * TROW];
-    __shared__ __attribute__((aligned(16))) unsigned short dS[NT * TROW];
-    __shared__ float tb[TBL];
-    __shared__ float lseS[NT], dlt[NT];
-    __shared__ int tokS[NT], kinf[NT];  // kinf = (row*23 + col) | region << 16
-    int b, w, h;
-    decode_block(g, b, w, h);
+    __shared__ __attribute__((aligned(16))) unsigned short Qs[NR * RS];
+    __shared__ __attribute__((aligned(16))) unsigned short dOs[NR * RS];
+    __shared__ __attribute__((aligned(16))) unsigned short Ks[NR * RS];
+    __shared__ __attribute__((aligned(16))) unsigned short Vs[NT * RS];
+    __shared__ __attribute__((aligned(16))) unsigned short dSs[NT * DSR];
+    __shared__ __attribute__((aligned(16))) float lseS[NT], dltS[NT];
+    __shared__ int tokS[NT];
+    const Chunk ck = decode_chunk(g, cw);
+    const int h = ck.h;
     const long C3 = 3 * g.C;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int l16 = lane & 15, grp = lane >> 4;
-    const long rowbase = (((long)b * g.nW + w) * g.nH + h) * NT;
-    for (int t = tid; t < NT; t += 192) {
-        int tok, reg;
-        token_info(g, w, t, b, tok, reg);
-        tokS[t] = tok;
-        kinf[t] = ((t / WS) * (2 * WS - 1) + t % WS) | (reg << 16);
-        lseS[t] = lse[rowbase + t];
+    for (int i = tid; i < (NR - NT) * RS; i += 576) {
+        Qs[NT * RS + i] = 0;
+        dOs[NT * RS + i] = 0;
+        Ks[NT * RS + i] = 0;
     }
-    for (int i = tid; i < TBL; i += 192) tb[i] = table[i * g.nH + h];
-    __syncthreads();
-    for (int e = tid; e < NT * 4; e += 192) {
-        const int t = e >> 2, ch = e & 3, tok = tokS[t];
-        const u16x8 qf = load_frag(qkv, qbias, tok, C3, h * HD + ch * 8);
-        const u16x8 kf = load_frag(qkv, qbias, tok, C3, g.C + h * HD + ch * 8);
-        u16x8 df;
-        if (tok >= 0)
-            df = *(const u16x8 *)(gout + (long)tok * g.C + h * HD + ch * 8);
-        else
-            df = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    for (int i = tid; i < NT * (DSR - NT); i += 576) dSs[(i / (DSR - NT)) * DSR + NT + i % (DSR - NT)] = 0;
+    // per-lane biases (key on the lane): key = 16 wave + l16, query = 16 qt + 4 grp + r
+    const int kkey = wave * 16 + l16;
+    unsigned bias[18];  // fp16 pairs
+    unsigned long long hb = 0, wb = 0;  // query class bits (MM == 1)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            Qt[(ch * 8 + j) * TROW + t] = qf[j];
-            Kt[(ch * 8 + j) * TROW + t] = kf[j];
-            dOt[(ch * 8 + j) * TROW + t] = df[j];
-        }
-    }
-    // delta_q = dO_q · O_q (fp32)
-    for (int t = tid; t < NT; t += 192) {
-        const int tok = tokS[t];
-        float s = 0.f;
-        if (tok >= 0) {
-            const unsigned short *dp = gout + (long)tok * g.C + h * HD;
-            const unsigned short *op = out + (long)tok * g.C + h * HD;
-            for (int d = 0; d < HD; ++d) s = fmaf(bf2f(dp[d]), bf2f(op[d]), s);
-        }
-        dlt[t] = s;
-    }
-    __syncthreads();
-    // ---------------- phase 1: key tiles 3*wave .. 3*wave+2, key on the lane
-    bf16x8_t kb[3], vb[3];
-    int ktok[3];
+    for (int qt = 0; qt < 9; ++qt)
 #pragma unroll
-    for (int j = 0; j < 3; ++j) {
-        const int ki = (wave * 3 + j) * 16 + l16;
-        ktok[j] = tokS[ki];
-        kb[j] = as_bf(load_frag(qkv, qbias, ktok[j], C3, g.C + h * HD + grp * 8));
-        vb[j] = as_bf(load_frag(qkv, qbias, ktok[j], C3, 2 * g.C + h * HD + grp * 8));
-    }
-    f32x4 dv[3][2], dk[3][2];
-#pragma unroll
-    for (int j = 0; j < 3; ++j)
-#pragma unroll
-        for (int dt = 0; dt < 2; ++dt) dv[j][dt] = dk[j][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 1
-    for (int ks = 0; ks < 5; ++ks) {
-        bf16x8_t pb[3], sb[3];
-#pragma unroll
-        for (int half = 0; half < 2; ++half) {
-            const int qt = 2 * ks + half;
-            if (qt >= 9) {
-#pragma unroll
-                for (int j = 0; j < 3; ++j)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        pb[j][4 * half + r] = (__bf16)0.f;
-                        sb[j][4 * half + r] = (__bf16)0.f;
-                    }
-                continue;
-            }
-            const int qa = qt * 16 + l16;  // A-operand row (query) for this lane
-            const int qtokA = tokS[qa];
-            const bf16x8_t qf = as_bf(load_frag(qkv, qbias, qtokA, C3, h * HD + grp * 8));
-            u16x8 dof;
-            if (qtokA >= 0)
-                dof = *(const u16x8 *)(gout + (long)qtokA * g.C + h * HD + grp * 8);
-            else
-                dof = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
-            const bf16x8_t df = as_bf(dof);
-#pragma unroll
-            for (int j = 0; j < 3; ++j) {
-                const int ki = (wave * 3 + j) * 16 + l16;
-                const int kinfo = kinf[ki];
-                const int kpos = (kinfo & 0xffff) - 264, kreg = kinfo >> 16;
-                f32x4 sa = mfma16(qf, kb[j], f32x4{0.f, 0.f, 0.f, 0.f});  // S[q][key]
-                f32x4 da = mfma16(df, vb[j], f32x4{0.f, 0.f, 0.f, 0.f});  // dP[q][key]
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int qi = qt * 16 + grp * 4 + r;
-                    const int qinfo = kinf[qi];
-                    const int ri = (qinfo & 0xffff) - kpos;
-                    float sv = sa[r] * g.scale + tb[ri];
-                    if (MM == 1) sv += ((qinfo >> 16) != kreg) ? -100.0f : 0.0f;
-                    if (MM == 2) sv += mask[((long)((b * g.nW + w) % g.n_mask) * NT + qi) * NT + ki];
-                    const float p = __expf(sv - lseS[qi]);
-                    const float ds = p * (da[r] - dlt[qi]);
-                    pb[j][4 * half + r] = (__bf16)p;
-                    sb[j][4 * half + r] = (__bf16)ds;
-                    dS[qi * TROW + ki] = f2bf(ds);
-                    if (gtable) atomicAdd(&gtable[ri * g.nH + h], ds);
-                }
+        for (int r = 0; r < 4; r += 2) {
+            const int q = qt * 16 + grp * 4 + r;
+            h2 pr;
+            pr[0] = (_Float16)(table[rel_idx(q, kkey) * g.nH + h] * LOG2E);
+            pr[1] = (_Float16)(table[rel_idx(q + 1, kkey) * g.nH + h] * LOG2E);
+            bias[qt * 2 + r / 2] = __builtin_bit_cast(unsigned, pr);
+            if (MM == 1) {
+                hb |= (unsigned long long)hi_row(g, q) << (qt * 4 + r);
+                wb |= (unsigned long long)hi_col(g, q) << (qt * 4 + r);
+                hb |= (unsigned long long)hi_row(g, q + 1) << (qt * 4 + r + 1);
+                wb |= (unsigned long long)hi_col(g, q + 1) << (qt * 4 + r + 1);
             }
         }
-        // dVᵀ += dOᵀ·P ; dKᵀ += Qᵀ·dS   (k = 32 queries, permuted order shared by A and B)
-        const int k0 = 32 * ks + 4 * grp, k1 = k0 + 16;
-        const bool second = (k1 < NT);
+    const bool k_hr = hi_row(g, kkey), k_hc = hi_col(g, kkey);
+    const float scale2 = g.scale * LOG2E;
+    const int st_t = tid >> 2, st_ch = tid & 3;
+    u16x8 qreg, oreg, dreg, kreg, vreg;
+    float lreg = 0.f;
+    int tok_next = -1;
+    auto prefetch = [&](int bw) {
+        const int tok = token_of(g, bw, st_t);
+        tok_next = tok;
+        qreg = load_frag_sel(qkv, qbias, tok, C3, h * HD + st_ch * 8);
+        kreg = load_frag_sel(qkv, qbias, tok, C3, g.C + h * HD + st_ch * 8);
+        vreg = load_frag_sel(qkv, qbias, tok, C3, 2 * g.C + h * HD + st_ch * 8);
+        // branch-free: pad tokens read token 0 and are zeroed (cropped tokens carry no gradient)
+        const long so = (long)(tok >= 0 ? tok : 0) * g.C + h * HD + st_ch * 8;
+        const u16x8 dz = *(const u16x8 *)(gout + so), oz = *(const u16x8 *)(out + so);
+        const u16x8 zero = {0, 0, 0, 0, 0, 0, 0, 0};
+        dreg = tok >= 0 ? dz : zero;
+        oreg = tok >= 0 ? oz : zero;
+        if (tid < NT) lreg = lse[((long)bw * g.nH + h) * NT + tid];
+    };
+    if (ck.w_begin < ck.w_end) prefetch(ck.w_begin);
+    const int tr_row = (l16 >> 2), tr_col = 4 * (l16 & 3);
+    for (int bw = ck.w_begin; bw < ck.w_end; ++bw) {
+        __syncthreads();
+        *(u16x8 *)(Qs + st_t * RS + st_ch * 8) = qreg;
+        *(u16x8 *)(dOs + st_t * RS + st_ch * 8) = dreg;
+        *(u16x8 *)(Ks + st_t * RS + st_ch * 8) = kreg;
+        *(u16x8 *)(Vs + st_t * RS + st_ch * 8) = vreg;
+        {
+            float part = 0.f;  // delta_q = dO_q · O_q, 4 lanes per token
 #pragma unroll
-        for (int dt = 0; dt < 2; ++dt) {
-            const int d = dt * 16 + l16;
-            u16x8 ao, aq;
-            const u16x4 o_a = *(const u16x4 *)(dOt + d * TROW + k0);
-            const u16x4 q_a = *(const u16x4 *)(Qt + d * TROW + k0);
-            u16x4 o_b = {0, 0, 0, 0}, q_b = {0, 0, 0, 0};
-            if (second) {
-                o_b = *(const u16x4 *)(dOt + d * TROW + k1);
-                q_b = *(const u16x4 *)(Qt + d * TROW + k1);
+            for (int j = 0; j < 8; ++j) part = fmaf(bf2f(dreg[j]), bf2f(oreg[j]), part);
+            part += __shfl_xor(part, 1, 64);
+            part += __shfl_xor(part, 2, 64);
+            if (st_ch == 0) {
+                dltS[st_t] = part;
+                tokS[st_t] = tok_next;
             }
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                ao[j] = o_a[j];
-                ao[4 + j] = o_b[j];
-                aq[j] = q_a[j];
-                aq[4 + j] = q_b[j];
-            }
-#pragma unroll
-            for (int j = 0; j < 3; ++j) {
-                dv[j][dt] = mfma16(as_bf(ao), pb[j], dv[j][dt]);
-                dk[j][dt] = mfma16(as_bf(aq), sb[j], dk[j][dt]);
-            }
+            if (tid < NT) lseS[tid] = lreg;
         }
-    }
-    // write dK, dV (lane: 4 consecutive channels of one key)
 #pragma unroll
-    for (int j = 0; j < 3; ++j) {
-        const int tk = ktok[j];
-#pragma unroll
-        for (int dt = 0; dt < 2; ++dt) {
-            const int c0 = h * HD + dt * 16 + grp * 4;
-            if (tk >= 0) {
-                u16x4 wk, wv;
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    wk[r] = f2bf(dk[j][dt][r] * g.scale);
-                    wv[r] = f2bf(dv[j][dt][r]);
-                }
-                *(u16x4 *)(gqkv + (long)tk * C3 + g.C + c0) = wk;
-                *(u16x4 *)(gqkv + (long)tk * C3 + 2 * g.C + c0) = wv;
-            } else if (gbias) {
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    atomicAdd(&gbias[g.C + c0 + r], dk[j][dt][r] * g.scale);
-                    atomicAdd(&gbias[2 * g.C + c0 + r], dv[j][dt][r]);
-                }
-            }
+        for (int i = 0; i < 18; ++i) asm volatile("" : "+v"(bias[i]));  // keep biases packed (no LICM unpack)
+        __syncthreads();
+        if (bw + 1 < ck.w_end) prefetch(bw + 1);
+        unsigned long long mbits = 0;
+        if (MM == 1) {
+            const int wi = bw % g.nW;
+            const bool lastH = wi / g.nWw == g.nWh - 1, lastW = wi % g.nWw == g.nWw - 1;
+            if (lastH) mbits |= k_hr ? ~hb : hb;
+            if (lastW) mbits |= k_hc ? ~wb : wb;
         }
-    }
-    __syncthreads();
-    // ---------------- phase 2: dQᵀ = Kᵀ·dSᵀ for query tiles 3*wave .. 3*wave+2
-#pragma unroll 1
-    for (int qq = 0; qq < 3; ++qq) {
-        const int qt = wave * 3 + qq;
-        const int qi = qt * 16 + l16;
-        f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+        // ---------------- phase 1: key tile = wave (key on the lane)
+        const bf16x8_t kb = as_bf(*(const u16x8 *)(Ks + kkey * RS + grp * 8));
+        const bf16x8_t vb = as_bf(*(const u16x8 *)(Vs + kkey * RS + grp * 8));
+        f32x4 dv0 = {0.f, 0.f, 0.f, 0.f}, dv1 = dv0, dk0 = dv0, dk1 = dv0;
 #pragma unroll
         for (int ks = 0; ks < 5; ++ks) {
-            const int k0 = 32 * ks + 8 * grp;
-            u16x8 bs, kt0, kt1;
-            if (k0 < NT) {
-                bs = *(const u16x8 *)(dS + qi * TROW + k0);
-                kt0 = *(const u16x8 *)(Kt + l16 * TROW + k0);
-                kt1 = *(const u16x8 *)(Kt + (16 + l16) * TROW + k0);
-            } else {
-                bs = kt0 = kt1 = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+            bf16x8_t pb, sb;
+#pragma unroll
+            for (int half = 0; half < 2; ++half) {
+                const int qt = 2 * ks + half;
+                if (qt >= 9) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        pb[4 * half + r] = (__bf16)0.f;
+                        sb[4 * half + r] = (__bf16)0.f;
+                    }
+                    continue;
+                }
+                const bf16x8_t qa = as_bf(*(const u16x8 *)(Qs + (qt * 16 + l16) * RS + grp * 8));
+                const bf16x8_t da = as_bf(*(const u16x8 *)(dOs + (qt * 16 + l16) * RS + grp * 8));
+                const f32x4 sa = mfma16(qa, kb, f32x4{0.f, 0.f, 0.f, 0.f});   // S[q][key]
+                const f32x4 dpa = mfma16(da, vb, f32x4{0.f, 0.f, 0.f, 0.f});  // dP[q][key]
+                const f32x4 l4 = *(const f32x4 *)(lseS + qt * 16 + grp * 4);
+                const f32x4 d4 = *(const f32x4 *)(dltS + qt * 16 + grp * 4);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    float v = fmaf(sa[r], scale2, (float)__builtin_bit_cast(h2, bias[qt * 2 + r / 2])[r & 1]);
+                    if (MM == 1) v += ((mbits >> (qt * 4 + r)) & 1ull) ? -100.0f * LOG2E : 0.0f;
+                    if (MM == 2)
+                        v += LOG2E * mask[((long)(bw % g.n_mask) * NT + qt * 16 + grp * 4 + r) * NT + kkey];
+                    const float p = exp2f(v - l4[r]);
+                    const float ds = p * (dpa[r] - d4[r]);
+                    pb[4 * half + r] = (__bf16)p;
+                    sb[4 * half + r] = (__bf16)ds;
+                    dSs[(qt * 16 + grp * 4 + r) * DSR + kkey] = f2bf(ds);
+                    if (EX && gtable) atomicAdd(&gtable[rel_idx(qt * 16 + grp * 4 + r, kkey) * g.nH + h], ds);
+                }
             }
-            a0 = mfma16(as_bf(kt0), as_bf(bs), a0);
-            a1 = mfma16(as_bf(kt1), as_bf(bs), a1);
+            // dVᵀ += dOᵀ·P ; dKᵀ += Qᵀ·dS   (k = 32 queries; A via transposed LDS reads)
+            const int r0 = (32 * ks + 4 * grp + tr_row) * RS + tr_col;
+            const int r1 = r0 + 16 * RS;
+            const u16x8 ao0 = cat4(tr_read(dOs + r0), tr_read(dOs + r1));
+            const u16x8 ao1 = cat4(tr_read(dOs + r0 + 16), tr_read(dOs + r1 + 16));
+            const u16x8 aq0 = cat4(tr_read(Qs + r0), tr_read(Qs + r1));
+            const u16x8 aq1 = cat4(tr_read(Qs + r0 + 16), tr_read(Qs + r1 + 16));
+            dv0 = mfma16(as_bf(ao0), pb, dv0);
+            dv1 = mfma16(as_bf(ao1), pb, dv1);
+            dk0 = mfma16(as_bf(aq0), sb, dk0);
+            dk1 = mfma16(as_bf(aq1), sb, dk1);
+            __builtin_amdgcn_sched_barrier(0);  // keep the next q pair's LDS reads from being hoisted
         }
-        const int qtok = tokS[qi];
-        const int c0 = h * HD + grp * 4;
-        if (qtok >= 0) {
-            u16x4 w0, w1;
+        {
+            const int tk = tokS[kkey];
+            const int c0 = h * HD + grp * 4;
+            if (tk >= 0) {
+                u16x4 k0, k1, v0, v1;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                w0[r] = f2bf(a0[r] * g.scale);
-                w1[r] = f2bf(a1[r] * g.scale);
+                for (int r = 0; r < 4; ++r) {
+                    k0[r] = f2bf(dk0[r] * g.scale);
+                    k1[r] = f2bf(dk1[r] * g.scale);
+                    v0[r] = f2bf(dv0[r]);
+                    v1[r] = f2bf(dv1[r]);
+                }
+                unsigned short *gp = gqkv + (long)tk * C3;
+                *(u16x4 *)(gp + g.C + c0) = k0;
+                *(u16x4 *)(gp + g.C + c0 + 16) = k1;
+                *(u16x4 *)(gp + 2 * g.C + c0) = v0;
+                *(u16x4 *)(gp + 2 * g.C + c0 + 16) = v1;
+            } else if (EX && gbias) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    atomicAdd(&gbias[g.C + c0 + r], dk0[r] * g.scale);
+                    atomicAdd(&gbias[g.C + c0 + 16 + r], dk1[r] * g.scale);
+                    atomicAdd(&gbias[2 * g.C + c0 + r], dv0[r]);
+                    atomicAdd(&gbias[2 * g.C + c0 + 16 + r], dv1[r]);
+                }
             }
-            *(u16x4 *)(gqkv + (long)qtok * C3 + c0) = w0;
-            *(u16x4 *)(gqkv + (long)qtok * C3 + c0 + 16) = w1;
-        } else if (gbias) {
+        }
+        __syncthreads();
+        // ---------------- phase 2: dQᵀ = Kᵀ·dSᵀ for query tile = wave
+        {
+            const int qq = wave * 16 + l16;
+            f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                atomicAdd(&gbias[c0 + r], a0[r] * g.scale);
-                atomicAdd(&gbias[c0 + 16 + r], a1[r] * g.scale);
+            for (int ks = 0; ks < 5; ++ks) {
+                const int k0 = 32 * ks + 8 * grp;
+                const u16x8 bs = (k0 < DSR) ? *(const u16x8 *)(dSs + qq * DSR + k0) : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+                const int r0 = (k0 + tr_row) * RS + tr_col;
+                const int r1 = r0 + 4 * RS;
+                const u16x8 ak0 = cat4(tr_read(Ks + r0), tr_read(Ks + r1));
+                const u16x8 ak1 = cat4(tr_read(Ks + r0 + 16), tr_read(Ks + r1 + 16));
+                a0 = mfma16(as_bf(ak0), as_bf(bs), a0);
+                a1 = mfma16(as_bf(ak1), as_bf(bs), a1);
+            }
+            const int qtok = tokS[qq];
+            const int c0 = h * HD + grp * 4;
+            if (qtok >= 0) {
+                u16x4 w0, w1;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    w0[r] = f2bf(a0[r] * g.scale);
+                    w1[r] = f2bf(a1[r] * g.scale);
+                }
+                *(u16x4 *)(gqkv + (long)qtok * C3 + c0) = w0;
+                *(u16x4 *)(gqkv + (long)qtok * C3 + c0 + 16) = w1;
+            } else if (EX && gbias) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    atomicAdd(&gbias[c0 + r], a0[r] * g.scale);
+                    atomicAdd(&gbias[c0 + 16 + r], a1[r] * g.scale);
+                }
             }
         }
     }
+}
+
+int chunk_windows(int total_windows, int nH) {
+    long target = 256;  // one persistent workgroup per CU
+    long cw = ((long)total_windows * nH + target - 1) / target;
+    return (int)(cw < 1 ? 1 : cw);
 }
 
 int make_geo(Geo &g, int dtype, int B, int H, int W, int C, int nH, int shift, float scale, const float *mask,
@@ -633,8 +697,10 @@ extern "C" int irads_winattn_fwd(int dtype, const void *qkv, const float *qkv_bi
     else
     {
         const int mm = mask ? 2 : (shift > 0 ? 1 : 0);
-#define IRADS_WF(M) winattn_fwd_bf16<M><<<nblk, 192, 0, st>>>((const unsigned short *)qkv, qkv_bias, rel_table, mask, \
-                                                              g, (unsigned short *)out, lse)
+        const int cw = chunk_windows(B * g.nW, nH);
+        const unsigned nwg = (unsigned)(((B * g.nW + cw - 1) / cw) * nH);
+#define IRADS_WF(M) winattn_fwd_bf16<M><<<nwg, 576, 0, st>>>((const unsigned short *)qkv, qkv_bias, rel_table, mask, \
+                                                             g, cw, (unsigned short *)out, lse)
         if (mm == 0) IRADS_WF(0); else if (mm == 1) IRADS_WF(1); else IRADS_WF(2);
 #undef IRADS_WF
     }
@@ -657,11 +723,18 @@ extern "C" int irads_winattn_bwd(int dtype, const void *qkv, const float *qkv_bi
     else
     {
         const int mm = mask ? 2 : (shift > 0 ? 1 : 0);
-#define IRADS_WB(M)                                                                                              \
-    winattn_bwd_bf16<M><<<nblk, 192, 0, st>>>((const unsigned short *)qkv, qkv_bias, rel_table, mask, g,         \
-                                              (const unsigned short *)out, lse, (const unsigned short *)grad_out, \
-                                              (unsigned short *)grad_qkv, grad_table, grad_bias_pad)
-        if (mm == 0) IRADS_WB(0); else if (mm == 1) IRADS_WB(1); else IRADS_WB(2);
+        const int cw = chunk_windows(B * g.nW, nH);
+        const unsigned nwg = (unsigned)(((B * g.nW + cw - 1) / cw) * nH);
+        const bool ex = grad_table || grad_bias_pad;
+#define IRADS_WB(M, X)                                                                                            \
+    winattn_bwd_bf16<M, X><<<nwg, 576, 0, st>>>((const unsigned short *)qkv, qkv_bias, rel_table, mask, g, cw,    \
+                                                (const unsigned short *)out, lse, (const unsigned short *)grad_out, \
+                                                (unsigned short *)grad_qkv, grad_table, grad_bias_pad)
+        if (ex) {
+            if (mm == 0) IRADS_WB(0, true); else if (mm == 1) IRADS_WB(1, true); else IRADS_WB(2, true);
+        } else {
+            if (mm == 0) IRADS_WB(0, false); else if (mm == 1) IRADS_WB(1, false); else IRADS_WB(2, false);
+        }
 #undef IRADS_WB
     }
     return check_launch("irads_winattn_bwd");

@@ -68,6 +68,16 @@ def test_window_attention_bf16_vs_fp32(shift):
     close(gbf.float(), g32, 5e-2, 5e-2, "bf16 backward")
     rel = (gbf.float() - g32).norm() / g32.norm()
     assert rel < 1e-2, f"bf16 grad relative L2 error {rel:.3e}"
+    # optional accumulators (rel-pos table, pad-token qkv bias): the EX kernel instantiation
+    b32, bbf = bias.clone().requires_grad_(), bias.clone().requires_grad_()
+    t32, tbf = table.clone().requires_grad_(), table.clone().requires_grad_()
+    o32 = ops.window_attention(qkv.float(), b32, t32, None, H, W, nH, shift, scale)
+    obf = ops.window_attention(qkv.clone(), bbf, tbf, None, H, W, nH, shift, scale)
+    gb32, gt32 = torch.autograd.grad(o32, (b32, t32), g.float())
+    gbbf, gtbf = torch.autograd.grad(obf, (bbf, tbf), g)
+    for a_, b_, what in ((gbbf, gb32, "pad qkv-bias grad"), (gtbf, gt32, "rel-table grad")):
+        err = (a_ - b_).norm() / b_.norm().clamp_min(1e-6)
+        assert err < 2e-2, f"bf16 {what} relative L2 error {err:.3e}"
 
 
 def test_window_msa_explicit_mask():
