@@ -21,6 +21,7 @@
 // fp32 path (parity / reference-precision mode): exact fp32 VALU kernels, thread per
 //   query (dQ) and thread per key (dK, dV).
 #include "common.h"
+#include <type_traits>
 
 namespace irads {
 namespace {
@@ -269,11 +270,12 @@ __device__ __forceinline__ u16x8 load_frag(const unsigned short *qkv, const floa
     return bias_frag(qbias, c0);
 }
 
-// branch-free variant for the staging loops (no divergent load / alloca selects)
-__device__ __forceinline__ u16x8 load_frag_sel(const unsigned short *qkv, const float *qbias, int tok, long C3,
+// branch-free variant for the staging loops: the pad-token value (the qkv bias, bf16)
+// is precomputed once per workgroup and selected
+__device__ __forceinline__ u16x8 load_frag_sel(const unsigned short *qkv, const u16x8 &padv, int tok, long C3,
                                                int c0) {
     const u16x8 v = *(const u16x8 *)(qkv + (long)(tok >= 0 ? tok : 0) * C3 + c0);
-    return tok >= 0 ? v : bias_frag(qbias, c0);
+    return tok >= 0 ? v : padv;
 }
 
 constexpr int RS = 40;    // LDS row stride (bf16) of the row-major tiles: 80 B
@@ -347,13 +349,16 @@ __global__ void __launch_bounds__(576) winattn_fwd_bf16(const unsigned short *__
     // staging map: thread -> (token t, 16-B chunk ch) of K and V
     const int st_t = tid >> 2, st_ch = tid & 3;
     u16x8 kreg, vreg, qreg;
+    const u16x8 kpad = bias_frag(qbias, g.C + h * HD + st_ch * 8);
+    const u16x8 vpad = bias_frag(qbias, 2 * g.C + h * HD + st_ch * 8);
+    const u16x8 qpad = bias_frag(qbias, h * HD + grp * 8);
     int qtok_next = -1;
     auto prefetch = [&](int bw) {
         const int tok = token_of(g, bw, st_t);
-        kreg = load_frag_sel(qkv, qbias, tok, C3, g.C + h * HD + st_ch * 8);
-        vreg = load_frag_sel(qkv, qbias, tok, C3, 2 * g.C + h * HD + st_ch * 8);
+        kreg = load_frag_sel(qkv, kpad, tok, C3, g.C + h * HD + st_ch * 8);
+        vreg = load_frag_sel(qkv, vpad, tok, C3, 2 * g.C + h * HD + st_ch * 8);
         qtok_next = token_of(g, bw, qi);
-        qreg = load_frag_sel(qkv, qbias, qtok_next, C3, h * HD + grp * 8);
+        qreg = load_frag_sel(qkv, qpad, qtok_next, C3, h * HD + grp * 8);
     };
     if (ck.w_begin < ck.w_end) prefetch(ck.w_begin);
     for (int bw = ck.w_begin; bw < ck.w_end; ++bw) {
@@ -366,15 +371,7 @@ __global__ void __launch_bounds__(576) winattn_fwd_bf16(const unsigned short *__
         for (int i = 0; i < 18; ++i) asm volatile("" : "+v"(bias[i]));  // keep biases packed (no LICM unpack)
         __syncthreads();
         if (bw + 1 < ck.w_end) prefetch(bw + 1);
-        unsigned long long mbits = 0;
-        if (MM == 1) {
-            const int wi = bw % g.nW;
-            const bool lastH = wi / g.nWw == g.nWh - 1, lastW = wi % g.nWw == g.nWw - 1;
-            if (lastH) mbits |= q_hr ? ~hb : hb;
-            if (lastW) mbits |= q_hc ? ~wb : wb;
-        }
         f32x4 s[9];
-        float mx = -INFINITY;
 #pragma unroll
         for (int kt = 0; kt < 9; ++kt) {
             const bf16x8_t kf = as_bf(*(const u16x8 *)(Ks + (kt * 16 + l16) * RS + grp * 8));
@@ -382,13 +379,30 @@ __global__ void __launch_bounds__(576) winattn_fwd_bf16(const unsigned short *__
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 float v = fmaf(s[kt][r], scale2, (float)__builtin_bit_cast(h2, bias[kt * 2 + r / 2])[r & 1]);
-                if (MM == 1) v += ((mbits >> (kt * 4 + r)) & 1ull) ? -100.0f * LOG2E : 0.0f;
                 if (MM == 2)
                     v += LOG2E * mask[((long)(bw % g.n_mask) * NT + qi) * NT + kt * 16 + grp * 4 + r];
                 s[kt][r] = v;
-                mx = fmaxf(mx, v);
             }
         }
+        if (MM == 1) {  // only windows on the last row / column of the shifted grid carry a mask (uniform branch)
+            const int wi = bw % g.nW;
+            const bool lastH = wi / g.nWw == g.nWh - 1, lastW = wi % g.nWw == g.nWw - 1;
+            if (lastH || lastW) {
+                unsigned long long mbits = 0;
+                if (lastH) mbits |= q_hr ? ~hb : hb;
+                if (lastW) mbits |= q_hc ? ~wb : wb;
+#pragma unroll
+                for (int kt = 0; kt < 9; ++kt)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        s[kt][r] += ((mbits >> (kt * 4 + r)) & 1ull) ? -100.0f * LOG2E : 0.0f;
+            }
+        }
+        float mx = -INFINITY;
+#pragma unroll
+        for (int kt = 0; kt < 9; ++kt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) mx = fmaxf(mx, s[kt][r]);
         mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
         mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
         float sum = 0.f;
@@ -396,7 +410,7 @@ __global__ void __launch_bounds__(576) winattn_fwd_bf16(const unsigned short *__
         for (int kt = 0; kt < 9; ++kt)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const float p = exp2f(s[kt][r] - mx);
+                const float p = fast_exp2(s[kt][r] - mx);
                 s[kt][r] = p;
                 sum += p;
             }
@@ -486,14 +500,18 @@ __global__ void __launch_bounds__(576) winattn_bwd_bf16(
     const float scale2 = g.scale * LOG2E;
     const int st_t = tid >> 2, st_ch = tid & 3;
     u16x8 qreg, oreg, dreg, kreg, vreg;
+    __shared__ __attribute__((aligned(16))) unsigned short padS[3 * HD];  // pad-token q, k, v (bf16)
+    if (tid < 3 * HD) padS[tid] = qbias ? f2bf(qbias[(tid / HD) * g.C + h * HD + tid % HD]) : (unsigned short)0;
+    __syncthreads();
     float lreg = 0.f;
     int tok_next = -1;
     auto prefetch = [&](int bw) {
         const int tok = token_of(g, bw, st_t);
         tok_next = tok;
-        qreg = load_frag_sel(qkv, qbias, tok, C3, h * HD + st_ch * 8);
-        kreg = load_frag_sel(qkv, qbias, tok, C3, g.C + h * HD + st_ch * 8);
-        vreg = load_frag_sel(qkv, qbias, tok, C3, 2 * g.C + h * HD + st_ch * 8);
+        qreg = load_frag_sel(qkv, *(const u16x8 *)(padS + st_ch * 8), tok, C3, h * HD + st_ch * 8);
+        kreg = load_frag_sel(qkv, *(const u16x8 *)(padS + HD + st_ch * 8), tok, C3, g.C + h * HD + st_ch * 8);
+        vreg = load_frag_sel(qkv, *(const u16x8 *)(padS + 2 * HD + st_ch * 8), tok, C3,
+                             2 * g.C + h * HD + st_ch * 8);
         // branch-free: pad tokens read token 0 and are zeroed (cropped tokens carry no gradient)
         const long so = (long)(tok >= 0 ? tok : 0) * g.C + h * HD + st_ch * 8;
         const u16x8 dz = *(const u16x8 *)(gout + so), oz = *(const u16x8 *)(out + so);
@@ -527,9 +545,11 @@ __global__ void __launch_bounds__(576) winattn_bwd_bf16(
         __syncthreads();
         if (bw + 1 < ck.w_end) prefetch(bw + 1);
         unsigned long long mbits = 0;
+        bool edge = false;  // uniform: window on the last row / column of the shifted grid
         if (MM == 1) {
             const int wi = bw % g.nW;
             const bool lastH = wi / g.nWw == g.nWh - 1, lastW = wi % g.nWw == g.nWw - 1;
+            edge = lastH || lastW;
             if (lastH) mbits |= k_hr ? ~hb : hb;
             if (lastW) mbits |= k_hc ? ~wb : wb;
         }
@@ -537,6 +557,9 @@ __global__ void __launch_bounds__(576) winattn_bwd_bf16(
         const bf16x8_t kb = as_bf(*(const u16x8 *)(Ks + kkey * RS + grp * 8));
         const bf16x8_t vb = as_bf(*(const u16x8 *)(Vs + kkey * RS + grp * 8));
         f32x4 dv0 = {0.f, 0.f, 0.f, 0.f}, dv1 = dv0, dk0 = dv0, dk1 = dv0;
+        // two copies of the phase, picked by a uniform branch, so interior windows skip the mask test
+        auto phase1 = [&](auto masked) {
+        constexpr bool MASKED = decltype(masked)::value;
 #pragma unroll
         for (int ks = 0; ks < 5; ++ks) {
             bf16x8_t pb, sb;
@@ -560,14 +583,14 @@ __global__ void __launch_bounds__(576) winattn_bwd_bf16(
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     float v = fmaf(sa[r], scale2, (float)__builtin_bit_cast(h2, bias[qt * 2 + r / 2])[r & 1]);
-                    if (MM == 1) v += ((mbits >> (qt * 4 + r)) & 1ull) ? -100.0f * LOG2E : 0.0f;
+                    if (MASKED) v += ((mbits >> (qt * 4 + r)) & 1ull) ? -100.0f * LOG2E : 0.0f;
                     if (MM == 2)
                         v += LOG2E * mask[((long)(bw % g.n_mask) * NT + qt * 16 + grp * 4 + r) * NT + kkey];
-                    const float p = exp2f(v - l4[r]);
+                    const float p = fast_exp2(v - l4[r]);
                     const float ds = p * (dpa[r] - d4[r]);
                     pb[4 * half + r] = (__bf16)p;
                     sb[4 * half + r] = (__bf16)ds;
-                    dSs[(qt * 16 + grp * 4 + r) * DSR + kkey] = f2bf(ds);
+                    dSs[(qt * 16 + grp * 4 + r) * DSR + kkey] = __builtin_bit_cast(unsigned short, sb[4 * half + r]);
                     if (EX && gtable) atomicAdd(&gtable[rel_idx(qt * 16 + grp * 4 + r, kkey) * g.nH + h], ds);
                 }
             }
@@ -584,6 +607,11 @@ __global__ void __launch_bounds__(576) winattn_bwd_bf16(
             dk1 = mfma16(as_bf(aq1), sb, dk1);
             __builtin_amdgcn_sched_barrier(0);  // keep the next q pair's LDS reads from being hoisted
         }
+        };
+        if (MM == 1 && edge)
+            phase1(std::true_type{});
+        else
+            phase1(std::false_type{});
         {
             const int tk = tokS[kkey];
             const int c0 = h * HD + grp * 4;
