@@ -91,7 +91,6 @@ def cpu_baseline(args):
     golden fixtures) doing the same training step on a bounded sample."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import irads_ref as R
-    from semseg.losses import get_loss, mmst_loss
     from semseg.optimizers import adapter_trainable
     threads = min(16, os.cpu_count() or 1)
     torch.set_num_threads(threads)
@@ -101,7 +100,6 @@ def cpu_baseline(args):
     for n, p in model.named_parameters():
         p.requires_grad_(adapter_trainable(n))
     opt = torch.optim.AdamW(params, 4e-4, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01)
-    loss_fn = get_loss("CrossEntropy", 255)
     model.train()
     B = args.cpu_batch
     rgb, dep, lbl = synthetic_batch(B, args.size, "cpu", 3407)
@@ -110,7 +108,7 @@ def cpu_baseline(args):
     def step():
         opt.zero_grad(set_to_none=True)
         y, yr, yd = model([batch[0], batch[1]])
-        mmst_loss(loss_fn, y, yr, yd, batch[2]).backward()
+        R.mmst_loss(y, yr, yd, batch[2]).backward()
         opt.step()
     step()  # warmup
     t0 = time.perf_counter()

@@ -135,6 +135,35 @@ int irads_sb_logits(int dtype, const void *x, const void *r, const void *S_log_d
                     const void *log_alpha_raw, double epsilon, int rows, int D, int K, void *logits,
                     void *log_C, void *stream);
 
+/* ------------------------------------------------------------------ segmentation head tail
+ * Bilinear resize, align_corners=False, explicit output size: the F.interpolate calls of
+ * SegFormerHead.forward (semseg/models/heads/segformer.py:44) and CMNeXt.forward
+ * (semseg/models/cmnext.py:30-32).  Tensors are logical (B, C, h, w) -> (B, C, H, W); strides
+ * are element strides and must describe NCHW- or channels-last-contiguous storage, the same
+ * for input and output.  fp32 or bf16 (dtype). */
+int irads_resize_fwd(int dtype, const void *in, const int64_t *in_strides, int B, int C, int h, int w,
+                     void *out, const int64_t *out_strides, int H, int W, void *stream);
+/* adjoint of the above: grad_in (B, C, h, w) from grad_out (B, C, H, W), written (not
+ * accumulated).  workspace: B*C*h*W floats. */
+int irads_resize_bwd(int dtype, const void *grad_out, const int64_t *go_strides, int B, int C, int H, int W,
+                     void *grad_in, const int64_t *gi_strides, int h, int w, float *workspace, void *stream);
+
+/* Softmax cross-entropy, mean over pixels whose target != ignore_index (nn.CrossEntropyLoss
+ * as wrapped by semseg/losses.py:6-19; class_weight may be NULL).  logits (B, C, H, W),
+ * C <= 128, NCHW- or channels-last-contiguous; target int64 (B, H, W).  Writes lse (B*H*W
+ * fp32, for the backward), loss[0] = the mean, loss[1] = the weight sum.  If match_target is
+ * not NULL it receives the MMST target of train_mm.py:137-141: target where
+ * argmax_c(logits) == target, ignore_index elsewhere.  workspace: IRADS_CE_WORKSPACE doubles.
+ * Targets outside [0, C) other than ignore_index are treated as ignored. */
+#define IRADS_CE_WORKSPACE 2048
+int irads_ce_fwd(int dtype, const void *logits, const int64_t *strides, int B, int C, int H, int W,
+                 const int64_t *target, int ignore_index, const float *class_weight, float *lse,
+                 int64_t *match_target, double *workspace, float *loss, void *stream);
+/* grad_logits (same shape and strides as logits) = grad_loss[0] * w_t (softmax - onehot) / loss[1] */
+int irads_ce_bwd(int dtype, const void *logits, const int64_t *strides, int B, int C, int H, int W,
+                 const int64_t *target, int ignore_index, const float *class_weight, const float *lse,
+                 const float *loss, const float *grad_loss, void *grad_logits, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,406 @@
+// Segmentation-head tail of the training step, gfx950.
+//
+//   resize   : bilinear resize, align_corners=False, explicit output size — the
+//              F.interpolate calls of SegFormerHead.forward (segformer.py:44) and
+//              CMNeXt.forward (cmnext.py:30-32).  Forward = 4-tap gather per output
+//              element.  Backward = the adjoint as two separable gather passes (rows,
+//              then columns) with an fp32 intermediate, no atomics.
+//   ce       : softmax cross-entropy with ignore_index and optional class weights, mean
+//              over the kept pixels — nn.CrossEntropyLoss as wrapped by
+//              semseg/losses.py:6-19.  One pass over the logits per pixel (the class
+//              row is held in registers), per-pixel log-sum-exp saved for the
+//              backward, deterministic two-level reduction (fixed grid, fp64 partials).
+//              Optionally emits the MMST target of train_mm.py:137-141 (the label where
+//              the arg-max prediction is right, ignore elsewhere) from the same pass.
+//
+// Both ops run on the two dense layouts the head produces: NCHW-contiguous and
+// channels-last-contiguous (the `permute(0, 2, 1).reshape(...)` views of
+// segformer.py:41-43 are channels-last).  All are HBM-bound streaming kernels.
+#include "common.h"
+
+namespace irads {
+namespace {
+
+typedef __attribute__((ext_vector_type(4))) float f4;
+
+template <typename T> __device__ __forceinline__ float ldf(const T *p, long i);
+template <> __device__ __forceinline__ float ldf<float>(const float *p, long i) { return p[i]; }
+template <> __device__ __forceinline__ float ldf<unsigned short>(const unsigned short *p, long i) {
+    return bf2f(p[i]);
+}
+template <typename T> __device__ __forceinline__ void stf(T *p, long i, float v);
+template <> __device__ __forceinline__ void stf<float>(float *p, long i, float v) { p[i] = v; }
+template <> __device__ __forceinline__ void stf<unsigned short>(unsigned short *p, long i, float v) {
+    p[i] = f2bf(v);
+}
+
+// Source coordinate of output index d (PyTorch area_pixel_compute_source_index, not
+// cubic, align_corners=False): src = max(scale·(d + 0.5) − 0.5, 0), scale = in/out.
+struct Tap {
+    int i0, i1;
+    float l0, l1;
+};
+__device__ __forceinline__ Tap tap_of(int d, float scale, int n_in) {
+    float src = scale * ((float)d + 0.5f) - 0.5f;
+    src = src < 0.f ? 0.f : src;
+    Tap t;
+    t.i0 = (int)src;
+    t.i1 = t.i0 + (t.i0 < n_in - 1 ? 1 : 0);
+    t.l1 = src - (float)t.i0;
+    t.l0 = 1.f - t.l1;
+    return t;
+}
+// weight with which output index d reads input index i
+__device__ __forceinline__ float tap_weight(const Tap &t, int i) {
+    return (t.i0 == i ? t.l0 : 0.f) + (t.i1 == i ? t.l1 : 0.f);
+}
+// output indices whose taps can reach input index i: a superset, filtered by tap_weight
+__device__ __forceinline__ void reach(int i, float inv_scale, int n_out, int &lo, int &hi) {
+    lo = (int)floorf(((float)i - 0.5f) * inv_scale - 0.5f) - 2;
+    hi = (int)ceilf(((float)i + 1.5f) * inv_scale - 0.5f) + 2;
+    lo = lo < 0 ? 0 : lo;
+    hi = hi > n_out - 1 ? n_out - 1 : hi;
+}
+
+struct Dims {
+    int B, C, H, W;  // logical (B, C, H, W)
+};
+// element offset of (b, c, y, x) in a dense NCHW or channels-last tensor
+template <bool CL> __device__ __forceinline__ long offs(const Dims &d, int b, int c, int y, int x) {
+    if (CL) return (((long)b * d.H + y) * d.W + x) * d.C + c;
+    return (((long)b * d.C + c) * d.H + y) * d.W + x;
+}
+
+// Launch geometry of the element-wise kernels: a workgroup covers 256 consecutive
+// elements of one "line" — an (H, W) plane for NCHW, a (W, C) pixel row for
+// channels-last — so the line coordinates come from one scalar division per workgroup
+// and the position inside the line from one 32-bit division per thread.
+struct Walk {
+    int b, c, y, x;
+    long e;  // linear element index (memory order)
+    bool ok;
+};
+template <bool CL> __device__ __forceinline__ Walk walk(const Dims &d) {
+    const int inner = CL ? d.W * d.C : d.H * d.W;
+    const int chunks = (inner + 255) / 256;
+    const int line = blockIdx.x / chunks;  // scalar
+    const int r = (blockIdx.x - line * chunks) * 256 + threadIdx.x;
+    Walk w;
+    w.ok = r < inner;
+    w.e = (long)line * inner + r;
+    if (CL) {
+        w.b = line / d.H;
+        w.y = line - w.b * d.H;
+        w.x = r / d.C;
+        w.c = r - w.x * d.C;
+    } else {
+        w.b = line / d.C;
+        w.c = line - w.b * d.C;
+        w.y = r / d.W;
+        w.x = r - w.y * d.W;
+    }
+    return w;
+}
+template <bool CL> static int walk_grid(const Dims &d) {
+    const long inner = CL ? (long)d.W * d.C : (long)d.H * d.W;
+    const long lines = CL ? (long)d.B * d.H : (long)d.B * d.C;
+    return (int)(lines * ((inner + 255) / 256));
+}
+
+// ------------------------------------------------------------------ resize forward
+template <typename T, bool CL>
+__global__ void __launch_bounds__(256) resize_fwd(const T *__restrict__ in, Dims di, T *__restrict__ out, Dims dout,
+                                                  float sh, float sw) {
+    const Walk w = walk<CL>(dout);
+    if (!w.ok) return;
+    const Tap ty = tap_of(w.y, sh, di.H), tx = tap_of(w.x, sw, di.W);
+    const float v00 = ldf(in, offs<CL>(di, w.b, w.c, ty.i0, tx.i0));
+    const float v01 = ldf(in, offs<CL>(di, w.b, w.c, ty.i0, tx.i1));
+    const float v10 = ldf(in, offs<CL>(di, w.b, w.c, ty.i1, tx.i0));
+    const float v11 = ldf(in, offs<CL>(di, w.b, w.c, ty.i1, tx.i1));
+    // upsample_bilinear2d_out_frame's expression and order
+    stf(out, w.e, ty.l0 * (tx.l0 * v00 + tx.l1 * v01) + ty.l1 * (tx.l0 * v10 + tx.l1 * v11));
+}
+
+// ------------------------------------------------------------------ resize backward
+// pass A (rows): tmp[b, c, i, x] = Σ_y wy(y→i) · g[b, c, y, x]      tmp: fp32 (B, C, h, W)
+template <typename T, bool CL>
+__global__ void __launch_bounds__(256) resize_bwd_rows(const T *__restrict__ g, Dims dg, float *__restrict__ tmp,
+                                                       Dims dt, float sh, float inv_sh) {
+    const Walk w = walk<CL>(dt);
+    if (!w.ok) return;
+    int lo, hi;
+    reach(w.y, inv_sh, dg.H, lo, hi);
+    float acc = 0.f;
+    for (int y = lo; y <= hi; ++y) {
+        const float wt = tap_weight(tap_of(y, sh, dt.H), w.y);
+        if (wt != 0.f) acc = fmaf(wt, ldf(g, offs<CL>(dg, w.b, w.c, y, w.x)), acc);
+    }
+    tmp[w.e] = acc;
+}
+// pass B (columns): gin[b, c, i, j] = Σ_x wx(x→j) · tmp[b, c, i, x]
+template <typename T, bool CL>
+__global__ void __launch_bounds__(256) resize_bwd_cols(const float *__restrict__ tmp, Dims dt, T *__restrict__ gin,
+                                                       Dims di, float sw, float inv_sw) {
+    const Walk w = walk<CL>(di);
+    if (!w.ok) return;
+    int lo, hi;
+    reach(w.x, inv_sw, dt.W, lo, hi);
+    float acc = 0.f;
+    for (int x = lo; x <= hi; ++x) {
+        const float wt = tap_weight(tap_of(x, sw, di.W), w.x);
+        if (wt != 0.f) acc = fmaf(wt, tmp[offs<CL>(dt, w.b, w.c, w.y, x)], acc);
+    }
+    stf(gin, w.e, acc);
+}
+
+// ------------------------------------------------------------------ cross-entropy
+constexpr int CE_GRID = 1024;  // fixed grid: deterministic partial sums (IRADS_CE_WORKSPACE)
+
+__device__ __forceinline__ double block_sum_d(double v, double *red) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    __syncthreads();
+    if (lane == 0) red[wave] = v;
+    __syncthreads();
+    double s = 0.0;
+    for (int k = 0; k < (int)(blockDim.x >> 6); ++k) s += red[k];
+    return s;
+}
+
+// one thread per pixel; the class row is held in registers (C <= CMAX)
+template <typename T, bool CL, int CMAX>
+__global__ void __launch_bounds__(256) ce_fwd(const T *__restrict__ x, Dims d, const int64_t *__restrict__ tgt,
+                                              int ignore, const float *__restrict__ cw, float *__restrict__ lse,
+                                              int64_t *__restrict__ match, double *__restrict__ part) {
+    __shared__ double red[4];
+    const long npix = (long)d.B * d.H * d.W, hw = (long)d.H * d.W;
+    float s_loss = 0.f, s_w = 0.f;
+    for (long p = blockIdx.x * 256L + threadIdx.x; p < npix; p += (long)gridDim.x * 256) {
+        const long b = p / hw, q = p % hw;
+        const long base = CL ? p * d.C : b * d.C * hw + q;
+        const long cs = CL ? 1 : hw;
+        float z[CMAX];
+        float m = -INFINITY;
+        int am = 0;
+#pragma unroll
+        for (int c = 0; c < CMAX; ++c) {
+            if (c < d.C) {
+                z[c] = ldf(x, base + c * cs);
+                if (z[c] > m) {  // first maximum, as argmax
+                    m = z[c];
+                    am = c;
+                }
+            }
+        }
+        float s = 0.f;
+#pragma unroll
+        for (int c = 0; c < CMAX; ++c)
+            if (c < d.C) s += expf(z[c] - m);
+        const float l = m + logf(s);
+        lse[p] = l;
+        const long t = tgt[p];
+        const bool keep = t != ignore && t >= 0 && t < d.C;
+        if (keep) {
+            float zt = 0.f;
+#pragma unroll
+            for (int c = 0; c < CMAX; ++c)
+                if (c == t) zt = z[c];
+            const float w = cw ? cw[t] : 1.f;
+            s_loss += w * (l - zt);
+            s_w += w;
+        }
+        if (match) match[p] = (keep && am == t) ? t : (int64_t)ignore;
+    }
+    const double a = block_sum_d((double)s_loss, red);
+    const double bsum = block_sum_d((double)s_w, red);
+    if (threadIdx.x == 0) {
+        part[2 * blockIdx.x] = a;
+        part[2 * blockIdx.x + 1] = bsum;
+    }
+}
+
+// loss[0] = Σ w·nll / Σ w, loss[1] = Σ w (fixed-order tree over the CE_GRID partials)
+__global__ void __launch_bounds__(1024) ce_finalize(const double *__restrict__ part, int nblk,
+                                                    float *__restrict__ loss) {
+    __shared__ double sa[1024], sb[1024];
+    const int t = threadIdx.x;
+    sa[t] = t < nblk ? part[2 * t] : 0.0;
+    sb[t] = t < nblk ? part[2 * t + 1] : 0.0;
+    __syncthreads();
+    for (int o = 512; o > 0; o >>= 1) {
+        if (t < o) {
+            sa[t] += sa[t + o];
+            sb[t] += sb[t + o];
+        }
+        __syncthreads();
+    }
+    if (t == 0) {
+        loss[0] = (float)(sa[0] / sb[0]);  // 0/0 = nan when every pixel is ignored, as PyTorch
+        loss[1] = (float)sb[0];
+    }
+}
+
+// grad[b, c, y, x] = g · w_t · (softmax_c − [c == t]) / Σw, zero at ignored pixels;
+// one thread per logit element in memory order
+template <typename T, bool CL>
+__global__ void __launch_bounds__(256) ce_bwd(const T *__restrict__ x, Dims d, const int64_t *__restrict__ tgt,
+                                              int ignore, const float *__restrict__ cw,
+                                              const float *__restrict__ lse, const float *__restrict__ loss,
+                                              const float *__restrict__ gloss, T *__restrict__ gx) {
+    const Walk w = walk<CL>(d);
+    if (!w.ok) return;
+    const float gs = gloss[0] / loss[1];
+    const long p = ((long)w.b * d.H + w.y) * d.W + w.x;
+    const long t = tgt[p];
+    float gv = 0.f;
+    if (t != ignore && t >= 0 && t < d.C) {
+        const float wt = cw ? cw[t] : 1.f;
+        gv = gs * wt * (expf(ldf(x, w.e) - lse[p]) - (w.c == t ? 1.f : 0.f));
+    }
+    stf(gx, w.e, gv);
+}
+
+// 0 = NCHW-contiguous, 1 = channels-last-contiguous, -1 = neither
+int layout_of(const int64_t *s, int B, int C, int H, int W) {
+    (void)B;
+    if (s[3] == 1 && s[2] == W && s[1] == (int64_t)H * W && s[0] == (int64_t)C * H * W) return 0;
+    if (s[1] == 1 && s[3] == C && s[2] == (int64_t)W * C && s[0] == (int64_t)H * W * C) return 1;
+    if (C == 1 || (H == 1 && W == 1)) return 0;  // degenerate: both layouts coincide
+    return -1;
+}
+
+}  // namespace
+}  // namespace irads
+
+using namespace irads;
+
+static bool small_enough(long n) { return n < (1L << 31); }
+
+extern "C" int irads_resize_fwd(int dtype, const void *in, const int64_t *in_strides, int B, int C, int h, int w,
+                                void *out, const int64_t *out_strides, int H, int W, void *stream) {
+    IRADS_REQUIRE(dtype == IRADS_F32 || dtype == IRADS_BF16, "resize: dtype must be float32 or bfloat16");
+    IRADS_REQUIRE(B >= 0 && C > 0 && h > 0 && w > 0 && H > 0 && W > 0, "resize: bad sizes");
+    IRADS_REQUIRE(small_enough((long)B * C * H * W) && small_enough((long)B * C * h * w), "resize: tensor too large");
+    const int li = layout_of(in_strides, B, C, h, w), lo = layout_of(out_strides, B, C, H, W);
+    IRADS_REQUIRE(li >= 0 && lo >= 0, "resize: tensors must be NCHW- or channels-last-contiguous");
+    IRADS_REQUIRE(li == lo || C == 1, "resize: input and output must share the memory format");
+    const bool cl = li == 1 && C > 1;
+    if (B == 0) return IRADS_OK;
+    hipStream_t st = (hipStream_t)stream;
+    const Dims di{B, C, h, w}, dout{B, C, H, W};
+    const float sh = (float)h / (float)H, sw = (float)w / (float)W;  // area_pixel_compute_scale
+    const int grid = cl ? walk_grid<true>(dout) : walk_grid<false>(dout);
+    if (dtype == IRADS_F32) {
+        if (cl) resize_fwd<float, true><<<grid, 256, 0, st>>>((const float *)in, di, (float *)out, dout, sh, sw);
+        else resize_fwd<float, false><<<grid, 256, 0, st>>>((const float *)in, di, (float *)out, dout, sh, sw);
+    } else {
+        using U = unsigned short;
+        if (cl) resize_fwd<U, true><<<grid, 256, 0, st>>>((const U *)in, di, (U *)out, dout, sh, sw);
+        else resize_fwd<U, false><<<grid, 256, 0, st>>>((const U *)in, di, (U *)out, dout, sh, sw);
+    }
+    return check_launch("irads_resize_fwd");
+}
+
+extern "C" int irads_resize_bwd(int dtype, const void *grad_out, const int64_t *go_strides, int B, int C, int H,
+                                int W, void *grad_in, const int64_t *gi_strides, int h, int w, float *workspace,
+                                void *stream) {
+    IRADS_REQUIRE(dtype == IRADS_F32 || dtype == IRADS_BF16, "resize: dtype must be float32 or bfloat16");
+    IRADS_REQUIRE(B >= 0 && C > 0 && h > 0 && w > 0 && H > 0 && W > 0, "resize: bad sizes");
+    IRADS_REQUIRE(small_enough((long)B * C * H * W) && small_enough((long)B * C * h * W), "resize: tensor too large");
+    const int lo = layout_of(go_strides, B, C, H, W), li = layout_of(gi_strides, B, C, h, w);
+    IRADS_REQUIRE(li >= 0 && lo >= 0, "resize: tensors must be NCHW- or channels-last-contiguous");
+    IRADS_REQUIRE(li == lo || C == 1, "resize: grad_out and grad_in must share the memory format");
+    IRADS_REQUIRE(workspace != nullptr, "resize: workspace (B*C*h*W floats) required");
+    const bool cl = li == 1 && C > 1;
+    if (B == 0) return IRADS_OK;
+    hipStream_t st = (hipStream_t)stream;
+    const Dims dg{B, C, H, W}, dt{B, C, h, W}, di{B, C, h, w};
+    const float sh = (float)h / (float)H, sw = (float)w / (float)W;
+    const float ish = (float)H / (float)h, isw = (float)W / (float)w;
+    int grid = cl ? walk_grid<true>(dt) : walk_grid<false>(dt);
+    using U = unsigned short;
+    if (dtype == IRADS_F32) {
+        if (cl) resize_bwd_rows<float, true><<<grid, 256, 0, st>>>((const float *)grad_out, dg, workspace, dt, sh, ish);
+        else resize_bwd_rows<float, false><<<grid, 256, 0, st>>>((const float *)grad_out, dg, workspace, dt, sh, ish);
+    } else {
+        if (cl) resize_bwd_rows<U, true><<<grid, 256, 0, st>>>((const U *)grad_out, dg, workspace, dt, sh, ish);
+        else resize_bwd_rows<U, false><<<grid, 256, 0, st>>>((const U *)grad_out, dg, workspace, dt, sh, ish);
+    }
+    grid = cl ? walk_grid<true>(di) : walk_grid<false>(di);
+    if (dtype == IRADS_F32) {
+        if (cl) resize_bwd_cols<float, true><<<grid, 256, 0, st>>>(workspace, dt, (float *)grad_in, di, sw, isw);
+        else resize_bwd_cols<float, false><<<grid, 256, 0, st>>>(workspace, dt, (float *)grad_in, di, sw, isw);
+    } else {
+        if (cl) resize_bwd_cols<U, true><<<grid, 256, 0, st>>>(workspace, dt, (U *)grad_in, di, sw, isw);
+        else resize_bwd_cols<U, false><<<grid, 256, 0, st>>>(workspace, dt, (U *)grad_in, di, sw, isw);
+    }
+    return check_launch("irads_resize_bwd");
+}
+
+template <typename T, bool CL>
+static void launch_ce_fwd(int C, hipStream_t st, const void *x, Dims d, const int64_t *tgt, int ignore,
+                          const float *cw, float *lse, int64_t *match, double *part) {
+    const T *xp = (const T *)x;
+    if (C <= 16) ce_fwd<T, CL, 16><<<CE_GRID, 256, 0, st>>>(xp, d, tgt, ignore, cw, lse, match, part);
+    else if (C <= 32) ce_fwd<T, CL, 32><<<CE_GRID, 256, 0, st>>>(xp, d, tgt, ignore, cw, lse, match, part);
+    else if (C <= 64) ce_fwd<T, CL, 64><<<CE_GRID, 256, 0, st>>>(xp, d, tgt, ignore, cw, lse, match, part);
+    else ce_fwd<T, CL, 128><<<CE_GRID, 256, 0, st>>>(xp, d, tgt, ignore, cw, lse, match, part);
+}
+
+extern "C" int irads_ce_fwd(int dtype, const void *logits, const int64_t *strides, int B, int C, int H, int W,
+                            const int64_t *target, int ignore_index, const float *class_weight, float *lse,
+                            int64_t *match_target, double *workspace, float *loss, void *stream) {
+    IRADS_REQUIRE(dtype == IRADS_F32 || dtype == IRADS_BF16, "cross_entropy: dtype must be float32 or bfloat16");
+    IRADS_REQUIRE(B > 0 && C > 0 && H > 0 && W > 0, "cross_entropy: bad sizes");
+    IRADS_REQUIRE(C <= 128, "cross_entropy: at most 128 classes (got %d)", C);
+    IRADS_REQUIRE(small_enough((long)B * C * H * W), "cross_entropy: tensor too large");
+    const int lay = layout_of(strides, B, C, H, W);
+    IRADS_REQUIRE(lay >= 0, "cross_entropy: logits must be NCHW- or channels-last-contiguous");
+    IRADS_REQUIRE(workspace && loss && lse && target, "cross_entropy: null buffer");
+    hipStream_t st = (hipStream_t)stream;
+    const Dims d{B, C, H, W};
+    const bool cl = lay == 1;
+    using U = unsigned short;
+    if (dtype == IRADS_F32) {
+        if (cl) launch_ce_fwd<float, true>(C, st, logits, d, target, ignore_index, class_weight, lse, match_target, workspace);
+        else launch_ce_fwd<float, false>(C, st, logits, d, target, ignore_index, class_weight, lse, match_target, workspace);
+    } else {
+        if (cl) launch_ce_fwd<U, true>(C, st, logits, d, target, ignore_index, class_weight, lse, match_target, workspace);
+        else launch_ce_fwd<U, false>(C, st, logits, d, target, ignore_index, class_weight, lse, match_target, workspace);
+    }
+    ce_finalize<<<1, 1024, 0, st>>>(workspace, CE_GRID, loss);
+    return check_launch("irads_ce_fwd");
+}
+
+extern "C" int irads_ce_bwd(int dtype, const void *logits, const int64_t *strides, int B, int C, int H, int W,
+                            const int64_t *target, int ignore_index, const float *class_weight, const float *lse,
+                            const float *loss, const float *grad_loss, void *grad_logits, void *stream) {
+    IRADS_REQUIRE(dtype == IRADS_F32 || dtype == IRADS_BF16, "cross_entropy: dtype must be float32 or bfloat16");
+    IRADS_REQUIRE(B > 0 && C > 0 && H > 0 && W > 0, "cross_entropy: bad sizes");
+    IRADS_REQUIRE(small_enough((long)B * C * H * W), "cross_entropy: tensor too large");
+    const int lay = layout_of(strides, B, C, H, W);
+    IRADS_REQUIRE(lay >= 0, "cross_entropy: logits must be NCHW- or channels-last-contiguous");
+    hipStream_t st = (hipStream_t)stream;
+    const Dims d{B, C, H, W};
+    const bool cl = lay == 1;
+    const int grid = cl ? walk_grid<true>(d) : walk_grid<false>(d);
+    using U = unsigned short;
+    if (dtype == IRADS_F32) {
+        if (cl)
+            ce_bwd<float, true><<<grid, 256, 0, st>>>((const float *)logits, d, target, ignore_index, class_weight,
+                                                      lse, loss, grad_loss, (float *)grad_logits);
+        else
+            ce_bwd<float, false><<<grid, 256, 0, st>>>((const float *)logits, d, target, ignore_index, class_weight,
+                                                       lse, loss, grad_loss, (float *)grad_logits);
+    } else {
+        if (cl)
+            ce_bwd<U, true><<<grid, 256, 0, st>>>((const U *)logits, d, target, ignore_index, class_weight, lse, loss,
+                                                  grad_loss, (U *)grad_logits);
+        else
+            ce_bwd<U, false><<<grid, 256, 0, st>>>((const U *)logits, d, target, ignore_index, class_weight, lse, loss,
+                                                   grad_loss, (U *)grad_logits);
+    }
+    return check_launch("irads_ce_bwd");
+}

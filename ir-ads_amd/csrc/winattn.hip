@@ -258,6 +258,14 @@ __device__ __forceinline__ u16x8 cat4(u16x4 a, u16x4 b) {
     return u16x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
 }
 
+// bf16(q · scale): the reference's `q = q * self.scale` (swin.py:95), rounded as AMP rounds it
+__device__ __forceinline__ bf16x8_t scale_q(const u16x8 &q, float scale) {
+    bf16x8_t r;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = (__bf16)(bf2f(q[j]) * scale);
+    return r;
+}
+
 __device__ __forceinline__ u16x8 bias_frag(const float *qbias, int c0) {
     u16x8 r;
 #pragma unroll
@@ -280,7 +288,7 @@ __device__ __forceinline__ u16x8 load_frag_sel(const unsigned short *qkv, const 
 
 constexpr int RS = 40;    // LDS row stride (bf16) of the row-major tiles: 80 B
 constexpr int NR = 160;   // rows incl. zero padding to 5 k-steps of 32
-constexpr int DSR = 152;  // dS row stride (keys 144..151 stay zero)
+constexpr int DSR = 152;  // dSᵀ row stride in bf16 (144 queries + 8 pad: 304-B rows)
 constexpr float LOG2E = 1.4426950408889634f;
 // Relative-position biases live in registers as fp16 pairs (pre-scaled by log2 e): abs
 // error <= 2^-11 |b|, far below the bf16 rounding the reference's AMP applies to the
@@ -316,72 +324,74 @@ __global__ void __launch_bounds__(576) winattn_fwd_bf16(const unsigned short *__
                                                          const float *__restrict__ table,
                                                          const float *__restrict__ mask, Geo g, int cw,
                                                          unsigned short *__restrict__ out, float *__restrict__ lse) {
-    __shared__ __attribute__((aligned(16))) unsigned short Ks[NT * RS];
-    __shared__ __attribute__((aligned(16))) unsigned short Vs[NR * RS];
+    // K/V tiles double-buffered: window w stages into buffer w&1 while other waves may
+    // still be reading w-1, so one barrier per window suffices
+    __shared__ __attribute__((aligned(16))) unsigned short Ks[2][NT * RS];
+    __shared__ __attribute__((aligned(16))) unsigned short Vs[2][NR * RS];
+    __shared__ __attribute__((aligned(16))) unsigned short padS[3 * HD];  // pad-token q, k, v (bf16)
     const Chunk ck = decode_chunk(g, cw);
     const int h = ck.h;
     const long C3 = 3 * g.C;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int l16 = lane & 15, grp = lane >> 4;
-    for (int i = tid; i < (NR - NT) * RS; i += 576) Vs[NT * RS + i] = 0;
+    for (int i = tid; i < (NR - NT) * RS; i += 576) {
+        Vs[0][NT * RS + i] = 0;
+        Vs[1][NT * RS + i] = 0;
+    }
+    if (tid < 3 * HD) padS[tid] = qbias ? f2bf(qbias[(tid / HD) * g.C + h * HD + tid % HD]) : (unsigned short)0;
     // per-lane biases, log2 domain: query qi = 16 wave + l16, key = 16 kt + 4 grp + r
     const int qi = wave * 16 + l16;
-    unsigned bias[18];  // fp16 pairs
+    // bias in natural units, rounded through fp16(b·log2 e) exactly as the backward sees it;
+    // it seeds the MFMA accumulator, so S + B costs no VALU op per window
+    f32x4 bias4[9];
     unsigned long long hb = 0, wb = 0;  // key class bits (MM == 1)
 #pragma unroll
     for (int kt = 0; kt < 9; ++kt)
 #pragma unroll
-        for (int r = 0; r < 4; r += 2) {
+        for (int r = 0; r < 4; ++r) {
             const int ki = kt * 16 + grp * 4 + r;
-            h2 pr;
-            pr[0] = (_Float16)(table[rel_idx(qi, ki) * g.nH + h] * LOG2E);
-            pr[1] = (_Float16)(table[rel_idx(qi, ki + 1) * g.nH + h] * LOG2E);
-            bias[kt * 2 + r / 2] = __builtin_bit_cast(unsigned, pr);
+            bias4[kt][r] = (float)(_Float16)(table[rel_idx(qi, ki) * g.nH + h] * LOG2E) * (1.0f / LOG2E);
             if (MM == 1) {
                 hb |= (unsigned long long)hi_row(g, ki) << (kt * 4 + r);
                 wb |= (unsigned long long)hi_col(g, ki) << (kt * 4 + r);
-                hb |= (unsigned long long)hi_row(g, ki + 1) << (kt * 4 + r + 1);
-                wb |= (unsigned long long)hi_col(g, ki + 1) << (kt * 4 + r + 1);
             }
         }
     const bool q_hr = hi_row(g, qi), q_hc = hi_col(g, qi);
-    const float scale2 = g.scale * LOG2E;
+    const bf16x8_t ones = as_bf(u16x8{0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80});
     // staging map: thread -> (token t, 16-B chunk ch) of K and V
     const int st_t = tid >> 2, st_ch = tid & 3;
-    u16x8 kreg, vreg, qreg;
-    const u16x8 kpad = bias_frag(qbias, g.C + h * HD + st_ch * 8);
-    const u16x8 vpad = bias_frag(qbias, 2 * g.C + h * HD + st_ch * 8);
-    const u16x8 qpad = bias_frag(qbias, h * HD + grp * 8);
-    int qtok_next = -1;
-    auto prefetch = [&](int bw) {
-        const int tok = token_of(g, bw, st_t);
-        kreg = load_frag_sel(qkv, kpad, tok, C3, g.C + h * HD + st_ch * 8);
-        vreg = load_frag_sel(qkv, vpad, tok, C3, 2 * g.C + h * HD + st_ch * 8);
-        qtok_next = token_of(g, bw, qi);
-        qreg = load_frag_sel(qkv, qpad, qtok_next, C3, h * HD + grp * 8);
+    __syncthreads();  // padS
+    // Two register stages: the loads for window w+2 are issued while w computes, so a
+    // window's HBM latency is covered by two windows of work.
+    struct Stage {
+        u16x8 k, v, q;
+        int qtok;
     };
-    if (ck.w_begin < ck.w_end) prefetch(ck.w_begin);
-    for (int bw = ck.w_begin; bw < ck.w_end; ++bw) {
+    auto load = [&](int bw, Stage &sg) {
+        const int tok = token_of(g, bw, st_t);
+        sg.k = load_frag_sel(qkv, *(const u16x8 *)(padS + HD + st_ch * 8), tok, C3, g.C + h * HD + st_ch * 8);
+        sg.v = load_frag_sel(qkv, *(const u16x8 *)(padS + 2 * HD + st_ch * 8), tok, C3,
+                             2 * g.C + h * HD + st_ch * 8);
+        sg.qtok = token_of(g, bw, qi);
+        sg.q = load_frag_sel(qkv, *(const u16x8 *)(padS + grp * 8), sg.qtok, C3, h * HD + grp * 8);
+    };
+    auto step = [&](int bw, int buf, Stage &sg) {
+        unsigned short *Kb = Ks[buf], *Vb = Vs[buf];
+        *(u16x8 *)(Kb + st_t * RS + st_ch * 8) = sg.k;
+        *(u16x8 *)(Vb + st_t * RS + st_ch * 8) = sg.v;
+        const bf16x8_t qf = scale_q(sg.q, g.scale);
+        const int qtok = sg.qtok;
         __syncthreads();
-        *(u16x8 *)(Ks + st_t * RS + st_ch * 8) = kreg;
-        *(u16x8 *)(Vs + st_t * RS + st_ch * 8) = vreg;
-        const bf16x8_t qf = as_bf(qreg);
-        const int qtok = qtok_next;
-#pragma unroll
-        for (int i = 0; i < 18; ++i) asm volatile("" : "+v"(bias[i]));  // keep biases packed (no LICM unpack)
-        __syncthreads();
-        if (bw + 1 < ck.w_end) prefetch(bw + 1);
+        if (bw + 2 < ck.w_end) load(bw + 2, sg);
         f32x4 s[9];
 #pragma unroll
         for (int kt = 0; kt < 9; ++kt) {
-            const bf16x8_t kf = as_bf(*(const u16x8 *)(Ks + (kt * 16 + l16) * RS + grp * 8));
-            s[kt] = mfma16(kf, qf, f32x4{0.f, 0.f, 0.f, 0.f});
+            const bf16x8_t kf = as_bf(*(const u16x8 *)(Kb + (kt * 16 + l16) * RS + grp * 8));
+            s[kt] = mfma16(kf, qf, bias4[kt]);  // Sᵀ + B (key rows, query on the lane)
+            if (MM == 2) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                float v = fmaf(s[kt][r], scale2, (float)__builtin_bit_cast(h2, bias[kt * 2 + r / 2])[r & 1]);
-                if (MM == 2)
-                    v += LOG2E * mask[((long)(bw % g.n_mask) * NT + qi) * NT + kt * 16 + grp * 4 + r];
-                s[kt][r] = v;
+                for (int r = 0; r < 4; ++r)
+                    s[kt][r] += mask[((long)(bw % g.n_mask) * NT + qi) * NT + kt * 16 + grp * 4 + r];
             }
         }
         if (MM == 1) {  // only windows on the last row / column of the shifted grid carry a mask (uniform branch)
@@ -394,8 +404,7 @@ __global__ void __launch_bounds__(576) winattn_fwd_bf16(const unsigned short *__
 #pragma unroll
                 for (int kt = 0; kt < 9; ++kt)
 #pragma unroll
-                    for (int r = 0; r < 4; ++r)
-                        s[kt][r] += ((mbits >> (kt * 4 + r)) & 1ull) ? -100.0f * LOG2E : 0.0f;
+                    for (int r = 0; r < 4; ++r) s[kt][r] += ((mbits >> (kt * 4 + r)) & 1ull) ? -100.0f : 0.0f;
             }
         }
         float mx = -INFINITY;
@@ -405,19 +414,14 @@ __global__ void __launch_bounds__(576) winattn_fwd_bf16(const unsigned short *__
             for (int r = 0; r < 4; ++r) mx = fmaxf(mx, s[kt][r]);
         mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
         mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-        float sum = 0.f;
+        const float mneg = -mx * LOG2E;
 #pragma unroll
         for (int kt = 0; kt < 9; ++kt)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const float p = fast_exp2(s[kt][r] - mx);
-                s[kt][r] = p;
-                sum += p;
-            }
-        sum += __shfl_xor(sum, 16, 64);
-        sum += __shfl_xor(sum, 32, 64);
-        // Oᵀ = Vᵀ·Pᵀ over 5 k-steps of 32 keys (key order permuted identically in A and B)
-        f32x4 o0 = {0.f, 0.f, 0.f, 0.f}, o1 = {0.f, 0.f, 0.f, 0.f};
+            for (int r = 0; r < 4; ++r) s[kt][r] = fast_exp2(fmaf(s[kt][r], LOG2E, mneg));
+        // Oᵀ = Vᵀ·Pᵀ over 5 k-steps of 32 keys (key order permuted identically in A and B);
+        // a third MFMA with an all-ones A gives the row sums of the bf16 P actually used
+        f32x4 o0 = {0.f, 0.f, 0.f, 0.f}, o1 = o0, os = o0;
         const int tr_row = (l16 >> 2), tr_col = 4 * (l16 & 3);
 #pragma unroll
         for (int ks = 0; ks < 5; ++ks) {
@@ -427,13 +431,15 @@ __global__ void __launch_bounds__(576) winattn_fwd_bf16(const unsigned short *__
                 pb[r] = (__bf16)s[2 * ks][r];
                 pb[4 + r] = (2 * ks + 1 < 9) ? (__bf16)s[2 * ks + 1][r] : (__bf16)0.f;
             }
-            const unsigned short *v0 = Vs + (32 * ks + 4 * grp + tr_row) * RS + tr_col;
+            const unsigned short *v0 = Vb + (32 * ks + 4 * grp + tr_row) * RS + tr_col;
             const unsigned short *v1 = v0 + 16 * RS;
             const u16x8 a0 = cat4(tr_read(v0), tr_read(v1));
             const u16x8 a1 = cat4(tr_read(v0 + 16), tr_read(v1 + 16));
             o0 = mfma16(as_bf(a0), pb, o0);
             o1 = mfma16(as_bf(a1), pb, o1);
+            os = mfma16(ones, pb, os);
         }
+        const float sum = os[0];
         const float inv = 1.f / sum;
         if (qtok >= 0) {
             u16x4 w0, w1;
@@ -446,7 +452,14 @@ __global__ void __launch_bounds__(576) winattn_fwd_bf16(const unsigned short *__
             *(u16x4 *)(op + grp * 4) = w0;
             *(u16x4 *)(op + 16 + grp * 4) = w1;
         }
-        if (grp == 0) lse[((long)bw * g.nH + h) * NT + qi] = mx + __log2f(sum);  // base-2 LSE
+        if (grp == 0) lse[((long)bw * g.nH + h) * NT + qi] = fmaf(mx, LOG2E, __log2f(sum));  // base-2 LSE
+    };
+    Stage sa, sb;
+    if (ck.w_begin < ck.w_end) load(ck.w_begin, sa);
+    if (ck.w_begin + 1 < ck.w_end) load(ck.w_begin + 1, sb);
+    for (int bw = ck.w_begin; bw < ck.w_end; bw += 2) {
+        step(bw, 0, sa);
+        if (bw + 1 < ck.w_end) step(bw + 1, 1, sb);
     }
 }
 
@@ -462,7 +475,7 @@ __global__ void __launch_bounds__(576) winattn_bwd_bf16(
     __shared__ __attribute__((aligned(16))) unsigned short dOs[NR * RS];
     __shared__ __attribute__((aligned(16))) unsigned short Ks[NR * RS];
     __shared__ __attribute__((aligned(16))) unsigned short Vs[NT * RS];
-    __shared__ __attribute__((aligned(16))) unsigned short dSs[NT * DSR];
+    __shared__ __attribute__((aligned(16))) unsigned short dSt[NR * DSR];  // dSᵀ: [key][query], keys >= 144 zero
     __shared__ __attribute__((aligned(16))) float lseS[NT], dltS[NT];
     __shared__ int tokS[NT];
     const Chunk ck = decode_chunk(g, cw);
@@ -475,7 +488,7 @@ __global__ void __launch_bounds__(576) winattn_bwd_bf16(
         dOs[NT * RS + i] = 0;
         Ks[NT * RS + i] = 0;
     }
-    for (int i = tid; i < NT * (DSR - NT); i += 576) dSs[(i / (DSR - NT)) * DSR + NT + i % (DSR - NT)] = 0;
+    for (int i = tid; i < (NR - NT) * DSR; i += 576) dSt[NT * DSR + i] = 0;
     // per-lane biases (key on the lane): key = 16 wave + l16, query = 16 qt + 4 grp + r
     const int kkey = wave * 16 + l16;
     unsigned bias[18];  // fp16 pairs
@@ -489,6 +502,7 @@ __global__ void __launch_bounds__(576) winattn_bwd_bf16(
             pr[0] = (_Float16)(table[rel_idx(q, kkey) * g.nH + h] * LOG2E);
             pr[1] = (_Float16)(table[rel_idx(q + 1, kkey) * g.nH + h] * LOG2E);
             bias[qt * 2 + r / 2] = __builtin_bit_cast(unsigned, pr);
+            asm volatile("" : "+v"(bias[qt * 2 + r / 2]));  // opaque: no re-packing from f32 in the loop
             if (MM == 1) {
                 hb |= (unsigned long long)hi_row(g, q) << (qt * 4 + r);
                 wb |= (unsigned long long)hi_col(g, q) << (qt * 4 + r);
@@ -497,7 +511,6 @@ __global__ void __launch_bounds__(576) winattn_bwd_bf16(
             }
         }
     const bool k_hr = hi_row(g, kkey), k_hc = hi_col(g, kkey);
-    const float scale2 = g.scale * LOG2E;
     const int st_t = tid >> 2, st_ch = tid & 3;
     u16x8 qreg, oreg, dreg, kreg, vreg;
     __shared__ __attribute__((aligned(16))) unsigned short padS[3 * HD];  // pad-token q, k, v (bf16)
@@ -524,18 +537,18 @@ __global__ void __launch_bounds__(576) winattn_bwd_bf16(
     const int tr_row = (l16 >> 2), tr_col = 4 * (l16 & 3);
     for (int bw = ck.w_begin; bw < ck.w_end; ++bw) {
         __syncthreads();
-        *(u16x8 *)(Qs + st_t * RS + st_ch * 8) = qreg;
+        *(bf16x8_t *)(Qs + st_t * RS + st_ch * 8) = scale_q(qreg, g.scale);  // Q' = bf16(q·scale), as forward
         *(u16x8 *)(dOs + st_t * RS + st_ch * 8) = dreg;
         *(u16x8 *)(Ks + st_t * RS + st_ch * 8) = kreg;
         *(u16x8 *)(Vs + st_t * RS + st_ch * 8) = vreg;
         {
-            float part = 0.f;  // delta_q = dO_q · O_q, 4 lanes per token
+            float part = 0.f;  // delta_q = dO_q · O_q, 4 lanes per token (stored negated)
 #pragma unroll
             for (int j = 0; j < 8; ++j) part = fmaf(bf2f(dreg[j]), bf2f(oreg[j]), part);
             part += __shfl_xor(part, 1, 64);
             part += __shfl_xor(part, 2, 64);
             if (st_ch == 0) {
-                dltS[st_t] = part;
+                dltS[st_t] = -part;
                 tokS[st_t] = tok_next;
             }
             if (tid < NT) lseS[tid] = lreg;
@@ -576,23 +589,25 @@ __global__ void __launch_bounds__(576) winattn_bwd_bf16(
                 }
                 const bf16x8_t qa = as_bf(*(const u16x8 *)(Qs + (qt * 16 + l16) * RS + grp * 8));
                 const bf16x8_t da = as_bf(*(const u16x8 *)(dOs + (qt * 16 + l16) * RS + grp * 8));
-                const f32x4 sa = mfma16(qa, kb, f32x4{0.f, 0.f, 0.f, 0.f});   // S[q][key]
-                const f32x4 dpa = mfma16(da, vb, f32x4{0.f, 0.f, 0.f, 0.f});  // dP[q][key]
                 const f32x4 l4 = *(const f32x4 *)(lseS + qt * 16 + grp * 4);
-                const f32x4 d4 = *(const f32x4 *)(dltS + qt * 16 + grp * 4);
+                const f32x4 nd4 = *(const f32x4 *)(dltS + qt * 16 + grp * 4);
+                const f32x4 sa = mfma16(qa, kb, f32x4{0.f, 0.f, 0.f, 0.f});  // S[q][key] (Q' pre-scaled)
+                const f32x4 dpa = mfma16(da, vb, nd4);                       // dP[q][key] - delta_q
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    float v = fmaf(sa[r], scale2, (float)__builtin_bit_cast(h2, bias[qt * 2 + r / 2])[r & 1]);
+                    float v = fmaf(sa[r], LOG2E, (float)__builtin_bit_cast(h2, bias[qt * 2 + r / 2])[r & 1]);
                     if (MASKED) v += ((mbits >> (qt * 4 + r)) & 1ull) ? -100.0f * LOG2E : 0.0f;
                     if (MM == 2)
                         v += LOG2E * mask[((long)(bw % g.n_mask) * NT + qt * 16 + grp * 4 + r) * NT + kkey];
                     const float p = fast_exp2(v - l4[r]);
-                    const float ds = p * (dpa[r] - d4[r]);
+                    const float ds = p * dpa[r];
                     pb[4 * half + r] = (__bf16)p;
                     sb[4 * half + r] = (__bf16)ds;
-                    dSs[(qt * 16 + grp * 4 + r) * DSR + kkey] = __builtin_bit_cast(unsigned short, sb[4 * half + r]);
                     if (EX && gtable) atomicAdd(&gtable[rel_idx(qt * 16 + grp * 4 + r, kkey) * g.nH + h], ds);
                 }
+                const u16x8 sbits = __builtin_bit_cast(u16x8, sb);
+                *(u16x4 *)(dSt + kkey * DSR + qt * 16 + grp * 4) =
+                    u16x4{sbits[4 * half], sbits[4 * half + 1], sbits[4 * half + 2], sbits[4 * half + 3]};
             }
             // dVᵀ += dOᵀ·P ; dKᵀ += Qᵀ·dS   (k = 32 queries; A via transposed LDS reads)
             const int r0 = (32 * ks + 4 * grp + tr_row) * RS + tr_col;
@@ -619,8 +634,8 @@ __global__ void __launch_bounds__(576) winattn_bwd_bf16(
                 u16x4 k0, k1, v0, v1;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    k0[r] = f2bf(dk0[r] * g.scale);
-                    k1[r] = f2bf(dk1[r] * g.scale);
+                    k0[r] = f2bf(dk0[r]);  // dK = dSᵀ·Q' (Q' already carries the scale)
+                    k1[r] = f2bf(dk1[r]);
                     v0[r] = f2bf(dv0[r]);
                     v1[r] = f2bf(dv1[r]);
                 }
@@ -632,8 +647,8 @@ __global__ void __launch_bounds__(576) winattn_bwd_bf16(
             } else if (EX && gbias) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    atomicAdd(&gbias[g.C + c0 + r], dk0[r] * g.scale);
-                    atomicAdd(&gbias[g.C + c0 + 16 + r], dk1[r] * g.scale);
+                    atomicAdd(&gbias[g.C + c0 + r], dk0[r]);
+                    atomicAdd(&gbias[g.C + c0 + 16 + r], dk1[r]);
                     atomicAdd(&gbias[2 * g.C + c0 + r], dv0[r]);
                     atomicAdd(&gbias[2 * g.C + c0 + 16 + r], dv1[r]);
                 }
@@ -647,7 +662,8 @@ __global__ void __launch_bounds__(576) winattn_bwd_bf16(
 #pragma unroll
             for (int ks = 0; ks < 5; ++ks) {
                 const int k0 = 32 * ks + 8 * grp;
-                const u16x8 bs = (k0 < DSR) ? *(const u16x8 *)(dSs + qq * DSR + k0) : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+                const int d0 = (k0 + tr_row) * DSR + wave * 16 + tr_col;
+                const u16x8 bs = cat4(tr_read(dSt + d0), tr_read(dSt + d0 + 4 * DSR));
                 const int r0 = (k0 + tr_row) * RS + tr_col;
                 const int r1 = r0 + 4 * RS;
                 const u16x8 ak0 = cat4(tr_read(Ks + r0), tr_read(Ks + r1));

@@ -33,7 +33,12 @@ SIGNATURES = {
     "irads_sb_drift": [_i, _vp, _vp, _vp, _vp, _vp, _d, _i, _i, _i, _vp, _vp],
     "irads_sb_em": [_i, _vp, _vp, _i, _vp, _vp, _vp, _d, _i, _i, _i, _vp, _vp],
     "irads_sb_logits": [_i, _vp, _vp, _vp, _vp, _d, _i, _i, _i, _vp, _vp, _vp],
+    "irads_resize_fwd": [_i, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _vp],
+    "irads_resize_bwd": [_i, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _vp, _vp],
+    "irads_ce_fwd": [_i, _vp, _vp, _i, _i, _i, _i, _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp],
+    "irads_ce_bwd": [_i, _vp, _vp, _i, _i, _i, _i, _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp],
 }
+CE_WORKSPACE = 2048
 
 _lib = None
 
@@ -83,6 +88,14 @@ def dtype_code(t, allowed, what):
         raise RuntimeError(f"{what}: dtype {t.dtype} not supported (expected one of "
                            f"{[names[a] for a in allowed]})")
     return code
+
+
+def check_device(t, what):
+    """GPU tensors only: the product path has no CPU fallback."""
+    if not t.is_cuda:
+        raise RuntimeError(f"{what} must be a CUDA tensor (no CPU path; the CPU restatement is oracle/, "
+                           f"test infrastructure only)")
+    return t
 
 
 def check(t, what, dtype=None):

@@ -5,6 +5,8 @@ device and passes the current HIP stream, so the ops are asynchronous and
 graph-capturable.  Gradient accumulators that the kernels add into atomically are
 zero-filled here.  There is no CPU fallback: CPU tensors raise.
 """
+import ctypes
+
 import torch
 
 from . import native as N
@@ -282,3 +284,98 @@ def sb_logits(x, r, S_log_diag, log_alpha_raw, epsilon, want_logits=True, want_l
     N.call("irads_sb_logits", code, N.ptr(x), N.ptr(r_), N.ptr(s_), N.ptr(a_), float(epsilon), rows, D, K,
            N.ptr(logits), N.ptr(log_c), N.stream())
     return logits, log_c
+
+
+# ------------------------------------------------------------------ segmentation head tail
+def _layout(x):
+    """(tensor, int64[4] strides) in one of the two dense layouts the kernels take."""
+    if not (x.is_contiguous() or x.is_contiguous(memory_format=torch.channels_last)):
+        x = x.contiguous()
+    st = (ctypes.c_int64 * 4)(*x.stride())
+    return x, st
+
+
+def _empty_like_layout(x, shape, dtype=None):
+    fmt = torch.channels_last if (not x.is_contiguous() and x.is_contiguous(memory_format=torch.channels_last)) \
+        else torch.contiguous_format
+    return torch.empty(shape, device=x.device, dtype=dtype or x.dtype, memory_format=fmt)
+
+
+class ResizeFn(torch.autograd.Function):
+    """F.interpolate(x, size=(H, W), mode='bilinear', align_corners=False) on the HIP
+    resize kernels (segformer.py:44, cmnext.py:30-32).  Output keeps the input's memory
+    format (NCHW or channels-last); the backward is the exact adjoint, fp32-accumulated."""
+
+    @staticmethod
+    def forward(ctx, x, size):
+        N.check_device(x, "resize input")
+        code = N.dtype_code(x, (N.F32, N.BF16), "resize")
+        x, xs = _layout(x)
+        B, C, h, w = x.shape
+        H, W = int(size[0]), int(size[1])
+        out = _empty_like_layout(x, (B, C, H, W))
+        os_ = (ctypes.c_int64 * 4)(*out.stride())
+        N.call("irads_resize_fwd", code, N.ptr(x), xs, B, C, h, w, N.ptr(out), os_, H, W, N.stream())
+        ctx.cfg = (code, B, C, h, w, H, W, x.is_contiguous())
+        return out
+
+    @staticmethod
+    def backward(ctx, go):
+        code, B, C, h, w, H, W, nchw = ctx.cfg
+        go = go.contiguous() if nchw or C == 1 else go.contiguous(memory_format=torch.channels_last)
+        gs = (ctypes.c_int64 * 4)(*go.stride())
+        gi = torch.empty((B, C, h, w), device=go.device, dtype=go.dtype,
+                         memory_format=torch.contiguous_format if nchw else torch.channels_last)
+        gis = (ctypes.c_int64 * 4)(*gi.stride())
+        ws = torch.empty((B * C * h * W,), device=go.device, dtype=torch.float32)
+        N.call("irads_resize_bwd", code, N.ptr(go), gs, B, C, H, W, N.ptr(gi), gis, h, w, N.ptr(ws), N.stream())
+        return gi, None
+
+
+def resize(x, size):
+    return ResizeFn.apply(x, tuple(size))
+
+
+class CrossEntropyFn(torch.autograd.Function):
+    """nn.CrossEntropyLoss(weight, ignore_index)(logits, target), mean reduction
+    (losses.py:6-19), one fused HIP pass each way; fp32 arithmetic on fp32 or bf16 logits
+    (the AMP-cast input of the reference).  Optionally also returns the MMST target of
+    train_mm.py:137-141 computed in the same pass (no gradient)."""
+
+    @staticmethod
+    def forward(ctx, logits, target, ignore_index, weight, want_match):
+        N.check_device(logits, "cross_entropy logits")
+        code = N.dtype_code(logits, (N.F32, N.BF16), "cross_entropy")
+        logits, ls = _layout(logits)
+        B, C, H, W = logits.shape
+        if target.shape != (B, H, W):
+            raise RuntimeError(f"cross_entropy: target shape {tuple(target.shape)} does not match logits "
+                               f"{tuple(logits.shape)}")
+        target = N.check(target.to(torch.int64).contiguous(), "target")
+        w = None if weight is None else N.check(weight.detach().float().contiguous(), "weight")
+        lse = torch.empty((B * H * W,), device=logits.device, dtype=torch.float32)
+        loss = torch.empty((2,), device=logits.device, dtype=torch.float32)
+        ws = torch.empty((N.CE_WORKSPACE,), device=logits.device, dtype=torch.float64)
+        match = torch.empty_like(target) if want_match else None
+        N.call("irads_ce_fwd", code, N.ptr(logits), ls, B, C, H, W, N.ptr(target), int(ignore_index), N.ptr(w),
+               N.ptr(lse), N.ptr(match), N.ptr(ws), N.ptr(loss), N.stream())
+        ctx.save_for_backward(logits, target, w, lse, loss)
+        ctx.cfg = (code, B, C, H, W, int(ignore_index))
+        if match is not None:
+            ctx.mark_non_differentiable(match)
+        return (loss[0], match) if want_match else loss[0]
+
+    @staticmethod
+    def backward(ctx, gloss, *_):
+        logits, target, w, lse, loss = ctx.saved_tensors
+        code, B, C, H, W, ignore = ctx.cfg
+        _, ls = _layout(logits)
+        g = N.check(gloss.float().reshape(1).contiguous(), "grad")
+        gx = torch.empty_like(logits)
+        N.call("irads_ce_bwd", code, N.ptr(logits), ls, B, C, H, W, N.ptr(target), ignore, N.ptr(w), N.ptr(lse),
+               N.ptr(loss), N.ptr(g), N.ptr(gx), N.stream())
+        return gx, None, None, None, None
+
+
+def cross_entropy(logits, target, ignore_index=255, weight=None, return_match=False):
+    return CrossEntropyFn.apply(logits, target, ignore_index, weight, bool(return_match))

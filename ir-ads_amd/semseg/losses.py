@@ -3,6 +3,8 @@ import torch
 from torch import nn, Tensor
 from torch.nn import functional as F
 
+from irads import ops
+
 
 class CrossEntropy(nn.Module):
     def __init__(self, ignore_label: int = 255, weight: Tensor = None, aux_weights: list = [1, 0.4, 0.4]) -> None:
@@ -11,7 +13,9 @@ class CrossEntropy(nn.Module):
         self.criterion = nn.CrossEntropyLoss(weight=weight, ignore_index=ignore_label)
 
     def _forward(self, preds: Tensor, labels: Tensor) -> Tensor:
-        return self.criterion(preds, labels)
+        # nn.CrossEntropyLoss semantics (mean over non-ignored pixels, optional class
+        # weights) on the fused HIP kernel; the criterion module keeps weight/ignore_index
+        return ops.cross_entropy(preds, labels, self.criterion.ignore_index, self.criterion.weight)
 
     def forward(self, preds, labels: Tensor) -> Tensor:
         if isinstance(preds, tuple):
@@ -75,8 +79,15 @@ def get_loss(loss_fn_name: str = 'CrossEntropy', ignore_label: int = 255, cls_we
 
 def mmst_loss(loss_fn, logits, logits_rgb, logits_dte, lbl, ignore_label=255):
     """train_mm.py:137-148: pixels the fused head gets wrong are ignored (255) for the
-    two auxiliary modality heads, each weighted 0.01."""
+    two auxiliary modality heads, each weighted 0.01.  With CrossEntropy the MMST target
+    (label where argmax(softmax(logits)) == label) comes out of the fused loss pass of the
+    main head; argmax of the softmax equals the first argmax of the logits, since
+    distinct bf16/fp32 logits give distinct fp32 probabilities."""
+    if isinstance(loss_fn, CrossEntropy) and not isinstance(logits, tuple):
+        crit = loss_fn.criterion
+        loss1, mask_lbl = ops.cross_entropy(logits, lbl, crit.ignore_index, crit.weight, return_match=True)
+        return loss1 + 0.01 * loss_fn(logits_rgb, mask_lbl) + 0.01 * loss_fn(logits_dte, mask_lbl)
     with torch.no_grad():
-        pred = logits.softmax(dim=1).argmax(dim=1)  # as train_mm.py:138 (ties after softmax rounding)
+        pred = logits.softmax(dim=1).argmax(dim=1)
         mask_lbl = torch.where(pred == lbl, lbl, torch.full_like(lbl, ignore_label))
     return loss_fn(logits, lbl) + 0.01 * loss_fn(logits_rgb, mask_lbl) + 0.01 * loss_fn(logits_dte, mask_lbl)

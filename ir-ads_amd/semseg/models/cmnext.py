@@ -1,6 +1,5 @@
 """CMNeXt with the two-stream Swin backbone (reference semseg/models/cmnext.py:11-36)."""
-from torch.nn import functional as F
-
+from irads import ops
 from semseg.models.base import BaseModel
 from semseg.models.heads import SegFormerHead
 
@@ -23,9 +22,10 @@ class CMNeXt(BaseModel):
     def forward(self, x: list):
         y, y_rgb, y_dte = self.backbone(x)
         size = x[0].shape[2:]
-        y = F.interpolate(self.decode_head(y), size=size, mode='bilinear', align_corners=False)
-        y_rgb = F.interpolate(self.decode_head_rgb(y_rgb), size=size, mode='bilinear', align_corners=False)
-        y_dte = F.interpolate(self.decode_head_dte(y_dte), size=size, mode='bilinear', align_corners=False)
+        # F.interpolate(..., mode='bilinear', align_corners=False) on the HIP resize kernels
+        y = ops.resize(self.decode_head(y), size)
+        y_rgb = ops.resize(self.decode_head_rgb(y_rgb), size)
+        y_dte = ops.resize(self.decode_head_dte(y_dte), size)
         return y, y_rgb, y_dte
 
     def init_pretrained(self, pretrained: str = None) -> None:

@@ -5,6 +5,8 @@ import torch
 from torch import nn, Tensor
 from torch.nn import functional as F
 
+from irads import ops
+
 
 class MLP(nn.Module):
     def __init__(self, dim, embed_dim):
@@ -40,6 +42,6 @@ class SegFormerHead(nn.Module):
         outs = [self.linear_c1(features[0]).permute(0, 2, 1).reshape(B, -1, H, W)]
         for i, f in enumerate(features[1:]):
             cf = getattr(self, f"linear_c{i + 2}")(f).permute(0, 2, 1).reshape(B, -1, *f.shape[-2:])
-            outs.append(F.interpolate(cf, size=(H, W), mode='bilinear', align_corners=False))
+            outs.append(ops.resize(cf, (H, W)))  # F.interpolate(bilinear, align_corners=False)
         seg = self.linear_fuse(torch.cat(outs[::-1], dim=1))
         return self.linear_pred(self.dropout(seg))

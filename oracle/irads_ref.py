@@ -589,3 +589,14 @@ def metrics_tp_fp_fn(pred_logits, gt, n_classes, ignore=255):
         fp.append(int((~g & p & valid).sum()))
         fn.append(int((g & ~p & valid).sum()))
     return tp, fp, fn
+
+
+# ====================================================================== training objective
+def mmst_loss(logits, logits_rgb, logits_dte, lbl, ignore_label=255, weight=None):
+    """train_mm.py:137-148 with CrossEntropy (semseg/losses.py:6-19): the two modality
+    heads are trained only on pixels the fused head classifies correctly."""
+    lf = nn.CrossEntropyLoss(weight=weight, ignore_index=ignore_label)
+    pred = logits.softmax(dim=1).argmax(dim=1)
+    mask_lbl = lbl.clone()
+    mask_lbl[pred != lbl] = ignore_label
+    return lf(logits, lbl) + 0.01 * lf(logits_rgb, mask_lbl) + 0.01 * lf(logits_dte, mask_lbl)

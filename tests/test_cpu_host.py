@@ -102,6 +102,15 @@ def test_product_refuses_cpu_tensors():
     with pytest.raises(RuntimeError):
         m(torch.randn(3, 1, 256), value=torch.randn(22, 1, 256), reference_points=torch.rand(1, 3, 4, 2),
           spatial_shapes=shapes, level_start_index=torch.tensor([0, 16, 20, 21]))
+    from irads import ops
+    from semseg.losses import get_loss, mmst_loss
+    with pytest.raises(RuntimeError):
+        ops.resize(torch.randn(1, 3, 4, 4), (8, 8))
+    x, t = torch.randn(4, 5, 6, 6), torch.randint(0, 5, (4, 6, 6))
+    with pytest.raises(RuntimeError):
+        get_loss("CrossEntropy", 255)(x, t)
+    with pytest.raises(RuntimeError):
+        mmst_loss(get_loss("CrossEntropy", 255), x, x, x, t)
 
 
 def test_unsupported_configs_raise():

@@ -1,0 +1,206 @@
+"""Segmentation-head tail on the HIP path: bilinear resize (segformer.py:44,
+cmnext.py:30-32) and the fused softmax cross-entropy / MMST objective (losses.py:6-19,
+train_mm.py:137-148).
+
+Oracle: the reference calls these as plain PyTorch ops, so the checker is the same call
+on the CPU in fp32/fp64 (F.interpolate, nn.CrossEntropyLoss and autograd through them),
+plus the MMST golden fixture generated from the reference's formula
+(tests/golden/metrics_loss.npz, oracle/gen_golden.py:394-413).
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from golden_util import Fixture, close
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _ops():
+    from irads import ops
+    return ops
+
+
+def _rand(shape, seed, dtype=torch.float32):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(shape, generator=g, dtype=torch.float64).to(dtype)
+
+
+def _fmt(x, cl):
+    return x.contiguous(memory_format=torch.channels_last) if cl else x.contiguous()
+
+
+RESIZE_CASES = [
+    # (B, C, h, w, H, W)
+    (2, 40, 32, 32, 128, 128),   # x4: CMNeXt logits -> image size (scaled down)
+    (2, 64, 16, 16, 32, 32),     # x2: SegFormer c2 -> c1 grid
+    (1, 16, 8, 8, 64, 64),       # x8: c4 -> c1
+    (2, 5, 13, 17, 50, 61),      # non-integer ratios
+    (1, 3, 37, 29, 30, 20),      # downscale
+    (1, 1, 1, 1, 7, 5),          # single source pixel
+    (3, 8, 9, 9, 9, 9),          # identity size
+]
+
+
+@pytest.mark.parametrize("cl", [False, True])
+@pytest.mark.parametrize("case", RESIZE_CASES)
+def test_resize_fp32_vs_interpolate(case, cl):
+    ops = _ops()
+    B, C, h, w, H, W = case
+    x = _fmt(_rand((B, C, h, w), 1), cl)
+    ref = F.interpolate(x, size=(H, W), mode="bilinear", align_corners=False)
+    xg = x.to(DEV).requires_grad_(True)
+    out = ops.resize(xg, (H, W))
+    assert out.is_contiguous(memory_format=torch.channels_last if (cl and C > 1) else torch.contiguous_format)
+    close(out, ref, 2e-6, 2e-6, f"resize fwd {case}")
+    # backward = adjoint, vs autograd through F.interpolate in fp64
+    go = _rand((B, C, H, W), 2)
+    xd = x.double().requires_grad_(True)
+    F.interpolate(xd, size=(H, W), mode="bilinear", align_corners=False).backward(go.double())
+    out.backward(_fmt(go, cl).to(DEV))
+    close(xg.grad, xd.grad, 2e-5, 1e-5, f"resize bwd {case}")
+
+
+@pytest.mark.parametrize("cl", [False, True])
+def test_resize_bf16(cl):
+    """bf16 storage, fp32 arithmetic: within one bf16 rounding of the exact value."""
+    ops = _ops()
+    B, C, h, w, H, W = 2, 40, 32, 32, 128, 128
+    x = _fmt(_rand((B, C, h, w), 3).to(torch.bfloat16), cl)
+    exact = F.interpolate(x.double(), size=(H, W), mode="bilinear", align_corners=False)
+    xg = x.to(DEV).requires_grad_(True)
+    out = ops.resize(xg, (H, W))
+    close(out.float(), exact, 1e-6, 2 ** -8, "resize bf16 fwd")
+    go = _rand((B, C, H, W), 4).to(torch.bfloat16)
+    xd = x.double().requires_grad_(True)
+    F.interpolate(xd, size=(H, W), mode="bilinear", align_corners=False).backward(go.double())
+    out.backward(_fmt(go, cl).to(DEV))
+    close(xg.grad.float(), xd.grad, 1e-5, 2 ** -7, "resize bf16 bwd")
+
+
+def test_resize_full_size_c2():
+    """C2 shapes: 8 x 40 x 128² logits to 512² (cmnext.py:30) — forward exact vs CPU fp32,
+    backward checked through <gin, x> = <gout, resize(x)> (adjointness, size-independent)."""
+    ops = _ops()
+    x = _rand((8, 40, 128, 128), 5)
+    out = ops.resize(x.to(DEV), (512, 512))
+    ref = F.interpolate(x, size=(512, 512), mode="bilinear", align_corners=False)
+    close(out, ref, 2e-6, 2e-6, "resize C2 fwd")
+    go = _rand((8, 40, 512, 512), 6).to(DEV)
+    xg = x.to(DEV).requires_grad_(True)
+    ops.resize(xg, (512, 512)).backward(go)
+    lhs = (xg.grad.double() * x.to(DEV).double()).sum()
+    rhs = (go.double() * out.double()).sum()
+    assert abs(float(lhs - rhs)) <= 1e-4 * abs(float(rhs)) + 1e-3
+
+
+def _targets(B, H, W, C, seed, ignore=255, p_ignore=0.1):
+    g = torch.Generator().manual_seed(seed)
+    t = torch.randint(0, C, (B, H, W), generator=g)
+    t[torch.rand((B, H, W), generator=g) < p_ignore] = ignore
+    return t
+
+
+@pytest.mark.parametrize("cl", [False, True])
+@pytest.mark.parametrize("C", [1, 7, 19, 40, 64, 100, 128])
+def test_cross_entropy_fp32(C, cl):
+    ops = _ops()
+    B, H, W = 2, 24, 31
+    x = _fmt(_rand((B, C, H, W), 10 + C) * 3, cl)
+    t = _targets(B, H, W, C, 20 + C)
+    xd = x.double().requires_grad_(True)
+    ref = F.cross_entropy(xd, t, ignore_index=255)
+    ref.backward()
+    xg = x.to(DEV).requires_grad_(True)
+    loss = ops.cross_entropy(xg, t.to(DEV), 255)
+    close(loss, ref, 1e-6, 1e-6, f"CE fwd C={C}")
+    loss.backward()
+    close(xg.grad, xd.grad, 1e-7, 1e-5, f"CE bwd C={C}")
+
+
+def test_cross_entropy_weights_and_grad_scale():
+    ops = _ops()
+    B, C, H, W = 2, 9, 16, 20
+    x = _rand((B, C, H, W), 30) * 2
+    t = _targets(B, H, W, C, 31)
+    wt = torch.rand(C, generator=torch.Generator().manual_seed(32)) + 0.5
+    xd = x.double().requires_grad_(True)
+    ref = F.cross_entropy(xd, t, weight=wt.double(), ignore_index=255)
+    (3.5 * ref).backward()
+    xg = x.to(DEV).requires_grad_(True)
+    loss = ops.cross_entropy(xg, t.to(DEV), 255, wt.to(DEV))
+    close(loss, ref, 1e-6, 1e-6, "weighted CE fwd")
+    (3.5 * loss).backward()
+    close(xg.grad, xd.grad, 1e-7, 1e-5, "weighted CE bwd")
+
+
+def test_cross_entropy_bf16():
+    """bf16 logits (the reference's AMP path casts them to fp32 before the loss)."""
+    ops = _ops()
+    B, C, H, W = 2, 40, 32, 48
+    x = (_rand((B, C, H, W), 40) * 4).to(torch.bfloat16)
+    t = _targets(B, H, W, C, 41)
+    xd = x.double().requires_grad_(True)
+    ref = F.cross_entropy(xd, t, ignore_index=255)
+    ref.backward()
+    xg = x.to(DEV).requires_grad_(True)
+    loss = ops.cross_entropy(xg, t.to(DEV), 255)
+    close(loss, ref, 1e-6, 1e-5, "CE bf16 fwd")
+    loss.backward()
+    assert xg.grad.dtype == torch.bfloat16
+    close(xg.grad.float(), xd.grad, 1e-9, 2 ** -8, "CE bf16 bwd")
+
+
+def test_cross_entropy_edges():
+    ops = _ops()
+    # every pixel ignored: nan, as nn.CrossEntropyLoss
+    x = _rand((1, 4, 3, 3), 50).to(DEV)
+    t = torch.full((1, 3, 3), 255, dtype=torch.int64, device=DEV)
+    assert torch.isnan(ops.cross_entropy(x, t, 255))
+    # a 1x1 image, custom ignore index
+    x = _rand((3, 6, 1, 1), 51)
+    t = torch.tensor([[[2]], [[-100]], [[5]]])
+    ref = F.cross_entropy(x, t, ignore_index=-100)
+    close(ops.cross_entropy(x.to(DEV), t.to(DEV), -100), ref, 1e-6, 1e-6, "1x1 CE")
+    with pytest.raises(RuntimeError):
+        ops.cross_entropy(_rand((1, 129, 2, 2), 52).to(DEV), torch.zeros(1, 2, 2, dtype=torch.int64, device=DEV))
+    with pytest.raises(RuntimeError):
+        ops.cross_entropy(_rand((1, 3, 2, 2), 53).to(DEV), torch.zeros(1, 2, 3, dtype=torch.int64, device=DEV))
+
+
+def test_mmst_target_and_loss_golden():
+    """MMST (train_mm.py:137-148) against the fixture made from the reference formula."""
+    from semseg.losses import get_loss, mmst_loss
+    ops = _ops()
+    fx = Fixture("metrics_loss.npz")
+    logits, gt = fx.t("logits", device=DEV), fx.t("gt", device=DEV)
+    loss = mmst_loss(get_loss("CrossEntropy", 255), logits, fx.t("logits_rgb", device=DEV),
+                     fx.t("logits_dte", device=DEV), gt)
+    close(loss, fx["mmst_loss"], 1e-6, 1e-6, "MMST loss")
+    _, match = ops.cross_entropy(logits, gt, 255, return_match=True)
+    pred = fx.t("logits").softmax(dim=1).argmax(dim=1)
+    want = fx.t("gt").clone()
+    want[pred != want] = 255
+    assert torch.equal(match.cpu(), want)
+
+
+def test_mmst_full_size_c2_bf16():
+    """C2 sizes (8 x 40 x 512², bf16 logits): loss vs the CPU restatement on the same
+    bf16 values, gradients of all three heads vs autograd in fp64."""
+    from semseg.losses import get_loss, mmst_loss
+    import irads_ref as R
+    B, C, H, W = 8, 40, 512, 512
+    xs = [(_rand((B, C, H, W), 60 + i) * 3).to(torch.bfloat16) for i in range(3)]
+    t = _targets(B, H, W, C, 63)
+    xd = [x.double().requires_grad_(True) for x in xs]
+    ref = R.mmst_loss(*xd, t)
+    ref.backward()
+    xg = [x.to(DEV).requires_grad_(True) for x in xs]
+    loss = mmst_loss(get_loss("CrossEntropy", 255), *xg, t.to(DEV))
+    close(loss, ref, 1e-5, 1e-5, "MMST C2 loss")
+    loss.backward()
+    for i in range(3):
+        scale = float(xd[i].grad.abs().max())
+        close(xg[i].grad.float(), xd[i].grad, 1e-3 * scale, 2 ** -7, f"MMST C2 grad head {i}")

@@ -293,3 +293,5 @@ def test_metrics_and_mmst_oracle():
     assert [a + b for a, b in zip(tp, tp2)] == fx["tp"].tolist()
     assert [a + b for a, b in zip(fp, fp2)] == fx["fp"].tolist()
     assert [a + b for a, b in zip(fn, fn2)] == fx["fn"].tolist()
+    loss = R.mmst_loss(logits, fx.t("logits_rgb"), fx.t("logits_dte"), gt)
+    close(loss, fx["mmst_loss"], 1e-6, 1e-6, "MMST loss (train_mm.py:137-148)")
