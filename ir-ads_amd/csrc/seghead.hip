@@ -22,6 +22,7 @@ namespace irads {
 namespace {
 
 typedef __attribute__((ext_vector_type(4))) float f4;
+typedef __attribute__((ext_vector_type(8))) unsigned short u16x8v;
 
 template <typename T> __device__ __forceinline__ float ldf(const T *p, long i);
 template <> __device__ __forceinline__ float ldf<float>(const float *p, long i) { return p[i]; }
@@ -154,6 +155,119 @@ __global__ void __launch_bounds__(256) resize_bwd_cols(const float *__restrict__
     stf(gin, w.e, acc);
 }
 
+// ------------------------------------------------------------------ channels-last x8 variants
+// When C % 8 == 0 (every head tensor of CMNeXt: 40 classes, 256 / 512 channels) a
+// thread owns 8 consecutive channels of one pixel: one 16-B (bf16) or 32-B (fp32)
+// access per tensor, tap arithmetic and index math amortised over 8 elements.
+template <typename T> struct V8;
+template <> struct V8<unsigned short> {
+    static __device__ __forceinline__ void ld(const unsigned short *p, float *f) {
+        const u16x8v v = *(const u16x8v *)p;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = bf2f(v[j]);
+    }
+    static __device__ __forceinline__ void st(unsigned short *p, const float *f) {
+        u16x8v v;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = f2bf(f[j]);
+        *(u16x8v *)p = v;
+    }
+};
+template <> struct V8<float> {
+    static __device__ __forceinline__ void ld(const float *p, float *f) {
+        const f4 a = *(const f4 *)p, b = *(const f4 *)(p + 4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            f[j] = a[j];
+            f[4 + j] = b[j];
+        }
+    }
+    static __device__ __forceinline__ void st(float *p, const float *f) {
+        *(f4 *)p = f4{f[0], f[1], f[2], f[3]};
+        *(f4 *)(p + 4) = f4{f[4], f[5], f[6], f[7]};
+    }
+};
+
+// line = (b, y) pixel row of the output; r = x * C8 + chunk within it
+struct Walk8 {
+    int b, y, x, c0, line;
+    bool ok;
+};
+__device__ __forceinline__ Walk8 walk8(int B, int H, int W, int C) {
+    (void)B;
+    const int C8 = C >> 3, inner = W * C8, chunks = (inner + 255) / 256;
+    Walk8 w;
+    w.line = blockIdx.x / chunks;
+    const int r = (blockIdx.x - w.line * chunks) * 256 + threadIdx.x;
+    w.ok = r < inner;
+    w.b = w.line / H;
+    w.y = w.line - w.b * H;
+    w.x = r / C8;
+    w.c0 = (r - w.x * C8) * 8;
+    return w;
+}
+static int walk8_grid(int B, int H, int W, int C) {
+    const long inner = (long)W * (C >> 3);
+    return (int)((long)B * H * ((inner + 255) / 256));
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) resize_fwd_cl8(const T *__restrict__ in, Dims di, T *__restrict__ out,
+                                                      Dims dout, float sh, float sw) {
+    const Walk8 w = walk8(dout.B, dout.H, dout.W, dout.C);
+    if (!w.ok) return;
+    const Tap ty = tap_of(w.y, sh, di.H), tx = tap_of(w.x, sw, di.W);
+    float v00[8], v01[8], v10[8], v11[8], o[8];
+    V8<T>::ld(in + offs<true>(di, w.b, w.c0, ty.i0, tx.i0), v00);
+    V8<T>::ld(in + offs<true>(di, w.b, w.c0, ty.i0, tx.i1), v01);
+    V8<T>::ld(in + offs<true>(di, w.b, w.c0, ty.i1, tx.i0), v10);
+    V8<T>::ld(in + offs<true>(di, w.b, w.c0, ty.i1, tx.i1), v11);
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+        o[j] = ty.l0 * (tx.l0 * v00[j] + tx.l1 * v01[j]) + ty.l1 * (tx.l0 * v10[j] + tx.l1 * v11[j]);
+    V8<T>::st(out + ((long)w.line * dout.W + w.x) * dout.C + w.c0, o);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) resize_bwd_rows_cl8(const T *__restrict__ g, Dims dg, float *__restrict__ tmp,
+                                                           Dims dt, float sh, float inv_sh) {
+    const Walk8 w = walk8(dt.B, dt.H, dt.W, dt.C);
+    if (!w.ok) return;
+    int lo, hi;
+    reach(w.y, inv_sh, dg.H, lo, hi);  // uniform per workgroup
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int y = lo; y <= hi; ++y) {
+        const float wt = tap_weight(tap_of(y, sh, dt.H), w.y);
+        if (wt != 0.f) {
+            float v[8];
+            V8<T>::ld(g + offs<true>(dg, w.b, w.c0, y, w.x), v);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc[j] = fmaf(wt, v[j], acc[j]);
+        }
+    }
+    V8<float>::st(tmp + ((long)w.line * dt.W + w.x) * dt.C + w.c0, acc);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) resize_bwd_cols_cl8(const float *__restrict__ tmp, Dims dt,
+                                                           T *__restrict__ gin, Dims di, float sw, float inv_sw) {
+    const Walk8 w = walk8(di.B, di.H, di.W, di.C);
+    if (!w.ok) return;
+    int lo, hi;
+    reach(w.x, inv_sw, dt.W, lo, hi);
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int x = lo; x <= hi; ++x) {
+        const float wt = tap_weight(tap_of(x, sw, di.W), w.x);
+        if (wt != 0.f) {
+            float v[8];
+            V8<float>::ld(tmp + offs<true>(dt, w.b, w.c0, w.y, x), v);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc[j] = fmaf(wt, v[j], acc[j]);
+        }
+    }
+    V8<T>::st(gin + ((long)w.line * di.W + w.x) * di.C + w.c0, acc);
+}
+
 // ------------------------------------------------------------------ cross-entropy
 constexpr int CE_GRID = 1024;  // fixed grid: deterministic partial sums (IRADS_CE_WORKSPACE)
 
@@ -262,13 +376,103 @@ __global__ void __launch_bounds__(256) ce_bwd(const T *__restrict__ x, Dims d, c
     stf(gx, w.e, gv);
 }
 
-// 0 = NCHW-contiguous, 1 = channels-last-contiguous, -1 = neither
+// channels-last, C % 8 == 0: 256 pixels per workgroup staged into LDS with 16-B
+// coalesced copies (a pixel's class row is C contiguous elements), then one thread per
+// pixel reads its row from LDS in 16-B pieces
+template <typename T, int CMAX>
+__global__ void __launch_bounds__(256) ce_fwd_cl8(const T *__restrict__ x, Dims d, const int64_t *__restrict__ tgt,
+                                                  int ignore, const float *__restrict__ cw, float *__restrict__ lse,
+                                                  int64_t *__restrict__ match, double *__restrict__ part) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char ce_smem[];
+    T *tile = (T *)ce_smem;
+    __shared__ double red[4];
+    const long npix = (long)d.B * d.H * d.W;
+    const int tid = threadIdx.x;
+    float s_loss = 0.f, s_w = 0.f;
+    for (long p0 = blockIdx.x * 256L; p0 < npix; p0 += (long)gridDim.x * 256) {
+        const int n = (int)min(256L, npix - p0);
+        const int nv = n * d.C * (int)sizeof(T) / 16;
+        const uint4 *src = (const uint4 *)(x + p0 * d.C);
+        uint4 *dst = (uint4 *)tile;
+        for (int i = tid; i < nv; i += 256) dst[i] = src[i];
+        __syncthreads();
+        if (tid < n) {
+            const long p = p0 + tid;
+            float z[CMAX];
+            float m = -INFINITY;
+            int am = 0;
+#pragma unroll
+            for (int k = 0; k < CMAX / 8; ++k) {
+                if (8 * k < d.C) {
+                    V8<T>::ld(tile + tid * d.C + 8 * k, z + 8 * k);
+#pragma unroll
+                    for (int j = 0; j < 8; ++j)
+                        if (z[8 * k + j] > m) {  // first maximum, as argmax
+                            m = z[8 * k + j];
+                            am = 8 * k + j;
+                        }
+                }
+            }
+            float sum = 0.f;
+#pragma unroll
+            for (int c = 0; c < CMAX; ++c)
+                if (c < d.C) sum += expf(z[c] - m);
+            const float l = m + logf(sum);
+            lse[p] = l;
+            const long t = tgt[p];
+            const bool keep = t != ignore && t >= 0 && t < d.C;
+            if (keep) {
+                float zt = 0.f;
+#pragma unroll
+                for (int c = 0; c < CMAX; ++c)
+                    if (c == t) zt = z[c];
+                const float wt = cw ? cw[t] : 1.f;
+                s_loss += wt * (l - zt);
+                s_w += wt;
+            }
+            if (match) match[p] = (keep && am == t) ? t : (int64_t)ignore;
+        }
+        __syncthreads();
+    }
+    const double a = block_sum_d((double)s_loss, red);
+    const double bsum = block_sum_d((double)s_w, red);
+    if (threadIdx.x == 0) {
+        part[2 * blockIdx.x] = a;
+        part[2 * blockIdx.x + 1] = bsum;
+    }
+}
+
+// channels-last, C % 8 == 0: one thread per 8 consecutive classes of one pixel
+template <typename T>
+__global__ void __launch_bounds__(256) ce_bwd_cl8(const T *__restrict__ x, Dims d, const int64_t *__restrict__ tgt,
+                                                  int ignore, const float *__restrict__ cw,
+                                                  const float *__restrict__ lse, const float *__restrict__ loss,
+                                                  const float *__restrict__ gloss, T *__restrict__ gx, int nchunks) {
+    const int r = blockIdx.x * 256 + threadIdx.x;
+    if (r >= nchunks) return;
+    const int C8 = d.C >> 3;
+    const int p = r / C8, c0 = (r - p * C8) * 8;
+    const long t = tgt[p];
+    float g[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (t != ignore && t >= 0 && t < d.C) {
+        const float gs = gloss[0] / loss[1] * (cw ? cw[t] : 1.f), l = lse[p];
+        float v[8];
+        V8<T>::ld(x + (long)r * 8, v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) g[j] = gs * (expf(v[j] - l) - (c0 + j == t ? 1.f : 0.f));
+    }
+    V8<T>::st(gx + (long)r * 8, g);
+}
+
+// 0 = NCHW-contiguous, 1 = channels-last-contiguous, -1 = neither (strides of size-1
+// dims are ignored, as torch's is_contiguous does)
 int layout_of(const int64_t *s, int B, int C, int H, int W) {
-    (void)B;
-    if (s[3] == 1 && s[2] == W && s[1] == (int64_t)H * W && s[0] == (int64_t)C * H * W) return 0;
-    if (s[1] == 1 && s[3] == C && s[2] == (int64_t)W * C && s[0] == (int64_t)H * W * C) return 1;
-    if (C == 1 || (H == 1 && W == 1)) return 0;  // degenerate: both layouts coincide
-    return -1;
+    const bool nchw = (W == 1 || s[3] == 1) && (H == 1 || s[2] == W) && (C == 1 || s[1] == (int64_t)H * W) &&
+                      (B == 1 || s[0] == (int64_t)C * H * W);
+    if (nchw) return 0;
+    const bool cl = (C == 1 || s[1] == 1) && (W == 1 || s[3] == C) && (H == 1 || s[2] == (int64_t)W * C) &&
+                    (B == 1 || s[0] == (int64_t)H * W * C);
+    return cl ? 1 : -1;
 }
 
 }  // namespace
@@ -277,6 +481,7 @@ int layout_of(const int64_t *s, int B, int C, int H, int W) {
 using namespace irads;
 
 static bool small_enough(long n) { return n < (1L << 31); }
+static bool aligned16(const void *a, const void *b) { return ((uintptr_t)a % 16 == 0) && ((uintptr_t)b % 16 == 0); }
 
 extern "C" int irads_resize_fwd(int dtype, const void *in, const int64_t *in_strides, int B, int C, int h, int w,
                                 void *out, const int64_t *out_strides, int H, int W, void *stream) {
@@ -291,6 +496,15 @@ extern "C" int irads_resize_fwd(int dtype, const void *in, const int64_t *in_str
     hipStream_t st = (hipStream_t)stream;
     const Dims di{B, C, h, w}, dout{B, C, H, W};
     const float sh = (float)h / (float)H, sw = (float)w / (float)W;  // area_pixel_compute_scale
+    if (cl && C % 8 == 0 && aligned16(in, out)) {
+        const int g8 = walk8_grid(B, H, W, C);
+        if (dtype == IRADS_F32)
+            resize_fwd_cl8<float><<<g8, 256, 0, st>>>((const float *)in, di, (float *)out, dout, sh, sw);
+        else
+            resize_fwd_cl8<unsigned short><<<g8, 256, 0, st>>>((const unsigned short *)in, di, (unsigned short *)out,
+                                                               dout, sh, sw);
+        return check_launch("irads_resize_fwd");
+    }
     const int grid = cl ? walk_grid<true>(dout) : walk_grid<false>(dout);
     if (dtype == IRADS_F32) {
         if (cl) resize_fwd<float, true><<<grid, 256, 0, st>>>((const float *)in, di, (float *)out, dout, sh, sw);
@@ -319,8 +533,19 @@ extern "C" int irads_resize_bwd(int dtype, const void *grad_out, const int64_t *
     const Dims dg{B, C, H, W}, dt{B, C, h, W}, di{B, C, h, w};
     const float sh = (float)h / (float)H, sw = (float)w / (float)W;
     const float ish = (float)H / (float)h, isw = (float)W / (float)w;
-    int grid = cl ? walk_grid<true>(dt) : walk_grid<false>(dt);
     using U = unsigned short;
+    if (cl && C % 8 == 0 && aligned16(grad_out, grad_in) && aligned16(workspace, workspace)) {
+        const int ga = walk8_grid(B, h, W, C), gb = walk8_grid(B, h, w, C);
+        if (dtype == IRADS_F32) {
+            resize_bwd_rows_cl8<float><<<ga, 256, 0, st>>>((const float *)grad_out, dg, workspace, dt, sh, ish);
+            resize_bwd_cols_cl8<float><<<gb, 256, 0, st>>>(workspace, dt, (float *)grad_in, di, sw, isw);
+        } else {
+            resize_bwd_rows_cl8<U><<<ga, 256, 0, st>>>((const U *)grad_out, dg, workspace, dt, sh, ish);
+            resize_bwd_cols_cl8<U><<<gb, 256, 0, st>>>(workspace, dt, (U *)grad_in, di, sw, isw);
+        }
+        return check_launch("irads_resize_bwd");
+    }
+    int grid = cl ? walk_grid<true>(dt) : walk_grid<false>(dt);
     if (dtype == IRADS_F32) {
         if (cl) resize_bwd_rows<float, true><<<grid, 256, 0, st>>>((const float *)grad_out, dg, workspace, dt, sh, ish);
         else resize_bwd_rows<float, false><<<grid, 256, 0, st>>>((const float *)grad_out, dg, workspace, dt, sh, ish);
@@ -337,6 +562,23 @@ extern "C" int irads_resize_bwd(int dtype, const void *grad_out, const int64_t *
         else resize_bwd_cols<U, false><<<grid, 256, 0, st>>>(workspace, dt, (U *)grad_in, di, sw, isw);
     }
     return check_launch("irads_resize_bwd");
+}
+
+template <typename T>
+static void launch_ce_fwd_cl8(int C, size_t sm, hipStream_t st, const void *x, Dims d, const int64_t *tgt, int ignore,
+                              const float *cw, float *lse, int64_t *match, double *part) {
+    const T *xp = (const T *)x;
+#define CE_CL8(CM)                                                                                             \
+    {                                                                                                          \
+        (void)hipFuncSetAttribute((const void *)ce_fwd_cl8<T, CM>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                  (int)sm);                                                                    \
+        ce_fwd_cl8<T, CM><<<CE_GRID, 256, sm, st>>>(xp, d, tgt, ignore, cw, lse, match, part);                 \
+    }
+    if (C <= 16) CE_CL8(16)
+    else if (C <= 32) CE_CL8(32)
+    else if (C <= 64) CE_CL8(64)
+    else CE_CL8(128)
+#undef CE_CL8
 }
 
 template <typename T, bool CL>
@@ -363,7 +605,15 @@ extern "C" int irads_ce_fwd(int dtype, const void *logits, const int64_t *stride
     const Dims d{B, C, H, W};
     const bool cl = lay == 1;
     using U = unsigned short;
-    if (dtype == IRADS_F32) {
+    if (cl && C % 8 == 0 && aligned16(logits, logits)) {
+        const size_t sm = (size_t)256 * C * (dtype == IRADS_F32 ? 4 : 2);
+        if (dtype == IRADS_F32)
+            launch_ce_fwd_cl8<float>(C, sm, st, logits, d, target, ignore_index, class_weight, lse, match_target,
+                                     workspace);
+        else
+            launch_ce_fwd_cl8<U>(C, sm, st, logits, d, target, ignore_index, class_weight, lse, match_target,
+                                 workspace);
+    } else if (dtype == IRADS_F32) {
         if (cl) launch_ce_fwd<float, true>(C, st, logits, d, target, ignore_index, class_weight, lse, match_target, workspace);
         else launch_ce_fwd<float, false>(C, st, logits, d, target, ignore_index, class_weight, lse, match_target, workspace);
     } else {
@@ -385,8 +635,18 @@ extern "C" int irads_ce_bwd(int dtype, const void *logits, const int64_t *stride
     hipStream_t st = (hipStream_t)stream;
     const Dims d{B, C, H, W};
     const bool cl = lay == 1;
-    const int grid = cl ? walk_grid<true>(d) : walk_grid<false>(d);
     using U = unsigned short;
+    if (cl && C % 8 == 0 && aligned16(logits, grad_logits)) {
+        const int nchunks = (int)((long)B * H * W * (C / 8)), g8 = (nchunks + 255) / 256;
+        if (dtype == IRADS_F32)
+            ce_bwd_cl8<float><<<g8, 256, 0, st>>>((const float *)logits, d, target, ignore_index, class_weight, lse,
+                                                  loss, grad_loss, (float *)grad_logits, nchunks);
+        else
+            ce_bwd_cl8<U><<<g8, 256, 0, st>>>((const U *)logits, d, target, ignore_index, class_weight, lse, loss,
+                                              grad_loss, (U *)grad_logits, nchunks);
+        return check_launch("irads_ce_bwd");
+    }
+    const int grid = cl ? walk_grid<true>(d) : walk_grid<false>(d);
     if (dtype == IRADS_F32) {
         if (cl)
             ce_bwd<float, true><<<grid, 256, 0, st>>>((const float *)logits, d, target, ignore_index, class_weight,

@@ -136,11 +136,12 @@ def test_cross_entropy_weights_and_grad_scale():
     close(xg.grad, xd.grad, 1e-7, 1e-5, "weighted CE bwd")
 
 
-def test_cross_entropy_bf16():
+@pytest.mark.parametrize("cl", [False, True])
+def test_cross_entropy_bf16(cl):
     """bf16 logits (the reference's AMP path casts them to fp32 before the loss)."""
     ops = _ops()
     B, C, H, W = 2, 40, 32, 48
-    x = (_rand((B, C, H, W), 40) * 4).to(torch.bfloat16)
+    x = _fmt((_rand((B, C, H, W), 40) * 4).to(torch.bfloat16), cl)
     t = _targets(B, H, W, C, 41)
     xd = x.double().requires_grad_(True)
     ref = F.cross_entropy(xd, t, ignore_index=255)
