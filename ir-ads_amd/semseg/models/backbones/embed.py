@@ -9,6 +9,8 @@ from typing import Sequence
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..layers.common import Linear
+
 
 def _pair(x):
     return tuple(x) if isinstance(x, (tuple, list)) else (x, x)
@@ -98,7 +100,7 @@ class PatchMerging(nn.Module):
         self.sampler = nn.Unfold(kernel_size=kernel_size, dilation=dilation, padding=padding, stride=stride)
         sample_dim = kernel_size[0] * kernel_size[1] * in_channels
         self.norm = nn.LayerNorm(sample_dim) if norm_cfg is not None else None
-        self.reduction = nn.Linear(sample_dim, out_channels, bias=bias)
+        self.reduction = Linear(sample_dim, out_channels, bias=bias)
 
     def forward(self, x, input_size, sub_mode=None):
         B, L, C = x.shape

@@ -29,7 +29,7 @@ import torch.utils.checkpoint as cp
 
 from irads import ops
 
-from ..layers.common import DropPath
+from ..layers.common import DropPath, Linear
 from .embed import PatchEmbed, PatchMerging
 
 
@@ -68,9 +68,9 @@ class WindowMSA(nn.Module):
         rel = coords[:, :, None] - coords[:, None, :]
         index = (rel[0] + Wh - 1) * (2 * Ww - 1) + (rel[1] + Ww - 1)
         self.register_buffer("relative_position_index", index.contiguous())
-        self.qkv = nn.Linear(embed_dims, embed_dims * 3, bias=qkv_bias)
+        self.qkv = Linear(embed_dims, embed_dims * 3, bias=qkv_bias)
         self.attn_drop = nn.Dropout(attn_drop_rate)
-        self.proj = nn.Linear(embed_dims, embed_dims)
+        self.proj = Linear(embed_dims, embed_dims)
         self.proj_drop = nn.Dropout(proj_drop_rate)
         self.softmax = nn.Softmax(dim=-1)
 
@@ -165,8 +165,8 @@ class FFN(nn.Module):
         assert num_fcs == 2, 'only the 2-layer FFN of the reference is supported'
         act = nn.GELU() if act_cfg.get('type', 'GELU') == 'GELU' else nn.ReLU(inplace=True)
         self.layers = nn.Sequential(
-            nn.Sequential(nn.Linear(embed_dims, feedforward_channels), act, nn.Dropout(ffn_drop)),
-            nn.Linear(feedforward_channels, embed_dims), nn.Dropout(ffn_drop))
+            nn.Sequential(Linear(embed_dims, feedforward_channels), act, nn.Dropout(ffn_drop)),
+            Linear(feedforward_channels, embed_dims), nn.Dropout(ffn_drop))
         self.dropout_layer = _build_dropout(dropout_layer)
         self.add_identity = add_identity
 

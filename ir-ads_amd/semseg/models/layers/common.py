@@ -21,3 +21,30 @@ class DropPath(nn.Module):
         keep = 1 - self.p
         mask = (keep + torch.rand((x.shape[0],) + (1,) * (x.ndim - 1), dtype=x.dtype, device=x.device)).floor_()
         return x.div(keep) * mask
+
+
+class Linear(nn.Linear):
+    """nn.Linear that casts a frozen weight to the autocast dtype once instead of per call.
+
+    Under torch.autocast, F.linear casts input, weight and bias to the autocast dtype on
+    every call, and autocast's cast cache only keeps casts of leaf tensors that require
+    grad, so a frozen weight (TRAIN_TYPE Adapter freezes the whole Swin trunk,
+    optimizers.py:7-30) is re-cast at every use.  Here the cast copy is kept and reused;
+    it is the same rounding autocast applies, and it is rebuilt whenever a parameter's
+    version counter moves (optimizer step, load_state_dict, in-place edits).  Outside
+    autocast, or for trainable weights, this is nn.Linear.  State-dict keys unchanged."""
+
+    def forward(self, x: Tensor) -> Tensor:
+        w, b = self.weight, self.bias
+        if (w.requires_grad or (b is not None and b.requires_grad) or not x.is_cuda
+                or not torch.is_autocast_enabled("cuda")):
+            return super().forward(x)
+        dt = torch.get_autocast_dtype("cuda")
+        key = (dt, w.data_ptr(), w._version, None if b is None else b._version)
+        cache = self.__dict__.get("_amp_cache")
+        if cache is None or cache[0] != key:
+            with torch.no_grad():
+                cache = (key, w.to(dt), None if b is None else b.to(dt))
+            self.__dict__["_amp_cache"] = cache
+        with torch.autocast("cuda", enabled=False):
+            return torch.nn.functional.linear(x.to(dt), cache[1], cache[2])
