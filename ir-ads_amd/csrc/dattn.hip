@@ -223,86 +223,130 @@ __global__ void __launch_bounds__(1024) dattn_attn_fwd_kernel(AttnArgs a, float 
     lse[(long)bh * HW + qi] = m + __logf(l);
 }
 
-__device__ __forceinline__ void scatter_lds(float *tg, int Ht, int Wt, const Corner &cr, float ds) {
+// Pass Q (thread per query): dq, delta = dO·O, and the rpe-table gradient.
+//  * The table gradient is accumulated per workgroup in LDS in FIXED POINT with integer
+//    atomics: on gfx950 ds_add_f32 retires ~0.3 lanes/clk/CU whatever the address
+//    pattern, ds_add_u32 ~4 (scripts/microbench/lds_atomic.hip).  The scale is a power of
+//    two per workgroup chosen from a bound on its total contribution: for query q,
+//    Σ_k |ds_qk| = Σ_k p_qk |dp_qk − δ_q| ≤ |δ_q| + Σ_c |dO_qc| · max_k |v_kc|, and the four
+//    bilinear weights of a sample sum to 1, so no cell can exceed B = Σ_q bound_q;
+//    scale = 2^(30 − ⌈log2 B⌉) keeps every partial sum inside int32 with a resolution of
+//    B·2^-31 (fp32 accumulation of the same sums carries 2^-24 relative error).  Each
+//    workgroup flushes its non-zero cells with one float atomic each (consecutive cells:
+//    the coalesced atomic pattern).
+//  * k, v and the key positions are read with wave-uniform addresses (scalar loads), so
+//    LDS holds only the gradient table and two workgroups fit per CU.
+__device__ __forceinline__ void scatter_fx(int *tg, int Ht, int Wt, const Corner &cr, float dsq) {
     const bool xl = cr.x0 >= 0 && cr.x0 < Wt, xh = cr.x0 + 1 >= 0 && cr.x0 + 1 < Wt;
     const bool yl = cr.y0 >= 0 && cr.y0 < Ht, yh = cr.y0 + 1 >= 0 && cr.y0 + 1 < Ht;
     const int o = cr.y0 * Wt + cr.x0;
-    if (yl && xl) atomicAdd(&tg[o], cr.nw * ds);
-    if (yl && xh) atomicAdd(&tg[o + 1], cr.ne * ds);
-    if (yh && xl) atomicAdd(&tg[o + Wt], cr.sw * ds);
-    if (yh && xh) atomicAdd(&tg[o + Wt + 1], cr.se * ds);
+    if (yl && xl) atomicAdd(&tg[o], __float2int_rn(cr.nw * dsq));
+    if (yl && xh) atomicAdd(&tg[o + 1], __float2int_rn(cr.ne * dsq));
+    if (yh && xl) atomicAdd(&tg[o + Wt], __float2int_rn(cr.sw * dsq));
+    if (yh && xh) atomicAdd(&tg[o + Wt + 1], __float2int_rn(cr.se * dsq));
 }
 
-// Pass Q (thread per query): dq, delta = dO·O, and the rpe-table gradient.  The 64
-// lanes of a wave are consecutive queries of one row, so for a fixed key their table
-// cells share a row and step ~0.6 cell per lane: the LDS atomics land on consecutive
-// addresses (near conflict-free).  The table itself is read through L1/L2 (a head's
-// 75.7 KB table is shared by every workgroup of that head); LDS holds the gradient.
-// LDS: tgrad[TT] | kv[2n][2*HC] | pos[2n][2]
+__device__ __forceinline__ float block_sum_f(float v, float *red) {
+    v = wave_sum(v);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    __syncthreads();
+    if (lane == 0) red[wave] = v;
+    __syncthreads();
+    float s = 0.f;
+    for (int k = 0; k < nw; ++k) s += red[k];
+    return s;
+}
+
+// LDS: tgrad[TT] (int32 fixed point)
 template <int HC>
-__global__ void __launch_bounds__(1024) dattn_attn_bwd_q_kernel(AttnArgs a, const float *__restrict__ out,
-                                                                const float *__restrict__ lse,
-                                                                const float *__restrict__ gout,
-                                                                float *__restrict__ delta, float *__restrict__ gq,
-                                                                float *__restrict__ grpe) {
-    extern __shared__ __attribute__((aligned(16))) float sm[];
+__global__ void __launch_bounds__(512) dattn_attn_bwd_q_kernel(AttnArgs a, const float *__restrict__ out,
+                                                               const float *__restrict__ lse,
+                                                               const float *__restrict__ gout,
+                                                               float *__restrict__ delta, float *__restrict__ gq,
+                                                               float *__restrict__ grpe) {
+    extern __shared__ __attribute__((aligned(16))) int tgi[];
+    __shared__ float red[8], vmx[8][HC];
     const int n2 = 2 * a.n, HW = a.H * a.W, TT = a.Ht * a.Wt;
-    float *tg = sm, *kv = sm + TT, *pos = kv + n2 * 2 * HC;
     const int bh = blockIdx.y, b = bh / a.nH, h = bh % a.nH;
     const int gi = h / (a.nH / a.G);
     const float *tab = a.rpe + (long)h * TT;
-    for (int i = threadIdx.x; i < TT; i += blockDim.x) tg[i] = 0.f;
-    for (int i = threadIdx.x; i < n2 * HC; i += blockDim.x) {
-        const int c = i / n2, j = i % n2;
-        kv[j * 2 * HC + c] = a.k[((long)bh * HC + c) * n2 + j];
-        kv[j * 2 * HC + HC + c] = a.v[((long)bh * HC + c) * n2 + j];
-    }
-    for (int j = threadIdx.x; j < n2; j += blockDim.x) {
-        const float *p = (j < a.n ? a.px : a.py) + ((long)(b * a.G + gi) * a.n + (j % a.n)) * 2;
-        pos[2 * j] = p[0];
-        pos[2 * j + 1] = p[1];
+    const float *kb = a.k + (long)bh * HC * n2, *vb = a.v + (long)bh * HC * n2;
+    const float *pxb = a.px + (long)(b * a.G + gi) * a.n * 2, *pyb = a.py + (long)(b * a.G + gi) * a.n * 2;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    for (int i = tid; i < TT; i += blockDim.x) tgi[i] = 0;
+    // max_k |v_kc| per channel
+    float vm[HC];
+#pragma unroll
+    for (int c = 0; c < HC; ++c) vm[c] = 0.f;
+    for (int j = tid; j < n2; j += blockDim.x)
+#pragma unroll
+        for (int c = 0; c < HC; ++c) vm[c] = fmaxf(vm[c], fabsf(vb[c * n2 + j]));
+#pragma unroll
+    for (int c = 0; c < HC; ++c) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) vm[c] = fmaxf(vm[c], __shfl_xor(vm[c], o, 64));
+        if (lane == 0) vmx[wave][c] = vm[c];
     }
     __syncthreads();
-    const int qi = blockIdx.x * blockDim.x + threadIdx.x;
-    if (qi < HW) {
-        const float qgy = a.qgy[qi / a.W], qgx = a.qgx[qi % a.W];
-        float qv[HC], dq[HC], dov[HC];
-        float dl = 0.f;
 #pragma unroll
-        for (int c = 0; c < HC; ++c) {
+    for (int c = 0; c < HC; ++c) {
+        vm[c] = 0.f;
+        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) vm[c] = fmaxf(vm[c], vmx[w][c]);
+    }
+    const int qi = blockIdx.x * blockDim.x + tid;
+    const bool valid = qi < HW;
+    float qv[HC], dq[HC], dov[HC];
+    float dl = 0.f, bound = 0.f, qgy = 0.f, qgx = 0.f, ls = 0.f;
+#pragma unroll
+    for (int c = 0; c < HC; ++c) {
+        qv[c] = dov[c] = dq[c] = 0.f;
+        if (valid) {
             const long o = ((long)bh * HC + c) * HW + qi;
             qv[c] = a.q[o];
             dov[c] = gout[o];
             dl = fmaf(dov[c], out[o], dl);
-            dq[c] = 0.f;
         }
-        const float ls = lse[(long)bh * HW + qi];
+    }
+    if (valid) {
+        qgy = a.qgy[qi / a.W];
+        qgx = a.qgx[qi % a.W];
+        ls = lse[(long)bh * HW + qi];
+        bound = fabsf(dl);
+#pragma unroll
+        for (int c = 0; c < HC; ++c) bound = fmaf(fabsf(dov[c]), vm[c], bound);
+    }
+    const float btot = block_sum_f(bound, red);
+    // fixed-point scale 2^e with btot·2^e <= 2^30 (exact power of two: scaling and unscaling are exact)
+    const int e = (btot > 0.f && btot < 1e30f) ? min(100, 30 - (int)ceilf(log2f(btot))) : 0;
+    const float fx = ldexpf(1.f, e), inv_fx = ldexpf(1.f, -e);
+    if (valid) {
         for (int j = 0; j < n2; ++j) {
-            const float *kr = kv + j * 2 * HC;
-            float s = 0.f, dp = 0.f;
+            float kr[HC], s = 0.f, dp = 0.f;
 #pragma unroll
             for (int c = 0; c < HC; ++c) {
+                kr[c] = kb[c * n2 + j];
                 s = fmaf(qv[c], kr[c], s);
-                dp = fmaf(dov[c], kr[HC + c], dp);
+                dp = fmaf(dov[c], vb[c * n2 + j], dp);
             }
+            const float *pp = (j < a.n ? pxb : pyb) + 2 * (j < a.n ? j : j - a.n);
             Corner cr;
             Taps tp;
-            s = s * a.scale + rpe_bias(tab, a.Ht, a.Wt, qgy, qgx, pos[2 * j], pos[2 * j + 1], cr, tp);
+            s = s * a.scale + rpe_bias(tab, a.Ht, a.Wt, qgy, qgx, pp[0], pp[1], cr, tp);
             const float p = __expf(s - ls);
             const float ds = p * (dp - dl);
             const float dss = ds * a.scale;
 #pragma unroll
             for (int c = 0; c < HC; ++c) dq[c] = fmaf(dss, kr[c], dq[c]);
-            scatter_lds(tg, a.Ht, a.Wt, cr, ds);
+            scatter_fx(tgi, a.Ht, a.Wt, cr, ds * fx);
         }
 #pragma unroll
         for (int c = 0; c < HC; ++c) gq[((long)bh * HC + c) * HW + qi] = dq[c];
         delta[(long)bh * HW + qi] = dl;
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < TT; i += blockDim.x) {
-        const float v = tg[i];
-        if (v != 0.f) atomicAdd(&grpe[(long)h * TT + i], v);
+    for (int i = tid; i < TT; i += blockDim.x) {
+        const int v = tgi[i];
+        if (v != 0) atomicAdd(&grpe[(long)h * TT + i], (float)v * inv_fx);
     }
 }
 
@@ -510,10 +554,11 @@ extern "C" int irads_dattn_attn_bwd(const float *q, const float *k, const float 
     if (B == 0) return IRADS_OK;
     hipStream_t st = (hipStream_t)stream;
     const int HW = H * W;
-    const size_t sh_q = ((size_t)Ht * Wt + (size_t)2 * n * 2 * hc + (size_t)2 * n * 2) * sizeof(float);
+    const size_t sh_q = (size_t)Ht * Wt * sizeof(int);
     const size_t sh_k = (size_t)QCH * (2 * hc + 4) * sizeof(float);
     IRADS_REQUIRE(sh_q <= 160 * 1024 && sh_k <= 160 * 1024, "dattn_attn_bwd: LDS request exceeds 160 KiB");
-    const int bs = attn_block(HW);
+    // pass Q: 512 queries per workgroup, or 256 when that leaves the chip under-filled
+    const int bs = ((long)((HW + 511) / 512) * B * nH >= 512) ? 512 : 256;
     dim3 gq_grid((HW + bs - 1) / bs, B * nH);
     // pass K: one thread per key; enough query chunks per (b, h) to fill the chip
     const int kthreads = ((2 * n + 63) / 64) * 64;

@@ -1,0 +1,96 @@
+"""Per-kernel timing of the hot-path ops at the C2 (Swin-B, 512², batch 8, rgb+dte) shapes.
+
+    python scripts/kbench.py [--only winattn,dattn,seghead] [--reps 20]
+
+Each op is timed with HIP events around `reps` back-to-back calls on synthetic inputs,
+after a warmup; the line reports µs per call and the algorithmic bytes / flops rate.
+"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "ir-ads_amd"))
+
+import torch  # noqa: E402
+
+from irads import ops  # noqa: E402
+
+DEV = "cuda"
+
+
+def timeit(fn, reps):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) * 1e3 / reps
+
+
+def winattn(reps):
+    # stage (tokens per side, C, heads): Swin-B at 512² input, rgb+dte batched (B = 16)
+    for side, C, nH in ((128, 128, 4), (64, 256, 8), (32, 512, 16), (16, 1024, 32)):
+        B = 16
+        L = side * side
+        qkv = (torch.randn(B, L, 3 * C, device=DEV) * 0.5).bfloat16().requires_grad_()
+        bias = torch.randn(3 * C, device=DEV) * 0.1
+        table = torch.randn(23 * 23, nH, device=DEV) * 0.1
+        for shift in (0, 6):
+            out = ops.window_attention(qkv, bias, table, None, side, side, nH, shift, 32 ** -0.5)
+            g = torch.randn_like(out)
+            tf = timeit(lambda: ops.window_attention(qkv, bias, table, None, side, side, nH, shift, 32 ** -0.5), reps)
+            tb = timeit(lambda: torch.autograd.grad(out, qkv, g, retain_graph=True), reps)
+            fb, bb = B * L * 4 * C * 2, B * L * 9 * C * 2
+            print(f"winattn side={side:3d} C={C:4d} shift={shift}: fwd {tf:7.1f} us ({fb / tf / 1e3:6.0f} GB/s)  "
+                  f"bwd {tb:7.1f} us ({bb / tb / 1e3:6.0f} GB/s)", flush=True)
+
+
+def dattn(reps):
+    from semseg.models.backbones.swin import DAttentionMM
+    for lvl, (side, dims, stride, groups, heads) in enumerate(((128, 16, 8, 1, 2), (64, 32, 4, 2, 4),
+                                                                (32, 64, 2, 4, 8), (16, 128, 1, 8, 16))):
+        m = DAttentionMM(dims, q_size=(60, 80), stride=stride, n_groups=groups, n_heads=heads, level=lvl).to(DEV)
+        x = torch.randn(8, dims, side, side, device=DEV, requires_grad=True)
+        y = torch.randn(8, dims, side, side, device=DEV, requires_grad=True)
+        out = m(x, y)
+        out = out[0] if isinstance(out, tuple) else out
+        g = torch.randn_like(out)
+        tf = timeit(lambda: m(x, y), reps)
+        tb = timeit(lambda: torch.autograd.grad(out, [x, y] + list(m.parameters()), g, retain_graph=True,
+                                                allow_unused=True), reps)
+        print(f"dattn level={lvl} side={side}: module fwd {tf:8.1f} us  bwd {tb:8.1f} us", flush=True)
+
+
+def seghead(reps):
+    x = torch.randn(8, 40, 128, 128, device=DEV).bfloat16().contiguous(memory_format=torch.channels_last)
+    x.requires_grad_()
+    t = torch.randint(0, 40, (8, 512, 512), device=DEV)
+    up = ops.resize(x, (512, 512))
+    g = torch.randn_like(up)
+    tf = timeit(lambda: ops.resize(x, (512, 512)), reps)
+    tb = timeit(lambda: torch.autograd.grad(up, x, g, retain_graph=True), reps)
+    print(f"resize 128->512 x40 bf16 CL: fwd {tf:6.1f} us ({up.numel() * 2 / tf / 1e3:5.0f} GB/s)  bwd {tb:6.1f} us")
+    upd = up.detach().requires_grad_()
+    loss = ops.cross_entropy(upd, t, 255)
+    tf = timeit(lambda: ops.cross_entropy(upd, t, 255), reps)
+    tb = timeit(lambda: torch.autograd.grad(loss, upd, retain_graph=True), reps)
+    print(f"cross_entropy 8x40x512² bf16 CL: fwd {tf:6.1f} us ({(upd.numel() * 2 + t.numel() * 12) / tf / 1e3:5.0f} "
+          f"GB/s)  bwd {tb:6.1f} us ({upd.numel() * 4 / tb / 1e3:5.0f} GB/s)")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="winattn,dattn,seghead")
+    ap.add_argument("--reps", type=int, default=20)
+    a = ap.parse_args()
+    for name in a.only.split(","):
+        globals()[name](a.reps)
+
+
+if __name__ == "__main__":
+    main()

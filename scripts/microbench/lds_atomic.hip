@@ -6,8 +6,15 @@
 
 #define CHECK(x) (void)(x)
 
-__global__ void __launch_bounds__(1024) k(int pattern, int atomic, int iters, float *out, long long *cyc) {
+// atomic: 0 = ds_write, 1 = ds_add_f32, 2 = ds_add_u32, 3 = ds_add_u64,
+//         4 = global_atomic_add_f32 (no return) into a per-CU 19200-float slab,
+//         5 = global_atomic_add_f32 into ONE slab shared by all CUs
+__global__ void __launch_bounds__(1024) k(int pattern, int atomic, int iters, float *out, long long *cyc,
+                                          float *gslab) {
     __shared__ float tg[19200];
+    unsigned *tu = (unsigned *)tg;
+    unsigned long long *tl = (unsigned long long *)tg;
+    float *gs = gslab + (atomic == 4 ? (long)blockIdx.x * 19200 : 0);
     for (int i = threadIdx.x; i < 19200; i += 1024) tg[i] = 0.f;
     __syncthreads();
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -28,8 +35,12 @@ __global__ void __launch_bounds__(1024) k(int pattern, int atomic, int iters, fl
     for (int it = 0; it < iters; it += 8) {
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-            if (atomic) atomicAdd(&tg[addr[u] + (it & 63)], 1.0f);
-            else tg[addr[u] + (it & 63)] = (float)it;
+            const int a = addr[u] + (it & 63);
+            if (atomic == 0) tg[a] = (float)it;
+            else if (atomic == 1) atomicAdd(&tg[a], 1.0f);
+            else if (atomic == 2) atomicAdd(&tu[a], 3u);
+            else if (atomic == 3) atomicAdd(&tl[a >> 1], 3ull);
+            else __hip_atomic_fetch_add(&gs[a], 1.0f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
     __syncthreads();
@@ -41,21 +52,23 @@ __global__ void __launch_bounds__(1024) k(int pattern, int atomic, int iters, fl
 }
 
 int main() {
-    float *out;
+    float *out, *gslab;
     long long *cyc;
     CHECK(hipMalloc(&out, 4));
     CHECK(hipMalloc(&cyc, 256 * 8));
+    CHECK(hipMalloc(&gslab, 256L * 19200 * 4));
+    const char *ops[] = {"ds_write", "ds_add_f32", "ds_add_u32", "ds_add_u64", "glb_add_f32", "glb_shared"};
     const char *names[] = {"consecutive", "0.62 cell/lane", "scattered", "same address", "stride 159"};
-    for (int atomic = 0; atomic < 2; ++atomic)
+    for (int atomic = 0; atomic < 6; ++atomic)
         for (int p = 0; p < 5; ++p) {
-            const int iters = 8192;
-            k<<<256, 1024>>>(p, atomic, 64, out, cyc);
-            k<<<256, 1024>>>(p, atomic, iters, out, cyc);
+            const int iters = atomic >= 4 ? 1024 : 8192;
+            k<<<256, 1024>>>(p, atomic, 64, out, cyc, gslab);
+            k<<<256, 1024>>>(p, atomic, iters, out, cyc, gslab);
             CHECK(hipDeviceSynchronize());
             long long c;
             CHECK(hipMemcpy(&c, cyc, 8, hipMemcpyDeviceToHost));
             printf("%-10s %-16s %7.1f cycles per wave-instruction per CU  (%5.1f lanes/clk/CU)\n",
-                   atomic ? "ds_add_f32" : "ds_write", names[p], (double)c / (16.0 * iters),
+                   ops[atomic], names[p], (double)c / (16.0 * iters),
                    16.0 * iters * 64 / (double)c);
         }
     return 0;
