@@ -192,6 +192,7 @@ def main():
         avg_ms = fwd["total_ms"] / fwd["launches"]
         per_launch_bytes = fwd["bytes"] / fwd["launches"]
         achieved = fwd["bytes"] / (fwd["total_ms"] * 1e-3) / 1e9
+        achieved_real = fwd["real_bytes"] / (fwd["total_ms"] * 1e-3) / 1e9
         traffic = traffic_from_profile()
         result["roofline"] = {
             "kernel": "irads_winattn_fwd (bf16, Swin-B shifted-window attention, all 4 stages x 2 streams)",
@@ -199,6 +200,8 @@ def main():
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
             "launches": fwd["launches"], "avg_launch_ms": round(avg_ms, 5),
             "algorithmic_bytes_per_launch": round(per_launch_bytes),
+            "bytes_definition": "SURVEY §8(d): read q,k,v + write o per padded token (8·Np·C bytes, bf16)",
+            "achieved_real_tokens_gbs": round(achieved_real, 1),
             "mfma_tflops": round(fwd["flops"] / (fwd["total_ms"] * 1e-3) / 1e12, 2)}
         if bwd:
             ab = bwd["bytes"] / (bwd["total_ms"] * 1e-3) / 1e9

@@ -23,7 +23,7 @@ class LaunchTimer:
 
     def __init__(self):
         self.enabled = set()
-        self.records = []  # (name, start_event, end_event, algorithmic_bytes, flops)
+        self.records = []  # (name, start_event, end_event, algorithmic_bytes, flops, real_token_bytes)
 
     def start(self, name):
         if name not in self.enabled:
@@ -32,12 +32,12 @@ class LaunchTimer:
         ev.record()
         return ev
 
-    def stop(self, name, ev, nbytes, flops):
+    def stop(self, name, ev, nbytes, flops, real_bytes=None):
         if ev is None:
             return
         end = torch.cuda.Event(enable_timing=True)
         end.record()
-        self.records.append((name, ev, end, nbytes, flops))
+        self.records.append((name, ev, end, nbytes, flops, nbytes if real_bytes is None else real_bytes))
 
     def summary(self, name):
         torch.cuda.synchronize()
@@ -46,7 +46,7 @@ class LaunchTimer:
             return None
         ms = [r[1].elapsed_time(r[2]) for r in rec]
         return {"launches": len(rec), "total_ms": sum(ms), "bytes": sum(r[3] for r in rec),
-                "flops": sum(r[4] for r in rec)}
+                "flops": sum(r[4] for r in rec), "real_bytes": sum(r[5] for r in rec)}
 
 
 TIMER = LaunchTimer()
@@ -75,9 +75,11 @@ class WindowAttentionFn(torch.autograd.Function):
         ev = TIMER.start("winattn_fwd")
         N.call("irads_winattn_fwd", code, N.ptr(qkv), N.ptr(bias_f), N.ptr(table_f), N.ptr(mask_f), n_mask, B, H, W,
                C, num_heads, shift, float(scale), N.ptr(out), N.ptr(lse), N.stream())
-        # algorithmic work: read q, k, v and write o for every real token; 4·N²·32 flops per (window, head)
-        TIMER.stop("winattn_fwd", ev, B * L * 4 * C * qkv.element_size(),
-                   4 * (WINDOW * WINDOW) ** 2 * HEAD_DIM * B * nW * num_heads)
+        # algorithmic work: read q, k, v and write o for every PADDED token
+        # (8·Np·C bytes in bf16); 4·N²·32 flops per (window, head).  Real-token bytes kept too.
+        es = qkv.element_size()
+        TIMER.stop("winattn_fwd", ev, B * Hp * Wp * 4 * C * es, 4 * (WINDOW * WINDOW) ** 2 * HEAD_DIM * B * nW * num_heads,
+                   B * L * 4 * C * es)
         ctx.save_for_backward(qkv, bias_f, table_f, mask_f, out, lse)
         ctx.cfg = (code, n_mask, B, H, W, C, num_heads, shift, float(scale))
         ctx.need = (qkv_bias is not None and ctx.needs_input_grad[1], ctx.needs_input_grad[2])
@@ -96,11 +98,14 @@ class WindowAttentionFn(torch.autograd.Function):
         N.call("irads_winattn_bwd", code, N.ptr(qkv), N.ptr(bias_f), N.ptr(table_f), N.ptr(mask_f), n_mask, B, H, W,
                C, nH, shift, scale, N.ptr(out), N.ptr(lse), N.ptr(gout), N.ptr(gqkv), N.ptr(gtable), N.ptr(gbias),
                N.stream())
-        # algorithmic: read q, k, v, o, dO and write dq, dk, dv per real token; 8·N²·32 flops
+        # algorithmic: read q, k, v, o, dO and write dq, dk, dv per padded token;
+        # 8·N²·32 flops per (window, head)
         L = H * W
-        nW = (-(-H // WINDOW)) * (-(-W // WINDOW))
-        TIMER.stop("winattn_bwd", ev, B * L * 9 * C * qkv.element_size(),
-                   8 * (WINDOW * WINDOW) ** 2 * HEAD_DIM * B * nW * nH)
+        Hp, Wp = -(-H // WINDOW) * WINDOW, -(-W // WINDOW) * WINDOW
+        nW = (Hp // WINDOW) * (Wp // WINDOW)
+        es = qkv.element_size()
+        TIMER.stop("winattn_bwd", ev, B * Hp * Wp * 8 * C * es, 8 * (WINDOW * WINDOW) ** 2 * HEAD_DIM * B * nW * nH,
+                   B * L * 8 * C * es)
         if gtable is not None:
             gtable = gtable.to(ctx.table_dtype)
         return gqkv, gbias, gtable, None, None, None, None, None, None

@@ -19,12 +19,30 @@ def short(name, n=90):
     return name if len(name) <= n else name[:n - 3] + "..."
 
 
+CATS = [("irads::winattn", "winattn (HIP)"), ("irads::dattn", "dattn (HIP)"), ("irads::msda", "msda (HIP)"),
+        ("irads::resize", "resize (HIP)"), ("irads::ce_", "cross-entropy (HIP)"), ("irads::", "other HIP"),
+        ("Cijk_", "GEMM (hipBLASLt/Tensile)"), ("ck::", "conv (CK)"), ("miopen", "conv (MIOpen)"),
+        ("naive_conv", "conv (MIOpen naive)"), ("igemm", "conv (MIOpen igemm)"), ("layer_norm", "layer norm"),
+        ("cuComputeGrad", "layer norm"), ("bfloat16_copy", "cast fp32->bf16"), ("bfloat16tofloat32", "cast bf16->fp32"),
+        ("adam", "optimizer"), ("reduce_kernel", "reductions"), ("batch_norm", "batch norm"),
+        ("Gelu", "gelu"), ("elementwise", "elementwise"), ("rocclr", "runtime copy/fill")]
+
+
+def category(name):
+    low = name.lower()
+    for pat, cat in CATS:
+        if pat.lower() in low:
+            return cat
+    return "other"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--top", type=int, default=30)
     ap.add_argument("--match", default=None)
+    ap.add_argument("--categories", action="store_true", help="group kernels into coarse categories")
     a = ap.parse_args()
     op = gzip.open if a.trace.endswith(".gz") else open
     with op(a.trace, "rt") as f:
@@ -45,6 +63,13 @@ def main():
     print(f"kernel time per step: {allms / a.steps:.2f} ms  ({len(rows) / a.steps:.0f} launches/step)")
     for k, v in sorted(tot.items(), key=lambda kv: -kv[1])[:a.top]:
         print(f"{v / a.steps:8.3f} ms  {cnt[k] / a.steps:6.1f}x  {short(k)}")
+    if a.categories:
+        cats = collections.defaultdict(float)
+        for k, v in tot.items():
+            cats[category(short(k, 400))] += v
+        print("-- by category (ms/step)")
+        for k, v in sorted(cats.items(), key=lambda kv: -kv[1]):
+            print(f"{v / a.steps:8.3f}  {k}")
     if a.match:
         groups = collections.defaultdict(list)
         for r in rows:
