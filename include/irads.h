@@ -164,6 +164,52 @@ int irads_ce_bwd(int dtype, const void *logits, const int64_t *strides, int B, i
                  const int64_t *target, int ignore_index, const float *class_weight, const float *lse,
                  const float *loss, const float *grad_loss, void *grad_logits, void *stream);
 
+/* ------------------------------------------------------------------ fused Swin block row kernels
+ * The non-GEMM work of SwinBlockAdapter.forward under bf16 autocast (swin.py:584-610:
+ * residual adds, DropPath (:254, mmcv FFN dropout_layer), norm1/norm2 LayerNorm, the
+ * fp32<->bf16 casts of the Linear operands, 0.5 * Adapter) as single passes over (M, C)
+ * row-major tensors.  C % 64 == 0 and C/64 in {2,3,4,6,8,12,16,24} (Swin-B/L).  bf16 is
+ * passed as uint16_t storage.  Sample of a row = row / rows_per_sample (DropPath is per
+ * sample).  A NULL optional pointer disables that term.
+ *
+ * Forward: y = x + DP(add1) + bf16(add2_mult * add2)   (fp32; DP(v) = bf16(v * s[sample]),
+ *   s = mask ? 1/keep : 0, identity if add1_scale is NULL)
+ *   x_out = y (fp32), xb_out = bf16(y), and if gamma != NULL: ln_out = bf16(LayerNorm(y)),
+ *   mean / rstd (M fp32) for the backward. */
+int irads_resln_fwd(const float *x, const uint16_t *add1, const float *add1_scale, const uint16_t *add2,
+                    float add2_mult, int M, int C, int rows_per_sample, const float *gamma, const float *beta,
+                    float eps, float *x_out, uint16_t *ln_out, uint16_t *xb_out, float *mean, float *rstd,
+                    void *stream);
+/* Backward: dx = g_res + g_add + LayerNorm_backward(dy; x, mean, rstd, gamma) (fp32; each term
+ *   optional, dy == NULL skips the LayerNorm term).  dx_out = dx; b1_out = DP(bf16(dx)) with
+ *   b1_scale (the gradient of a DropPath'd bf16 branch); b2_out = bf16(b2_mult * bf16(dx)).
+ *   LayerNorm weight/bias gradients are not produced (the trunk is frozen in TRAIN_TYPE
+ *   Adapter, optimizers.py:7-30). */
+int irads_resln_bwd(const uint16_t *dy, const float *x, const float *mean, const float *rstd, const float *gamma,
+                    const float *g_res, const uint16_t *g_add, int M, int C, int rows_per_sample, float *dx_out,
+                    uint16_t *b1_out, const float *b1_scale, uint16_t *b2_out, float b2_mult, void *stream);
+/* bf16 element passes (n elements): GELU (exact erf form, nn.GELU) and its backward;
+ * ReLU + dropout(p) of the Adapter (swin.py:492-497; keep with probability 1-p, scale
+ * 1/(1-p), counter-based draw from `seed`) and its backward from the saved output r. */
+int irads_gelu_fwd(const uint16_t *u, uint16_t *g, long n, void *stream);
+int irads_gelu_bwd(const uint16_t *u, const uint16_t *dg, uint16_t *du, long n, void *stream);
+int irads_relu_dropout_fwd(const uint16_t *a, uint16_t *r, long n, float p, uint64_t seed, void *stream);
+int irads_relu_dropout_bwd(const uint16_t *r, const uint16_t *dr, uint16_t *da, long n, float p, void *stream);
+
+/* ------------------------------------------------------------------ weight-gradient GEMM
+ * D (m x n) fp32 = alpha * A^T B (+ D if accumulate), A (K x m), B (K x n) bf16 row-major with
+ * row strides lda, ldb (multiples of 8, rows 16-byte aligned), m and n multiples of 8.  With
+ * transpose_out, element (i, j) is stored at D[j*m + i].  colsum_a (m) / colsum_b (n), if not
+ * NULL, receive alpha * the column sums (the bias gradient), accumulated likewise.
+ * Replaces the dW = dYᵀX / db = Σ dY of every trainable nn.Linear's backward under autocast
+ * (Adapter, MPG, DeformMPG, SegFormer MLP; swin.py:472-502, 1045-1091, segformer.py:11-18):
+ * split-K over the token dimension, deterministic (fixed-order reduction, no atomics).
+ * workspace: irads_wgrad_workspace(K, m, n) floats. */
+long irads_wgrad_workspace(int K, int m, int n);
+int irads_wgrad(const uint16_t *A, long lda, const uint16_t *B, long ldb, int K, int m, int n, float alpha,
+                int accumulate, int transpose_out, float *D, float *colsum_a, float *colsum_b, float *workspace,
+                void *stream);
+
 #ifdef __cplusplus
 }
 #endif

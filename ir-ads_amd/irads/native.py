@@ -15,6 +15,7 @@ F32, BF16, F64 = 0, 1, 2
 _DT = {torch.float32: F32, torch.bfloat16: BF16, torch.float64: F64}
 
 _vp, _i, _f, _d = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_double
+_l, _u64 = ctypes.c_long, ctypes.c_uint64
 
 # name -> argtypes (every entry returns int)
 SIGNATURES = {
@@ -37,7 +38,16 @@ SIGNATURES = {
     "irads_resize_bwd": [_i, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _vp, _vp],
     "irads_ce_fwd": [_i, _vp, _vp, _i, _i, _i, _i, _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp],
     "irads_ce_bwd": [_i, _vp, _vp, _i, _i, _i, _i, _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp],
+    "irads_resln_fwd": [_vp, _vp, _vp, _vp, _f, _i, _i, _i, _vp, _vp, _f, _vp, _vp, _vp, _vp, _vp, _vp],
+    "irads_resln_bwd": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _vp, _vp, _vp, _vp, _f, _vp],
+    "irads_gelu_fwd": [_vp, _vp, _l, _vp],
+    "irads_gelu_bwd": [_vp, _vp, _vp, _l, _vp],
+    "irads_relu_dropout_fwd": [_vp, _vp, _l, _f, _u64, _vp],
+    "irads_relu_dropout_bwd": [_vp, _vp, _vp, _l, _f, _vp],
+    "irads_wgrad": [_vp, _l, _vp, _l, _i, _i, _i, _f, _i, _i, _vp, _vp, _vp, _vp, _vp],
 }
+# entries that do not return an error code: name -> (restype, argtypes)
+QUERIES = {"irads_wgrad_workspace": (ctypes.c_long, [_i, _i, _i])}
 CE_WORKSPACE = 2048
 
 _lib = None
@@ -59,6 +69,10 @@ def load(require_gpu=False):
             fn = getattr(lib, name)
             fn.argtypes = argt
             fn.restype = ctypes.c_int
+        for name, (rt, argt) in QUERIES.items():
+            fn = getattr(lib, name)
+            fn.argtypes = argt
+            fn.restype = rt
         lib.irads_last_error.restype = ctypes.c_char_p
         lib.irads_last_error.argtypes = []
         lib.irads_version.restype = ctypes.c_int

@@ -53,35 +53,70 @@ TIMER = LaunchTimer()
 
 
 # ------------------------------------------------------------------ window attention
+def _winattn_geometry(H, W):
+    Hp, Wp = -(-H // WINDOW) * WINDOW, -(-W // WINDOW) * WINDOW
+    return Hp, Wp, (Hp // WINDOW) * (Wp // WINDOW)
+
+
+def winattn_fwd(qkv, bias_f, table_f, mask_f, H, W, num_heads, shift, scale):
+    """Raw forward launch: qkv (B, H*W, 3C) contiguous -> (out (B, H*W, C), lse)."""
+    N.check(qkv, "qkv")
+    B, L, C3 = qkv.shape
+    assert L == H * W, "input feature has wrong size"
+    C = C3 // 3
+    code = N.dtype_code(qkv, (N.F32, N.BF16), "window attention qkv")
+    N.check(table_f, "relative_position_bias_table", torch.float32)
+    n_mask = 0 if mask_f is None else int(mask_f.shape[0])
+    out = torch.empty((B, L, C), device=qkv.device, dtype=qkv.dtype)
+    Hp, Wp, nW = _winattn_geometry(H, W)
+    lse = torch.empty((B * nW * num_heads * WINDOW * WINDOW,), device=qkv.device, dtype=torch.float32)
+    ev = TIMER.start("winattn_fwd")
+    N.call("irads_winattn_fwd", code, N.ptr(qkv), N.ptr(bias_f), N.ptr(table_f), N.ptr(mask_f), n_mask, B, H, W,
+           C, num_heads, shift, float(scale), N.ptr(out), N.ptr(lse), N.stream())
+    # algorithmic work (SURVEY §8(d)): read q, k, v and write o for every PADDED token
+    # (8·Np·C bytes in bf16); 4·N²·32 flops per (window, head).  Real-token bytes kept too.
+    es = qkv.element_size()
+    TIMER.stop("winattn_fwd", ev, B * Hp * Wp * 4 * C * es, 4 * (WINDOW * WINDOW) ** 2 * HEAD_DIM * B * nW * num_heads,
+               B * L * 4 * C * es)
+    return out, lse
+
+
+def winattn_bwd(qkv, bias_f, table_f, mask_f, H, W, nH, shift, scale, out, lse, gout, need_bias=False,
+                need_table=False):
+    """Raw backward launch -> (grad_qkv, grad_table or None, grad_bias_pad or None)."""
+    B, L, C3 = qkv.shape
+    C = C3 // 3
+    code = N.dtype_code(qkv, (N.F32, N.BF16), "window attention qkv")
+    n_mask = 0 if mask_f is None else int(mask_f.shape[0])
+    gout = N.check(gout.contiguous().to(qkv.dtype), "grad_out")
+    gqkv = torch.empty_like(qkv)
+    gtable = torch.zeros_like(table_f) if need_table else None
+    gbias = torch.zeros((3 * C,), device=qkv.device, dtype=torch.float32) if need_bias else None
+    ev = TIMER.start("winattn_bwd")
+    N.call("irads_winattn_bwd", code, N.ptr(qkv), N.ptr(bias_f), N.ptr(table_f), N.ptr(mask_f), n_mask, B, H, W,
+           C, nH, shift, float(scale), N.ptr(out), N.ptr(lse), N.ptr(gout), N.ptr(gqkv), N.ptr(gtable), N.ptr(gbias),
+           N.stream())
+    # algorithmic (SURVEY §8(d)): read q, k, v, o, dO and write dq, dk, dv per padded token;
+    # 8·N²·32 flops per (window, head)
+    Hp, Wp, nW = _winattn_geometry(H, W)
+    es = qkv.element_size()
+    TIMER.stop("winattn_bwd", ev, B * Hp * Wp * 8 * C * es, 8 * (WINDOW * WINDOW) ** 2 * HEAD_DIM * B * nW * nH,
+               B * L * 8 * C * es)
+    return gqkv, gtable, gbias
+
+
 class WindowAttentionFn(torch.autograd.Function):
     """ShiftWindowMSA/WindowMSA core between the qkv and proj Linears
     (swin.py:180-254 + :95-116).  qkv: (B, H*W, 3C) token order."""
 
     @staticmethod
     def forward(ctx, qkv, qkv_bias, table, mask, H, W, num_heads, shift, scale):
-        N.check(qkv, "qkv")
-        B, L, C3 = qkv.shape
-        assert L == H * W, "input feature has wrong size"
-        C = C3 // 3
-        code = N.dtype_code(qkv, (N.F32, N.BF16), "window attention qkv")
-        table_f = N.check(table.detach().float().contiguous(), "relative_position_bias_table")
+        table_f = table.detach().float().contiguous()
         bias_f = None if qkv_bias is None else qkv_bias.detach().float().contiguous()
         mask_f = None if mask is None else mask.detach().float().contiguous()
-        n_mask = 0 if mask is None else int(mask.shape[0])
-        out = torch.empty((B, L, C), device=qkv.device, dtype=qkv.dtype)
-        Hp, Wp = -(-H // WINDOW) * WINDOW, -(-W // WINDOW) * WINDOW
-        nW = (Hp // WINDOW) * (Wp // WINDOW)
-        lse = torch.empty((B * nW * num_heads * WINDOW * WINDOW,), device=qkv.device, dtype=torch.float32)
-        ev = TIMER.start("winattn_fwd")
-        N.call("irads_winattn_fwd", code, N.ptr(qkv), N.ptr(bias_f), N.ptr(table_f), N.ptr(mask_f), n_mask, B, H, W,
-               C, num_heads, shift, float(scale), N.ptr(out), N.ptr(lse), N.stream())
-        # algorithmic work (SURVEY §8(d)): read q, k, v and write o for every PADDED token
-        # (8·Np·C bytes in bf16); 4·N²·32 flops per (window, head).  Real-token bytes kept too.
-        es = qkv.element_size()
-        TIMER.stop("winattn_fwd", ev, B * Hp * Wp * 4 * C * es, 4 * (WINDOW * WINDOW) ** 2 * HEAD_DIM * B * nW * num_heads,
-                   B * L * 4 * C * es)
+        out, lse = winattn_fwd(qkv, bias_f, table_f, mask_f, H, W, num_heads, shift, scale)
         ctx.save_for_backward(qkv, bias_f, table_f, mask_f, out, lse)
-        ctx.cfg = (code, n_mask, B, H, W, C, num_heads, shift, float(scale))
+        ctx.cfg = (H, W, num_heads, shift, float(scale))
         ctx.need = (qkv_bias is not None and ctx.needs_input_grad[1], ctx.needs_input_grad[2])
         ctx.table_dtype = table.dtype
         return out
@@ -89,23 +124,9 @@ class WindowAttentionFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gout):
         qkv, bias_f, table_f, mask_f, out, lse = ctx.saved_tensors
-        code, n_mask, B, H, W, C, nH, shift, scale = ctx.cfg
-        gout = gout.contiguous().to(qkv.dtype)
-        gqkv = torch.empty_like(qkv)
-        gtable = torch.zeros_like(table_f) if ctx.need[1] else None
-        gbias = torch.zeros((3 * C,), device=qkv.device, dtype=torch.float32) if ctx.need[0] else None
-        ev = TIMER.start("winattn_bwd")
-        N.call("irads_winattn_bwd", code, N.ptr(qkv), N.ptr(bias_f), N.ptr(table_f), N.ptr(mask_f), n_mask, B, H, W,
-               C, nH, shift, scale, N.ptr(out), N.ptr(lse), N.ptr(gout), N.ptr(gqkv), N.ptr(gtable), N.ptr(gbias),
-               N.stream())
-        # algorithmic: read q, k, v, o, dO and write dq, dk, dv per padded token;
-        # 8·N²·32 flops per (window, head)
-        L = H * W
-        Hp, Wp = -(-H // WINDOW) * WINDOW, -(-W // WINDOW) * WINDOW
-        nW = (Hp // WINDOW) * (Wp // WINDOW)
-        es = qkv.element_size()
-        TIMER.stop("winattn_bwd", ev, B * Hp * Wp * 8 * C * es, 8 * (WINDOW * WINDOW) ** 2 * HEAD_DIM * B * nW * nH,
-                   B * L * 8 * C * es)
+        H, W, nH, shift, scale = ctx.cfg
+        gqkv, gtable, gbias = winattn_bwd(qkv, bias_f, table_f, mask_f, H, W, nH, shift, scale, out, lse, gout,
+                                          need_bias=ctx.need[0], need_table=ctx.need[1])
         if gtable is not None:
             gtable = gtable.to(ctx.table_dtype)
         return gqkv, gbias, gtable, None, None, None, None, None, None
@@ -384,3 +405,73 @@ class CrossEntropyFn(torch.autograd.Function):
 
 def cross_entropy(logits, target, ignore_index=255, weight=None, return_match=False):
     return CrossEntropyFn.apply(logits, target, ignore_index, weight, bool(return_match))
+
+
+# ------------------------------------------------------------------ weight gradients
+def wgrad(A, B, D, colsum_a=None, colsum_b=None, alpha=1.0, accumulate=False):
+    """D (m, n) fp32 = alpha * A^T B (+ D), A (K, m) / B (K, n) bf16 with unit column stride;
+    colsum_a (m) / colsum_b (n) fp32 receive alpha * the column sums (bias gradients).
+    The smaller of m, n is put on the kernel's narrow tile side (transposed write)."""
+    K, m = A.shape
+    n = B.shape[1]
+    for t, nm in ((A, "A"), (B, "B")):
+        if t.dtype != torch.bfloat16 or t.stride(1) != 1 or not t.is_cuda:
+            raise RuntimeError(f"wgrad: {nm} must be a CUDA bf16 matrix with unit column stride")
+    if D.dtype != torch.float32 or tuple(D.shape) != (m, n) or not D.is_contiguous():
+        raise RuntimeError("wgrad: D must be a contiguous fp32 (m, n) tensor")
+    swap = n < m
+    if swap:
+        A, B, m, n, colsum_a, colsum_b = B, A, n, m, colsum_b, colsum_a
+    ws = torch.empty((N.load().irads_wgrad_workspace(K, m, n),), device=A.device, dtype=torch.float32)
+    N.call("irads_wgrad", N.ptr(A), A.stride(0), N.ptr(B), B.stride(0), K, m, n, float(alpha), int(accumulate),
+           int(swap), N.ptr(D), N.ptr(colsum_a), N.ptr(colsum_b), N.ptr(ws), N.stream())
+    return D
+
+
+def wgrad_ok(in_features, out_features):
+    return in_features % 8 == 0 and out_features % 8 == 0
+
+
+class LinearFn(torch.autograd.Function):
+    """F.linear under bf16 autocast for a TRAINABLE weight: the forward is the same hipBLASLt
+    GEMM autocast issues (bf16 operands, fp32 accumulate, bf16 out); the backward computes
+    dX with hipBLASLt and dW / db with the split-K irads_wgrad kernel straight into fp32."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        shape = x.shape
+        xb = x.reshape(-1, shape[-1])
+        xb = xb.to(torch.bfloat16).contiguous() if (xb.dtype != torch.bfloat16 or xb.stride(-1) != 1
+                                                     or xb.stride(0) % 8) else xb
+        wb = weight.detach().to(torch.bfloat16)
+        bb = None if bias is None else bias.detach().to(torch.bfloat16)
+        y = torch.nn.functional.linear(xb, wb, bb)
+        ctx.save_for_backward(xb, wb)
+        ctx.has_bias = bias is not None
+        ctx.shape = shape
+        return y.view(*shape[:-1], weight.shape[0])
+
+    @staticmethod
+    def backward(ctx, gy):
+        xb, wb = ctx.saved_tensors
+        g = gy.reshape(-1, gy.shape[-1])
+        if g.dtype != torch.bfloat16 or g.stride(-1) != 1 or g.stride(0) % 8:
+            g = g.to(torch.bfloat16).contiguous()
+        gx = gw = gb = None
+        if ctx.needs_input_grad[0]:
+            gx = torch.mm(g, wb).view(ctx.shape)
+        if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
+            gw = torch.empty(wb.shape, device=g.device, dtype=torch.float32)
+            gb = torch.empty((wb.shape[0],), device=g.device, dtype=torch.float32) if ctx.has_bias else None
+            wgrad(g, xb, gw, colsum_a=gb)
+        return gx, gw, gb
+
+
+def linear(x, weight, bias=None):
+    """Trainable-weight Linear: LinearFn under bf16 autocast on the GPU, F.linear otherwise."""
+    if (x.is_cuda and weight.requires_grad and torch.is_autocast_enabled("cuda")
+            and torch.get_autocast_dtype("cuda") == torch.bfloat16
+            and wgrad_ok(weight.shape[1], weight.shape[0])):
+        with torch.autocast("cuda", enabled=False):
+            return LinearFn.apply(x, weight, bias)
+    return torch.nn.functional.linear(x, weight, bias)

@@ -27,9 +27,9 @@ import torch.nn as nn
 import torch.nn.functional as F
 import torch.utils.checkpoint as cp
 
-from irads import ops
+from irads import ops, swin_fused
 
-from ..layers.common import DropPath, Linear
+from ..layers.common import DropPath, Linear, TrainLinear
 from .embed import PatchEmbed, PatchMerging
 
 
@@ -208,8 +208,8 @@ class Adapter(nn.Module):
         self.skip_connect = skip_connect
         hidden = int(D_features * mlp_ratio)
         self.act = act_layer()
-        self.D_fc1 = nn.Linear(D_features, hidden)
-        self.D_fc2 = nn.Linear(hidden, D_features)
+        self.D_fc1 = TrainLinear(D_features, hidden)
+        self.D_fc2 = TrainLinear(hidden, D_features)
         with torch.no_grad():
             nn.init.kaiming_uniform_(self.D_fc1.weight, a=math.sqrt(5))
             nn.init.zeros_(self.D_fc2.weight)
@@ -288,6 +288,7 @@ class SwinBlockSequence(nn.Module):
                              qk_scale, drop_rate, attn_drop_rate, rates[i], act_cfg, norm_cfg, with_cp, None,
                              adapter_ratio) for i in range(depth)])
         self.downsample = downsample
+        self.fused = True  # use the fused stage (irads/swin_fused.py) when it applies
 
     def forward(self, x, hw_shape, sub_mode):
         for block in self.blocks:
@@ -298,8 +299,13 @@ class SwinBlockSequence(nn.Module):
         return x, hw_shape, x, hw_shape
 
     def forward_pair(self, x, hw_shape, n_rgb):
-        for block in self.blocks:
-            x = block.forward_pair(x, hw_shape, n_rgb)
+        if self.fused and 2 * n_rgb == x.shape[0] and swin_fused.usable(self, x):
+            # frozen trunk under bf16 autocast: the whole stage is one hand-scheduled
+            # autograd node (irads/swin_fused.py); results follow the module path below
+            x = swin_fused.stage_forward(self, x, hw_shape)
+        else:
+            for block in self.blocks:
+                x = block.forward_pair(x, hw_shape, n_rgb)
         if self.downsample:
             x_down, hw_down = self.downsample(x, hw_shape, None)
             return x_down, hw_down, x, hw_shape
@@ -442,10 +448,10 @@ class MPGBlock(nn.Module):
     def __init__(self, dim, ratio):
         super().__init__()
         d = int(dim * ratio)
-        self.D_fc1 = nn.Linear(dim, d)
-        self.D_fc2 = nn.Linear(dim, d)
-        self.P_fc2 = nn.Linear(int(dim * ratio * 2), d)
-        self.U_fc1 = nn.Linear(d, dim)
+        self.D_fc1 = TrainLinear(dim, d)
+        self.D_fc2 = TrainLinear(dim, d)
+        self.P_fc2 = TrainLinear(int(dim * ratio * 2), d)
+        self.U_fc1 = TrainLinear(d, dim)
         self.act = nn.GELU()
         self.tfts_gamma_rgb, self.tfts_beta_rgb = init_tfts(dim)
         self.tfts_gamma_dte, self.tfts_beta_dte = init_tfts(dim)
@@ -463,9 +469,9 @@ class DeformMPGBlock(nn.Module):
     def __init__(self, dims, stride, n_groups, n_heads, dpr, level, ratio):
         super().__init__()
         d = int(dims * ratio)
-        self.D_fc1 = nn.Linear(dims, d)
-        self.D_fc2 = nn.Linear(dims, d)
-        self.U_fc1 = nn.Linear(d, dims)
+        self.D_fc1 = TrainLinear(dims, d)
+        self.D_fc2 = TrainLinear(dims, d)
+        self.U_fc1 = TrainLinear(d, dims)
         self.act = nn.GELU()
         self.deform_atten = DAttentionMM(dims=d, stride=stride, n_groups=n_groups, n_heads=n_heads, dpr=dpr,
                                          level=level)

@@ -6,12 +6,13 @@ from torch import nn, Tensor
 from torch.nn import functional as F
 
 from irads import ops
+from semseg.models.layers.common import TrainLinear
 
 
 class MLP(nn.Module):
     def __init__(self, dim, embed_dim):
         super().__init__()
-        self.proj = nn.Linear(dim, embed_dim)
+        self.proj = TrainLinear(dim, embed_dim)
 
     def forward(self, x: Tensor) -> Tensor:
         return self.proj(x.flatten(2).transpose(1, 2))

@@ -34,17 +34,34 @@ class Linear(nn.Linear):
     version counter moves (optimizer step, load_state_dict, in-place edits).  Outside
     autocast, or for trainable weights, this is nn.Linear.  State-dict keys unchanged."""
 
+    def amp_weights(self, dt):
+        """(weight, bias) rounded to `dt`, cached until a parameter's version moves."""
+        w, b = self.weight, self.bias
+        key = (dt, w.data_ptr(), w._version, None if b is None else b._version)
+        cache = self.__dict__.get("_amp_cache")
+        if cache is None or cache[0] != key:
+            with torch.no_grad():
+                cache = (key, w.detach().to(dt), None if b is None else b.detach().to(dt))
+            self.__dict__["_amp_cache"] = cache
+        return cache[1], cache[2]
+
     def forward(self, x: Tensor) -> Tensor:
         w, b = self.weight, self.bias
         if (w.requires_grad or (b is not None and b.requires_grad) or not x.is_cuda
                 or not torch.is_autocast_enabled("cuda")):
             return super().forward(x)
         dt = torch.get_autocast_dtype("cuda")
-        key = (dt, w.data_ptr(), w._version, None if b is None else b._version)
-        cache = self.__dict__.get("_amp_cache")
-        if cache is None or cache[0] != key:
-            with torch.no_grad():
-                cache = (key, w.to(dt), None if b is None else b.to(dt))
-            self.__dict__["_amp_cache"] = cache
+        wc, bc = self.amp_weights(dt)
         with torch.autocast("cuda", enabled=False):
-            return torch.nn.functional.linear(x.to(dt), cache[1], cache[2])
+            return torch.nn.functional.linear(x.to(dt), wc, bc)
+
+
+class TrainLinear(nn.Linear):
+    """nn.Linear for trainable weights (Adapters, MPG / DeformMPG projections, SegFormer
+    MLPs): under bf16 autocast on the GPU the backward's weight/bias gradients come from the
+    split-K irads_wgrad kernel (irads.ops.LinearFn); otherwise plain nn.Linear.
+    State-dict keys unchanged."""
+
+    def forward(self, x: Tensor) -> Tensor:
+        from irads import ops
+        return ops.linear(x, self.weight, self.bias)

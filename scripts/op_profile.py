@@ -1,0 +1,44 @@
+"""Operator-level profile of the bench training step (torch.profiler, GPU time per aten op
+and input shapes), to attribute the non-irads kernels to the model code that issues them.
+
+    python scripts/op_profile.py [--steps 3] [--rows 60] > gpurun_out/ops.txt
+"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "ir-ads_amd"))
+
+import torch  # noqa: E402
+from torch.profiler import ProfilerActivity, profile  # noqa: E402
+
+import bench  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--rows", type=int, default=60)
+    ap.add_argument("--batch", type=int, default=8)
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(3407)
+    model, opt, sched, loss_fn = bench.build(dev, 1, 0, 1000)
+    model.train()
+    batch = bench.synthetic_batch(a.batch, 512, dev, 3407)
+    for _ in range(3):
+        bench.train_step(model, opt, sched, loss_fn, batch)
+    torch.cuda.synchronize()
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True) as prof:
+        for _ in range(a.steps):
+            bench.train_step(model, opt, sched, loss_fn, batch)
+        torch.cuda.synchronize()
+    ka = prof.key_averages(group_by_input_shape=True)
+    print(ka.table(sort_by="self_cuda_time_total", row_limit=a.rows, max_name_column_width=50,
+                   max_shapes_column_width=70))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,265 @@
+"""Fused Swin stage (irads/swin_fused.py, csrc/swinblock.hip) on the GPU.
+
+The fused stage must reproduce the module-by-module autocast path (itself checked against
+the reference in test_gpu_swin.py), which is the reference's own arithmetic under bf16 AMP.
+Kernel-level checks compare each row/element kernel with the torch ops it replaces, in
+the rounding the autocast reference applies.  Tolerances: bit-exact where the arithmetic
+is the same formula (GELU, ReLU, dropout scaling, casts, DropPath); LayerNorm differs from
+torch's Welford reduction in summation order only (1 bf16 ulp on a few elements); the
+whole stage at bf16 GEMM scale (relative L2 1e-2, stated per test)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from fill import fill_module
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _N():
+    from irads import native as N
+    return N
+
+
+def _rel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+@pytest.mark.parametrize("C", [128, 192, 512, 1024])
+def test_resln_fwd_matches_torch(C):
+    from irads import swin_fused as SF
+    torch.manual_seed(C)
+    S, L = 4, 37
+    M = S * L
+    x = torch.randn(M, C, device=DEV)
+    o = torch.randn(M, C, device=DEV).bfloat16()
+    f = torch.randn(M, C, device=DEV).bfloat16()
+    d = torch.randn(M, C, device=DEV).bfloat16()
+    norm = torch.nn.LayerNorm(C).to(DEV)
+    with torch.no_grad():
+        norm.weight.uniform_(0.5, 1.5)
+        norm.bias.uniform_(-0.2, 0.2)
+    s = torch.tensor([0.0, 1.0 / 0.7, 1.0, 1.0 / 0.7], device=DEV)  # per-sample DropPath factors
+    # X1 = x + DP(o); LN; bf16 copy
+    X1, h, xb, mean, rstd = SF._resln_fwd(x, M, C, L, add1=o, add1_scale=s, norm=norm, x_out=True, xb_out=True)
+    dp = (o.view(S, L, C) * s.view(S, 1, 1)).bfloat16().float().view(M, C)  # bf16(v * s); s = 0 drops
+    ref = x + dp
+    assert torch.equal(X1, ref)
+    assert torch.equal(xb, ref.bfloat16())
+    href = F.layer_norm(ref, (C,), norm.weight, norm.bias, 1e-5)
+    err = (h.float() - href).abs() / href.abs().clamp_min(1e-2)
+    assert err.max().item() < 2 ** -7, err.max().item()
+    torch.testing.assert_close(mean, ref.mean(-1), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(rstd, torch.rsqrt(ref.var(-1, unbiased=False) + 1e-5), rtol=1e-4, atol=1e-6)
+    # Xout = (X1 + f) + bf16(0.5 d), no LN
+    xo, _, _, _, _ = SF._resln_fwd(X1, M, C, L, add1=f, add2=d, add2_mult=0.5, x_out=True)
+    assert torch.equal(xo, (X1 + f.float()) + (0.5 * d.float()).bfloat16().float())
+
+
+@pytest.mark.parametrize("C", [128, 384, 1024])
+def test_resln_bwd_matches_autograd(C):
+    from irads import swin_fused as SF
+    torch.manual_seed(C + 1)
+    S, L = 2, 50
+    M = S * L
+    x = torch.randn(M, C, device=DEV, requires_grad=True)
+    norm = torch.nn.LayerNorm(C).to(DEV)
+    with torch.no_grad():
+        norm.weight.uniform_(0.5, 1.5)
+    _, _, _, mean, rstd = SF._resln_fwd(x.detach(), M, C, L, norm=norm)
+    dy = torch.randn(M, C, device=DEV).bfloat16()
+    gres = torch.randn(M, C, device=DEV)
+    gadd = torch.randn(M, C, device=DEV).bfloat16()
+    s = torch.tensor([1.0 / 0.8, 0.0], device=DEV)
+    dx, b1, b2 = SF._resln_bwd(M, C, L, dy=dy, x=x.detach(), mean=mean, rstd=rstd, norm=norm, g_res=gres,
+                               g_add=gadd, b1=True, b1_scale=s, b2=True, b2_mult=0.5)
+    y = F.layer_norm(x, (C,), norm.weight, norm.bias, 1e-5)
+    (gx,) = torch.autograd.grad(y, x, dy.float())
+    ref = gx + gres + gadd.float()
+    torch.testing.assert_close(dx, ref, rtol=1e-4, atol=1e-4)
+    gb = dx.bfloat16().float()
+    assert torch.equal(b1.float(), (gb.view(S, L, C) * s.view(S, 1, 1)).bfloat16().float().view(M, C))
+    assert torch.equal(b2.float(), (0.5 * gb).bfloat16().float())
+
+
+def test_gelu_and_relu_dropout_kernels():
+    N = _N()
+    torch.manual_seed(3)
+    n = 8 * 1000 + 5  # ragged tail
+    u = (torch.randn(n, device=DEV) * 3).bfloat16()
+    g = torch.empty_like(u)
+    N.call("irads_gelu_fwd", N.ptr(u), N.ptr(g), n, N.stream())
+    ref = F.gelu(u)  # torch bf16 GELU: fp32 erf, rounded
+    assert (g.float() - ref.float()).abs().max().item() <= 2 ** -8 * ref.float().abs().max().item()
+    assert (g != ref).float().mean().item() < 0.01
+    dg = torch.randn(n, device=DEV).bfloat16()
+    du = torch.empty_like(u)
+    N.call("irads_gelu_bwd", N.ptr(u), N.ptr(dg), N.ptr(du), n, N.stream())
+    uu = u.float().requires_grad_()
+    (ref,) = torch.autograd.grad(F.gelu(uu), uu, dg.float())
+    torch.testing.assert_close(du.float(), ref.bfloat16().float(), rtol=2 ** -7, atol=1e-3)
+    # ReLU (p = 0) and ReLU + dropout(0.1)
+    r = torch.empty_like(u)
+    N.call("irads_relu_dropout_fwd", N.ptr(u), N.ptr(r), n, 0.0, 1234, N.stream())
+    assert torch.equal(r, F.relu(u))
+    N.call("irads_relu_dropout_fwd", N.ptr(u), N.ptr(r), n, 0.1, 1234, N.stream())
+    pos = u.float() > 0
+    kept = pos & (r.float() != 0)
+    frac = kept.sum().item() / pos.sum().item()
+    assert 0.87 < frac < 0.93, frac
+    scale = torch.tensor(1.0 / (1.0 - 0.1), dtype=torch.float32)
+    assert torch.equal(r[kept].float(), (u[kept].float() * scale.item()).bfloat16().float())
+    assert torch.all(r[~kept] == 0)
+    r2 = torch.empty_like(u)
+    N.call("irads_relu_dropout_fwd", N.ptr(u), N.ptr(r2), n, 0.1, 1234, N.stream())
+    assert torch.equal(r, r2)  # counter-based: same seed, same mask
+    da = torch.empty_like(u)
+    N.call("irads_relu_dropout_bwd", N.ptr(r), N.ptr(dg), N.ptr(da), n, 0.1, N.stream())
+    ref = torch.where(kept, (dg.float() * scale.item()), torch.zeros_like(dg.float())).bfloat16()
+    assert torch.equal(da, ref)
+
+
+def _stage(C=128, heads=4, depth=2, dpr=0.0, seed=5):
+    from semseg.models.backbones import swin
+    seq = swin.SwinBlockSequence(C, heads, 4 * C, depth, 12, drop_path_rate=dpr).to(DEV)
+    fill_module(seq, seed=seed)
+    for n, p in seq.named_parameters():
+        p.requires_grad_("Adapter" in n)
+    return seq
+
+
+def _run(seq, x, hw, fused, g):
+    seq.fused = fused
+    xx = x.clone().requires_grad_()
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = seq.forward_pair(xx, hw, x.shape[0] // 2)[2]
+    params = [p for n, p in seq.named_parameters() if p.requires_grad]
+    grads = torch.autograd.grad((y.float() * g).sum(), [xx] + params)
+    return y.float(), grads
+
+
+@pytest.mark.parametrize("C,heads,H,W", [(128, 4, 28, 28), (256, 8, 24, 20), (512, 16, 16, 16)])
+def test_fused_stage_matches_module_path(C, heads, H, W):
+    """Eval mode (no randomness): the fused stage against the op-by-op autocast path.
+    Tolerance: relative L2 5e-3 on the output and 2e-2 on every gradient (bf16 operand
+    rounding of the GEMMs; the only differences are LayerNorm summation order flipping a
+    bf16 rounding here and there)."""
+    from irads import swin_fused as SF
+    torch.manual_seed(0)
+    seq = _stage(C, heads)
+    seq.eval()
+    x = torch.randn(4, H * W, C, device=DEV)
+    assert SF.usable(seq, x) is False  # autocast is off here
+    g = torch.randn(4, H * W, C, device=DEV)
+    y0, g0 = _run(seq, x, (H, W), False, g)
+    calls = {"n": 0}
+    orig = SF.SwinStageFn.forward
+
+    def spy(*a, **k):
+        calls["n"] += 1
+        return orig(*a, **k)
+    SF.SwinStageFn.forward = staticmethod(spy)
+    try:
+        y1, g1 = _run(seq, x, (H, W), True, g)
+    finally:
+        SF.SwinStageFn.forward = staticmethod(orig)
+    assert calls["n"] == 1, "fused stage was not taken"
+    assert _rel(y1, y0) < 5e-3, _rel(y1, y0)
+    for a, b in zip(g1, g0):
+        assert _rel(a, b) < 2e-2, _rel(a, b)
+
+
+def test_fused_stage_training_deterministic_parts():
+    """Training mode with DropPath and adapter dropout switched off equals eval mode;
+    with them on, the output stays finite, the dropout mask differs per call and the
+    gradient matches a finite-difference check along the input direction."""
+    from irads import swin_fused as SF
+    torch.manual_seed(1)
+    seq = _stage(128, 4, dpr=0.0)
+    x = torch.randn(4, 24 * 24, 128, device=DEV)
+    g = torch.randn_like(x)
+    seq.eval()
+    ye, ge = _run(seq, x, (24, 24), True, g)
+    seq.train()
+    old = SF.ADAPTER_DROPOUT
+    SF.ADAPTER_DROPOUT = 0.0
+    try:
+        yt, gt = _run(seq, x, (24, 24), True, g)
+    finally:
+        SF.ADAPTER_DROPOUT = old
+    assert torch.equal(ye, yt)
+    for a, b in zip(ge, gt):
+        assert torch.equal(a, b)
+    y1, _ = _run(seq, x, (24, 24), True, g)
+    y2, _ = _run(seq, x, (24, 24), True, g)
+    assert torch.isfinite(y1).all() and not torch.equal(y1, y2)
+
+
+def test_fused_stage_droppath_semantics():
+    """DropPath (drop_path_rate 0.3 over 2 blocks): per-sample factors are either 0 or
+    1/keep, and a dropped sample's branch contributes nothing: with every branch dropped
+    the stage output equals its input plus the adapter terms only."""
+    from irads import swin_fused as SF
+    seq = _stage(128, 4, depth=2, dpr=[0.2, 0.3])
+    seq.train()
+    s = SF._droppath_scales(seq, 64, torch.device(DEV))
+    assert s.shape == (2, 2, 64)
+    keep = torch.tensor([[0.8, 0.8], [0.7, 0.7]], device=DEV)[..., None]
+    inv = (1.0 / keep.float())
+    ok = (s == 0) | (s == inv)
+    assert ok.all()
+    frac = (s != 0).float().mean(-1)
+    assert ((frac - keep[..., 0]).abs() < 0.25).all()
+
+
+@pytest.mark.parametrize("K,m,n", [(131072, 8, 128), (8192, 512, 32), (1000, 16, 24), (300, 64, 256), (77, 128, 136),
+                                   (4096, 1024, 64), (2048, 256, 512)])
+def test_wgrad_split_k(K, m, n):
+    """irads_wgrad against fp32 torch on the same bf16 operands: the products are exact in
+    fp32 and only the summation order differs (relative error ~1e-6)."""
+    from irads import ops
+    torch.manual_seed(K + m + n)
+    Aw = torch.randn(K, m + 8, device=DEV).bfloat16()
+    A = Aw[:, 8:]  # row stride m + 8: a column slice, as the fused stage passes
+    B = torch.randn(K, n, device=DEV).bfloat16()
+    D = torch.empty(m, n, device=DEV)
+    ca, cb = torch.empty(m, device=DEV), torch.zeros(n, device=DEV)
+    ops.wgrad(A, B, D, colsum_a=ca)
+    ref = A.float().t() @ B.float()
+    assert _rel(D, ref) < 1e-5, _rel(D, ref)
+    torch.testing.assert_close(ca, A.float().sum(0), rtol=1e-4, atol=1e-3)
+    # accumulate + alpha + the other operand's column sums
+    D2 = D.clone()
+    ops.wgrad(A, B, D2, colsum_b=cb, alpha=0.5, accumulate=True)
+    assert _rel(D2, 1.5 * ref) < 1e-5
+    torch.testing.assert_close(cb, 0.5 * B.float().sum(0), rtol=1e-4, atol=1e-3)
+    # deterministic: fixed-order reduction
+    D3 = torch.empty_like(D)
+    ops.wgrad(A, B, D3)
+    assert torch.equal(D, D3)
+
+
+def test_linear_fn_matches_autocast_linear():
+    """ops.linear (trainable weight, bf16 autocast): forward is the autocast GEMM bit for bit;
+    dX equals autocast's; dW / db are the fp32 sums autocast rounds to bf16 (tolerance: one
+    bf16 rounding, 2^-8 relative)."""
+    from semseg.models.layers.common import TrainLinear
+    torch.manual_seed(2)
+    lin = torch.nn.Linear(128, 16).to(DEV)
+    tl = TrainLinear(128, 16).to(DEV)
+    tl.load_state_dict(lin.state_dict())
+    x = torch.randn(2, 300, 128, device=DEV)
+    g = torch.randn(2, 300, 16, device=DEV).bfloat16()
+    outs = []
+    for mod in (lin, tl):
+        xx = x.clone().requires_grad_()
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = mod(xx)
+        gx, gw, gb = torch.autograd.grad(y, [xx, mod.weight, mod.bias], g)
+        outs.append((y, gx, gw, gb))
+    (y0, gx0, gw0, gb0), (y1, gx1, gw1, gb1) = outs
+    assert y1.dtype == torch.bfloat16 and torch.equal(y0, y1)
+    assert torch.equal(gx0, gx1)
+    assert _rel(gw1, gw0) < 4e-3 and _rel(gb1, gb0) < 4e-3
