@@ -190,10 +190,13 @@ int irads_resln_bwd(const uint16_t *dy, const float *x, const float *mean, const
                     uint16_t *b1_out, const float *b1_scale, uint16_t *b2_out, float b2_mult, void *stream);
 /* bf16 element passes (n elements): GELU (exact erf form, nn.GELU) and its backward;
  * ReLU + dropout(p) of the Adapter (swin.py:492-497; keep with probability 1-p, scale
- * 1/(1-p), counter-based draw from `seed`) and its backward from the saved output r. */
+ * 1/(1-p)) and its backward from the saved output r.  The dropout draw is counter-based,
+ * keyed by seed ^ *seed_dev (seed_dev: one device uint64, or NULL for seed alone) so that a
+ * captured HIP graph draws a fresh mask on every replay. */
 int irads_gelu_fwd(const uint16_t *u, uint16_t *g, long n, void *stream);
 int irads_gelu_bwd(const uint16_t *u, const uint16_t *dg, uint16_t *du, long n, void *stream);
-int irads_relu_dropout_fwd(const uint16_t *a, uint16_t *r, long n, float p, uint64_t seed, void *stream);
+int irads_relu_dropout_fwd(const uint16_t *a, uint16_t *r, long n, float p, uint64_t seed, const uint64_t *seed_dev,
+                           void *stream);
 int irads_relu_dropout_bwd(const uint16_t *r, const uint16_t *dr, uint16_t *da, long n, float p, void *stream);
 
 /* ------------------------------------------------------------------ weight-gradient GEMM

@@ -290,9 +290,13 @@ __device__ __forceinline__ float uniform01(unsigned long long seed, unsigned lon
 template <int OP>  // 0 gelu fwd, 1 gelu bwd, 2 relu+dropout fwd, 3 relu+dropout bwd
 __global__ __launch_bounds__(256) void elem_kernel(const u16 *__restrict__ a, const u16 *__restrict__ b,
                                                    u16 *__restrict__ out, long n, float p, float scale,
-                                                   unsigned long long seed) {
+                                                   unsigned long long salt,
+                                                   const unsigned long long *__restrict__ seed_dev) {
     const long i8 = ((long)blockIdx.x * 256 + threadIdx.x) * 8;
     if (i8 >= n) return;
+    // the draw's seed lives in device memory (written by the torch generator on the same
+    // stream), so a captured HIP graph draws a fresh mask on every replay
+    const unsigned long long seed = (OP == 2 && seed_dev != nullptr) ? (*seed_dev ^ salt) : salt;
     auto f = [&](float av, float bv, long i) -> float {
         if (OP == 0) return gelu_f(av);
         if (OP == 1) return bv * gelu_grad(av);
@@ -422,16 +426,17 @@ extern "C" int irads_resln_bwd(const uint16_t *dy, const float *x, const float *
 }
 
 static int elem_launch(int op, const uint16_t *a, const uint16_t *b, uint16_t *out, long n, float p, float scale,
-                       unsigned long long seed, void *stream) {
+                       unsigned long long seed, void *stream, const uint64_t *seed_dev = nullptr) {
+    const unsigned long long *sd = reinterpret_cast<const unsigned long long *>(seed_dev);
     if (n <= 0) return IRADS_OK;
     const long threads = (n + 7) / 8;
     dim3 grid((unsigned)((threads + 255) / 256)), block(256);
     hipStream_t st = (hipStream_t)stream;
     switch (op) {
-        case 0: hipLaunchKernelGGL(elem_kernel<0>, grid, block, 0, st, a, b, out, n, p, scale, seed); break;
-        case 1: hipLaunchKernelGGL(elem_kernel<1>, grid, block, 0, st, a, b, out, n, p, scale, seed); break;
-        case 2: hipLaunchKernelGGL(elem_kernel<2>, grid, block, 0, st, a, b, out, n, p, scale, seed); break;
-        default: hipLaunchKernelGGL(elem_kernel<3>, grid, block, 0, st, a, b, out, n, p, scale, seed); break;
+        case 0: hipLaunchKernelGGL(elem_kernel<0>, grid, block, 0, st, a, b, out, n, p, scale, seed, sd); break;
+        case 1: hipLaunchKernelGGL(elem_kernel<1>, grid, block, 0, st, a, b, out, n, p, scale, seed, sd); break;
+        case 2: hipLaunchKernelGGL(elem_kernel<2>, grid, block, 0, st, a, b, out, n, p, scale, seed, sd); break;
+        default: hipLaunchKernelGGL(elem_kernel<3>, grid, block, 0, st, a, b, out, n, p, scale, seed, sd); break;
     }
     return check_launch("irads_elementwise");
 }
@@ -444,9 +449,10 @@ extern "C" int irads_gelu_bwd(const uint16_t *u, const uint16_t *dg, uint16_t *d
     IRADS_REQUIRE(u && dg && du, "irads_gelu_bwd: null pointer");
     return elem_launch(1, u, dg, du, n, 0.f, 1.f, 0, stream);
 }
-extern "C" int irads_relu_dropout_fwd(const uint16_t *a, uint16_t *r, long n, float p, uint64_t seed, void *stream) {
+extern "C" int irads_relu_dropout_fwd(const uint16_t *a, uint16_t *r, long n, float p, uint64_t seed,
+                                      const uint64_t *seed_dev, void *stream) {
     IRADS_REQUIRE(a && r && p >= 0.f && p < 1.f, "irads_relu_dropout_fwd: bad arguments (p=%f)", (double)p);
-    return elem_launch(2, a, nullptr, r, n, p, 1.f / (1.f - p), seed, stream);
+    return elem_launch(2, a, nullptr, r, n, p, 1.f / (1.f - p), seed, stream, seed_dev);
 }
 extern "C" int irads_relu_dropout_bwd(const uint16_t *r, const uint16_t *dr, uint16_t *da, long n, float p,
                                       void *stream) {

@@ -440,9 +440,12 @@ class LinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias):
         shape = x.shape
-        xb = x.reshape(-1, shape[-1])
-        xb = xb.to(torch.bfloat16).contiguous() if (xb.dtype != torch.bfloat16 or xb.stride(-1) != 1
-                                                     or xb.stride(0) % 8) else xb
+        if x.dtype == torch.bfloat16 and x.is_contiguous():
+            xb = x.view(-1, shape[-1])
+        else:  # cast and re-layout in one copy kernel
+            xb = torch.empty(shape, device=x.device, dtype=torch.bfloat16)
+            xb.copy_(x)
+            xb = xb.view(-1, shape[-1])
         wb = weight.detach().to(torch.bfloat16)
         bb = None if bias is None else bias.detach().to(torch.bfloat16)
         y = torch.nn.functional.linear(xb, wb, bb)

@@ -160,7 +160,8 @@ class SwinStageFn(torch.autograd.Function):
         dp = _droppath_scales(seq, S, dev)
         train = blocks[0].training
         p_drop = ADAPTER_DROPOUT if train else 0.
-        seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if p_drop > 0 else 0
+        # dropout seed drawn on the device by torch's generator: graph-capturable, fresh per replay
+        seed = torch.randint(0, 2 ** 62, (1,), device=dev, dtype=torch.int64) if p_drop > 0 else None
         # all adapter weights of the stage cast to bf16 in two launches (autocast casts each per call)
         flat = torch.cat([p.detach().reshape(-1) for p in aparams]).to(_BF16)
         abf = list(torch.split(flat, [p.numel() for p in aparams]))
@@ -193,7 +194,7 @@ class SwinStageFn(torch.autograd.Function):
                 a1 = F.linear(X1b[rows], wa1, ba1)
                 r = torch.empty_like(a1)
                 N.call("irads_relu_dropout_fwd", N.ptr(a1), N.ptr(r), r.numel(), float(p_drop),
-                       (seed + 0x9E3779B97F4A7C15 * (2 * i + half + 1)) & 0xFFFFFFFFFFFFFFFF, N.stream())
+                       (0x9E3779B97F4A7C15 * (2 * i + half + 1)) & 0xFFFFFFFFFFFFFFFF, N.ptr(seed), N.stream())
                 torch.addmm(ba2, r, wa2.t(), out=d[rows])
                 rs.append(r)
             nxt = blocks[i + 1].norm1 if i + 1 < nb else None

@@ -18,7 +18,6 @@ What changed under the hood (MI355X-first):
 There is no CPU path: the HIP library and a GPU are required (CPU tensors raise).
 """
 import math
-import random
 import warnings
 from copy import deepcopy
 
@@ -482,16 +481,21 @@ class DeformMPGBlock(nn.Module):
         xr = xr.reshape(B, H, W, c).permute(0, 3, 1, 2).contiguous()
         xd = xd.reshape(B, H, W, c).permute(0, 3, 1, 2).contiguous()
         fused = self.deform_atten(xr, xd)
-        return self.U_fc1(fused.reshape(B, c, -1).permute(0, 2, 1).contiguous())
+        return self.U_fc1(fused.reshape(B, c, -1).permute(0, 2, 1))
 
 
 def apply_mask(rgb, dte):
     """MMST modality masking (reference swin.py:1094-1105): zero the rgb tokens of one
-    random image and the dte tokens of another.  Needs batch >= 4 like the reference."""
+    random image and the dte tokens of another (two distinct images, the first two of a
+    random permutation, as random.sample(range(B), B // 2)[:2]).  Needs batch >= 4 like the
+    reference.  The draw happens on the device (argsort of uniform keys, torch's generator),
+    so the step has no host round trip and replays correctly inside a captured HIP graph."""
     batch_size = rgb.size(0)
-    idx = random.sample(range(batch_size), batch_size // 2)
-    rgb[idx[0]] = torch.zeros_like(rgb[idx[0]])
-    dte[idx[1]] = torch.zeros_like(dte[idx[1]])
+    if batch_size // 2 < 2:  # the reference indexes idx[1] of a batch_size // 2 sample
+        raise IndexError(f'apply_mask needs a per-GPU batch >= 4 (got {batch_size}; swin.py:1098-1103)')
+    idx = torch.rand(batch_size, device=rgb.device).argsort()[:2]
+    rgb.index_fill_(0, idx[0:1], 0.)
+    dte.index_fill_(0, idx[1:2], 0.)
     return rgb, dte
 
 
@@ -614,7 +618,9 @@ class SwinTransformer(nn.Module):
         c = self.num_features[i]
 
         def nchw(t):
-            return t.view(-1, *out_hw, c).permute(0, 3, 1, 2).contiguous()
+            # (B, C, H, W) in channels-last memory: the reference's values and shape without the
+            # transpose copy; SegFormerHead's flatten(2).transpose(1, 2) turns it back into a view
+            return t.view(-1, *out_hw, c).permute(0, 3, 1, 2)
         return nchw(fused), nchw(x_rgb_out), nchw(x_dte_out)
 
     def forward(self, x):

@@ -3,6 +3,7 @@
 TRAIN_TYPE 'Adapter' trains only parameters whose name contains Adapter /
 extra_patch_embed / head / MPG (optimizers.py:7-30) and freezes the rest.  On GPU the
 AdamW update runs as PyTorch's fused multi-tensor kernel (one launch per step)."""
+import torch
 from torch import nn
 from torch.optim import AdamW, SGD
 
@@ -12,7 +13,9 @@ def adapter_trainable(name: str) -> bool:
 
 
 def get_optimizer(model: nn.Module, optimizer: str, lr: float, train_type: str, weight_decay: float = 0.01,
-                  verbose: bool = False):
+                  verbose: bool = False, lr_on_device: bool = False):
+    """lr_on_device: keep the learning rate as a device tensor (fused AdamW reads it on the GPU,
+    the scheduler fills it in place), which makes the optimizer step graph-capturable."""
     fused = {}
     if 'Adapter' in train_type:
         params = [p for n, p in model.named_parameters() if adapter_trainable(n) and p.requires_grad]
@@ -30,5 +33,9 @@ def get_optimizer(model: nn.Module, optimizer: str, lr: float, train_type: str, 
     if optimizer == 'adamw':
         if on_gpu:
             fused = {"fused": True}
+            if lr_on_device:
+                dev = groups[0]["params"][0].device
+                lr = torch.tensor(float(lr), device=dev)
+                fused["capturable"] = True
         return AdamW(groups, lr, betas=(0.9, 0.999), eps=1e-8, weight_decay=weight_decay, **fused)
     return SGD(groups, lr, momentum=0.9, weight_decay=weight_decay)

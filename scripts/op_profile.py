@@ -38,6 +38,27 @@ def main():
     ka = prof.key_averages(group_by_input_shape=True)
     print(ka.table(sort_by="self_cuda_time_total", row_limit=a.rows, max_name_column_width=50,
                    max_shapes_column_width=70))
+    # aten ops with full shapes: GPU time per step and achieved rate for the GEMMs
+    rows = []
+    for e in ka:
+        if not e.key.startswith("aten::") or e.self_device_time_total <= 0:
+            continue
+        rows.append((e.self_device_time_total / a.steps, e.count / a.steps, e.key, str(e.input_shapes)))
+    rows.sort(reverse=True)
+    print("\n# aten ops by GPU time per step (us), calls per step, shapes")
+    for us, n, k, shp in rows[:a.rows]:
+        extra = ""
+        try:
+            sh = eval(shp)
+            if k in ("aten::mm",) and len(sh[0]) == 2:
+                M, K = sh[0]; N_ = sh[1][1]
+                extra = f"  {2 * M * K * N_ * n / us / 1e6:8.1f} TF/s"
+            if k in ("aten::addmm",) and len(sh[1]) == 2:
+                M, K = sh[1]; N_ = sh[2][1]
+                extra = f"  {2 * M * K * N_ * n / us / 1e6:8.1f} TF/s"
+        except Exception:
+            pass
+        print(f"{us:9.1f} {n:6.1f}  {k:34s} {shp[:150]}{extra}")
 
 
 if __name__ == "__main__":

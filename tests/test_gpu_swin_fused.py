@@ -102,9 +102,9 @@ def test_gelu_and_relu_dropout_kernels():
     torch.testing.assert_close(du.float(), ref.bfloat16().float(), rtol=2 ** -7, atol=1e-3)
     # ReLU (p = 0) and ReLU + dropout(0.1)
     r = torch.empty_like(u)
-    N.call("irads_relu_dropout_fwd", N.ptr(u), N.ptr(r), n, 0.0, 1234, N.stream())
+    N.call("irads_relu_dropout_fwd", N.ptr(u), N.ptr(r), n, 0.0, 1234, None, N.stream())
     assert torch.equal(r, F.relu(u))
-    N.call("irads_relu_dropout_fwd", N.ptr(u), N.ptr(r), n, 0.1, 1234, N.stream())
+    N.call("irads_relu_dropout_fwd", N.ptr(u), N.ptr(r), n, 0.1, 1234, None, N.stream())
     pos = u.float() > 0
     kept = pos & (r.float() != 0)
     frac = kept.sum().item() / pos.sum().item()
@@ -113,8 +113,11 @@ def test_gelu_and_relu_dropout_kernels():
     assert torch.equal(r[kept].float(), (u[kept].float() * scale.item()).bfloat16().float())
     assert torch.all(r[~kept] == 0)
     r2 = torch.empty_like(u)
-    N.call("irads_relu_dropout_fwd", N.ptr(u), N.ptr(r2), n, 0.1, 1234, N.stream())
+    N.call("irads_relu_dropout_fwd", N.ptr(u), N.ptr(r2), n, 0.1, 1234, None, N.stream())
     assert torch.equal(r, r2)  # counter-based: same seed, same mask
+    sd = torch.tensor([1234 ^ 77], device=DEV, dtype=torch.int64)  # device seed: salt ^ *seed_dev
+    N.call("irads_relu_dropout_fwd", N.ptr(u), N.ptr(r2), n, 0.1, 77, N.ptr(sd), N.stream())
+    assert torch.equal(r, r2)
     da = torch.empty_like(u)
     N.call("irads_relu_dropout_bwd", N.ptr(r), N.ptr(dg), N.ptr(da), n, 0.1, N.stream())
     ref = torch.where(kept, (dg.float() * scale.item()), torch.zeros_like(dg.float())).bfloat16()
