@@ -1,0 +1,92 @@
+"""HBM traffic of the window-attention forward kernel from rocprofv3 PMC counters.
+
+    rocprofv3 --pmc FETCH_SIZE --kernel-trace -d <dirF> -o run -- python3 scripts/pmc_winattn.py run
+    rocprofv3 --pmc WRITE_SIZE --kernel-trace -d <dirW> -o run -- python3 scripts/pmc_winattn.py run
+    python3 scripts/pmc_winattn.py parse <dirF> <dirW> > profiles/pmc_winattn_fwd.json
+
+`run` issues exactly the 24 irads_winattn_fwd launches of one bench step (Swin-B at 512²,
+rgb+dte batched: B = 16; depths 2/2/18/2, shift 0/6 alternating), on the same synthetic
+scale as bench.py, after one untimed pass of the same sequence.  `parse` takes the last 24
+dispatches of the kernel and applies MI355X_MICROARCH.md's gfx950 corrections: FETCH_SIZE
+counts half the bytes of wide (16 B/lane) streaming reads, so it is doubled; WRITE_SIZE is
+exact for 16 B/lane stores.  Both counters are in KiB.  FETCH_SIZE and WRITE_SIZE need
+separate passes (TCC slots: 3 + 2 > 4).
+"""
+import csv
+import glob
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+STAGES = ((128, 128, 4, 2), (64, 256, 8, 2), (32, 512, 16, 18), (16, 1024, 32, 2))  # side, C, heads, depth
+
+
+def run():
+    sys.path.insert(0, os.path.join(ROOT, "ir-ads_amd"))
+    import torch
+    from irads import ops
+    B = 16
+    ins = []
+    for side, C, nH, depth in STAGES:
+        L = side * side
+        qkv = (torch.randn(B, L, 3 * C, device="cuda") * 0.5).bfloat16()
+        bias = torch.randn(3 * C, device="cuda") * 0.1
+        table = torch.randn(23 * 23, nH, device="cuda") * 0.1
+        ins.append((qkv, bias, table, side, nH, depth))
+
+    def step():
+        for qkv, bias, table, side, nH, depth in ins:
+            for blk in range(depth):
+                ops.winattn_fwd(qkv, bias, table, None, side, side, nH, 6 if blk % 2 else 0, 32 ** -0.5)
+    step()
+    step()
+    torch.cuda.synchronize()
+
+
+def algorithmic_bytes():
+    tot = 0
+    for side, C, nH, depth in STAGES:
+        Np = (-(-side // 12) * 12) ** 2
+        tot += depth * 16 * Np * 4 * C * 2  # read q, k, v + write o per padded token, bf16
+    return tot / 24
+
+
+def _values(d, counter):
+    files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    vals = []
+    for f in files:
+        with open(f) as fh:
+            for r in csv.DictReader(fh):
+                if "winattn_fwd" in r.get("Kernel_Name", "") and r.get("Counter_Name") == counter:
+                    vals.append((int(r.get("Dispatch_Id", 0)), float(r["Counter_Value"])))
+    vals.sort()
+    return [v for _, v in vals][-24:]
+
+
+def parse(dir_fetch, dir_write):
+    fetch = _values(dir_fetch, "FETCH_SIZE")
+    write = _values(dir_write, "WRITE_SIZE")
+    if len(fetch) != 24 or len(write) != 24:
+        raise SystemExit(f"expected 24 dispatches per counter, got {len(fetch)} / {len(write)}")
+    kib = 1024.0
+    read_b = 2.0 * sum(fetch) / 24 * kib  # gfx950: FETCH_SIZE = half the bytes of 16-B/lane reads
+    write_b = sum(write) / 24 * kib
+    out = {"kernel": "irads_winattn_fwd (bf16)", "launches": 24,
+           "fetch_size_kib_per_launch_raw": sum(fetch) / 24, "write_size_kib_per_launch": sum(write) / 24,
+           "hbm_read_bytes_per_launch": round(read_b), "hbm_write_bytes_per_launch": round(write_b),
+           "hbm_bytes_per_launch": round(read_b + write_b),
+           "algorithmic_bytes_per_launch": round(algorithmic_bytes()),
+           "correction": "FETCH_SIZE x2 (gfx950 counts half of 16-B/lane streaming reads), WRITE_SIZE as is; "
+                         "MI355X_MICROARCH.md §HBM",
+           "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE --kernel-trace, separate passes, "
+                     "scripts/pmc_winattn.py run (the 24 launches of one bench step)"}
+    out["traffic_over_algorithmic"] = round(out["hbm_bytes_per_launch"] / out["algorithmic_bytes_per_launch"], 3)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    if sys.argv[1] == "run":
+        run()
+    else:
+        parse(sys.argv[2], sys.argv[3])

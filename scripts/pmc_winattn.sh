@@ -1,0 +1,11 @@
+#!/bin/bash
+# Two PMC passes (FETCH_SIZE, WRITE_SIZE) over the 24 window-attention launches of one step.
+cd "$(dirname "$0")/.."
+R=$PWD
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+rm -rf gpurun_out/pmc_fetch gpurun_out/pmc_write
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $R/gpurun_out/pmc_fetch -o run -- python3 $R/scripts/pmc_winattn.py run > gpurun_out/pmc_fetch.log 2>&1 || { echo "fetch pass failed"; tail gpurun_out/pmc_fetch.log; exit 1; }
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $R/gpurun_out/pmc_write -o run -- python3 $R/scripts/pmc_winattn.py run > gpurun_out/pmc_write.log 2>&1 || { echo "write pass failed"; tail gpurun_out/pmc_write.log; exit 1; }
+python3 scripts/pmc_winattn.py parse gpurun_out/pmc_fetch gpurun_out/pmc_write > gpurun_out/pmc_winattn_fwd.json && cat gpurun_out/pmc_winattn_fwd.json
+find gpurun_out/pmc_fetch gpurun_out/pmc_write -name '*kernel_trace.csv' -delete
