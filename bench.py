@@ -46,6 +46,7 @@ def parse():
     p.add_argument("--cpu-steps", type=int, default=1)
     p.add_argument("--profile-only", action="store_true", help="run warmup + steps, print nothing extra")
     p.add_argument("--eager", action="store_true", help="launch op by op (default: replay a captured HIP graph)")
+    p.add_argument("--no-tuned-gemms", action="store_true", help="hipBLASLt default picks (ignore irads/tuned/)")
     return p.parse_args()
 
 
@@ -149,6 +150,8 @@ def main():
     np.random.seed(3407 + rank)
     torch.manual_seed(3407 + rank)
     graph = not args.eager
+    from irads.gemm_tuning import use_tuned_gemms
+    tuned = False if args.no_tuned_gemms else use_tuned_gemms()
     model, opt, sched, loss_fn = build(device, world, local_rank, 100000, graph=graph)
     model.train()
     batch = synthetic_batch(args.batch, args.size, device, 3407 + rank)
@@ -224,7 +227,8 @@ def main():
                                "(fwd+bwd+AdamW, TRAIN_TYPE Adapter, MMST loss)",
                    "per_gpu_batch": args.batch, "global_batch": args.batch * world,
                    "image_size": [args.size, args.size], "parallelism": f"dp{world}",
-                   "execution": "hip-graph replay" if graph else "eager"},
+                   "execution": "hip-graph replay" if graph else "eager",
+                   "gemm_selection": "TunableOp table irads/tuned" if tuned else "hipBLASLt heuristic"},
         "loss": round(loss_val, 5),
     }
     if fwd:

@@ -148,6 +148,14 @@ int irads_resize_fwd(int dtype, const void *in, const int64_t *in_strides, int B
 int irads_resize_bwd(int dtype, const void *grad_out, const int64_t *go_strides, int B, int C, int H, int W,
                      void *grad_in, const int64_t *gi_strides, int h, int w, float *workspace, void *stream);
 
+/* out = base + sum_s resize(src_s) (bilinear, align_corners=False, the resize_fwd taps), all
+ * channels-last (B, C, ., .) tensors of one dtype with C % 8 == 0, fp32 sum rounded once.
+ * srcs / src_h / src_w are HOST arrays of n_src <= 4 device pointers and sizes.  The fuse of
+ * SegFormerHead.forward (segformer.py:39-47) once each branch's share of linear_fuse is
+ * applied at the branch's own resolution; the backward is irads_resize_bwd per source. */
+int irads_upsample_sum_fwd(int dtype, const void *base, const void *const *srcs, const int *src_h, const int *src_w,
+                           int n_src, int B, int C, int H, int W, void *out, void *stream);
+
 /* Softmax cross-entropy, mean over pixels whose target != ignore_index (nn.CrossEntropyLoss
  * as wrapped by semseg/losses.py:6-19; class_weight may be NULL).  logits (B, C, H, W),
  * C <= 128, NCHW- or channels-last-contiguous; target int64 (B, H, W).  Writes lse (B*H*W

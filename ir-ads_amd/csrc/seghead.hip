@@ -268,6 +268,42 @@ __global__ void __launch_bounds__(256) resize_bwd_cols_cl8(const float *__restri
     V8<T>::st(gin + ((long)w.line * di.W + w.x) * di.C + w.c0, acc);
 }
 
+// ------------------------------------------------------------------ fused upsample-and-sum
+// out = base + Σ_s resize(src_s) on channels-last tensors (C % 8 == 0), fp32 sum and one
+// rounding: the SegFormer fuse of the restructured head (heads/segformer.py), where each
+// branch's 1x1 projection runs at its own resolution and only the E-channel result is
+// upsampled.  Same taps as resize_fwd (upsample_bilinear2d, align_corners=False).
+constexpr int kMaxSrc = 4;
+template <typename T> struct Srcs {
+    const T *p[kMaxSrc];
+    int h[kMaxSrc], w[kMaxSrc];
+    int n;
+};
+template <typename T>
+__global__ void __launch_bounds__(256) upsample_sum_cl8(const T *__restrict__ base, Srcs<T> srcs, T *__restrict__ out,
+                                                        int B, int H, int W, int C) {
+    const Walk8 w = walk8(B, H, W, C);
+    if (!w.ok) return;
+    float acc[8];
+    const long o = ((long)w.line * W + w.x) * C + w.c0;
+    V8<T>::ld(base + o, acc);
+#pragma unroll
+    for (int s = 0; s < kMaxSrc; ++s) {
+        if (s >= srcs.n) break;
+        const Dims di{B, C, srcs.h[s], srcs.w[s]};
+        const Tap ty = tap_of(w.y, (float)di.H / (float)H, di.H), tx = tap_of(w.x, (float)di.W / (float)W, di.W);
+        float v00[8], v01[8], v10[8], v11[8];
+        V8<T>::ld(srcs.p[s] + offs<true>(di, w.b, w.c0, ty.i0, tx.i0), v00);
+        V8<T>::ld(srcs.p[s] + offs<true>(di, w.b, w.c0, ty.i0, tx.i1), v01);
+        V8<T>::ld(srcs.p[s] + offs<true>(di, w.b, w.c0, ty.i1, tx.i0), v10);
+        V8<T>::ld(srcs.p[s] + offs<true>(di, w.b, w.c0, ty.i1, tx.i1), v11);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            acc[j] += ty.l0 * (tx.l0 * v00[j] + tx.l1 * v01[j]) + ty.l1 * (tx.l0 * v10[j] + tx.l1 * v11[j]);
+    }
+    V8<T>::st(out + o, acc);
+}
+
 // ------------------------------------------------------------------ cross-entropy
 constexpr int CE_GRID = 1024;  // fixed grid: deterministic partial sums (IRADS_CE_WORKSPACE)
 
@@ -663,4 +699,33 @@ extern "C" int irads_ce_bwd(int dtype, const void *logits, const int64_t *stride
                                                    grad_loss, (U *)grad_logits);
     }
     return check_launch("irads_ce_bwd");
+}
+
+extern "C" int irads_upsample_sum_fwd(int dtype, const void *base, const void *const *srcs, const int *src_h,
+                                      const int *src_w, int n_src, int B, int C, int H, int W, void *out,
+                                      void *stream) {
+    IRADS_REQUIRE(dtype == IRADS_F32 || dtype == IRADS_BF16, "upsample_sum: dtype must be float32 or bfloat16");
+    IRADS_REQUIRE(n_src >= 0 && n_src <= kMaxSrc, "upsample_sum: at most %d sources", kMaxSrc);
+    IRADS_REQUIRE(B >= 0 && C > 0 && C % 8 == 0 && H > 0 && W > 0, "upsample_sum: need C %% 8 == 0 (C=%d)", C);
+    IRADS_REQUIRE(small_enough((long)B * C * H * W), "upsample_sum: tensor too large");
+    IRADS_REQUIRE(base && out && aligned16(base, out), "upsample_sum: base/out must be 16-byte aligned");
+    for (int s = 0; s < n_src; ++s)
+        IRADS_REQUIRE(srcs[s] && src_h[s] > 0 && src_w[s] > 0 && ((uintptr_t)srcs[s] % 16) == 0,
+                      "upsample_sum: bad source %d", s);
+    if (B == 0) return IRADS_OK;
+    hipStream_t st = (hipStream_t)stream;
+    const int g8 = walk8_grid(B, H, W, C);
+    if (dtype == IRADS_F32) {
+        Srcs<float> ss{};
+        ss.n = n_src;
+        for (int s = 0; s < n_src; ++s) ss.p[s] = (const float *)srcs[s], ss.h[s] = src_h[s], ss.w[s] = src_w[s];
+        upsample_sum_cl8<float><<<g8, 256, 0, st>>>((const float *)base, ss, (float *)out, B, H, W, C);
+    } else {
+        using U = unsigned short;
+        Srcs<U> ss{};
+        ss.n = n_src;
+        for (int s = 0; s < n_src; ++s) ss.p[s] = (const U *)srcs[s], ss.h[s] = src_h[s], ss.w[s] = src_w[s];
+        upsample_sum_cl8<U><<<g8, 256, 0, st>>>((const U *)base, ss, (U *)out, B, H, W, C);
+    }
+    return check_launch("irads_upsample_sum_fwd");
 }

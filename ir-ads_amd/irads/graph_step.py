@@ -13,10 +13,12 @@ What makes the step capturable (all in this package):
     draws fresh values, as the eager step does;
   * the learning rate is a device tensor that the host-side scheduler fills between replays
     (fused AdamW reads it on the device);
-  * gradients live in one flat fp32 buffer (each trainable parameter's .grad is a view of
-    it), zeroed inside the graph; with several ranks the buffer is all-reduced (RCCL, AVG)
-    between the backward graph and the optimizer graph, i.e. one bucket of 30 MB instead of
-    DDP's per-bucket hooks (data-parallel semantics of train_mm.py:94 unchanged).
+  * gradients are allocated by the captured backward itself (no .grad before capture, so
+    autograd hands each parameter its freshly computed gradient instead of adding it into a
+    zeroed one: no per-parameter add kernels); with several ranks they are packed into one
+    flat fp32 buffer inside the backward graph, all-reduced (RCCL sum, then 1/world) between the backward
+    graph and the optimizer graph, and unpacked by the optimizer graph: one 30 MB bucket
+    instead of DDP's per-bucket hooks (data-parallel semantics of train_mm.py:94 unchanged).
 """
 import torch
 import torch.distributed as dist
@@ -28,47 +30,67 @@ class GraphedTrainStep:
         self.world = world
         self.opt = optimizer
         dev = self.params[0].device
-        total = sum(p.numel() for p in self.params)
-        self.flat = torch.zeros((total,), device=dev, dtype=torch.float32)
-        off = 0
-        for p in self.params:
-            n = p.numel()
-            p.grad = self.flat[off:off + n].view_as(p)
-            off += n
+        self.flat = None
+        if world > 1:
+            self.flat = torch.zeros((sum(p.numel() for p in self.params),), device=dev, dtype=torch.float32)
         side = torch.cuda.Stream(device=dev)
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):  # warm-up (kernel selection, allocator pools) off the capture
             for _ in range(warmup):
-                self.flat.zero_()
+                optimizer.zero_grad(set_to_none=True)
                 fwd_bwd()
-                self._allreduce()
+                if world > 1:
+                    self._pack()
+                    dist.all_reduce(self.flat)
+                    self._unpack()
                 optimizer.step()
         torch.cuda.current_stream(dev).wait_stream(side)
         torch.cuda.synchronize(dev)
+        optimizer.zero_grad(set_to_none=True)
         if before_capture is not None:
             before_capture()
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
-            self.flat.zero_()
             self.loss = fwd_bwd()
             if world == 1:
                 optimizer.step()
+            else:
+                self._pack()
         self.opt_graph = None
         if world > 1:
             self.opt_graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.opt_graph, pool=self.graph.pool()):
+                self._unpack()
                 optimizer.step()
 
-    def _allreduce(self):
-        if self.world > 1:
-            dist.all_reduce(self.flat, op=dist.ReduceOp.AVG)
+    def _pack(self):
+        pack_grads(self.params, self.flat)
+
+    def _unpack(self):
+        unpack_grads(self.params, self.flat, 1.0 / self.world)
 
     def step(self):
         self.graph.replay()
         if self.opt_graph is not None:
-            self._allreduce()
+            dist.all_reduce(self.flat)  # RCCL sum over xGMI; the optimizer graph scales by 1/world
             self.opt_graph.replay()
         return self.loss
+
+
+def pack_grads(params, flat):
+    """Concatenate the parameters' gradients (zeros for a missing one) into `flat`."""
+    torch.cat([(p.grad if p.grad is not None else torch.zeros_like(p)).reshape(-1) for p in params], out=flat)
+
+
+def unpack_grads(params, flat, scale=1.0):
+    """Write `scale * flat` back into the parameters' gradients (created where missing)."""
+    if scale != 1.0:
+        flat.mul_(scale)
+    for p in params:
+        if p.grad is None:
+            p.grad = torch.zeros_like(p)
+    views = torch.split(flat, [p.numel() for p in params])
+    torch._foreach_copy_([p.grad for p in params], [v.view_as(p) for v, p in zip(views, params)])
 
 
 def events_capturable(device):

@@ -348,18 +348,55 @@ class ResizeFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, go):
         code, B, C, h, w, H, W, nchw = ctx.cfg
-        go = go.contiguous() if nchw or C == 1 else go.contiguous(memory_format=torch.channels_last)
-        gs = (ctypes.c_int64 * 4)(*go.stride())
-        gi = torch.empty((B, C, h, w), device=go.device, dtype=go.dtype,
-                         memory_format=torch.contiguous_format if nchw else torch.channels_last)
-        gis = (ctypes.c_int64 * 4)(*gi.stride())
-        ws = torch.empty((B * C * h * W,), device=go.device, dtype=torch.float32)
-        N.call("irads_resize_bwd", code, N.ptr(go), gs, B, C, H, W, N.ptr(gi), gis, h, w, N.ptr(ws), N.stream())
-        return gi, None
+        return _resize_bwd(go, code, B, C, h, w, H, W, nchw), None
+
+
+def _resize_bwd(go, code, B, C, h, w, H, W, nchw):
+    go = go.contiguous() if nchw or C == 1 else go.contiguous(memory_format=torch.channels_last)
+    gs = (ctypes.c_int64 * 4)(*go.stride())
+    gi = torch.empty((B, C, h, w), device=go.device, dtype=go.dtype,
+                     memory_format=torch.contiguous_format if nchw else torch.channels_last)
+    gis = (ctypes.c_int64 * 4)(*gi.stride())
+    ws = torch.empty((B * C * h * W,), device=go.device, dtype=torch.float32)
+    N.call("irads_resize_bwd", code, N.ptr(go), gs, B, C, H, W, N.ptr(gi), gis, h, w, N.ptr(ws), N.stream())
+    return gi
 
 
 def resize(x, size):
     return ResizeFn.apply(x, tuple(size))
+
+
+class UpsampleSumFn(torch.autograd.Function):
+    """base + Σ_s F.interpolate(src_s, base's size, bilinear, align_corners=False) on
+    channels-last tensors in one pass (fp32 sum, one rounding); backward: the identity for
+    base and the resize adjoint for each source."""
+
+    @staticmethod
+    def forward(ctx, base, *srcs):
+        N.check_device(base, "upsample_sum base")
+        code = N.dtype_code(base, (N.F32, N.BF16), "upsample_sum")
+        B, C, H, W = base.shape
+        cl = torch.channels_last
+        base = base.contiguous(memory_format=cl)
+        srcs = [s_.to(base.dtype).contiguous(memory_format=cl) for s_ in srcs]
+        out = torch.empty((B, C, H, W), device=base.device, dtype=base.dtype, memory_format=cl)
+        n = len(srcs)
+        ptrs = (ctypes.c_void_p * max(n, 1))(*[s_.data_ptr() for s_ in srcs])
+        hs = (ctypes.c_int * max(n, 1))(*[s_.shape[2] for s_ in srcs])
+        ws = (ctypes.c_int * max(n, 1))(*[s_.shape[3] for s_ in srcs])
+        N.call("irads_upsample_sum_fwd", code, N.ptr(base), ptrs, hs, ws, n, B, C, H, W, N.ptr(out), N.stream())
+        ctx.cfg = (code, B, C, H, W, [(s_.shape[2], s_.shape[3], s_.dtype) for s_ in srcs])
+        return out
+
+    @staticmethod
+    def backward(ctx, go):
+        code, B, C, H, W, shapes = ctx.cfg
+        gs = [_resize_bwd(go, code, B, C, h, w, H, W, False) for h, w, _ in shapes]
+        return (go, *gs)
+
+
+def upsample_sum(base, srcs):
+    return UpsampleSumFn.apply(base, *srcs)
 
 
 class CrossEntropyFn(torch.autograd.Function):

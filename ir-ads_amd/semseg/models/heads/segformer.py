@@ -39,10 +39,28 @@ class SegFormerHead(nn.Module):
         self.dropout = nn.Dropout2d(0.1)
 
     def forward(self, features: Tuple[Tensor, Tensor, Tensor, Tensor]) -> Tensor:
+        """Reference (segformer.py:37-48):
+            c_i = resize(MLP_i(f_i))  (i = 2..4; c_1 = MLP_1(f_1));  seg = BN-ReLU(W · cat[c4, c3, c2, c1])
+        Computed here as the algebraically identical
+            seg = BN-ReLU(z_1 + Σ_{i>1} resize(z_i)),  z_i = (W_i M_i) f_i + W_i b_i
+        where W_i is linear_fuse's column block for branch i and (M_i, b_i) the MLP: resize and a
+        1x1 projection commute, so each branch is ONE GEMM at its own resolution (1/4 ... 1/32)
+        into E channels, and the 4E-channel concatenation at 1/4 resolution never exists.  The
+        composed weights W_i M_i are formed each call (E x E x dim_i flops), so gradients reach
+        linear_fuse.conv.weight and every MLP through autograd.  Parameters and keys unchanged."""
         B, _, H, W = features[0].shape
-        outs = [self.linear_c1(features[0]).permute(0, 2, 1).reshape(B, -1, H, W)]
-        for i, f in enumerate(features[1:]):
-            cf = getattr(self, f"linear_c{i + 2}")(f).permute(0, 2, 1).reshape(B, -1, *f.shape[-2:])
-            outs.append(ops.resize(cf, (H, W)))  # F.interpolate(bilinear, align_corners=False)
-        seg = self.linear_fuse(torch.cat(outs[::-1], dim=1))
+        E = self.linear_fuse.conv.weight.shape[0]
+        Wf = self.linear_fuse.conv.weight.view(E, -1)  # column blocks: [c4 | c3 | c2 | c1]
+        n = len(features)
+        zs = []
+        for i, f in enumerate(features):
+            mlp = getattr(self, f"linear_c{i + 1}").proj
+            Wi = Wf[:, (n - 1 - i) * E:(n - i) * E]
+            with torch.autocast("cuda", enabled=False):
+                A = Wi @ mlp.weight  # (E, dim_i), fp32 composition
+                c = Wi @ mlp.bias
+            z = ops.linear(f.flatten(2).transpose(1, 2), A, c)  # (B, h*w, E)
+            zs.append(z.transpose(1, 2).reshape(B, E, *f.shape[-2:]))  # channels-last (B, E, h, w) view
+        seg = ops.upsample_sum(zs[0], zs[1:])
+        seg = self.linear_fuse.activate(self.linear_fuse.bn(seg))
         return self.linear_pred(self.dropout(seg))

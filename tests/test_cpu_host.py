@@ -124,3 +124,45 @@ def test_unsupported_configs_raise():
     w = WindowMSA(96, 4, (12, 12))  # head_dim 24
     with pytest.raises((NotImplementedError, RuntimeError)):
         w(torch.randn(1, 144, 96))
+
+
+def _dp_worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    from irads.graph_step import pack_grads, unpack_grads
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    torch.manual_seed(0)
+    params = [torch.nn.Parameter(torch.randn(s)) for s in ((3, 4), (5,), (2, 2, 2))]
+    for p in params:
+        p.grad = torch.full_like(p, float(rank + 1)) * torch.arange(p.numel()).view_as(p)
+    params[1].grad = None if rank == 1 else params[1].grad  # a rank without this gradient counts as zero
+    flat = torch.empty(sum(p.numel() for p in params))
+    pack_grads(params, flat)
+    dist.all_reduce(flat)
+    unpack_grads(params, flat, 1.0 / world)
+    q.put((rank, [p.grad.clone() for p in params]))
+    dist.destroy_process_group()
+
+
+def test_graph_step_gradient_allreduce_gloo():
+    """The data-parallel exchange of the graphed step (irads/graph_step.py): pack the
+    gradients, all-reduce (sum), unpack scaled by 1/world = DDP's gradient average."""
+    import socket
+    import torch
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_dp_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    for i, shape in enumerate(((3, 4), (5,), (2, 2, 2))):
+        base = torch.arange(torch.Size(shape).numel()).view(shape).float()
+        want = base * (1.5 if i != 1 else 0.5)  # mean of 1x and 2x (rank 1 lacks grad #1: 0)
+        for r in range(2):
+            torch.testing.assert_close(res[r][i], want)
