@@ -221,6 +221,14 @@ int irads_wgrad(const uint16_t *A, long lda, const uint16_t *B, long ldb, int K,
                 int accumulate, int transpose_out, float *D, float *colsum_a, float *colsum_b, float *workspace,
                 void *stream);
 
+/* Metrics.update (semseg/metrics.py:58-69): hist ((C+1) x C int64, accumulated) += the
+ * confusion of target (row; C = valid targets outside [0, C)) and arg-max over the C scores
+ * (column; first maximum, NaN maximal as torch.argmax), over pixels whose target !=
+ * ignore_index.  scores (B, C, H, W) fp32 or bf16, NCHW- or channels-last-contiguous,
+ * C <= 128; target int64 (B, H, W).  tp = diag, fp = column sum - diag, fn = row sum - diag. */
+int irads_confusion_update(int dtype, const void *scores, const int64_t *strides, int B, int C, int H, int W,
+                           const int64_t *target, int ignore_index, int64_t *hist, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

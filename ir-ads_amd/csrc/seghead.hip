@@ -16,6 +16,8 @@
 // Both ops run on the two dense layouts the head produces: NCHW-contiguous and
 // channels-last-contiguous (the `permute(0, 2, 1).reshape(...)` views of
 // segformer.py:41-43 are channels-last).  All are HBM-bound streaming kernels.
+#include <algorithm>
+
 #include "common.h"
 
 namespace irads {
@@ -302,6 +304,45 @@ __global__ void __launch_bounds__(256) upsample_sum_cl8(const T *__restrict__ ba
             acc[j] += ty.l0 * (tx.l0 * v00[j] + tx.l1 * v01[j]) + ty.l1 * (tx.l0 * v10[j] + tx.l1 * v11[j]);
     }
     V8<T>::st(out + o, acc);
+}
+
+// ------------------------------------------------------------------ confusion matrix (Metrics)
+// Metrics.update (semseg/metrics.py:58-69): arg-max over classes (first maximum, NaN counts
+// as maximal, as torch.argmax) and per-class tp / fp / fn over pixels whose target is not
+// ignore_index.  One pass over the scores: hist[t][p] += 1 with t = target (row C collects
+// targets outside [0, C) that are not ignored: they still make fp for the prediction) and
+// p = arg-max, privatised in LDS per workgroup and flushed with one 64-bit atomic per
+// non-zero cell.  tp/fp/fn follow from the matrix on the host, once per evaluation, instead
+// of the reference's 3·n_cls .item() synchronisations per batch.
+template <typename T, bool CL>
+__global__ void __launch_bounds__(256) confusion_kernel(const T *__restrict__ x, Dims d, const int64_t *__restrict__ tgt,
+                                                        int ignore, unsigned long long *__restrict__ hist) {
+    extern __shared__ unsigned int lh[];
+    const int C = d.C, cells = (C + 1) * C;
+    for (int i = threadIdx.x; i < cells; i += blockDim.x) lh[i] = 0;
+    __syncthreads();
+    const long npix = (long)d.B * d.H * d.W, HW = (long)d.H * d.W;
+    for (long pix = (long)blockIdx.x * blockDim.x + threadIdx.x; pix < npix; pix += (long)gridDim.x * blockDim.x) {
+        const long t = tgt[pix];
+        if (t == ignore) continue;
+        const long b = pix / HW, r = pix - b * HW;
+        const long base = CL ? pix * C : b * C * HW + r;
+        const long step = CL ? 1 : HW;
+        float best = ldf(x, base);
+        int arg = 0;
+        for (int c = 1; c < C; ++c) {
+            const float v = ldf(x, base + c * step);
+            if (!(best != best) && (v > best || v != v)) {  // first max; the first NaN wins
+                best = v;
+                arg = c;
+            }
+        }
+        const int row = (t >= 0 && t < C) ? (int)t : C;
+        atomicAdd(&lh[row * C + arg], 1u);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < cells; i += blockDim.x)
+        if (lh[i]) atomicAdd(&hist[i], (unsigned long long)lh[i]);
 }
 
 // ------------------------------------------------------------------ cross-entropy
@@ -728,4 +769,30 @@ extern "C" int irads_upsample_sum_fwd(int dtype, const void *base, const void *c
         upsample_sum_cl8<U><<<g8, 256, 0, st>>>((const U *)base, ss, (U *)out, B, H, W, C);
     }
     return check_launch("irads_upsample_sum_fwd");
+}
+
+extern "C" int irads_confusion_update(int dtype, const void *scores, const int64_t *strides, int B, int C, int H, int W,
+                                      const int64_t *target, int ignore_index, int64_t *hist, void *stream) {
+    IRADS_REQUIRE(dtype == IRADS_F32 || dtype == IRADS_BF16, "confusion: dtype must be float32 or bfloat16");
+    IRADS_REQUIRE(B >= 0 && C > 0 && C <= 128 && H > 0 && W > 0, "confusion: need 0 < C <= 128 (C=%d)", C);
+    IRADS_REQUIRE(scores && target && hist, "confusion: null pointer");
+    const int lay = layout_of(strides, B, C, H, W);
+    IRADS_REQUIRE(lay >= 0, "confusion: scores must be NCHW- or channels-last-contiguous");
+    if (B == 0) return IRADS_OK;
+    hipStream_t st = (hipStream_t)stream;
+    const Dims d{B, C, H, W};
+    const long npix = (long)B * H * W;
+    const int grid = (int)std::min<long>(1024, (npix + 255) / 256);
+    const size_t lds = sizeof(unsigned) * (C + 1) * C;
+    unsigned long long *h = (unsigned long long *)hist;
+    const bool cl = lay == 1 && C > 1;
+    if (dtype == IRADS_F32) {
+        if (cl) confusion_kernel<float, true><<<grid, 256, lds, st>>>((const float *)scores, d, target, ignore_index, h);
+        else confusion_kernel<float, false><<<grid, 256, lds, st>>>((const float *)scores, d, target, ignore_index, h);
+    } else {
+        using U = unsigned short;
+        if (cl) confusion_kernel<U, true><<<grid, 256, lds, st>>>((const U *)scores, d, target, ignore_index, h);
+        else confusion_kernel<U, false><<<grid, 256, lds, st>>>((const U *)scores, d, target, ignore_index, h);
+    }
+    return check_launch("irads_confusion_update");
 }

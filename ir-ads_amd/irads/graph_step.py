@@ -25,8 +25,13 @@ import torch.distributed as dist
 
 
 class GraphedTrainStep:
-    def __init__(self, params, fwd_bwd, optimizer, world=1, warmup=3, before_capture=None):
+    """restore: tensors (parameters, BN buffers) to snapshot before the warm-up iterations and
+    put back after capture, together with a zeroed optimizer state, so that the warm-up
+    leaves no trace on the training run (train_mm.py); the bench keeps its warm-up updates."""
+
+    def __init__(self, params, fwd_bwd, optimizer, world=1, warmup=3, before_capture=None, restore=None):
         self.params = [p for p in params if p.requires_grad]
+        snap = None if restore is None else [(t, t.detach().clone()) for t in restore]
         self.world = world
         self.opt = optimizer
         dev = self.params[0].device
@@ -62,6 +67,15 @@ class GraphedTrainStep:
             with torch.cuda.graph(self.opt_graph, pool=self.graph.pool()):
                 self._unpack()
                 optimizer.step()
+        if snap is not None:
+            with torch.no_grad():
+                for t, v in snap:
+                    t.copy_(v)
+                for st in optimizer.state.values():  # in place: the graph holds these addresses
+                    for v in st.values():
+                        if torch.is_tensor(v):
+                            v.zero_()
+            torch.cuda.synchronize(dev)
 
     def _pack(self):
         pack_grads(self.params, self.flat)

@@ -515,3 +515,20 @@ def linear(x, weight, bias=None):
         with torch.autocast("cuda", enabled=False):
             return LinearFn.apply(x, weight, bias)
     return torch.nn.functional.linear(x, weight, bias)
+
+
+# ------------------------------------------------------------------ evaluation metrics
+def confusion_update(scores, target, ignore_index, hist):
+    """hist ((C+1)*C int64) += confusion(target, argmax_c scores) over non-ignored pixels."""
+    N.check_device(scores, "metrics scores")
+    code = N.dtype_code(scores, (N.F32, N.BF16), "metrics scores")
+    scores, st = _layout(scores)
+    B, C, H, W = scores.shape
+    if tuple(target.shape) != (B, H, W):
+        raise RuntimeError(f"metrics: target shape {tuple(target.shape)} does not match scores {tuple(scores.shape)}")
+    target = N.check(target.to(torch.int64).contiguous(), "target")
+    N.check(hist, "hist", torch.int64)
+    if hist.numel() != (C + 1) * C:
+        raise RuntimeError("metrics: hist must hold (C+1)*C counters")
+    N.call("irads_confusion_update", code, N.ptr(scores), st, B, C, H, W, N.ptr(target), int(ignore_index),
+           N.ptr(hist), N.stream())

@@ -1,0 +1,98 @@
+"""Drivers and metrics on the GPU: Metrics (semseg/metrics.py, irads_confusion_update)
+against the reference's own tp/fp/fn/IoU fixture (exact integers), and a short
+train_mm.py / val_mm.py run on the synthetic dataset (graph-captured training step,
+evaluation, checkpoint round trip, multi-scale + flip evaluation)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+import yaml
+
+from golden_util import Fixture
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.parametrize("dtype,cl", [(torch.float32, False), (torch.bfloat16, True)])
+def test_metrics_golden(dtype, cl):
+    """Two updates (logits, flipped logits) as the fixture generator did with the reference
+    Metrics (oracle/gen_golden.py): tp/fp/fn exact, IoU list and mIoU as the reference's."""
+    from semseg.metrics import Metrics
+    fx = Fixture("metrics_loss.npz")
+    logits, gt = fx.t("logits", device=DEV), fx.t("gt", device=DEV)
+    if dtype == torch.bfloat16:
+        # bf16 rounding could create ties the fp32 reference does not have: only use it when the
+        # arg-max is unchanged
+        if not torch.equal(logits.argmax(1), logits.bfloat16().argmax(1)):
+            pytest.skip("bf16 rounding changes the arg-max of this fixture")
+    x = logits.to(dtype)
+    xf = logits.flip(-1).to(dtype)
+    if cl:
+        x, xf = x.contiguous(memory_format=torch.channels_last), xf.contiguous(memory_format=torch.channels_last)
+    m = Metrics(7, 255, DEV)
+    m.update(x.softmax(dim=1) if dtype == torch.float32 else x, gt)
+    m.update(xf.softmax(dim=1) if dtype == torch.float32 else xf, gt)
+    assert m.tp == fx["tp"].tolist() and m.fp == fx["fp"].tolist() and m.fn == fx["fn"].tolist()
+    ious, miou = m.compute_iou()
+    np.testing.assert_allclose(ious, fx["ious"], rtol=0, atol=1e-12)
+    assert miou == float(fx["miou"])
+    m.reset()
+    assert sum(m.tp) == 0
+
+
+def test_metrics_edge_cases():
+    """ignore pixels skipped; targets outside [0, C) that are not ignored still count as a
+    false positive of the predicted class (reference: valid & pred == i & gt != i); ties
+    go to the first class, NaN wins the arg-max as in torch.argmax."""
+    from semseg.metrics import Metrics
+    C = 3
+    s = torch.tensor([[1., 0., 0.], [0., 2., 2.], [0., 0., 5.], [float('nan'), 9., 0.], [0., 1., 0.]], device=DEV)
+    scores = s.t().reshape(1, C, 1, 5).contiguous()
+    gt = torch.tensor([[[0, 1, 255, 2, 7]]], device=DEV)
+    m = Metrics(C, 255, DEV)
+    m.update(scores, gt)
+    # pixel0: gt0 pred0 -> tp0; pixel1: gt1 pred1 (tie -> first) -> tp1; pixel2 ignored;
+    # pixel3: gt2 pred0 (NaN) -> fp0, fn2; pixel4: gt7 (valid, out of range) pred1 -> fp1
+    assert m.tp == [1, 1, 0] and m.fp == [1, 1, 0] and m.fn == [0, 0, 1]
+    assert scores.argmax(1).flatten().tolist()[:4] == [0, 1, 2, 0]
+
+
+def _cfg(tmp, **over):
+    with open(os.path.join(ROOT, "configs", "nyu_rgbd.yaml")) as f:
+        cfg = yaml.safe_load(f)
+    cfg["SAVE_DIR"] = str(tmp)
+    cfg["DATASET"].update(NAME="Synthetic", LENGTH=8)
+    cfg["TRAIN"].update(IMAGE_SIZE=[128, 128], BATCH_SIZE=4, EPOCHS=2, EVAL_START=0, EVAL_INTERVAL=1, WORKERS=0)
+    cfg["EVAL"].update(IMAGE_SIZE=[128, 128], BATCH_SIZE=2)
+    cfg["EVAL"]["MSF"].update(ENABLE=True, FLIP=True, SCALES=[0.5, 1.0])
+    cfg["SCHEDULER"]["WARMUP"] = 1
+    for k, v in over.items():
+        cfg["TRAIN"][k] = v
+    return cfg
+
+
+@pytest.mark.parametrize("graph", [True, False])
+def test_train_and_val_drivers(tmp_path, graph):
+    import train_mm
+    import val_mm
+    from pathlib import Path
+    from semseg.utils.utils import get_logger
+    torch.manual_seed(0)
+    cfg = _cfg(tmp_path, GRAPH=graph, AMP=True)
+    save = Path(tmp_path)
+    best = train_mm.main(cfg, 0, save, get_logger(save / "train.log"))
+    assert 0.0 <= best <= 100.0
+    ckpts = sorted(p for p in os.listdir(save) if p.endswith("_checkpoint.pth"))
+    assert len(ckpts) == 1
+    ck = torch.load(save / ckpts[0], map_location="cpu", weights_only=True)
+    assert set(ck) == {"epoch", "model_state_dict", "optimizer_state_dict", "loss", "scheduler_state_dict",
+                       "best_miou"}
+    assert np.isfinite(ck["loss"])
+    weights = [p for p in os.listdir(save) if p.endswith(".pth") and "checkpoint" not in p][0]
+    cfg["EVAL"]["MODEL_PATH"] = str(save / weights)
+    (miou,) = val_mm.main(cfg)
+    assert 0.0 <= miou <= 100.0
+    assert any(p.startswith("eval_") for p in os.listdir(save))
