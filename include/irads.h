@@ -96,16 +96,19 @@ int irads_dattn_sample_bwd(const float *x, const float *y, const float *q, const
                            int B, int C, int H, int W, int G, int n, float *grad_x, float *grad_y,
                            float *grad_q, float *grad_pos_x, float *grad_pos_y, void *stream);
 /* Fused attention with on-the-fly bilinear rpe bias (swin.py:950-1016):
- *   q (B*nH, hc, HW)  k, v (B*nH, hc, 2n)  rpe (nH, Ht, Wt)  qgrid_y (H), qgrid_x (W)
+ *   q (B*nH, hc, HW)  k, v KEY-MAJOR (B*nH, 2n, hc)  rpe (nH, Ht, Wt)  qgrid_y (H), qgrid_x (W)
  *   (the reference's _get_q_grid values)  out (B*nH, hc, HW)  lse (B*nH, HW).
- * hc in {2, 4, 8, 12, 16, 24}. */
+ * hc in {2, 4, 8, 12, 16}.  Positions and the query grid must lie in [-1, 1] (DAttentionMM
+ * clamps the positions, swin.py:905-906): the bias sample then stays on the table, which the
+ * kernels rely on (addresses are clamped, so other inputs read edge cells instead of the
+ * zero padding). */
 int irads_dattn_attn_fwd(const float *q, const float *k, const float *v, const float *pos_x,
                          const float *pos_y, const float *rpe, const float *qgrid_y, const float *qgrid_x,
                          int B, int nH, int G, int hc, int H, int W, int n, int Ht, int Wt, float scale,
                          float *out, float *lse, void *stream);
-/* grad_q fully written; grad_k, grad_v, grad_rpe, grad_pos_x, grad_pos_y zero-filled by
- * the caller (per-workgroup partial sums are added atomically). delta (B*nH, HW) fp32
- * workspace. */
+/* grad_q, grad_k, grad_v (key-major), grad_rpe, grad_pos_x, grad_pos_y zero-filled by the
+ * caller (per-workgroup / per-key-split partial sums are added atomically). delta (B*nH, HW)
+ * fp32 workspace. */
 int irads_dattn_attn_bwd(const float *q, const float *k, const float *v, const float *pos_x,
                          const float *pos_y, const float *rpe, const float *qgrid_y, const float *qgrid_x,
                          int B, int nH, int G, int hc, int H, int W, int n, int Ht, int Wt, float scale,

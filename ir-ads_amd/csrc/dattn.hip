@@ -161,89 +161,58 @@ struct AttnArgs {
     float scale;
 };
 
-// bias of (query at grid (gy, gx)) for a key at pos (py, px): table sampled at
-// 0.5 * (q_grid - pos) (swin.py:983-1007), align_corners=True, zero padding.
-__device__ __forceinline__ float rpe_bias(const float *tab, int Ht, int Wt, float qgy, float qgx, float pyk, float pxk,
-                                          Corner &cr, Taps &tp) {
-    const float dy = (qgy - pyk) * 0.5f, dx = (qgx - pxk) * 0.5f;
-    cr = corner_ac(dx, dy, Ht, Wt);
-    tp = taps(tab, Ht, Wt, cr);
-    return interp(tp, cr);
+// ---------------------------------------------------------------- shared pieces
+// The rpe table lives in LDS padded to (Ht+1) x (Wt+1) with a zero last row and column.
+// Displacements 0.5·(q_grid − pos) of clamped positions lie in [−1, 1], so the corner is
+// always inside the table and the +1 taps land on the zero pad: no bounds tests and no
+// branches on the hot path (include/irads.h states the [-1, 1] precondition).
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kLn2 = 0.6931471805599453f;
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2 pk_fma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+
+// Bias of one (query, key) pair with packed fp32 (v_pk_*): (x, y) travel together.
+// disp = 0.5·(q_grid − pos) and idx = (disp + 1)·((size − 1)/2) are rounded exactly as the
+// scalar corner_ac (same operations, same order); the four taps are two ds_read2_b32 of the
+// padded table and the interpolation is one packed multiply + one packed fma + one add.
+struct BiasPk {
+    int o;        // (y0, x0) cell in the padded table
+    f2 fr;        // (fx, fy)
+    f2 wt, wb;    // weights (nw, ne), (sw, se)
+    f2 t0, t1;    // taps (nw, ne), (sw, se)
+    float v;
+};
+__device__ __forceinline__ BiasPk rpe_bias_pk(const float *tab, int Ht, int Wt, f2 qg, f2 pk, f2 sc) {
+    BiasPk b;
+    const f2 d = (qg - pk) * (f2){0.5f, 0.5f};
+    const f2 ii = (d + (f2){1.f, 1.f}) * sc;
+    const f2 fl = {floorf(ii.x), floorf(ii.y)};
+    b.fr = ii - fl;
+    // positions are clamped to [-1, 1] by DAttentionMM (swin.py:905-906) and the query grid
+    // lies in [-1, 1], so the corner is on the table; the clamp only guards the addresses
+    // (branch-free: the four keys of an unrolled step schedule together)
+    const int x0 = min(max((int)fl.x, 0), Wt - 1), y0 = min(max((int)fl.y, 0), Ht - 1), TP = Wt + 1;
+    const f2 om = (f2){1.f, 1.f} - b.fr;
+    const f2 wx = {om.x, b.fr.x};
+    b.wt = wx * (f2){om.y, om.y};
+    b.wb = wx * (f2){b.fr.y, b.fr.y};
+    b.o = y0 * TP + x0;
+    b.t0 = (f2){tab[b.o], tab[b.o + 1]};
+    b.t1 = (f2){tab[b.o + TP], tab[b.o + TP + 1]};
+    const f2 v = pk_fma(b.t1, b.wb, b.t0 * b.wt);
+    b.v = v.x + v.y;
+    return b;
 }
 
-// LDS layout (floats): table[Ht*Wt] | kv[2n][2*HC] (k then v per key) | pos[2n][2]
-template <int HC>
-__global__ void __launch_bounds__(1024) dattn_attn_fwd_kernel(AttnArgs a, float *__restrict__ out,
-                                                              float *__restrict__ lse) {
-    extern __shared__ __attribute__((aligned(16))) float sm[];
-    const int n2 = 2 * a.n, HW = a.H * a.W, TT = a.Ht * a.Wt;
-    float *tab = sm, *kv = sm + TT, *pos = kv + n2 * 2 * HC;
-    const int bh = blockIdx.y, b = bh / a.nH, h = bh % a.nH;
-    const int gi = h / (a.nH / a.G);
-    for (int i = threadIdx.x; i < TT; i += blockDim.x) tab[i] = a.rpe[(long)h * TT + i];
-    for (int i = threadIdx.x; i < n2 * HC; i += blockDim.x) {
-        const int c = i / n2, j = i % n2;
-        kv[j * 2 * HC + c] = a.k[((long)bh * HC + c) * n2 + j];
-        kv[j * 2 * HC + HC + c] = a.v[((long)bh * HC + c) * n2 + j];
-    }
-    for (int j = threadIdx.x; j < n2; j += blockDim.x) {
-        const float *p = (j < a.n ? a.px : a.py) + ((long)(b * a.G + gi) * a.n + (j % a.n)) * 2;
-        pos[2 * j] = p[0];
-        pos[2 * j + 1] = p[1];
-    }
-    __syncthreads();
-    const int qi = blockIdx.x * blockDim.x + threadIdx.x;
-    if (qi >= HW) return;
-    const float qgy = a.qgy[qi / a.W], qgx = a.qgx[qi % a.W];
-    float qv[HC], acc[HC];
-#pragma unroll
-    for (int c = 0; c < HC; ++c) {
-        qv[c] = a.q[((long)bh * HC + c) * HW + qi];
-        acc[c] = 0.f;
-    }
-    float m = -INFINITY, l = 0.f;
-    for (int j = 0; j < n2; ++j) {
-        const float *kr = kv + j * 2 * HC;
-        float s = 0.f;
-#pragma unroll
-        for (int c = 0; c < HC; ++c) s = fmaf(qv[c], kr[c], s);
-        Corner cr;
-        Taps tp;
-        s = s * a.scale + rpe_bias(tab, a.Ht, a.Wt, qgy, qgx, pos[2 * j], pos[2 * j + 1], cr, tp);
-        const float mn = fmaxf(m, s);
-        const float corr = __expf(m - mn), p = __expf(s - mn);
-        l = l * corr + p;
-#pragma unroll
-        for (int c = 0; c < HC; ++c) acc[c] = fmaf(p, kr[HC + c], acc[c] * corr);
-        m = mn;
-    }
-    const float inv = 1.f / l;
-#pragma unroll
-    for (int c = 0; c < HC; ++c) out[((long)bh * HC + c) * HW + qi] = acc[c] * inv;
-    lse[(long)bh * HW + qi] = m + __logf(l);
-}
+__device__ __forceinline__ int pad_cells(int Ht, int Wt) { return ((Ht + 1) * (Wt + 1) + 3) & ~3; }
 
-// Pass Q (thread per query): dq, delta = dO·O, and the rpe-table gradient.
-//  * The table gradient is accumulated per workgroup in LDS in FIXED POINT with integer
-//    atomics: on gfx950 ds_add_f32 retires ~0.3 lanes/clk/CU whatever the address
-//    pattern, ds_add_u32 ~4 (scripts/microbench/lds_atomic.hip).  The scale is a power of
-//    two per workgroup chosen from a bound on its total contribution: for query q,
-//    Σ_k |ds_qk| = Σ_k p_qk |dp_qk − δ_q| ≤ |δ_q| + Σ_c |dO_qc| · max_k |v_kc|, and the four
-//    bilinear weights of a sample sum to 1, so no cell can exceed B = Σ_q bound_q;
-//    scale = 2^(30 − ⌈log2 B⌉) keeps every partial sum inside int32 with a resolution of
-//    B·2^-31 (fp32 accumulation of the same sums carries 2^-24 relative error).  Each
-//    workgroup flushes its non-zero cells with one float atomic each (consecutive cells:
-//    the coalesced atomic pattern).
-//  * k, v and the key positions are read with wave-uniform addresses (scalar loads), so
-//    LDS holds only the gradient table and two workgroups fit per CU.
-__device__ __forceinline__ void scatter_fx(int *tg, int Ht, int Wt, const Corner &cr, float dsq) {
-    const bool xl = cr.x0 >= 0 && cr.x0 < Wt, xh = cr.x0 + 1 >= 0 && cr.x0 + 1 < Wt;
-    const bool yl = cr.y0 >= 0 && cr.y0 < Ht, yh = cr.y0 + 1 >= 0 && cr.y0 + 1 < Ht;
-    const int o = cr.y0 * Wt + cr.x0;
-    if (yl && xl) atomicAdd(&tg[o], __float2int_rn(cr.nw * dsq));
-    if (yl && xh) atomicAdd(&tg[o + 1], __float2int_rn(cr.ne * dsq));
-    if (yh && xl) atomicAdd(&tg[o + Wt], __float2int_rn(cr.sw * dsq));
-    if (yh && xh) atomicAdd(&tg[o + Wt + 1], __float2int_rn(cr.se * dsq));
+__device__ __forceinline__ void load_table_padded(float *tab, const float *__restrict__ src, int Ht, int Wt) {
+    const int TP = Wt + 1, TT = pad_cells(Ht, Wt);
+    for (int i = threadIdx.x; i < TT; i += blockDim.x) {
+        const int r = i / TP, c = i - r * TP;
+        tab[i] = (r < Ht && c < Wt) ? src[r * Wt + c] : 0.f;
+    }
 }
 
 __device__ __forceinline__ float block_sum_f(float v, float *red) {
@@ -257,30 +226,181 @@ __device__ __forceinline__ float block_sum_f(float v, float *red) {
     return s;
 }
 
-// LDS: tgrad[TT] (int32 fixed point)
+// Key data are read with wave-uniform addresses: k and v come KEY-MAJOR, (B*nH, 2n, hc), so a
+// key's channels are one scalar load each (s_load_dwordx8 for hc = 8) through the scalar
+// cache; positions likewise.  LDS is left to the bias table (and, in pass Q, the fixed-point
+// table gradient).
+struct KeyRef {
+    const float *k, *v, *px, *py;  // this (b, head)'s keys, this (b, group)'s positions
+};
+__device__ __forceinline__ KeyRef key_ref(const AttnArgs &a, const float *__restrict__ kg, const float *__restrict__ vg,
+                                         const float *__restrict__ pxg, const float *__restrict__ pyg, int bh, int b,
+                                         int gi, int HC) {
+    const int n2 = 2 * a.n;
+    KeyRef r;
+    r.k = kg + (long)bh * n2 * HC;
+    r.v = vg + (long)bh * n2 * HC;
+    r.px = pxg + (long)(b * a.G + gi) * a.n * 2;
+    r.py = pyg + (long)(b * a.G + gi) * a.n * 2;
+    return r;
+}
+// position (x, y) of key j (uniform)
+__device__ __forceinline__ f2 key_pos(const KeyRef &r, int n, int j) {
+    const float *p = j < n ? r.px + 2 * j : r.py + 2 * (j - n);
+    return (f2){p[1], p[0]};
+}
+
+// Work split: lanes = queries (64 consecutive per wave: the bias samples of a key are then
+// neighbouring table cells, few LDS bank conflicts), a workgroup = QW query-waves x KSP
+// key-splits (QW * KSP = 16 waves); each wave runs an online softmax over its 2n/KSP keys,
+// four keys per step, and the KSP partial states of a query are merged through LDS.
+__device__ __forceinline__ int uniform_int(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// ---------------------------------------------------------------- forward
+// LDS: table[pad_cells] | part[16 waves][HC + 2][64]
 template <int HC>
-__global__ void __launch_bounds__(512) dattn_attn_bwd_q_kernel(AttnArgs a, const float *__restrict__ out,
-                                                               const float *__restrict__ lse,
-                                                               const float *__restrict__ gout,
-                                                               float *__restrict__ delta, float *__restrict__ gq,
-                                                               float *__restrict__ grpe) {
-    extern __shared__ __attribute__((aligned(16))) int tgi[];
-    __shared__ float red[8], vmx[8][HC];
-    const int n2 = 2 * a.n, HW = a.H * a.W, TT = a.Ht * a.Wt;
+__global__ void __launch_bounds__(1024) dattn_attn_fwd_kernel(AttnArgs a, int KSP, const float *__restrict__ kg,
+                                                              const float *__restrict__ vg,
+                                                              const float *__restrict__ pxg,
+                                                              const float *__restrict__ pyg, float *__restrict__ out,
+                                                              float *__restrict__ lse) {
+    static_assert(HC % 2 == 0, "packed fp32 needs an even head size");
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    const int n2 = 2 * a.n, HW = a.H * a.W;
+    float *tab = sm, *part = sm + pad_cells(a.Ht, a.Wt);
     const int bh = blockIdx.y, b = bh / a.nH, h = bh % a.nH;
     const int gi = h / (a.nH / a.G);
-    const float *tab = a.rpe + (long)h * TT;
-    const float *kb = a.k + (long)bh * HC * n2, *vb = a.v + (long)bh * HC * n2;
-    const float *pxb = a.px + (long)(b * a.G + gi) * a.n * 2, *pyb = a.py + (long)(b * a.G + gi) * a.n * 2;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    for (int i = tid; i < TT; i += blockDim.x) tgi[i] = 0;
-    // max_k |v_kc| per channel
+    load_table_padded(tab, a.rpe + (long)h * a.Ht * a.Wt, a.Ht, a.Wt);
+    __syncthreads();
+    const KeyRef kr = key_ref(a, kg, vg, pxg, pyg, bh, b, gi, HC);
+    const int wave = uniform_int(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int QW = 16 / KSP, qw = wave % QW, sp = wave / QW;
+    const int kb = uniform_int(sp * n2 / KSP), ke = uniform_int((sp + 1) * n2 / KSP);
+    const f2 sc = {((float)a.Wt - 1.0f) / 2.0f, ((float)a.Ht - 1.0f) / 2.0f};
+    float *mypart = part + (long)wave * (HC + 2) * 64 + lane;
+    for (int q0 = blockIdx.x * QW * 64; q0 < HW; q0 += gridDim.x * QW * 64) {
+        const int qi = q0 + qw * 64 + lane;
+        const bool valid = qi < HW;
+        const int qc = valid ? qi : HW - 1;
+        const f2 qg = {a.qgx[qc % a.W], a.qgy[qc / a.W]};
+        f2 qv[HC / 2], acc[HC / 2];
+#pragma unroll
+        for (int c = 0; c < HC / 2; ++c) {
+            qv[c] = (f2){a.q[((long)bh * HC + 2 * c) * HW + qc], a.q[((long)bh * HC + 2 * c + 1) * HW + qc]};
+            acc[c] = (f2){0.f, 0.f};
+        }
+        float m = -1e30f, l = 0.f;
+        for (int j0 = kb; j0 < ke; j0 += 4) {
+            float s2[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int j = min(j0 + u, ke - 1);
+                const f2 *kk = reinterpret_cast<const f2 *>(kr.k + (long)j * HC);
+                f2 d = {0.f, 0.f};
+#pragma unroll
+                for (int c = 0; c < HC / 2; ++c) d = pk_fma(qv[c], kk[c], d);
+                const BiasPk bi = rpe_bias_pk(tab, a.Ht, a.Wt, qg, key_pos(kr, a.n, j), sc);
+                s2[u] = (j0 + u < ke) ? ((d.x + d.y) * a.scale + bi.v) * kLog2e : -1e30f;  // swin.py:951-1010
+            }
+            const float mx = fmaxf(fmaxf(m, fmaxf(s2[0], s2[1])), fmaxf(s2[2], s2[3]));
+            const float corr = fast_exp2(m - mx);
+            l *= corr;
+#pragma unroll
+            for (int c = 0; c < HC / 2; ++c) acc[c] *= (f2){corr, corr};
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int j = min(j0 + u, ke - 1);
+                const float p = (j0 + u < ke) ? fast_exp2(s2[u] - mx) : 0.f;
+                l += p;
+                const f2 *vv = reinterpret_cast<const f2 *>(kr.v + (long)j * HC);
+#pragma unroll
+                for (int c = 0; c < HC / 2; ++c) acc[c] = pk_fma((f2){p, p}, vv[c], acc[c]);
+            }
+            m = mx;
+        }
+        if (KSP > 1) {  // merge the key splits of this query wave through LDS
+            mypart[0] = m;
+            mypart[64] = l;
+#pragma unroll
+            for (int c = 0; c < HC / 2; ++c) {
+                mypart[(2 + 2 * c) * 64] = acc[c].x;
+                mypart[(3 + 2 * c) * 64] = acc[c].y;
+            }
+            __syncthreads();
+            if (sp == 0) {
+                float M = m;
+                for (int o = 1; o < KSP; ++o) M = fmaxf(M, part[((long)(o * QW + qw) * (HC + 2)) * 64 + lane]);
+                const float f0 = fast_exp2(m - M);
+                l *= f0;
+#pragma unroll
+                for (int c = 0; c < HC / 2; ++c) acc[c] *= (f2){f0, f0};
+                for (int o = 1; o < KSP; ++o) {
+                    const float *pp = part + ((long)(o * QW + qw) * (HC + 2)) * 64 + lane;
+                    const float f = fast_exp2(pp[0] - M);
+                    l = fmaf(pp[64], f, l);
+#pragma unroll
+                    for (int c = 0; c < HC / 2; ++c)
+                        acc[c] = pk_fma((f2){f, f}, (f2){pp[(2 + 2 * c) * 64], pp[(3 + 2 * c) * 64]}, acc[c]);
+                }
+                m = M;
+            }
+            __syncthreads();
+        }
+        if (sp == 0 && valid) {
+            const float inv = 1.f / l;
+#pragma unroll
+            for (int c = 0; c < HC / 2; ++c) {
+                out[((long)bh * HC + 2 * c) * HW + qi] = acc[c].x * inv;
+                out[((long)bh * HC + 2 * c + 1) * HW + qi] = acc[c].y * inv;
+            }
+            lse[(long)bh * HW + qi] = m * kLn2 + logf(l);
+        }
+    }
+}
+
+// ---------------------------------------------------------------- backward, pass Q
+// dq (key splits add into the zero-filled gq with float atomics, one per query channel and
+// split), delta = dO·O, and the rpe-table gradient.  The table gradient is accumulated per
+// workgroup in LDS in FIXED POINT with integer atomics (on gfx950 ds_add_f32 retires ~0.3
+// lanes/clk/CU whatever the address pattern, ds_add_u32 ~4: scripts/microbench/lds_atomic.hip);
+// a wave's lanes are consecutive queries of one key, so their four taps are neighbouring
+// cells.  The scale is a power of two chosen from a bound on the workgroup's total
+// contribution: Σ_k |ds_qk| = Σ_k p_qk |dp_qk − δ_q| ≤ |δ_q| + Σ_c |dO_qc| · max_k |v_kc|, and
+// the four bilinear weights of a sample sum to 1, so no cell exceeds B = Σ_q bound_q;
+// scale = 2^(30 − ⌈log2 B⌉) keeps every partial sum inside int32 (resolution B·2^-31; fp32
+// accumulation of the same sums carries 2^-24 relative error).  The workgroup flushes its
+// non-zero cells with one float atomic each.
+// LDS: table[pad] (float) | tgi[pad] (int)
+template <int HC>
+__global__ void __launch_bounds__(1024) dattn_attn_bwd_q_kernel(AttnArgs a, int KSP, const float *__restrict__ kg,
+                                                                const float *__restrict__ vg,
+                                                                const float *__restrict__ pxg,
+                                                                const float *__restrict__ pyg,
+                                                                const float *__restrict__ out,
+                                                                const float *__restrict__ lse,
+                                                                const float *__restrict__ gout,
+                                                                float *__restrict__ delta, float *__restrict__ gq,
+                                                                float *__restrict__ grpe) {
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    __shared__ float red[16], vmx[16][HC];
+    const int n2 = 2 * a.n, HW = a.H * a.W, PC = pad_cells(a.Ht, a.Wt);
+    float *tab = sm;
+    int *tgi = reinterpret_cast<int *>(sm + PC);
+    const int bh = blockIdx.y, b = bh / a.nH, h = bh % a.nH;
+    const int gi = h / (a.nH / a.G);
+    load_table_padded(tab, a.rpe + (long)h * a.Ht * a.Wt, a.Ht, a.Wt);
+    for (int i = threadIdx.x; i < PC; i += blockDim.x) tgi[i] = 0;
+    const KeyRef kr = key_ref(a, kg, vg, pxg, pyg, bh, b, gi, HC);
+    const int wave = uniform_int(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int QW = 16 / KSP, qw = wave % QW, sp = wave / QW;
+    const int kb = uniform_int(sp * n2 / KSP), ke = uniform_int((sp + 1) * n2 / KSP);
+    // max_k |v_kc| over this (b, head)'s keys
     float vm[HC];
 #pragma unroll
     for (int c = 0; c < HC; ++c) vm[c] = 0.f;
-    for (int j = tid; j < n2; j += blockDim.x)
+    for (int j = threadIdx.x; j < n2; j += blockDim.x)
 #pragma unroll
-        for (int c = 0; c < HC; ++c) vm[c] = fmaxf(vm[c], fabsf(vb[c * n2 + j]));
+        for (int c = 0; c < HC; ++c) vm[c] = fmaxf(vm[c], fabsf(kr.v[(long)j * HC + c]));
 #pragma unroll
     for (int c = 0; c < HC; ++c) {
 #pragma unroll
@@ -291,103 +411,134 @@ __global__ void __launch_bounds__(512) dattn_attn_bwd_q_kernel(AttnArgs a, const
 #pragma unroll
     for (int c = 0; c < HC; ++c) {
         vm[c] = 0.f;
-        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) vm[c] = fmaxf(vm[c], vmx[w][c]);
+        for (int w = 0; w < 16; ++w) vm[c] = fmaxf(vm[c], vmx[w][c]);
     }
-    const int qi = blockIdx.x * blockDim.x + tid;
-    const bool valid = qi < HW;
-    float qv[HC], dq[HC], dov[HC];
-    float dl = 0.f, bound = 0.f, qgy = 0.f, qgx = 0.f, ls = 0.f;
-#pragma unroll
-    for (int c = 0; c < HC; ++c) {
-        qv[c] = dov[c] = dq[c] = 0.f;
-        if (valid) {
-            const long o = ((long)bh * HC + c) * HW + qi;
-            qv[c] = a.q[o];
-            dov[c] = gout[o];
-            dl = fmaf(dov[c], out[o], dl);
-        }
-    }
-    if (valid) {
-        qgy = a.qgy[qi / a.W];
-        qgx = a.qgx[qi % a.W];
-        ls = lse[(long)bh * HW + qi];
-        bound = fabsf(dl);
-#pragma unroll
-        for (int c = 0; c < HC; ++c) bound = fmaf(fabsf(dov[c]), vm[c], bound);
-    }
-    const float btot = block_sum_f(bound, red);
-    // fixed-point scale 2^e with btot·2^e <= 2^30 (exact power of two: scaling and unscaling are exact)
-    const int e = (btot > 0.f && btot < 1e30f) ? min(100, 30 - (int)ceilf(log2f(btot))) : 0;
-    const float fx = ldexpf(1.f, e), inv_fx = ldexpf(1.f, -e);
-    if (valid) {
-        for (int j = 0; j < n2; ++j) {
-            float kr[HC], s = 0.f, dp = 0.f;
+    // bound over the queries this workgroup visits (each counted once: split 0's lanes)
+    float bound = 0.f;
+    for (int q0 = blockIdx.x * QW * 64; q0 < HW; q0 += gridDim.x * QW * 64) {
+        const int qi = q0 + qw * 64 + lane;
+        if (sp == 0 && qi < HW) {
+            float dl = 0.f, bq = 0.f;
 #pragma unroll
             for (int c = 0; c < HC; ++c) {
-                kr[c] = kb[c * n2 + j];
-                s = fmaf(qv[c], kr[c], s);
-                dp = fmaf(dov[c], vb[c * n2 + j], dp);
+                const long o = ((long)bh * HC + c) * HW + qi;
+                const float g = gout[o];
+                dl = fmaf(g, out[o], dl);
+                bq = fmaf(fabsf(g), vm[c], bq);
             }
-            const float *pp = (j < a.n ? pxb : pyb) + 2 * (j < a.n ? j : j - a.n);
-            Corner cr;
-            Taps tp;
-            s = s * a.scale + rpe_bias(tab, a.Ht, a.Wt, qgy, qgx, pp[0], pp[1], cr, tp);
+            bound += bq + fabsf(dl);
+        }
+    }
+    const float btot = block_sum_f(bound, red);
+    const int e = (btot > 0.f && btot < 1e30f) ? min(100, 30 - (int)ceilf(log2f(btot))) : 0;
+    const float fxs = ldexpf(1.f, e), inv_fx = ldexpf(1.f, -e);
+    const f2 sc = {((float)a.Wt - 1.0f) / 2.0f, ((float)a.Ht - 1.0f) / 2.0f};
+    const int TP = a.Wt + 1;
+    for (int q0 = blockIdx.x * QW * 64; q0 < HW; q0 += gridDim.x * QW * 64) {
+        const int qi = q0 + qw * 64 + lane;
+        const bool valid = qi < HW;
+        const int qc = valid ? qi : HW - 1;
+        const f2 qg = {a.qgx[qc % a.W], a.qgy[qc / a.W]};
+        const float ls = lse[(long)bh * HW + qc];
+        f2 qv[HC / 2], dov[HC / 2], dq[HC / 2];
+        float dl = 0.f;
+#pragma unroll
+        for (int c = 0; c < HC / 2; ++c) {
+            const long o0 = ((long)bh * HC + 2 * c) * HW + qc, o1 = o0 + HW;
+            qv[c] = (f2){a.q[o0], a.q[o1]};
+            dov[c] = (f2){gout[o0], gout[o1]};
+            dl = fmaf(dov[c].x, out[o0], dl);
+            dl = fmaf(dov[c].y, out[o1], dl);
+            dq[c] = (f2){0.f, 0.f};
+        }
+        const float dsv = valid ? 1.f : 0.f;  // invalid lanes contribute nothing to the table
+        for (int j = kb; j < ke; ++j) {
+            const f2 *kk = reinterpret_cast<const f2 *>(kr.k + (long)j * HC);
+            const f2 *vv = reinterpret_cast<const f2 *>(kr.v + (long)j * HC);
+            f2 d = {0.f, 0.f}, dp = {0.f, 0.f};
+#pragma unroll
+            for (int c = 0; c < HC / 2; ++c) {
+                d = pk_fma(qv[c], kk[c], d);
+                dp = pk_fma(dov[c], vv[c], dp);
+            }
+            const BiasPk bi = rpe_bias_pk(tab, a.Ht, a.Wt, qg, key_pos(kr, a.n, j), sc);
+            const float s = (d.x + d.y) * a.scale + bi.v;
             const float p = __expf(s - ls);
-            const float ds = p * (dp - dl);
+            const float ds = p * ((dp.x + dp.y) - dl) * dsv;
             const float dss = ds * a.scale;
 #pragma unroll
-            for (int c = 0; c < HC; ++c) dq[c] = fmaf(dss, kr[c], dq[c]);
-            scatter_fx(tgi, a.Ht, a.Wt, cr, ds * fx);
+            for (int c = 0; c < HC / 2; ++c) dq[c] = pk_fma((f2){dss, dss}, kk[c], dq[c]);
+            const float dsq = ds * fxs;
+            atomicAdd(&tgi[bi.o], __float2int_rn(bi.wt.x * dsq));
+            atomicAdd(&tgi[bi.o + 1], __float2int_rn(bi.wt.y * dsq));
+            atomicAdd(&tgi[bi.o + TP], __float2int_rn(bi.wb.x * dsq));
+            atomicAdd(&tgi[bi.o + TP + 1], __float2int_rn(bi.wb.y * dsq));
         }
+        if (valid) {
+            if (KSP > 1) {
 #pragma unroll
-        for (int c = 0; c < HC; ++c) gq[((long)bh * HC + c) * HW + qi] = dq[c];
-        delta[(long)bh * HW + qi] = dl;
+                for (int c = 0; c < HC / 2; ++c) {
+                    atomicAdd(&gq[((long)bh * HC + 2 * c) * HW + qi], dq[c].x);
+                    atomicAdd(&gq[((long)bh * HC + 2 * c + 1) * HW + qi], dq[c].y);
+                }
+            } else {
+#pragma unroll
+                for (int c = 0; c < HC / 2; ++c) {
+                    gq[((long)bh * HC + 2 * c) * HW + qi] = dq[c].x;
+                    gq[((long)bh * HC + 2 * c + 1) * HW + qi] = dq[c].y;
+                }
+            }
+            if (sp == 0) delta[(long)bh * HW + qi] = dl;
+        }
     }
     __syncthreads();
-    for (int i = tid; i < TT; i += blockDim.x) {
-        const int v = tgi[i];
-        if (v != 0) atomicAdd(&grpe[(long)h * TT + i], (float)v * inv_fx);
+    for (int i = threadIdx.x; i < a.Ht * a.Wt; i += blockDim.x) {
+        const int r = i / a.Wt, c = i - r * a.Wt;
+        const int v = tgi[r * TP + c];
+        if (v != 0) atomicAdd(&grpe[(long)h * a.Ht * a.Wt + i], (float)v * inv_fx);
     }
 }
 
-constexpr int QCH = 64;  // queries staged per LDS round in pass K
+// ---------------------------------------------------------------- backward, pass K
+// Thread per key, looping over a range of queries staged through LDS (broadcast reads): dk,
+// dv and d(pos) of its key stay in registers and are added into the zero-filled outputs
+// once per workgroup.  The bias is recomputed from the padded table in LDS.
+// LDS: tab[pad] | qst[QCH][2*HC + 4]
+constexpr int QCH = 64;
 
-// Pass K (thread per key): loops over a chunk of queries staged in LDS and keeps dk, dv
-// and d(pos) of its key in registers (no reduction over lanes).  The bias is recomputed
-// from the table through L1/L2; LDS is only the query staging, so several workgroups
-// share a CU.  LDS: qst[QCH][2*HC + 4] (q, dO, lse, delta, qgy, qgx)
 template <int HC>
-__global__ void __launch_bounds__(1024) dattn_attn_bwd_k_kernel(AttnArgs a, const float *__restrict__ lse,
+__global__ void __launch_bounds__(1024) dattn_attn_bwd_k_kernel(AttnArgs a, const float *__restrict__ kg,
+                                                                const float *__restrict__ vg,
+                                                                const float *__restrict__ pxg,
+                                                                const float *__restrict__ pyg,
+                                                                const float *__restrict__ lse,
                                                                 const float *__restrict__ delta,
                                                                 const float *__restrict__ gout, int q_per_block,
                                                                 float *__restrict__ gk, float *__restrict__ gv,
                                                                 float *__restrict__ gpx, float *__restrict__ gpy) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
-    const int n2 = 2 * a.n, HW = a.H * a.W, TT = a.Ht * a.Wt;
+    const int n2 = 2 * a.n, HW = a.H * a.W, PC = pad_cells(a.Ht, a.Wt);
     constexpr int QS = 2 * HC + 4;
-    float *qst = sm;
+    float *tab = sm, *qst = sm + PC;
     const int bh = blockIdx.y, b = bh / a.nH, h = bh % a.nH;
     const int gi = h / (a.nH / a.G);
-    const float *tab = a.rpe + (long)h * TT;
+    load_table_padded(tab, a.rpe + (long)h * a.Ht * a.Wt, a.Ht, a.Wt);
+    const KeyRef kr = key_ref(a, kg, vg, pxg, pyg, bh, b, gi, HC);
     const int j = threadIdx.x;
     const bool active = j < n2;
-    float kr[HC], vr[HC], dk[HC], dv[HC];
-    float pyk = 0.f, pxk = 0.f, dpy = 0.f, dpx = 0.f;
+    const int jc = active ? j : n2 - 1;
+    float kk[HC], vv[HC], dk[HC], dv[HC];
 #pragma unroll
-    for (int c = 0; c < HC; ++c) kr[c] = vr[c] = dk[c] = dv[c] = 0.f;
-    if (active) {
-#pragma unroll
-        for (int c = 0; c < HC; ++c) {
-            kr[c] = a.k[((long)bh * HC + c) * n2 + j];
-            vr[c] = a.v[((long)bh * HC + c) * n2 + j];
-        }
-        const float *p = (j < a.n ? a.px : a.py) + ((long)(b * a.G + gi) * a.n + (j % a.n)) * 2;
-        pyk = p[0];
-        pxk = p[1];
+    for (int c = 0; c < HC; ++c) {
+        kk[c] = kr.k[(long)jc * HC + c];
+        vv[c] = kr.v[(long)jc * HC + c];
+        dk[c] = dv[c] = 0.f;
     }
+    const f2 pk = key_pos(kr, a.n, jc);
+    float dpy = 0.f, dpx = 0.f;
     const int q_begin = blockIdx.x * q_per_block;
     const int q_end = min(HW, q_begin + q_per_block);
-    const float sxt = ((float)a.Wt - 1.0f) / 2.0f, syt = ((float)a.Ht - 1.0f) / 2.0f;
+    const f2 sc = {((float)a.Wt - 1.0f) / 2.0f, ((float)a.Ht - 1.0f) / 2.0f};
     for (int q0 = q_begin; q0 < q_end; q0 += QCH) {
         const int nq = min(QCH, q_end - q0);
         __syncthreads();
@@ -409,38 +560,37 @@ __global__ void __launch_bounds__(1024) dattn_attn_bwd_k_kernel(AttnArgs a, cons
             qst[qq * QS + f] = val;
         }
         __syncthreads();
-        if (active) {
-            for (int qq = 0; qq < nq; ++qq) {
-                const float *qs = qst + qq * QS;
-                float s = 0.f, dp = 0.f;
+        for (int qq = 0; qq < nq; ++qq) {
+            const float *qs = qst + qq * QS;
+            float d = 0.f, dp = 0.f;
 #pragma unroll
-                for (int c = 0; c < HC; ++c) {
-                    s = fmaf(qs[c], kr[c], s);
-                    dp = fmaf(qs[HC + c], vr[c], dp);
-                }
-                Corner cr;
-                Taps tp;
-                s = s * a.scale + rpe_bias(tab, a.Ht, a.Wt, qs[2 * HC + 2], qs[2 * HC + 3], pyk, pxk, cr, tp);
-                const float p = __expf(s - qs[2 * HC]);
-                const float ds = p * (dp - qs[2 * HC + 1]);
-                const float dss = ds * a.scale;
-#pragma unroll
-                for (int c = 0; c < HC; ++c) {
-                    dk[c] = fmaf(dss, qs[c], dk[c]);
-                    dv[c] = fmaf(p, qs[HC + c], dv[c]);
-                }
-                float dix = 0.f, diy = 0.f;  // d bias / d disp; disp = 0.5 (q_grid - pos)
-                dsample(tp, cr, ds, dix, diy);
-                dpx -= 0.5f * dix * sxt;
-                dpy -= 0.5f * diy * syt;
+            for (int c = 0; c < HC; ++c) {
+                d = fmaf(qs[c], kk[c], d);
+                dp = fmaf(qs[HC + c], vv[c], dp);
             }
+            const BiasPk bi = rpe_bias_pk(tab, a.Ht, a.Wt, (f2){qs[2 * HC + 3], qs[2 * HC + 2]}, pk, sc);
+            const float s = d * a.scale + bi.v;
+            const float p = __expf(s - qs[2 * HC]);
+            const float ds = p * (dp - qs[2 * HC + 1]);
+            const float dss = ds * a.scale;
+#pragma unroll
+            for (int c = 0; c < HC; ++c) {
+                dk[c] = fmaf(dss, qs[c], dk[c]);
+                dv[c] = fmaf(p, qs[HC + c], dv[c]);
+            }
+            // d bias / d disp (disp = 0.5 (q_grid - pos)), the dsample expression
+            const float om_x = 1.0f - bi.fr.x, om_y = 1.0f - bi.fr.y;
+            const float dix = ds * ((bi.t0.y - bi.t0.x) * om_y + (bi.t1.y - bi.t1.x) * bi.fr.y);
+            const float diy = ds * ((bi.t1.x - bi.t0.x) * om_x + (bi.t1.y - bi.t0.y) * bi.fr.x);
+            dpx -= 0.5f * dix * sc.x;
+            dpy -= 0.5f * diy * sc.y;
         }
     }
     if (active) {
 #pragma unroll
         for (int c = 0; c < HC; ++c) {
-            atomicAdd(&gk[((long)bh * HC + c) * n2 + j], dk[c]);
-            atomicAdd(&gv[((long)bh * HC + c) * n2 + j], dv[c]);
+            atomicAdd(&gk[(long)bh * n2 * HC + (long)j * HC + c], dk[c]);
+            atomicAdd(&gv[(long)bh * n2 * HC + (long)j * HC + c], dv[c]);
         }
         float *gp = (j < a.n ? gpx : gpy) + ((long)(b * a.G + gi) * a.n + (j % a.n)) * 2;
         atomicAdd(gp, dpy);
@@ -465,8 +615,17 @@ int check_attn(const AttnArgs &a) {
     return IRADS_OK;
 }
 
-size_t fwd_smem(const AttnArgs &a) {
-    return ((size_t)a.Ht * a.Wt + (size_t)2 * a.n * 2 * a.hc + (size_t)2 * a.n * 2) * sizeof(float);
+size_t pad_cells_h(int Ht, int Wt) { return (size_t)(((Ht + 1) * (Wt + 1) + 3) & ~3); }
+
+size_t fwd_smem(const AttnArgs &a) { return (pad_cells_h(a.Ht, a.Wt) + (size_t)16 * (a.hc + 2) * 64) * sizeof(float); }
+
+// key splits per query wave and query-wave workgroups per (b, head): ~8192 waves per launch
+void split_plan(int HW, int BH, int &ksp, int &blocks) {
+    const long qwaves = (long)BH * ((HW + 63) / 64);
+    ksp = 1;
+    while (ksp < 16 && qwaves * ksp < 8192) ksp <<= 1;
+    const int qw = 16 / ksp;
+    blocks = (HW + qw * 64 - 1) / (qw * 64);
 }
 
 }  // namespace
@@ -529,16 +688,18 @@ extern "C" int irads_dattn_attn_fwd(const float *q, const float *k, const float 
                                     float *out, float *lse, void *stream) {
     AttnArgs a{q, k, v, pos_x, pos_y, rpe, qgrid_y, qgrid_x, B, nH, G, hc, H, W, n, Ht, Wt, scale};
     if (int e = check_attn(a)) return e;
+    IRADS_REQUIRE(hc <= 16, "dattn_attn: head channels %d > 16", hc);
     if (B == 0) return IRADS_OK;
     const size_t sh = fwd_smem(a);
     IRADS_REQUIRE(sh <= 160 * 1024, "dattn_attn: LDS request %zu exceeds 160 KiB", sh);
-    const int HW = H * W, bs = attn_block(HW);
-    dim3 grid((HW + bs - 1) / bs, B * nH);
+    int ksp, blocks;
+    split_plan(H * W, B * nH, ksp, blocks);
+    dim3 grid(blocks, B * nH);
     hipStream_t st = (hipStream_t)stream;
     IRADS_HC_DISPATCH(hc, {
         (void)hipFuncSetAttribute((const void *)dattn_attn_fwd_kernel<HC>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)sh);
-        dattn_attn_fwd_kernel<HC><<<grid, bs, sh, st>>>(a, out, lse);
+                                  (int)sh);
+        dattn_attn_fwd_kernel<HC><<<grid, 1024, sh, st>>>(a, ksp, k, v, pos_x, pos_y, out, lse);
     })
     return check_launch("irads_dattn_attn_fwd");
 }
@@ -551,25 +712,30 @@ extern "C" int irads_dattn_attn_bwd(const float *q, const float *k, const float 
                                     float *grad_pos_y, void *stream) {
     AttnArgs a{q, k, v, pos_x, pos_y, rpe, qgrid_y, qgrid_x, B, nH, G, hc, H, W, n, Ht, Wt, scale};
     if (int e = check_attn(a)) return e;
+    IRADS_REQUIRE(hc <= 16, "dattn_attn: head channels %d > 16", hc);
     if (B == 0) return IRADS_OK;
     hipStream_t st = (hipStream_t)stream;
     const int HW = H * W;
-    const size_t sh_q = (size_t)Ht * Wt * sizeof(int);
-    const size_t sh_k = (size_t)QCH * (2 * hc + 4) * sizeof(float);
+    const size_t sh_q = 2 * pad_cells_h(Ht, Wt) * sizeof(float);
+    const size_t sh_k = (pad_cells_h(Ht, Wt) + (size_t)QCH * (2 * hc + 4)) * sizeof(float);
     IRADS_REQUIRE(sh_q <= 160 * 1024 && sh_k <= 160 * 1024, "dattn_attn_bwd: LDS request exceeds 160 KiB");
-    // pass Q: 512 queries per workgroup, or 256 when that leaves the chip under-filled
-    const int bs = ((long)((HW + 511) / 512) * B * nH >= 512) ? 512 : 256;
-    dim3 gq_grid((HW + bs - 1) / bs, B * nH);
-    // pass K: one thread per key; enough query chunks per (b, h) to fill the chip
+    int ksp, blocks;
+    split_plan(HW, B * nH, ksp, blocks);
+    dim3 gq_grid(blocks, B * nH);
+    // pass K: one thread per key; query ranges sized for ~1024 workgroups (2 per CU fit in LDS)
     const int kthreads = ((2 * n + 63) / 64) * 64;
-    int qpb = 1024;
-    while (qpb > QCH && (long)((HW + qpb - 1) / qpb) * B * nH < 1024) qpb /= 2;
+    int chunks = (1024 + B * nH - 1) / (B * nH);
+    int qpb = (HW + chunks - 1) / chunks;
+    qpb = ((qpb + QCH - 1) / QCH) * QCH;
     dim3 gk_grid((HW + qpb - 1) / qpb, B * nH);
     IRADS_HC_DISPATCH(hc, {
         (void)hipFuncSetAttribute((const void *)dattn_attn_bwd_q_kernel<HC>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)sh_q);
-        dattn_attn_bwd_q_kernel<HC><<<gq_grid, bs, sh_q, st>>>(a, out, lse, grad_out, delta, grad_q, grad_rpe);
-        dattn_attn_bwd_k_kernel<HC><<<gk_grid, kthreads, sh_k, st>>>(a, lse, delta, grad_out, qpb, grad_k, grad_v,
+        (void)hipFuncSetAttribute((const void *)dattn_attn_bwd_k_kernel<HC>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)sh_k);
+        dattn_attn_bwd_q_kernel<HC><<<gq_grid, 1024, sh_q, st>>>(a, ksp, k, v, pos_x, pos_y, out, lse, grad_out, delta,
+                                                                 grad_q, grad_rpe);
+        dattn_attn_bwd_k_kernel<HC><<<gk_grid, kthreads, sh_k, st>>>(a, k, v, pos_x, pos_y, lse, delta, grad_out, qpb, grad_k, grad_v,
                                                                      grad_pos_x, grad_pos_y);
     })
     return check_launch("irads_dattn_attn_bwd");

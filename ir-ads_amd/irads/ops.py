@@ -233,9 +233,10 @@ class DAttnAttentionFn(torch.autograd.Function):
     def forward(ctx, q, k, v, pos_x, pos_y, rpe_table, qgrid_y, qgrid_x, B, n_heads, groups, H, W, scale):
         hc = q.shape[1]
         n = pos_x.shape[1] * pos_x.shape[2]
+        # k, v (B*nH, hc, 2n) -> key-major (B*nH, 2n, hc): one scalar load per key in the kernels
         ts = [N.check(t.contiguous(), nm, torch.float32) for t, nm in
-              ((q, "q"), (k, "k"), (v, "v"), (pos_x, "pos_x"), (pos_y, "pos_y"), (rpe_table, "rpe_table"),
-               (qgrid_y, "qgrid_y"), (qgrid_x, "qgrid_x"))]
+              ((q, "q"), (k.transpose(1, 2), "k"), (v.transpose(1, 2), "v"), (pos_x, "pos_x"), (pos_y, "pos_y"),
+               (rpe_table, "rpe_table"), (qgrid_y, "qgrid_y"), (qgrid_x, "qgrid_x"))]
         Ht, Wt = rpe_table.shape[1], rpe_table.shape[2]
         out = torch.empty_like(ts[0])
         lse = torch.empty((B * n_heads, H * W), device=q.device, dtype=torch.float32)
@@ -251,14 +252,15 @@ class DAttnAttentionFn(torch.autograd.Function):
         B, nH, G, hc, H, W, n, Ht, Wt, scale = ctx.cfg
         gout = gout.contiguous().float()
         delta = torch.empty_like(lse)
-        gq = torch.empty_like(q)
-        gk, gv = torch.zeros_like(k), torch.zeros_like(v)
+        gq = torch.zeros_like(q)  # key splits add into it
+        gk, gv = torch.zeros_like(k), torch.zeros_like(v)  # key-major, like k and v here
         grpe = torch.zeros_like(rpe)
         gpx, gpy = torch.zeros_like(px), torch.zeros_like(py)
         N.call("irads_dattn_attn_bwd", N.ptr(q), N.ptr(k), N.ptr(v), N.ptr(px), N.ptr(py), N.ptr(rpe), N.ptr(qgy),
                N.ptr(qgx), B, nH, G, hc, H, W, n, Ht, Wt, scale, N.ptr(out), N.ptr(lse), N.ptr(gout), N.ptr(delta),
                N.ptr(gq), N.ptr(gk), N.ptr(gv), N.ptr(grpe), N.ptr(gpx), N.ptr(gpy), N.stream())
-        return gq, gk, gv, gpx, gpy, grpe, None, None, None, None, None, None, None, None
+        return (gq, gk.transpose(1, 2), gv.transpose(1, 2), gpx, gpy, grpe, None, None, None, None, None, None, None,
+                None)
 
 
 def dattn_sample_index(grid, H, W):
