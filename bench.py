@@ -47,6 +47,7 @@ def parse():
     p.add_argument("--profile-only", action="store_true", help="run warmup + steps, print nothing extra")
     p.add_argument("--eager", action="store_true", help="launch op by op (default: replay a captured HIP graph)")
     p.add_argument("--no-tuned-gemms", action="store_true", help="hipBLASLt default picks (ignore irads/tuned/)")
+    p.add_argument("--no-kernels", action="store_true", help="skip the MSDeformAttn (C5) kernel roofline lines")
     return p.parse_args()
 
 
@@ -126,6 +127,68 @@ def cpu_baseline(args):
     return {"value": round(B * args.cpu_steps / dt, 4), "unit": "images/s", "cores": threads, "kind": "port",
             "sample": f"oracle CPU restatement (fp32 PyTorch), same train step at batch {B}, {args.size}x{args.size}, "
                       f"1 warmup + {args.cpu_steps} timed steps, {dt:.1f} s"}
+
+
+DINO_SHAPES = ((100, 167), (50, 84), (25, 42), (13, 21))  # 800x1333 input, strides 8..64
+
+
+def msda_inputs(device, bs=2, Q=None, seed=0):
+    """C5 MSDeformAttn core inputs: value N(0,1); loc = reference point +
+    N(0, 0.02) (about 2 % outside [0, 1]); aw = softmax over the L*P samples of N(0,1)."""
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    shapes = torch.tensor(DINO_SHAPES, dtype=torch.long)
+    S = int((shapes[:, 0] * shapes[:, 1]).sum())
+    Q = S if Q is None else Q
+    M, D, L, P = 8, 32, 4, 4
+    lsi = torch.cat([shapes.new_zeros(1), (shapes[:, 0] * shapes[:, 1]).cumsum(0)[:-1]])
+    value = torch.randn(bs, S, M, D, generator=g)
+    ref = torch.rand(bs, Q, 1, 1, 1, 2, generator=g)
+    loc = (ref + 0.02 * torch.randn(bs, Q, M, L, P, 2, generator=g)).contiguous()
+    aw = torch.randn(bs, Q, M, L * P, generator=g).softmax(-1).view(bs, Q, M, L, P)
+    return [t.to(device) for t in (value, shapes, lsi, loc, aw)]
+
+
+def msda_rooflines(device, reps=20):
+    """MSDeformAttn forward / backward at the DINO encoder (Q = S = 22 223) and decoder
+    (Q = 2200) shapes, bs = 2 (C5 per GPU), timed with HIP events; algorithmic bytes of
+    SURVEY §8(d): fwd = 4(S·M·D + Q·M·L·P·3 + Q·M·D), bwd adds dOut, dValue, dLoc, dAw."""
+    from irads import ops, native as N
+    out = {}
+    for name, Q in (("encoder", None), ("decoder", 2200)):
+        value, shapes, lsi, loc, aw = msda_inputs(device, Q=Q)
+        bs, S, M, D = value.shape
+        Qn, L, P = loc.shape[1], loc.shape[3], loc.shape[4]
+        fwd_b = 4 * bs * (S * M * D + Qn * M * L * P * 3 + Qn * M * D)
+        bwd_b = 4 * bs * (2 * S * M * D + 2 * Qn * M * L * P * 3 + Qn * M * D)
+        o = ops.MSDAFn.apply(value, shapes, lsi, loc, aw, 64)
+        go = torch.randn_like(o)
+        gv, gl, ga = torch.zeros_like(value), torch.empty_like(loc), torch.empty_like(aw)
+
+        def fwd():
+            ops.MSDAFn.apply(value, shapes, lsi, loc, aw, 64)
+
+        def bwd():
+            gv.zero_()
+            N.call("irads_msda_bwd", N.F32, N.ptr(value), N.ptr(shapes), N.ptr(lsi), N.ptr(loc), N.ptr(aw),
+                   N.ptr(go), bs, S, M, D, L, Qn, P, N.ptr(gv), N.ptr(gl), N.ptr(ga), N.stream())
+        for fn, tag, nbytes in ((fwd, "fwd", fwd_b), (bwd, "bwd", bwd_b)):
+            for _ in range(3):
+                fn()
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda.synchronize()
+            a.record()
+            for _ in range(reps):
+                fn()
+            b.record()
+            torch.cuda.synchronize()
+            ms = a.elapsed_time(b) / reps
+            gbs = nbytes / (ms * 1e-3) / 1e9
+            out[f"msda_{tag}_{name}"] = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
+                                         "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
+                                         "avg_launch_ms": round(ms, 4), "algorithmic_bytes_per_launch": nbytes,
+                                         "shape": f"bs={bs} Q={Qn} S={S} M={M} D={D} L={L} P={P} fp32"
+                                                  + (" (incl. grad_value zero-fill)" if tag == "bwd" else "")}
+    return out
 
 
 def traffic_from_profile():
@@ -255,6 +318,11 @@ def main():
                                       "avg_launch_ms": round(bwd["total_ms"] / bwd["launches"], 5),
                                       "share_of_step": round(bwd["total_ms"] / timer_steps / (1e3 * elapsed / args.steps), 4)}
             result["roofline"]["share_of_step"] = round(fwd["total_ms"] / timer_steps / (1e3 * elapsed / args.steps), 4)
+    if rank == 0 and not args.no_kernels:
+        try:
+            result["kernels"] = msda_rooflines(device)
+        except Exception as e:  # report, never fake
+            result["kernels"] = {"error": repr(e)[:200]}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             result["cpu_baseline"] = cpu_baseline(args)
