@@ -179,7 +179,7 @@ int irads_ce_bwd(int dtype, const void *logits, const int64_t *strides, int B, i
  * The non-GEMM work of SwinBlockAdapter.forward under bf16 autocast (swin.py:584-610:
  * residual adds, DropPath (:254, mmcv FFN dropout_layer), norm1/norm2 LayerNorm, the
  * fp32<->bf16 casts of the Linear operands, 0.5 * Adapter) as single passes over (M, C)
- * row-major tensors.  C % 64 == 0 and C/64 in {2,3,4,6,8,12,16,24} (Swin-B/L).  bf16 is
+ * row-major tensors.  C % 64 == 0 and C/64 in {2,3,4,6,8,12,16,24,32,48} (Swin-B/L, PatchMerging's 4C).  bf16 is
  * passed as uint16_t storage.  Sample of a row = row / rows_per_sample (DropPath is per
  * sample).  A NULL optional pointer disables that term.
  *

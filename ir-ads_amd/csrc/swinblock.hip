@@ -17,8 +17,8 @@
 //                (DropPath-backward, 0.5 * for the adapter)
 //   gelu_fwd / gelu_bwd, relu_dropout_fwd / relu_dropout_bwd : bf16 element passes
 //
-// One wave64 per row for the row kernels (C = 64 * VPT, VPT in {2,3,4,6,8,12,16,24}
-// covers Swin-B and Swin-L), the row held in registers: reductions are wave shuffles, and
+// One wave64 per row for the row kernels (C = 64 * VPT, VPT in {2,3,4,6,8,12,16,24,32,48}
+// covers Swin-B and Swin-L, including the 4C rows of PatchMerging), the row held in registers: reductions are wave shuffles, and
 // every tensor is touched exactly once.  All kernels are HBM-bound streaming passes.
 //
 // Rounding follows the autocast reference op by op: DropPath on a bf16 branch is
@@ -386,6 +386,8 @@ using namespace irads;
         case 12: return CALL(12);                         \
         case 16: return CALL(16);                         \
         case 24: return CALL(24);                         \
+        case 32: return CALL(32);                         \
+        case 48: return CALL(48);                         \
         default: break;                                   \
     }
 
@@ -403,7 +405,7 @@ extern "C" int irads_resln_fwd(const float *x, const uint16_t *add1, const float
                                  ln_out, xb_out, mean, rstd, st)
     IRADS_VPT_SWITCH(C, CALL)
 #undef CALL
-    set_error("irads_resln_fwd: C=%d not supported (C/64 in {2,3,4,6,8,12,16,24})", C);
+    set_error("irads_resln_fwd: C=%d not supported (C/64 in {2,3,4,6,8,12,16,24,32,48})", C);
     return IRADS_EINVAL;
 }
 
@@ -421,7 +423,7 @@ extern "C" int irads_resln_bwd(const uint16_t *dy, const float *x, const float *
                                  b2_out, b2_mult, st)
     IRADS_VPT_SWITCH(C, CALL)
 #undef CALL
-    set_error("irads_resln_bwd: C=%d not supported (C/64 in {2,3,4,6,8,12,16,24})", C);
+    set_error("irads_resln_bwd: C=%d not supported (C/64 in {2,3,4,6,8,12,16,24,32,48})", C);
     return IRADS_EINVAL;
 }
 

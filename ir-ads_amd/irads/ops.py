@@ -534,3 +534,59 @@ def confusion_update(scores, target, ignore_index, hist):
         raise RuntimeError("metrics: hist must hold (C+1)*C counters")
     N.call("irads_confusion_update", code, N.ptr(scores), st, B, C, H, W, N.ptr(target), int(ignore_index),
            N.ptr(hist), N.stream())
+
+
+# ------------------------------------------------------------------ LayerNorm -> bf16 GEMM operand
+LN_ROW_WIDTHS = (2, 3, 4, 6, 8, 12, 16, 24, 32, 48)  # C / 64 the row kernels take
+
+
+def ln_bf16_ok(x, norm):
+    C = x.shape[-1]
+    return (x.is_cuda and isinstance(norm, torch.nn.LayerNorm) and norm.elementwise_affine
+            and not norm.weight.requires_grad and not (norm.bias is not None and norm.bias.requires_grad)
+            and norm.bias is not None and C % 64 == 0 and C // 64 in LN_ROW_WIDTHS
+            and torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16)
+
+
+class LayerNormBF16Fn(torch.autograd.Function):
+    """nn.LayerNorm (frozen affine) under bf16 autocast when every consumer is a Linear:
+    LayerNorm runs in fp32 as autocast runs it, and the result is rounded to bf16 in the same
+    pass — the value the consuming Linear's autocast cast would produce — instead of a fp32
+    output plus a separate cast kernel.  Backward: one irads_resln_bwd pass, bf16 dy -> fp32 dx."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, eps):
+        shape = x.shape
+        C = shape[-1]
+        x2 = x.reshape(-1, C)
+        if x2.dtype != torch.float32 or not x2.is_contiguous():
+            x2 = x2.float().contiguous()
+        M = x2.shape[0]
+        y = torch.empty((M, C), device=x.device, dtype=torch.bfloat16)
+        mean = torch.empty((M,), device=x.device, dtype=torch.float32)
+        rstd = torch.empty_like(mean)
+        N.call("irads_resln_fwd", N.ptr(x2), None, None, None, 0.0, M, C, max(M, 1), N.ptr(weight.detach()),
+               N.ptr(bias.detach()), float(eps), None, N.ptr(y), None, N.ptr(mean), N.ptr(rstd), N.stream())
+        ctx.save_for_backward(x2, weight, mean, rstd)
+        ctx.shape, ctx.in_dtype = shape, x.dtype
+        return y.view(*shape)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x2, weight, mean, rstd = ctx.saved_tensors
+        M, C = x2.shape
+        g = gy.reshape(M, C)
+        if g.dtype != torch.bfloat16 or not g.is_contiguous():
+            g = g.to(torch.bfloat16).contiguous()
+        dx = torch.empty((M, C), device=x2.device, dtype=torch.float32)
+        N.call("irads_resln_bwd", N.ptr(g), N.ptr(x2), N.ptr(mean), N.ptr(rstd), N.ptr(weight.detach()), None, None,
+               M, C, max(M, 1), N.ptr(dx), None, None, None, 0.0, N.stream())
+        return dx.view(ctx.shape).to(ctx.in_dtype), None, None, None
+
+
+def layer_norm_bf16(x, norm):
+    """norm(x) as the bf16 operand of a following Linear (fused path) or plain norm(x)."""
+    if ln_bf16_ok(x, norm):
+        with torch.autocast("cuda", enabled=False):
+            return LayerNormBF16Fn.apply(x, norm.weight, norm.bias, norm.eps)
+    return norm(x)

@@ -1,13 +1,15 @@
 """Patch embedding / merging of the Swin backbone (reference semseg/models/backbones/embed.py).
 
-Plain PyTorch ops (conv / unfold / LayerNorm / Linear go to MIOpen and hipBLASLt); kept
-here for shape and state-dict parity (keys ``projection``, ``norm``, ``reduction``).
+Conv and Linear go to MIOpen / hipBLASLt.  PatchMerging's non-overlapping unfold is one
+permute copy, and its LayerNorm writes the bf16 operand of `reduction` directly under AMP
+(ops.layer_norm_bf16).  State-dict keys as the reference (``projection``, ``norm``, ``reduction``).
 """
 import math
 from typing import Sequence
 
 import torch.nn as nn
 import torch.nn.functional as F
+from irads import ops
 
 from ..layers.common import Linear
 
@@ -111,10 +113,16 @@ class PatchMerging(nn.Module):
         if self.adap_padding:
             x = self.adap_padding(x)
             H, W = x.shape[-2:]
-        x = self.sampler(x)
         s = self.sampler
         out_hw = tuple((size + 2 * s.padding[i] - s.dilation[i] * (s.kernel_size[i] - 1) - 1) // s.stride[i] + 1
                        for i, size in enumerate((H, W)))
-        x = x.transpose(1, 2)
-        x = self.norm(x) if self.norm else x
+        if (s.kernel_size == s.stride and s.padding == (0, 0) and s.dilation == (1, 1)
+                and H % s.kernel_size[0] == 0 and W % s.kernel_size[1] == 0):
+            # non-overlapping 2x2 unfold == a reshape: channel index c*kh*kw + i*kw + j, as
+            # nn.Unfold orders it, gathered by one permute copy (no im2col / col2im)
+            kh, kw = s.kernel_size
+            x = x.reshape(B, C, H // kh, kh, W // kw, kw).permute(0, 2, 4, 1, 3, 5).reshape(B, -1, C * kh * kw)
+        else:
+            x = self.sampler(x).transpose(1, 2)
+        x = ops.layer_norm_bf16(x, self.norm) if self.norm else x  # the bf16 operand of `reduction`
         return self.reduction(x), out_hw

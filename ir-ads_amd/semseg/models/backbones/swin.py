@@ -612,9 +612,12 @@ class SwinTransformer(nn.Module):
         self.load_state_dict(sd, strict=False)
 
     def _outputs(self, i, x_rgb_out, x_dte_out, out_hw):
-        x_rgb_out = getattr(self, f'norm{i}')(x_rgb_out)
-        x_dte_out = getattr(self, f'extra_norm{i}')(x_dte_out)
-        fused = getattr(self, f'fuse_norm{i}')(self.DeformMPGBlocks[i](x_rgb_out, x_dte_out, *out_hw, i))
+        # every consumer of these norms is a Linear (DeformMPG D_fc1/D_fc2, the heads' MLPs):
+        # under bf16 autocast they are produced directly as the bf16 GEMM operand
+        x_rgb_out = ops.layer_norm_bf16(x_rgb_out, getattr(self, f'norm{i}'))
+        x_dte_out = ops.layer_norm_bf16(x_dte_out, getattr(self, f'extra_norm{i}'))
+        fused = ops.layer_norm_bf16(self.DeformMPGBlocks[i](x_rgb_out, x_dte_out, *out_hw, i),
+                                    getattr(self, f'fuse_norm{i}'))
         c = self.num_features[i]
 
         def nchw(t):

@@ -56,9 +56,9 @@ class SegFormerHead(nn.Module):
         for i, f in enumerate(features):
             mlp = getattr(self, f"linear_c{i + 1}").proj
             Wi = Wf[:, (n - 1 - i) * E:(n - i) * E]
+            A = Wi @ mlp.weight  # (E, dim_i): under autocast a bf16 GEMM, as the two Linears' own operands
             with torch.autocast("cuda", enabled=False):
-                A = Wi @ mlp.weight  # (E, dim_i), fp32 composition
-                c = Wi @ mlp.bias
+                c = Wi @ mlp.bias  # bias in fp32
             z = ops.linear(f.flatten(2).transpose(1, 2), A, c)  # (B, h*w, E)
             zs.append(z.transpose(1, 2).reshape(B, E, *f.shape[-2:]))  # channels-last (B, E, h, w) view
         seg = ops.upsample_sum(zs[0], zs[1:])

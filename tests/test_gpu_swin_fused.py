@@ -266,3 +266,50 @@ def test_linear_fn_matches_autocast_linear():
     assert y1.dtype == torch.bfloat16 and torch.equal(y0, y1)
     assert torch.equal(gx0, gx1)
     assert _rel(gw1, gw0) < 4e-3 and _rel(gb1, gb0) < 4e-3
+
+
+@pytest.mark.parametrize("C", [128, 512, 1024, 2048, 3072])
+def test_layer_norm_bf16_matches_autocast(C):
+    """ops.layer_norm_bf16 (frozen affine LN feeding a Linear): the bf16 output is autocast's
+    fp32 LayerNorm rounded to bf16 (1 ulp on a few elements: reduction order), and dX is
+    autograd's through that cast (relative L2 1e-3)."""
+    from irads import ops
+    torch.manual_seed(C)
+    norm = torch.nn.LayerNorm(C).to(DEV)
+    with torch.no_grad():
+        norm.weight.uniform_(0.5, 1.5)
+        norm.bias.uniform_(-0.2, 0.2)
+    norm.requires_grad_(False)
+    x = (torch.randn(2, 333, C, device=DEV) * 2 + 0.3)
+    g = torch.randn(2, 333, C, device=DEV).bfloat16()
+    outs = []
+    for fused in (False, True):
+        xx = x.clone().requires_grad_()
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            assert ops.ln_bf16_ok(xx, norm)
+            y = ops.layer_norm_bf16(xx, norm) if fused else norm(xx).to(torch.bfloat16)
+        (gx,) = torch.autograd.grad(y, [xx], g)
+        outs.append((y, gx))
+    (y0, gx0), (y1, gx1) = outs
+    assert y1.dtype == torch.bfloat16 and y1.shape == y0.shape
+    d = (y1.float() - y0.float()).abs()
+    assert (d <= y0.float().abs() * 2 ** -7 + 1e-6).all()
+    assert gx1.dtype == torch.float32 and _rel(gx1, gx0) < 1e-3
+
+
+def test_patch_merging_reshape_matches_unfold():
+    """PatchMerging's permute-reshape equals nn.Unfold's 2x2 sampling (same channel order),
+    and under AMP the block output matches the unfold + LayerNorm + Linear path."""
+    from semseg.models.backbones.embed import PatchMerging
+    torch.manual_seed(4)
+    pm = PatchMerging(128, 256).to(DEV)
+    fill_module(pm)
+    pm.requires_grad_(False)
+    B, H, W = 2, 32, 48
+    x = torch.randn(B, H * W, 128, device=DEV)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y, hw = pm(x, (H, W))
+        ref_cols = pm.sampler(x.view(B, H, W, 128).permute(0, 3, 1, 2)).transpose(1, 2)
+        ref = pm.reduction(pm.norm(ref_cols))
+    assert hw == (H // 2, W // 2) and y.shape == ref.shape
+    assert _rel(y, ref) < 5e-3
