@@ -210,6 +210,24 @@ int irads_relu_dropout_fwd(const uint16_t *a, uint16_t *r, long n, float p, uint
                            void *stream);
 int irads_relu_dropout_bwd(const uint16_t *r, const uint16_t *dr, uint16_t *da, long n, float p, void *stream);
 
+/* The two Adapters of a block (MLP_RGB_Adapter / MLP_DTE_Adapter, swin.py:472-502:
+ * D_fc2(dropout(ReLU(D_fc1(x)))), D_fc1: C -> R, D_fc2: R -> C) on the rgb+dte row batch:
+ * rows [0, Mh) use weights w0 / b0, rows [Mh, M) w1 / b1 (M, Mh multiples of 16, R <= 128).
+ *   adapter_down: out (M x R) from a (M x C), w (R x C), C a multiple of 32.
+ *     mode 0: out = dropout_p(ReLU(bf16(a wᵀ + b)))   (draw as irads_relu_dropout_fwd, salt
+ *             salt0 / salt1 per half, element index within the half)
+ *     mode 1: out = r_saved > 0 ? bf16(a wᵀ) / (1 - p) : 0    (b unused; w = D_fc2.weightᵀ)
+ *   adapter_up:   out (M x C) = bf16(h wᵀ + b), h (M x R), w (C x R), b (C) or NULL,
+ *                 C a multiple of 16 (forward: D_fc2; backward: dX = dA D_fc1.weight with
+ *                 w = D_fc1.weightᵀ).
+ * Replaces the F.linear calls of Adapter.forward and their input-gradient GEMMs, fused with
+ * the ReLU / dropout element passes; bf16 in and out, fp32 accumulation. */
+int irads_adapter_down(int mode, const uint16_t *a, const uint16_t *w0, const uint16_t *w1, const uint16_t *b0,
+                       const uint16_t *b1, const uint16_t *r_saved, long M, long Mh, int C, int R, float p,
+                       uint64_t salt0, uint64_t salt1, const uint64_t *seed_dev, uint16_t *out, void *stream);
+int irads_adapter_up(const uint16_t *h, const uint16_t *w0, const uint16_t *w1, const uint16_t *b0,
+                     const uint16_t *b1, long M, long Mh, int C, int R, uint16_t *out, void *stream);
+
 /* ------------------------------------------------------------------ weight-gradient GEMM
  * D (m x n) fp32 = alpha * A^T B (+ D if accumulate), A (K x m), B (K x n) bf16 row-major with
  * row strides lda, ldb (multiples of 8, rows 16-byte aligned), m and n multiples of 8.  With

@@ -1,0 +1,244 @@
+// MAPA Adapter of the Swin trunk (reference semseg/models/backbones/swin.py:472-502):
+//   d = D_fc2(dropout(ReLU(D_fc1(x))))      D_fc1: C -> R, D_fc2: R -> C, R = C / 16
+// in the fused stage (irads/swin_fused.py) the rgb and dte Adapters act on the two halves
+// of one (M, C) row batch, so every launch here serves both halves, each with its own
+// weights.  R is 8..64 for Swin-B, which hipBLASLt tiles poorly (~1 TB/s on these shapes);
+// these kernels stream the wide operand once at HBM rate and fuse the element-wise work:
+//
+//   irads_adapter_down  out[m, n] = epi(sum_k A[m, k] W[n, k])   A (M, C), W (R, C), out (M, R)
+//       mode 0 (forward):  epi = dropout(ReLU(bf16(acc + b[n])))        -> r
+//       mode 1 (backward): epi = r_saved > 0 ? bf16(acc) * 1/(1-p) : 0  -> dD_fc1 output
+//   irads_adapter_up    out[m, c] = bf16(sum_j H[m, j] W[c, j] + b[c])  H (M, R), W (C, R)
+//
+// Rounding follows autocast op by op: the GEMM result (with its bias) is rounded to bf16
+// before the ReLU / dropout, as F.linear's bf16 output is, and the dropout draw is the
+// counter-based stream of irads_relu_dropout_fwd (same seed, salt and element index).
+//
+// MFMA v_mfma_f32_16x16x32_bf16.  Both kernels are HBM-bound (the wide (M, C) operand is
+// read or written once); they issue all of a wave's loads before its first MFMA, so a
+// launch costs one memory round trip per wave rather than one per K step.
+#include "common.h"
+
+namespace irads {
+namespace {
+
+typedef unsigned short u16;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
+typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+typedef __attribute__((ext_vector_type(2))) unsigned u32x2;
+
+__device__ __forceinline__ f32x4 mfma16(const bf16x8_t &a, const bf16x8_t &b, const f32x4 &c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ bf16x8_t zero8() { return __builtin_bit_cast(bf16x8_t, u32x4{0u, 0u, 0u, 0u}); }
+
+// 8 bf16 at p[0..7], elements at index >= lim (relative to p) read as zero.  VEC: the row
+// stride keeps p 16-byte aligned and the 8 elements are either all valid or all invalid.
+template <bool VEC>
+__device__ __forceinline__ bf16x8_t ld8(const u16 *p, int lim) {
+    if (VEC) return lim > 0 ? __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u32x4 *>(p)) : zero8();
+    u16 e[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) e[j] = j < lim ? p[j] : (u16)0;
+    u32x4 w;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) w[j] = (unsigned)e[2 * j] | ((unsigned)e[2 * j + 1] << 16);
+    return __builtin_bit_cast(bf16x8_t, w);
+}
+
+// ---------------------------------------------------------------- down: (M, C) x (R, C)^T
+// A workgroup owns 16 rows; its 4 waves split K (wave w takes the 32-wide chunks w, w+4, ...)
+// and issue every load of their share up front (no loop-carried memory round trips), then
+// the four partial tiles are summed through LDS in wave order (a fixed summation order).
+template <int NT, int CH, int MODE>
+__global__ __launch_bounds__(256) void adapter_down_kernel(
+    const u16 *__restrict__ a, const u16 *__restrict__ w0, const u16 *__restrict__ w1, const u16 *__restrict__ b0,
+    const u16 *__restrict__ b1, const u16 *__restrict__ rsaved, long M, long Mh, int C, int R, float p, float scale,
+    unsigned long long salt0, unsigned long long salt1, const unsigned long long *__restrict__ seed_dev,
+    u16 *__restrict__ out) {
+    __shared__ f32x4 red[4][NT][64];
+    const int lane = threadIdx.x & 63, li = lane & 15, lg = lane >> 4, wave = threadIdx.x >> 6;
+    const long row0 = (long)blockIdx.x * 16;
+    const bool hi = row0 >= Mh;
+    const u16 *w = hi ? w1 : w0;
+    const int nch = C / 32;
+    bf16x8_t af[CH], wf[CH][NT];
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+        const int kc = wave + 4 * c;
+        const bool ok = kc < nch;
+        af[c] = ld8<true>(a + (row0 + li) * C + kc * 32 + 8 * lg, ok ? 8 : 0);
+#pragma unroll
+        for (int n = 0; n < NT; ++n) {
+            const int col = n * 16 + li;
+            wf[c][n] = ld8<true>(w + (long)(col < R ? col : 0) * C + kc * 32 + 8 * lg, ok && col < R ? 8 : 0);
+        }
+    }
+    f32x4 acc[NT];
+#pragma unroll
+    for (int n = 0; n < NT; ++n) acc[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < CH; ++c)
+#pragma unroll
+        for (int n = 0; n < NT; ++n) acc[n] = mfma16(af[c], wf[c][n], acc[n]);
+#pragma unroll
+    for (int n = 0; n < NT; ++n) red[wave][n][lane] = acc[n];
+    __syncthreads();
+    // epilogue: wave w finishes column tiles n = w, w+4, ...; D[row][col] with col = li,
+    // rows 4 lg + 0..3
+    const u16 *bias = hi ? b1 : b0;
+    const long hbase = hi ? Mh : 0;
+    const unsigned long long seed =
+        MODE == 0 ? (seed_dev != nullptr ? (*seed_dev ^ (hi ? salt1 : salt0)) : (hi ? salt1 : salt0)) : 0ull;
+#pragma unroll
+    for (int n = 0; n < NT; ++n) {
+        const int col = n * 16 + li;
+        if ((n & 3) != wave || col >= R) continue;
+        const f32x4 t = ((red[0][n][lane] + red[1][n][lane]) + red[2][n][lane]) + red[3][n][lane];
+        const float bv = (MODE == 0 && bias != nullptr) ? bf2f(bias[col]) : 0.f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const long row = row0 + 4 * lg + r;
+            const long o = row * R + col;
+            float v;
+            if (MODE == 0) {
+                const float lin = bf2f(f2bf(t[r] + bv));  // F.linear's bf16 output
+                const float rl = lin > 0.f ? lin : 0.f;
+                v = p <= 0.f ? rl
+                             : (uniform01(seed, (unsigned long long)((row - hbase) * R + col)) >= p ? rl * scale : 0.f);
+            } else {
+                const float dr = bf2f(f2bf(t[r]));  // torch.mm's bf16 output
+                v = bf2f(rsaved[o]) > 0.f ? dr * scale : 0.f;
+            }
+            out[o] = f2bf(v);
+        }
+    }
+}
+
+// ---------------------------------------------------------------- up: (M, R) x (C, R)^T
+// computed transposed, Dᵀ = W Hᵀ: the lane then holds 4 consecutive output columns of one
+// row (one 8-byte store).  A wave owns 16*TMT rows x 16*CT columns and loads all of its
+// operands before the first MFMA; the 4 waves of a workgroup take adjacent column slices of
+// the same rows, so each 128-byte output line is completed by one workgroup.
+template <int KC, int CT, int TMT, bool VEC>
+__global__ __launch_bounds__(256) void adapter_up_kernel(const u16 *__restrict__ h, const u16 *__restrict__ w0,
+                                                         const u16 *__restrict__ w1, const u16 *__restrict__ b0,
+                                                         const u16 *__restrict__ b1, long M, long Mh, int C, int R,
+                                                         u16 *__restrict__ out) {
+    const int lane = threadIdx.x & 63, li = lane & 15, lg = lane >> 4;
+    const long row0 = (long)blockIdx.x * (16 * TMT);
+    const int c0 = (blockIdx.y * 4 + (threadIdx.x >> 6)) * (16 * CT);
+    if (c0 >= C) return;  // no block-level synchronisation in this kernel
+    const bool hi = row0 >= Mh;
+    const u16 *w = hi ? w1 : w0;
+    const u16 *bias = hi ? b1 : b0;
+    bf16x8_t hf[TMT][KC], wf[CT][KC];
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc) {
+        const int k0 = kc * 32 + 8 * lg;
+#pragma unroll
+        for (int t = 0; t < TMT; ++t) hf[t][kc] = ld8<VEC>(h + (row0 + t * 16 + li) * R + k0, R - k0);
+#pragma unroll
+        for (int j = 0; j < CT; ++j) {
+            const int c = c0 + j * 16 + li;
+            wf[j][kc] = ld8<VEC>(w + (long)(c < C ? c : 0) * R + k0, c < C ? R - k0 : 0);
+        }
+    }
+    float bv[CT][4];
+#pragma unroll
+    for (int j = 0; j < CT; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int c = c0 + j * 16 + 4 * lg + r;
+            bv[j][r] = (bias != nullptr && c < C) ? bf2f(bias[c]) : 0.f;
+        }
+#pragma unroll
+    for (int t = 0; t < TMT; ++t)
+#pragma unroll
+        for (int j = 0; j < CT; ++j) {
+            f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int kc = 0; kc < KC; ++kc) acc = mfma16(wf[j][kc], hf[t][kc], acc);
+            // Dᵀ[c][m]: lane holds m = li, c = c0 + 16 j + 4 lg + 0..3
+            const int c = c0 + j * 16 + 4 * lg;
+            if (c >= C) continue;
+            u32x2 o;
+            o[0] = (unsigned)f2bf(acc[0] + bv[j][0]) | ((unsigned)f2bf(acc[1] + bv[j][1]) << 16);
+            o[1] = (unsigned)f2bf(acc[2] + bv[j][2]) | ((unsigned)f2bf(acc[3] + bv[j][3]) << 16);
+            *reinterpret_cast<u32x2 *>(out + (row0 + t * 16 + li) * C + c) = o;
+        }
+}
+
+}  // namespace
+}  // namespace irads
+
+using namespace irads;
+
+#define IRADS_ADAPTER_CHECK(fn)                                                                                     \
+    IRADS_REQUIRE(M > 0 && Mh > 0 && Mh <= M && M % 16 == 0 && Mh % 16 == 0,                                      \
+                  fn ": rows M=%ld, Mh=%ld must be multiples of 16 with 0 < Mh <= M", M, Mh);                     \
+    IRADS_REQUIRE(R >= 1 && R <= 128, fn ": R=%d outside [1, 128]", R);                                            \
+    IRADS_REQUIRE(w0 && w1 && out, fn ": null pointer")
+
+extern "C" int irads_adapter_down(int mode, const uint16_t *a, const uint16_t *w0, const uint16_t *w1,
+                                  const uint16_t *b0, const uint16_t *b1, const uint16_t *r_saved, long M, long Mh,
+                                  int C, int R, float p, uint64_t salt0, uint64_t salt1, const uint64_t *seed_dev,
+                                  uint16_t *out, void *stream) {
+    IRADS_ADAPTER_CHECK("irads_adapter_down");
+    IRADS_REQUIRE(a && (mode == 0 || (mode == 1 && r_saved)), "irads_adapter_down: bad mode %d / null input", mode);
+    IRADS_REQUIRE(C > 0 && C % 32 == 0 && C <= 2048, "irads_adapter_down: C=%d must be a multiple of 32, <= 2048", C);
+    IRADS_REQUIRE(p >= 0.f && p < 1.f, "irads_adapter_down: p=%f outside [0, 1)", (double)p);
+    const float scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
+    const int nt = (R + 15) / 16;
+    const int ch = (C / 32 + 3) / 4;  // 32-wide K chunks per wave
+    const int chq = ch <= 1 ? 1 : ch <= 2 ? 2 : ch <= 4 ? 4 : ch <= 8 ? 8 : 16;
+    dim3 grid((unsigned)(M / 16)), block(256);
+    hipStream_t st = (hipStream_t)stream;
+    const unsigned long long *sd = reinterpret_cast<const unsigned long long *>(seed_dev);
+#define IRADS_DOWN(NT_, CH_, MODE_)                                                                               \
+    if (nt == NT_ && chq == CH_ && mode == MODE_) {                                                              \
+        hipLaunchKernelGGL((adapter_down_kernel<NT_, CH_, MODE_>), grid, block, 0, st, a, w0, w1, b0, b1, r_saved,  \
+                           M, Mh, C, R, p, scale, salt0, salt1, sd, out);                                          \
+        return check_launch("irads_adapter_down");                                                               \
+    }
+#define IRADS_DOWN_M(NT_, CH_) IRADS_DOWN(NT_, CH_, 0) IRADS_DOWN(NT_, CH_, 1)
+#define IRADS_DOWN_C(NT_) IRADS_DOWN_M(NT_, 1) IRADS_DOWN_M(NT_, 2) IRADS_DOWN_M(NT_, 4) IRADS_DOWN_M(NT_, 8) \
+    IRADS_DOWN_M(NT_, 16)
+    IRADS_DOWN_C(1) IRADS_DOWN_C(2) IRADS_DOWN_C(3) IRADS_DOWN_C(4)
+    IRADS_DOWN_C(5) IRADS_DOWN_C(6) IRADS_DOWN_C(7) IRADS_DOWN_C(8)
+#undef IRADS_DOWN_C
+#undef IRADS_DOWN_M
+#undef IRADS_DOWN
+    set_error("irads_adapter_down: unsupported R=%d", R);
+    return IRADS_EINVAL;
+}
+
+extern "C" int irads_adapter_up(const uint16_t *h, const uint16_t *w0, const uint16_t *w1, const uint16_t *b0,
+                                const uint16_t *b1, long M, long Mh, int C, int R, uint16_t *out, void *stream) {
+    IRADS_ADAPTER_CHECK("irads_adapter_up");
+    IRADS_REQUIRE(h != nullptr, "irads_adapter_up: null input");
+    IRADS_REQUIRE(C > 0 && C % 16 == 0, "irads_adapter_up: C=%d must be a positive multiple of 16", C);
+    IRADS_REQUIRE((b0 == nullptr) == (b1 == nullptr), "irads_adapter_up: give both biases or none");
+    constexpr int CT = 2;
+    const int kc = (R + 31) / 32;
+    // rows per wave 16 * TMT: the largest that tiles both halves
+    int tmt = 4;
+    while (tmt > 1 && (Mh % (16 * tmt) != 0 || (M - Mh) % (16 * tmt) != 0)) tmt >>= 1;
+    const bool vec = R % 8 == 0;
+    const int slices = (C + 16 * CT - 1) / (16 * CT);
+    dim3 grid((unsigned)(M / (16 * tmt)), (unsigned)((slices + 3) / 4)), block(256);
+    hipStream_t st = (hipStream_t)stream;
+#define IRADS_UP(KC_, TMT_, VEC_)                                                                                 \
+    if (kc == KC_ && tmt == TMT_ && vec == VEC_) {                                                               \
+        hipLaunchKernelGGL((adapter_up_kernel<KC_, CT, TMT_, VEC_>), grid, block, 0, st, h, w0, w1, b0, b1, M, Mh, \
+                           C, R, out);                                                                            \
+        return check_launch("irads_adapter_up");                                                                 \
+    }
+#define IRADS_UP_T(KC_, VEC_) IRADS_UP(KC_, 1, VEC_) IRADS_UP(KC_, 2, VEC_) IRADS_UP(KC_, 4, VEC_)
+    IRADS_UP_T(1, true) IRADS_UP_T(1, false) IRADS_UP_T(2, true) IRADS_UP_T(2, false)
+    IRADS_UP_T(3, true) IRADS_UP_T(3, false) IRADS_UP_T(4, true) IRADS_UP_T(4, false)
+#undef IRADS_UP_T
+#undef IRADS_UP
+    set_error("irads_adapter_up: unsupported R=%d", R);
+    return IRADS_EINVAL;
+}

@@ -70,4 +70,14 @@ __device__ __forceinline__ float wave_sum(float v) {
     return v;
 }
 
+// counter-based dropout draw: splitmix64 of (seed, element index) -> uniform [0, 1)
+// (the Adapter dropout of swinblock.hip and adapter.hip draw from the same stream)
+__device__ __forceinline__ float uniform01(unsigned long long seed, unsigned long long i) {
+    unsigned long long z = seed + (i + 1) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    return (float)(unsigned)(z >> 40) * (1.f / 16777216.f);
+}
+
 }  // namespace irads

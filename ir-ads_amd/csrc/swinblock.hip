@@ -278,15 +278,6 @@ __device__ __forceinline__ float gelu_grad(float x) {
     return cdf + x * pdf;
 }
 
-// counter-based dropout draw: splitmix64 of (seed, element index) -> uniform [0, 1)
-__device__ __forceinline__ float uniform01(unsigned long long seed, unsigned long long i) {
-    unsigned long long z = seed + (i + 1) * 0x9E3779B97F4A7C15ull;
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-    z ^= z >> 31;
-    return (float)(unsigned)(z >> 40) * (1.f / 16777216.f);
-}
-
 template <int OP>  // 0 gelu fwd, 1 gelu bwd, 2 relu+dropout fwd, 3 relu+dropout bwd
 __global__ __launch_bounds__(256) void elem_kernel(const u16 *__restrict__ a, const u16 *__restrict__ b,
                                                    u16 *__restrict__ out, long n, float p, float scale,

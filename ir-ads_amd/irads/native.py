@@ -44,6 +44,8 @@ SIGNATURES = {
     "irads_gelu_bwd": [_vp, _vp, _vp, _l, _vp],
     "irads_relu_dropout_fwd": [_vp, _vp, _l, _f, _u64, _vp, _vp],
     "irads_relu_dropout_bwd": [_vp, _vp, _vp, _l, _f, _vp],
+    "irads_adapter_down": [_i, _vp, _vp, _vp, _vp, _vp, _vp, _l, _l, _i, _i, _f, _u64, _u64, _vp, _vp, _vp],
+    "irads_adapter_up": [_vp, _vp, _vp, _vp, _vp, _l, _l, _i, _i, _vp, _vp],
     "irads_upsample_sum_fwd": [_i, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _vp, _vp],
     "irads_confusion_update": [_i, _vp, _vp, _i, _i, _i, _i, _vp, _i, _vp, _vp],
     "irads_wgrad": [_vp, _l, _vp, _l, _i, _i, _i, _f, _i, _i, _vp, _vp, _vp, _vp, _vp],

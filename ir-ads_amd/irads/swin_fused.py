@@ -19,7 +19,7 @@ stage is a single torch.autograd.Function whose forward and backward are hand-sc
     X1, h2, X1b   = x + DP(o), LN2(.), bf16(.)            [resln_fwd]
     g             = GELU(h2 W1ᵀ + b1)                      [hipBLASLt + gelu_fwd]
     f             = g W2ᵀ + b2                             [hipBLASLt]
-    d[rgb|dte]    = Adapter_{rgb|dte}(X1b[rgb|dte])        [hipBLASLt + relu_dropout_fwd]
+    d[rgb|dte]    = Adapter_{rgb|dte}(X1b[rgb|dte])        [adapter_down + adapter_up]
     x'            = (X1 + DP(f)) + 0.5 d ; h1' = LN1'(x')  [resln_fwd]
   backward mirrors it with resln_bwd producing, in one pass, the fp32 residual gradient
   and the bf16 operands of the branches (DropPath-backward, 0.5 * for the adapter).
@@ -134,6 +134,35 @@ def _resln_bwd(M, C, rps, dy=None, x=None, mean=None, rstd=None, norm=None, g_re
     return dx, o1, o2
 
 
+def _salt(block, half):
+    """Dropout stream of one Adapter (block, modality half): the seed is *seed_dev ^ salt."""
+    return (0x9E3779B97F4A7C15 * (2 * block + half + 1)) & 0xFFFFFFFFFFFFFFFF
+
+
+def _adapter_kernels_ok(M, Mh, C, R):
+    return M == 2 * Mh and Mh % 16 == 0 and C % 32 == 0 and 1 <= R <= 128
+
+
+def _adapter_weights(aparams, nb):
+    """bf16 copies of a stage's Adapter parameters (aparams in adapter_params order: per block
+    rgb then dte, each D_fc1.weight, D_fc1.bias, D_fc2.weight, D_fc2.bias) in one cast,
+    grouped: W1 (2nb, R, C), W2 (2nb, C, R), B1 (2nb, R), B2 (2nb, C), index 2*block + half.
+    `abf` lists the same storage in aparams order."""
+    order = [8 * b + 4 * h + j for j in (0, 2, 1, 3) for b in range(nb) for h in (0, 1)]
+    flat = torch.cat([aparams[k].detach().reshape(-1) for k in order]).to(_BF16)
+    R, C = aparams[0].shape
+    n_w, n = 2 * nb * R * C, 2 * nb
+    W1 = flat[:n_w].view(n, R, C)
+    W2 = flat[n_w:2 * n_w].view(n, C, R)
+    B1 = flat[2 * n_w:2 * n_w + n * R].view(n, R)
+    B2 = flat[2 * n_w + n * R:].view(n, C)
+    abf = []
+    for b in range(nb):
+        for h in (0, 1):
+            abf += [W1[2 * b + h], B1[2 * b + h], W2[2 * b + h], B2[2 * b + h]]
+    return {"W1": W1, "W2": W2, "B1": B1, "B2": B2, "abf": abf, "R": R}
+
+
 def _elem(name, *tensors, out_like, extra=()):
     out = torch.empty_like(out_like)
     N.call(name, *[N.ptr(t) for t in tensors], N.ptr(out), out.numel(), *extra, N.stream())
@@ -162,10 +191,12 @@ class SwinStageFn(torch.autograd.Function):
         p_drop = ADAPTER_DROPOUT if train else 0.
         # dropout seed drawn on the device by torch's generator: graph-capturable, fresh per replay
         seed = torch.randint(0, 2 ** 62, (1,), device=dev, dtype=torch.int64) if p_drop > 0 else None
-        # all adapter weights of the stage cast to bf16 in two launches (autocast casts each per call)
-        flat = torch.cat([p.detach().reshape(-1) for p in aparams]).to(_BF16)
-        abf = list(torch.split(flat, [p.numel() for p in aparams]))
-        abf = [t.view(p.shape) for t, p in zip(abf, aparams)]
+        # all adapter weights of the stage cast to bf16 in two launches (autocast casts each per
+        # call), grouped as (2nb, R, C) D_fc1 weights, (2nb, C, R) D_fc2 weights and the biases
+        aw = _adapter_weights(aparams, nb)
+        abf = aw["abf"]
+        R = aw["R"]
+        fast = _adapter_kernels_ok(M, Mh, C, R)
         _, h1, _, mean1, rstd1 = _resln_fwd(x, M, C, L, norm=blocks[0].norm1)
         saved = []
         cur = x
@@ -187,16 +218,26 @@ class SwinStageFn(torch.autograd.Function):
             g = _elem("irads_gelu_fwd", u, out_like=u)
             f = F.linear(g, w2, b2)
             d = torch.empty((M, C), device=dev, dtype=_BF16)
-            rs = []
-            for half in (0, 1):
-                wa1, ba1, wa2, ba2 = abf[8 * i + 4 * half: 8 * i + 4 * half + 4]
-                rows = slice(half * Mh, (half + 1) * Mh)
-                a1 = F.linear(X1b[rows], wa1, ba1)
-                r = torch.empty_like(a1)
-                N.call("irads_relu_dropout_fwd", N.ptr(a1), N.ptr(r), r.numel(), float(p_drop),
-                       (0x9E3779B97F4A7C15 * (2 * i + half + 1)) & 0xFFFFFFFFFFFFFFFF, N.ptr(seed), N.stream())
-                torch.addmm(ba2, r, wa2.t(), out=d[rows])
-                rs.append(r)
+            if fast:
+                # both Adapters in two launches: D_fc1 + ReLU + dropout, then D_fc2 (+ bias)
+                W1, B1, W2, B2 = aw["W1"], aw["B1"], aw["W2"], aw["B2"]
+                rs = torch.empty((M, R), device=dev, dtype=_BF16)
+                N.call("irads_adapter_down", 0, N.ptr(X1b), N.ptr(W1[2 * i]), N.ptr(W1[2 * i + 1]),
+                       N.ptr(B1[2 * i]), N.ptr(B1[2 * i + 1]), None, M, Mh, C, R, float(p_drop),
+                       _salt(i, 0), _salt(i, 1), N.ptr(seed), N.ptr(rs), N.stream())
+                N.call("irads_adapter_up", N.ptr(rs), N.ptr(W2[2 * i]), N.ptr(W2[2 * i + 1]), N.ptr(B2[2 * i]),
+                       N.ptr(B2[2 * i + 1]), M, Mh, C, R, N.ptr(d), N.stream())
+            else:
+                rs = []
+                for half in (0, 1):
+                    wa1, ba1, wa2, ba2 = abf[8 * i + 4 * half: 8 * i + 4 * half + 4]
+                    rows = slice(half * Mh, (half + 1) * Mh)
+                    a1 = F.linear(X1b[rows], wa1, ba1)
+                    r = torch.empty_like(a1)
+                    N.call("irads_relu_dropout_fwd", N.ptr(a1), N.ptr(r), r.numel(), float(p_drop), _salt(i, half),
+                           N.ptr(seed), N.stream())
+                    torch.addmm(ba2, r, wa2.t(), out=d[rows])
+                    rs.append(r)
             nxt = blocks[i + 1].norm1 if i + 1 < nb else None
             xn, h1, _, mean1n, rstd1n = _resln_fwd(X1, M, C, L, add1=f, add1_scale=None if dp is None else dp[i, 1],
                                                   add2=d, add2_mult=0.5, norm=nxt, x_out=True)
@@ -204,7 +245,7 @@ class SwinStageFn(torch.autograd.Function):
             cur, mean1, rstd1 = xn, mean1n, rstd1n
         ctx.saved = saved
         ctx.cfg = (S, L, C, H, W, M, Mh, p_drop)
-        ctx.seq, ctx.dp, ctx.abf = seq, dp, abf
+        ctx.seq, ctx.dp, ctx.aw, ctx.fast = seq, dp, aw, fast
         ctx.nparams = len(aparams)
         return cur.view(S, L, C)
 
@@ -218,7 +259,11 @@ class SwinStageFn(torch.autograd.Function):
         S, L, C, H, W, M, Mh, p_drop = ctx.cfg
         blocks = list(ctx.seq.blocks)
         nb = len(blocks)
-        dp, abf = ctx.dp, ctx.abf
+        dp, aw, fast = ctx.dp, ctx.aw, ctx.fast
+        abf, R = aw["abf"], aw["R"]
+        if fast:  # operands of the input-gradient GEMMs: D_fc2.weightᵀ (R, C), D_fc1.weightᵀ (C, R)
+            W2t = aw["W2"].transpose(1, 2).contiguous()
+            W1t = aw["W1"].transpose(1, 2).contiguous()
         need = ctx.needs_input_grad[3:]
         gflat = torch.empty((sum(t.numel() for t in abf),), device=gy.device, dtype=torch.float32)
         gparts = [t.view(p.shape) for t, p in zip(torch.split(gflat, [t.numel() for t in abf]), abf)]
@@ -235,7 +280,19 @@ class SwinStageFn(torch.autograd.Function):
             w2, _ = blk.ffn.layers[1].amp_weights(_BF16)
             # Adapters (per modality half): D_fc2, ReLU+dropout, D_fc1
             dX1b = torch.empty((M, C), device=g.device, dtype=_BF16)
-            for half in (0, 1):
+            if fast:
+                dA = torch.empty((M, R), device=g.device, dtype=_BF16)  # grad of the D_fc1 output
+                N.call("irads_adapter_down", 1, N.ptr(dd), N.ptr(W2t[2 * i]), N.ptr(W2t[2 * i + 1]), None, None,
+                       N.ptr(rs), M, Mh, C, R, float(p_drop), 0, 0, None, N.ptr(dA), N.stream())
+                for half in (0, 1):
+                    k = 8 * i + 4 * half
+                    gwa1, gba1, gwa2, gba2 = gparts[k: k + 4]
+                    rows = slice(half * Mh, (half + 1) * Mh)
+                    ops.wgrad(dd[rows], rs[rows], gwa2, colsum_a=gba2)  # dW, db of D_fc2 in fp32 (split-K)
+                    ops.wgrad(dA[rows], X1b[rows], gwa1, colsum_a=gba1)
+                N.call("irads_adapter_up", N.ptr(dA), N.ptr(W1t[2 * i]), N.ptr(W1t[2 * i + 1]), None, None, M, Mh,
+                       C, R, N.ptr(dX1b), N.stream())
+            for half in (() if fast else (0, 1)):
                 k = 8 * i + 4 * half
                 wa1, _, wa2, _ = abf[k: k + 4]
                 gwa1, gba1, gwa2, gba2 = gparts[k: k + 4]

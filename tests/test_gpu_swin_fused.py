@@ -313,3 +313,52 @@ def test_patch_merging_reshape_matches_unfold():
         ref = pm.reduction(pm.norm(ref_cols))
     assert hw == (H // 2, W // 2) and y.shape == ref.shape
     assert _rel(y, ref) < 5e-3
+
+
+@pytest.mark.parametrize("C,Mh", [(128, 4096), (256, 1024), (512, 512), (1024, 256), (192, 240)])
+def test_adapter_kernels_match_linear_path(C, Mh):
+    """irads_adapter_down / _up (both modality halves per launch) against the per-half
+    F.linear + relu_dropout element path they replace, in autocast rounding.  The GEMM
+    accumulation order differs (hipBLASLt vs one MFMA chain), so a bf16 GEMM output may
+    differ by one ulp; the dropout mask is the same draw (same seed, salt, index)."""
+    N = _N()
+    torch.manual_seed(C)
+    R, M, p = C // 16, 2 * Mh, 0.1
+    x = (torch.randn(M, C, device=DEV) * 0.5).bfloat16()
+    W1 = (torch.randn(2, R, C, device=DEV) * C ** -0.5).bfloat16()
+    B1 = (torch.randn(2, R, device=DEV) * 0.1).bfloat16()
+    W2 = (torch.randn(2, C, R, device=DEV) * R ** -0.5).bfloat16()
+    B2 = (torch.randn(2, C, device=DEV) * 0.1).bfloat16()
+    seed = torch.tensor([123456789], device=DEV, dtype=torch.int64)
+    salts = (0x1234567, 0x7654321)
+    st = N.stream()
+    r = torch.empty(M, R, device=DEV, dtype=torch.bfloat16)
+    N.call("irads_adapter_down", 0, N.ptr(x), N.ptr(W1[0]), N.ptr(W1[1]), N.ptr(B1[0]), N.ptr(B1[1]), None, M, Mh,
+           C, R, p, salts[0], salts[1], N.ptr(seed), N.ptr(r), st)
+    d = torch.empty(M, C, device=DEV, dtype=torch.bfloat16)
+    N.call("irads_adapter_up", N.ptr(r), N.ptr(W2[0]), N.ptr(W2[1]), N.ptr(B2[0]), N.ptr(B2[1]), M, Mh, C, R,
+           N.ptr(d), st)
+    dd = (torch.randn(M, C, device=DEV) * 0.1).bfloat16()
+    W2t, W1t = W2.transpose(1, 2).contiguous(), W1.transpose(1, 2).contiguous()
+    dA = torch.empty(M, R, device=DEV, dtype=torch.bfloat16)
+    N.call("irads_adapter_down", 1, N.ptr(dd), N.ptr(W2t[0]), N.ptr(W2t[1]), None, None, N.ptr(r), M, Mh, C, R, p,
+           0, 0, None, N.ptr(dA), st)
+    dx = torch.empty(M, C, device=DEV, dtype=torch.bfloat16)
+    N.call("irads_adapter_up", N.ptr(dA), N.ptr(W1t[0]), N.ptr(W1t[1]), None, None, M, Mh, C, R, N.ptr(dx), st)
+    for h in (0, 1):
+        rows = slice(h * Mh, (h + 1) * Mh)
+        lin = F.linear(x[rows], W1[h], B1[h])
+        r_ref = torch.empty_like(lin)
+        N.call("irads_relu_dropout_fwd", N.ptr(lin), N.ptr(r_ref), r_ref.numel(), p, salts[h], N.ptr(seed), st)
+        # same mask: where the reference kept a positive value the kernel did too
+        keep_ref, keep = r_ref != 0, r[rows] != 0
+        assert (keep_ref != keep).float().mean().item() < 1e-3  # only ulp-level flips at lin ~ 0
+        assert _rel(r[rows], r_ref) < 4e-3
+        d_ref = torch.addmm(B2[h], r[rows], W2[h].t())
+        assert _rel(d[rows], d_ref) < 4e-3
+        dr = torch.mm(dd[rows], W2[h])
+        dA_ref = torch.empty_like(dr)
+        N.call("irads_relu_dropout_bwd", N.ptr(r[rows].contiguous()), N.ptr(dr), N.ptr(dA_ref), dr.numel(), p, st)
+        assert torch.equal(dA[rows] != 0, dA_ref != 0) or (dA[rows] != 0).ne(dA_ref != 0).float().mean() < 1e-3
+        assert _rel(dA[rows], dA_ref) < 4e-3
+        assert _rel(dx[rows], torch.mm(dA[rows], W1[h])) < 4e-3
