@@ -117,6 +117,28 @@ int irads_dattn_attn_bwd(const float *q, const float *k, const float *v, const f
                          float *grad_pos_x, float *grad_pos_y, void *stream);
 /* Debug export: integer corners (x0, y0) of align_corners=True sampling at `grid`
  * ((N, 2) in (x, y) order, the grid_sample convention) on an H x W map. */
+/* Offset networks conv_offset_x / conv_offset_y of DAttentionMM (swin.py:777-786, :880-905) for
+ * both modalities in one call, under bf16 autocast:
+ *   pos_m = clamp(bf16(Conv1x1(GELU(LN(DWConv_{ks,stride,pad}(x_m)))) + ref), -1, 1)
+ * x, y: bf16 (B, G*gc, H, W) with element strides x_strides[4] / y_strides[4] (any layout);
+ * params_{x,y}: 5 fp32 pointers {dw weight (gc,1,ks,ks), dw bias (gc), LN weight (gc),
+ * LN bias (gc), 1x1 weight (2,gc)}; ref: (Hk*Wk, 2) bf16 reference points (y, x);
+ * pos_x, pos_y: fp32 (B*G, Hk, Wk, 2), Hk = (H + 2 pad - ks) / stride + 1.  gc <= 32,
+ * ks in {3, 5, 7, 9}.  Backward takes the pos gradients and writes dv_{x,y} (B*G*Hk*Wk*gc
+ * floats, scratch), partials (irads_dattn_offset_partials(...) floats: per-block sums of the
+ * 1x1 weight, LN weight, LN bias and conv bias gradients, layout [m][block][5][gc], to be
+ * summed over blocks), dw (2*gc*ks*ks floats: the depthwise weight gradients [m][c][ky][kx])
+ * and dx, dy (bf16, the strides of x, y). */
+int irads_dattn_offset_fwd(const uint16_t *x, const long *x_strides, const uint16_t *y, const long *y_strides,
+                           const float *const *params_x, const float *const *params_y, const uint16_t *ref, int B,
+                           int G, int gc, int H, int W, int ks, int stride, int pad, float eps, float *pos_x,
+                           float *pos_y, void *stream);
+int irads_dattn_offset_bwd(const uint16_t *x, const long *x_strides, const uint16_t *y, const long *y_strides,
+                           const float *const *params_x, const float *const *params_y, const uint16_t *ref, int B,
+                           int G, int gc, int H, int W, int ks, int stride, int pad, float eps, const float *gpos_x,
+                           const float *gpos_y, float *dv_x, float *dv_y, float *partials, float *dw, uint16_t *dx,
+                           uint16_t *dy, void *stream);
+long irads_dattn_offset_partials(int B, int G, int gc, int H, int W, int ks, int stride, int pad);
 int irads_dattn_sample_index(const float *grid, int N, int H, int W, int32_t *corners, void *stream);
 
 /* ------------------------------------------------------------------ LightSB (diagonal)

@@ -44,6 +44,8 @@ SIGNATURES = {
     "irads_gelu_bwd": [_vp, _vp, _vp, _l, _vp],
     "irads_relu_dropout_fwd": [_vp, _vp, _l, _f, _u64, _vp, _vp],
     "irads_relu_dropout_bwd": [_vp, _vp, _vp, _l, _f, _vp],
+    "irads_dattn_offset_fwd": [_vp] * 7 + [_i] * 8 + [_f] + [_vp] * 3,
+    "irads_dattn_offset_bwd": [_vp] * 7 + [_i] * 8 + [_f] + [_vp] * 9,
     "irads_adapter_down": [_i, _vp, _vp, _vp, _vp, _vp, _vp, _l, _l, _i, _i, _f, _u64, _u64, _vp, _vp, _vp],
     "irads_adapter_up": [_vp, _vp, _vp, _vp, _vp, _l, _l, _i, _i, _vp, _vp],
     "irads_upsample_sum_fwd": [_i, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _vp, _vp],
@@ -51,7 +53,8 @@ SIGNATURES = {
     "irads_wgrad": [_vp, _l, _vp, _l, _i, _i, _i, _f, _i, _i, _vp, _vp, _vp, _vp, _vp],
 }
 # entries that do not return an error code: name -> (restype, argtypes)
-QUERIES = {"irads_wgrad_workspace": (ctypes.c_long, [_i, _i, _i])}
+QUERIES = {"irads_wgrad_workspace": (ctypes.c_long, [_i, _i, _i]),
+           "irads_dattn_offset_partials": (ctypes.c_long, [_i] * 8)}
 CE_WORKSPACE = 2048
 
 _lib = None

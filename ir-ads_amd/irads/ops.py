@@ -226,6 +226,94 @@ class DAttnSampleFn(torch.autograd.Function):
         return gx, gy, gq, gpx, gpy, None
 
 
+def _ptr_array(tensors):
+    return (ctypes.c_void_p * len(tensors))(*[t.data_ptr() for t in tensors])
+
+
+def _stride_array(t):
+    return (ctypes.c_long * t.dim())(*t.stride())
+
+
+def dattn_offset_ok(x, y, net):
+    """Whether DAttnOffsetFn reproduces `net` (an offset network, swin.py:777-786) on x, y:
+    bf16 autocast, bf16 inputs, the reference structure DWConv-LN-GELU-1x1, gc <= 32."""
+    if not (x.is_cuda and x.dtype == torch.bfloat16 and y.dtype == torch.bfloat16 and x.shape == y.shape
+            and torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16):
+        return False
+    try:
+        conv, lnp, act, proj = net
+    except (TypeError, ValueError):
+        return False
+    gc = conv.in_channels
+    return (isinstance(conv, torch.nn.Conv2d) and conv.groups == gc == conv.out_channels and conv.bias is not None
+            and gc <= 32 and conv.kernel_size[0] == conv.kernel_size[1] in (3, 5, 7, 9)
+            and conv.stride[0] == conv.stride[1] and conv.padding[0] == conv.padding[1]
+            and conv.dilation == (1, 1) and isinstance(act, torch.nn.GELU) and act.approximate == "none"
+            and isinstance(proj, torch.nn.Conv2d) and proj.bias is None and proj.kernel_size == (1, 1)
+            and proj.out_channels == 2 and hasattr(lnp, "norm") and lnp.norm.elementwise_affine)
+
+
+def _offset_params(net):
+    conv, lnp, _, proj = net
+    return [conv.weight, conv.bias, lnp.norm.weight, lnp.norm.bias, proj.weight]
+
+
+class DAttnOffsetFn(torch.autograd.Function):
+    """conv_offset_x / conv_offset_y, + reference points, clamp (swin.py:880-905) under bf16
+    autocast: x, y bf16 (B, G*gc, H, W) -> pos_x, pos_y fp32 (B*G, Hk, Wk, 2)."""
+
+    @staticmethod
+    def forward(ctx, x, y, ref, cfg, *params):
+        B, _, H, W = x.shape
+        G, gc, ks, stride, pad, eps = cfg
+        Hk, Wk = (H + 2 * pad - ks) // stride + 1, (W + 2 * pad - ks) // stride + 1
+        params = [N.check(p.detach().contiguous(), "offset parameter", torch.float32) for p in params]
+        ref = N.check(ref.contiguous(), "ref", torch.bfloat16)
+        pos_x = torch.empty((B * G, Hk, Wk, 2), device=x.device, dtype=torch.float32)
+        pos_y = torch.empty_like(pos_x)
+        N.call("irads_dattn_offset_fwd", N.ptr(x), _stride_array(x), N.ptr(y), _stride_array(y),
+               _ptr_array(params[:5]), _ptr_array(params[5:]), N.ptr(ref), B, G, gc, H, W, ks, stride, pad,
+               float(eps), N.ptr(pos_x), N.ptr(pos_y), N.stream())
+        ctx.save_for_backward(x, y, ref, *params)
+        ctx.cfg = (B, G, gc, H, W, ks, stride, pad, float(eps), Hk, Wk)
+        return pos_x, pos_y
+
+    @staticmethod
+    def backward(ctx, gpx, gpy):
+        x, y, ref, *params = ctx.saved_tensors
+        B, G, gc, H, W, ks, stride, pad, eps, Hk, Wk = ctx.cfg
+        dev = x.device
+        cells = B * G * Hk * Wk
+
+        def g(t):
+            return torch.zeros((cells, 2), device=dev) if t is None else t.contiguous().float()
+        gpx, gpy = g(gpx), g(gpy)
+        dv = torch.empty((2, cells * gc), device=dev, dtype=torch.float32)
+        parts = torch.empty((N.load().irads_dattn_offset_partials(B, G, gc, H, W, ks, stride, pad),), device=dev,
+                            dtype=torch.float32)
+        dw = torch.empty((2, gc, 1, ks, ks), device=dev, dtype=torch.float32)
+        dx = torch.empty_strided(x.shape, x.stride(), device=dev, dtype=x.dtype)
+        dy = torch.empty_strided(y.shape, y.stride(), device=dev, dtype=y.dtype)
+        N.call("irads_dattn_offset_bwd", N.ptr(x), _stride_array(x), N.ptr(y), _stride_array(y),
+               _ptr_array(params[:5]), _ptr_array(params[5:]), N.ptr(ref), B, G, gc, H, W, ks, stride, pad, eps,
+               N.ptr(gpx), N.ptr(gpy), N.ptr(dv[0]), N.ptr(dv[1]), N.ptr(parts), N.ptr(dw), N.ptr(dx), N.ptr(dy),
+               N.stream())
+        ps = parts.view(2, -1, 5, gc).sum(1)  # (m, [1x1 w row 0, row 1, LN w, LN b, conv b], gc)
+        grads = []
+        for m in (0, 1):
+            grads += [dw[m], ps[m, 4], ps[m, 2], ps[m, 3], ps[m, 0:2].reshape(2, gc, 1, 1)]
+        need = ctx.needs_input_grad
+        return (dx if need[0] else None, dy if need[1] else None, None, None,
+                *[t if need[4 + j] else None for j, t in enumerate(grads)])
+
+
+def dattn_offsets(x, y, net_x, net_y, groups, ref):
+    """pos_x, pos_y of DAttentionMM from the two offset networks (see DAttnOffsetFn)."""
+    conv = net_x[0]
+    cfg = (groups, conv.in_channels, conv.kernel_size[0], conv.stride[0], conv.padding[0], net_x[1].norm.eps)
+    return DAttnOffsetFn.apply(x, y, ref, cfg, *_offset_params(net_x), *_offset_params(net_y))
+
+
 class DAttnAttentionFn(torch.autograd.Function):
     """softmax(scale·qᵀk + bilinear rpe bias)·v of DAttentionMM (swin.py:950-1016)."""
 

@@ -403,13 +403,21 @@ class DAttentionMM(nn.Module):
         dtype, device = x.dtype, x.device
         xy = self.fuse_q(torch.cat([x, y], dim=1))
         q = self.proj_q(xy)
-        x_offset = self.conv_offset_x(x.reshape(B * g, gc, H, W))
-        y_offset = self.conv_offset_y(y.reshape(B * g, gc, H, W))
-        Hk, Wk = x_offset.size(2), x_offset.size(3)
+        if ops.dattn_offset_ok(x, y, self.conv_offset_x):
+            # both offset networks, the reference points and the clamp in one HIP kernel each way
+            conv = self.conv_offset_x[0]
+            Hk = (H + 2 * conv.padding[0] - conv.kernel_size[0]) // conv.stride[0] + 1
+            Wk = (W + 2 * conv.padding[1] - conv.kernel_size[1]) // conv.stride[1] + 1
+            ref = self._get_ref_points(Hk, Wk, 1, dtype, device)[0].reshape(Hk * Wk, 2)
+            pos_x, pos_y = ops.dattn_offsets(x, y, self.conv_offset_x, self.conv_offset_y, g, ref)
+        else:
+            x_offset = self.conv_offset_x(x.reshape(B * g, gc, H, W))
+            y_offset = self.conv_offset_y(y.reshape(B * g, gc, H, W))
+            Hk, Wk = x_offset.size(2), x_offset.size(3)
+            ref = self._get_ref_points(Hk, Wk, B, dtype, device)
+            pos_x = (x_offset.permute(0, 2, 3, 1) + ref).clamp(-1., 1.).float()
+            pos_y = (y_offset.permute(0, 2, 3, 1) + ref).clamp(-1., 1.).float()
         n = Hk * Wk
-        ref = self._get_ref_points(Hk, Wk, B, dtype, device)
-        pos_x = (x_offset.permute(0, 2, 3, 1) + ref).clamp(-1., 1.).float()
-        pos_y = (y_offset.permute(0, 2, 3, 1) + ref).clamp(-1., 1.).float()
         xs, ys, qs = ops.DAttnSampleFn.apply(x.float(), y.float(), q.float(), pos_x, pos_y, g)
         xs, ys, qs = (t.view(B, C, 1, 2 * n) for t in (xs, ys, qs))
         w = self.softmax(self.get_sample_weight(qs)).squeeze(2).unsqueeze(1)

@@ -1,0 +1,82 @@
+"""Native DAttentionMM pieces under bf16 autocast vs the module path they replace.
+
+The module path (MIOpen convolutions, torch LayerNorm / GELU, autocast casts) is itself
+checked against the reference in test_gpu_swin.py; here the fused HIP kernels must give
+the same values in the same rounding.  Tolerances: positions within one bf16 ulp of the
+module path (the 81-tap conv and the 1x1 conv sum in a different order, which can move a
+bf16 rounding), and >= 98% bit-identical; gradients relative L2 2e-2 (bf16 chain whose
+roundings can flip with that order)."""
+import pytest
+import torch
+
+from fill import fill_module
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+# (dims, stride, groups, heads, level, H, W, B): the four Swin-B stages at 512², Swin-L stage 0
+CFGS = {"s0": (16, 8, 1, 2, 0, 128, 128, 2), "s1": (32, 4, 2, 4, 1, 64, 64, 2), "s2": (64, 2, 4, 8, 2, 32, 32, 2),
+        "s3": (128, 1, 8, 16, 3, 16, 16, 4), "swinl_s0": (24, 8, 1, 2, 0, 128, 128, 2)}
+
+
+def _rel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+def _module_offsets(m, x, y):
+    B, C, H, W = x.shape
+    g, gc = m.n_groups, m.n_group_channels
+    xo = m.conv_offset_x(x.reshape(B * g, gc, H, W))
+    yo = m.conv_offset_y(y.reshape(B * g, gc, H, W))
+    Hk, Wk = xo.shape[2:]
+    ref = m._get_ref_points(Hk, Wk, B, x.dtype, x.device)
+    return ((xo.permute(0, 2, 3, 1) + ref).clamp(-1., 1.).float(), (yo.permute(0, 2, 3, 1) + ref).clamp(-1., 1.).float())
+
+
+@pytest.mark.parametrize("tag", list(CFGS))
+@pytest.mark.parametrize("channels_last", [False, True])
+def test_dattn_offset_kernel_matches_module_path(tag, channels_last):
+    from irads import ops
+    from semseg.models.backbones import swin
+    dims, stride, g, h, level, H, W, B = CFGS[tag]
+    torch.manual_seed(level + 7)
+    m = swin.DAttentionMM(dims, stride=stride, n_groups=g, n_heads=h, level=level).to(DEV)
+    fill_module(m, seed=13)
+    with torch.no_grad():  # offsets of O(0.1): positions move off the reference grid, few clamps
+        for net in (m.conv_offset_x, m.conv_offset_y):
+            net[3].weight.mul_(4.0)
+    x = (torch.randn(B, H, W, dims, device=DEV) * 0.7).bfloat16()
+    y = (torch.rand(B, H, W, dims, device=DEV)).bfloat16()
+    if channels_last:  # (B, C, H, W) views of NHWC memory, as DeformMPG produces them
+        x, y = x.permute(0, 3, 1, 2), y.permute(0, 3, 1, 2)
+    else:
+        x, y = x.permute(0, 3, 1, 2).contiguous(), y.permute(0, 3, 1, 2).contiguous()
+    params = [p for net in (m.conv_offset_x, m.conv_offset_y) for p in ops._offset_params(net)]
+    outs = []
+    for native in (False, True):
+        xx, yy = x.detach().clone().requires_grad_(), y.detach().clone().requires_grad_()
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            if native:
+                assert ops.dattn_offset_ok(xx, yy, m.conv_offset_x)
+                conv = m.conv_offset_x[0]
+                Hk = (H + 2 * conv.padding[0] - conv.kernel_size[0]) // conv.stride[0] + 1
+                Wk = (W + 2 * conv.padding[1] - conv.kernel_size[1]) // conv.stride[1] + 1
+                ref = m._get_ref_points(Hk, Wk, 1, xx.dtype, DEV)[0].reshape(Hk * Wk, 2)
+                px, py = ops.dattn_offsets(xx, yy, m.conv_offset_x, m.conv_offset_y, g, ref)
+            else:
+                px, py = _module_offsets(m, xx, yy)
+        torch.manual_seed(99)
+        gpx, gpy = torch.randn_like(px), torch.randn_like(py)
+        grads = torch.autograd.grad([px, py], [xx, yy] + params, [gpx, gpy])
+        outs.append((px, py, grads))
+    (px0, py0, g0), (px1, py1, g1) = outs
+    for a, b in ((px1, px0), (py1, py0)):
+        assert a.shape == b.shape
+        d = (a - b).abs()
+        assert (d <= 2 ** -7 + 1e-7).all(), d.max().item()
+        assert (d == 0).float().mean().item() >= 0.98
+    names = ["dx", "dy"] + [f"{mod}.{n}" for mod in ("x", "y") for n in ("w", "b", "ln_w", "ln_b", "w2")]
+    for n, a, b in zip(names, g1, g0):
+        assert a.shape == b.shape and a.dtype == b.dtype, n
+        assert _rel(a, b) < 2e-2, (n, _rel(a, b))
