@@ -260,6 +260,22 @@ int irads_adapter_up(const uint16_t *h, const uint16_t *w0, const uint16_t *w1, 
  * split-K over the token dimension, deterministic (fixed-order reduction, no atomics).
  * workspace: irads_wgrad_workspace(K, m, n) floats. */
 long irads_wgrad_workspace(int K, int m, int n);
+/* Batched form: `count` (1..4) problems of the same K, m, n in one launch pair; problem q uses
+ * workspace + q * (irads_wgrad_batched_workspace(count, K, m, n) / count). */
+typedef struct {
+    const uint16_t *A;
+    long lda;
+    const uint16_t *B;
+    long ldb;
+    float *D;
+    float *colsum_a;
+    float *colsum_b;
+    int transpose_out;
+} irads_wgrad_problem;
+long irads_wgrad_batched_workspace(int count, int K, int m, int n);
+int irads_wgrad_batched(int count, const irads_wgrad_problem *problems, int K, int m, int n, float alpha,
+                        int accumulate, float *workspace, void *stream);
+
 int irads_wgrad(const uint16_t *A, long lda, const uint16_t *B, long ldb, int K, int m, int n, float alpha,
                 int accumulate, int transpose_out, float *D, float *colsum_a, float *colsum_b, float *workspace,
                 void *stream);

@@ -18,7 +18,9 @@
 //   * the bias gradients (column sums) ride on the global loads: each thread owns a fixed
 //     8-column group for the whole K-range, so the sums cost 8 adds per 16-byte load;
 //   * per-split partials go to a workspace and a second kernel sums them in a fixed order:
-//     deterministic, no atomics.
+//     deterministic, no atomics;
+//   * up to 4 problems of one shape go in one launch pair (the rgb / dte Adapters' D_fc1 and
+//     D_fc2 gradients of a block), which also lets each split cover more rows.
 // The problem is HBM-bound (A and B are each read once: 2(m+n)K bytes for 2mnK flops).
 #include <type_traits>
 
@@ -87,12 +89,35 @@ __device__ __forceinline__ bf16x8_t frag(const u16 *lds, int b, int lane) {
     return __builtin_bit_cast(bf16x8_t, u16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]});
 }
 
-// TI x TJ output tile per workgroup, 4 waves as WI x WJ, each wave (TI/WI) x (TJ/WJ)
+// one problem of a batched launch (all share K, m, n): operands and its workspace slices
+struct WProb {
+    const u16 *A;
+    long lda;
+    const u16 *B;
+    long ldb;
+    float *ws, *ws_sa, *ws_sb;  // (nsplit, m, n), (nsplit, m), (nsplit, n); sums NULL = not wanted
+};
+constexpr int kMaxBatch = 4;
+struct WProbs {
+    WProb p[kMaxBatch];
+};
+
+// TI x TJ output tile per workgroup, 4 waves as WI x WJ, each wave (TI/WI) x (TJ/WJ);
+// blockIdx = (tile, K-split, problem)
 template <int TI, int TJ, int WI>
-__global__ __launch_bounds__(256) void wgrad_partial_kernel(const u16 *__restrict__ A, long lda,
-                                                            const u16 *__restrict__ B, long ldb, int K, int m,
-                                                            int n, int chunk, int tiles_j, float *__restrict__ ws,
-                                                            float *__restrict__ ws_sa, float *__restrict__ ws_sb) {
+__global__ __launch_bounds__(256) void wgrad_partial_kernel(WProbs probs, int K, int m, int n, int chunk,
+                                                            int tiles_j) {
+    // constant indices only: a dynamic index into the by-value argument would copy it to scratch
+    WProb pr = probs.p[0];
+    if (blockIdx.z == 1) pr = probs.p[1];
+    else if (blockIdx.z == 2) pr = probs.p[2];
+    else if (blockIdx.z == 3) pr = probs.p[3];
+    const u16 *__restrict__ A = pr.A;
+    const u16 *__restrict__ B = pr.B;
+    const long lda = pr.lda, ldb = pr.ldb;
+    float *__restrict__ ws = pr.ws;
+    float *__restrict__ ws_sa = pr.ws_sa;
+    float *__restrict__ ws_sb = pr.ws_sb;
     constexpr int WJ = 4 / WI;
     constexpr int BI = TI / WI / 16, BJ = TJ / WJ / 16;  // MFMA blocks per wave
     __shared__ __attribute__((aligned(16))) u16 lA[KS * TI];
@@ -174,8 +199,8 @@ __global__ __launch_bounds__(256) void wgrad_partial_kernel(const u16 *__restric
     if (sum_b) colsum(csb, std::integral_constant<int, TJ>{}, j0, n, ws_sb + (long)split * n);
 }
 
-// sum the per-split partials: out[e] = alpha * sum_s ws[s][e] (+ out[e]), for the weight
-// block and the two column-sum vectors in one launch (segments by blockIdx).  A workgroup
+// sum the per-split partials: out[e] = alpha * sum_s ws[s][e] (+ out[e]), for every problem's
+// weight block and column-sum vectors in one launch (segments by blockIdx).  A workgroup
 // owns 64 consecutive elements (coalesced across lanes); its 4 waves take the splits
 // s = w, w+4, ... and are combined in wave order through LDS: a fixed summation order.
 struct Seg {
@@ -184,12 +209,22 @@ struct Seg {
     long count;
     int blocks, transpose;
 };
-__global__ __launch_bounds__(256) void wgrad_reduce_kernel(Seg s0, Seg s1, Seg s2, int nsplit, float alpha,
-                                                           int accumulate, int m, int n) {
+struct Segs {
+    Seg s[3 * kMaxBatch];
+    int nseg;
+};
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(Segs segs, int nsplit, float alpha, int accumulate, int m,
+                                                           int n) {
     __shared__ float part[4][64];
     int blk = blockIdx.x;
-    const Seg &sg = blk < s0.blocks ? s0 : (blk < s0.blocks + s1.blocks ? s1 : s2);
-    blk -= blk < s0.blocks ? 0 : (blk < s0.blocks + s1.blocks ? s0.blocks : s0.blocks + s1.blocks);
+    Seg sg = segs.s[0];  // segment walk with constant indices (no scratch copy of the argument)
+#pragma unroll
+    for (int i = 1; i < 3 * kMaxBatch; ++i) {
+        if (i < segs.nseg && blk >= sg.blocks) {
+            blk -= sg.blocks;
+            sg = segs.s[i];
+        }
+    }
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const long e = (long)blk * 64 + lane;
     const long count = sg.count;
@@ -217,13 +252,32 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(Seg s0, Seg s1, Seg s
 }
 
 template <int TI, int TJ, int WI>
-int launch_partial(const u16 *A, long lda, const u16 *B, long ldb, int K, int m, int n, int nsplit, int chunk,
-                   float *ws, float *ws_sa, float *ws_sb, hipStream_t st) {
+int launch_partial(const WProbs &probs, int count, int K, int m, int n, int nsplit, int chunk, hipStream_t st) {
     const int tiles_i = (m + TI - 1) / TI, tiles_j = (n + TJ - 1) / TJ;
-    dim3 grid(tiles_i * tiles_j, nsplit), block(256);
-    hipLaunchKernelGGL((wgrad_partial_kernel<TI, TJ, WI>), grid, block, 0, st, A, lda, B, ldb, K, m, n, chunk, tiles_j,
-                       ws, ws_sa, ws_sb);
+    dim3 grid(tiles_i * tiles_j, nsplit, count), block(256);
+    hipLaunchKernelGGL((wgrad_partial_kernel<TI, TJ, WI>), grid, block, 0, st, probs, K, m, n, chunk, tiles_j);
     return check_launch("irads_wgrad partial");
+}
+
+int tile_i(int m) { return m <= 16 ? 16 : (m <= 32 ? 32 : (m <= 64 ? 64 : 128)); }
+
+// K-splits: enough workgroups to fill the chip (~1024 over the batch), but each split covers
+// at least max(256, 4mn/(m+n)) rows so that the fp32 partials it writes stay below ~half of
+// the bf16 operand bytes it reads (partials: 4mn per split; operands: 2(m+n) per row).
+void plan(int count, int K, int m, int n, long *nsplit_out, long *chunk_out) {
+    const long tiles = (long)((m + tile_i(m) - 1) / tile_i(m)) * ((n + 127) / 128);
+    long nsplit = (1024 + tiles * count - 1) / (tiles * count);
+    long rows = 4L * m * n / (m + n);
+    if (rows < 256) rows = 256;
+    const long maxsplit = (K + rows - 1) / rows;
+    if (nsplit > maxsplit) nsplit = maxsplit;
+    if (nsplit < 1) nsplit = 1;
+    long chunk = (K + nsplit - 1) / nsplit;
+    chunk = (chunk + KS - 1) / KS * KS;
+    if (chunk == 0) chunk = KS;
+    nsplit = (K + chunk - 1) / chunk;
+    if (nsplit < 1) nsplit = 1;
+    *nsplit_out = nsplit, *chunk_out = chunk;
 }
 
 }  // namespace
@@ -232,61 +286,70 @@ int launch_partial(const u16 *A, long lda, const u16 *B, long ldb, int K, int m,
 using namespace irads;
 
 extern "C" long irads_wgrad_workspace(int K, int m, int n) {
-    // splits chosen below; workspace = nsplit * (m*n + m + n) floats
-    const int TI = m <= 16 ? 16 : (m <= 32 ? 32 : (m <= 64 ? 64 : 128));
-    const int TJ = 128;
-    const long tiles = (long)((m + TI - 1) / TI) * ((n + TJ - 1) / TJ);
-    long nsplit = (1024 + tiles - 1) / tiles;  // ~4 workgroups per CU
-    const long maxsplit = (K + 63) / 64;      // >= 64 rows (2 MFMA steps) per workgroup
-    if (nsplit > maxsplit) nsplit = maxsplit;
-    if (nsplit < 1) nsplit = 1;
+    long nsplit, chunk;
+    plan(1, K, m, n, &nsplit, &chunk);
     return nsplit * ((long)m * n + m + n);
+}
+
+extern "C" long irads_wgrad_batched_workspace(int count, int K, int m, int n) {
+    long nsplit, chunk;
+    plan(count, K, m, n, &nsplit, &chunk);
+    return count * nsplit * ((long)m * n + m + n);
+}
+
+extern "C" int irads_wgrad_batched(int count, const irads_wgrad_problem *problems, int K, int m, int n, float alpha,
+                                   int accumulate, float *workspace, void *stream) {
+    IRADS_REQUIRE(count >= 1 && count <= kMaxBatch && problems && workspace,
+                  "irads_wgrad: batch of %d problems (1..%d) / null pointer", count, kMaxBatch);
+    IRADS_REQUIRE(K >= 0 && m > 0 && n > 0 && m % 8 == 0 && n % 8 == 0,
+                  "irads_wgrad: need m, n multiples of 8 (m=%d n=%d)", m, n);
+    long nsplit, chunk;
+    plan(count, K, m, n, &nsplit, &chunk);
+    const long per = nsplit * ((long)m * n + m + n);
+    WProbs probs;
+    Segs segs;
+    segs.nseg = 0;
+    const long cnt = (long)m * n;
+    for (int q = 0; q < count; ++q) {
+        const irads_wgrad_problem &p = problems[q];
+        IRADS_REQUIRE(p.A && p.B && p.D, "irads_wgrad: null pointer in problem %d", q);
+        IRADS_REQUIRE(p.lda % 8 == 0 && p.ldb % 8 == 0 && p.lda >= m && p.ldb >= n &&
+                          ((uintptr_t)p.A % 16) == 0 && ((uintptr_t)p.B % 16) == 0,
+                      "irads_wgrad: rows must be 16-byte aligned (lda=%ld ldb=%ld)", p.lda, p.ldb);
+        float *ws = workspace + q * per;
+        probs.p[q] = WProb{p.A, p.lda, p.B, p.ldb, ws, p.colsum_a ? ws + nsplit * cnt : nullptr,
+                           p.colsum_b ? ws + nsplit * (cnt + m) : nullptr};
+        segs.s[segs.nseg++] = Seg{ws, p.D, cnt, (int)((cnt + 63) / 64), p.transpose_out};
+        if (p.colsum_a) segs.s[segs.nseg++] = Seg{probs.p[q].ws_sa, p.colsum_a, m, (m + 63) / 64, 0};
+        if (p.colsum_b) segs.s[segs.nseg++] = Seg{probs.p[q].ws_sb, p.colsum_b, n, (n + 63) / 64, 0};
+    }
+    hipStream_t st = (hipStream_t)stream;
+    if (K == 0) {
+        (void)hipMemsetAsync(workspace, 0, sizeof(float) * count * per, st);
+    } else {
+        const int TI = tile_i(m);
+        int rc;
+        if (TI == 16)
+            rc = launch_partial<16, 128, 1>(probs, count, K, m, n, (int)nsplit, (int)chunk, st);
+        else if (TI == 32)
+            rc = launch_partial<32, 128, 1>(probs, count, K, m, n, (int)nsplit, (int)chunk, st);
+        else if (TI == 64)
+            rc = launch_partial<64, 128, 2>(probs, count, K, m, n, (int)nsplit, (int)chunk, st);
+        else
+            rc = launch_partial<128, 128, 2>(probs, count, K, m, n, (int)nsplit, (int)chunk, st);
+        if (rc) return rc;
+    }
+    int blocks = 0;
+    for (int i = 0; i < segs.nseg; ++i) blocks += segs.s[i].blocks;
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, segs, (int)nsplit, alpha, accumulate, m,
+                       n);
+    return check_launch("irads_wgrad reduce");
 }
 
 extern "C" int irads_wgrad(const uint16_t *A, long lda, const uint16_t *B, long ldb, int K, int m, int n, float alpha,
                            int accumulate, int transpose_out, float *D, float *colsum_a, float *colsum_b,
                            float *workspace, void *stream) {
     IRADS_REQUIRE(A && B && D && workspace, "irads_wgrad: null pointer");
-    IRADS_REQUIRE(K >= 0 && m > 0 && n > 0 && m % 8 == 0 && n % 8 == 0,
-                  "irads_wgrad: need m, n multiples of 8 (m=%d n=%d)", m, n);
-    IRADS_REQUIRE(lda % 8 == 0 && ldb % 8 == 0 && lda >= m && ldb >= n &&
-                      ((uintptr_t)A % 16) == 0 && ((uintptr_t)B % 16) == 0,
-                  "irads_wgrad: rows must be 16-byte aligned (lda=%ld ldb=%ld)", lda, ldb);
-    hipStream_t st = (hipStream_t)stream;
-    const int TI = m <= 16 ? 16 : (m <= 32 ? 32 : (m <= 64 ? 64 : 128));
-    const int TJ = 128;
-    const long tiles = (long)((m + TI - 1) / TI) * ((n + TJ - 1) / TJ);
-    long nsplit = (1024 + tiles - 1) / tiles;  // ~4 workgroups per CU
-    const long maxsplit = (K + 63) / 64;      // >= 64 rows (2 MFMA steps) per workgroup
-    if (nsplit > maxsplit) nsplit = maxsplit;
-    if (nsplit < 1) nsplit = 1;
-    long chunk = (K + nsplit - 1) / nsplit;
-    chunk = (chunk + KS - 1) / KS * KS;
-    nsplit = chunk > 0 ? (K + chunk - 1) / chunk : 1;
-    if (nsplit < 1) nsplit = 1;
-    if (chunk == 0) chunk = KS;
-    float *ws = workspace;
-    float *ws_sa = colsum_a ? ws + nsplit * (long)m * n : nullptr;
-    float *ws_sb = colsum_b ? ws + nsplit * ((long)m * n + m) : nullptr;
-    if (K == 0) {
-        (void)hipMemsetAsync(ws, 0, sizeof(float) * nsplit * ((long)m * n + m + n), st);
-    } else {
-        int rc;
-        if (TI == 16)
-            rc = launch_partial<16, 128, 1>(A, lda, B, ldb, K, m, n, (int)nsplit, (int)chunk, ws, ws_sa, ws_sb, st);
-        else if (TI == 32)
-            rc = launch_partial<32, 128, 1>(A, lda, B, ldb, K, m, n, (int)nsplit, (int)chunk, ws, ws_sa, ws_sb, st);
-        else if (TI == 64)
-            rc = launch_partial<64, 128, 2>(A, lda, B, ldb, K, m, n, (int)nsplit, (int)chunk, ws, ws_sa, ws_sb, st);
-        else
-            rc = launch_partial<128, 128, 2>(A, lda, B, ldb, K, m, n, (int)nsplit, (int)chunk, ws, ws_sa, ws_sb, st);
-        if (rc) return rc;
-    }
-    const long cnt = (long)m * n;
-    Seg s0{ws, D, cnt, (int)((cnt + 63) / 64), transpose_out};
-    Seg s1{ws_sa, colsum_a, m, colsum_a ? (m + 63) / 64 : 0, 0};
-    Seg s2{ws_sb, colsum_b, n, colsum_b ? (n + 63) / 64 : 0, 0};
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(s0.blocks + s1.blocks + s2.blocks), dim3(256), 0, st, s0, s1, s2,
-                       (int)nsplit, alpha, accumulate, m, n);
-    return check_launch("irads_wgrad reduce");
+    const irads_wgrad_problem p{A, lda, B, ldb, D, colsum_a, colsum_b, transpose_out};
+    return irads_wgrad_batched(1, &p, K, m, n, alpha, accumulate, workspace, stream);
 }

@@ -44,6 +44,7 @@ SIGNATURES = {
     "irads_gelu_bwd": [_vp, _vp, _vp, _l, _vp],
     "irads_relu_dropout_fwd": [_vp, _vp, _l, _f, _u64, _vp, _vp],
     "irads_relu_dropout_bwd": [_vp, _vp, _vp, _l, _f, _vp],
+    "irads_wgrad_batched": [_i, _vp, _i, _i, _i, _f, _i, _vp, _vp],
     "irads_dattn_offset_fwd": [_vp] * 7 + [_i] * 8 + [_f] + [_vp] * 3,
     "irads_dattn_offset_bwd": [_vp] * 7 + [_i] * 8 + [_f] + [_vp] * 9,
     "irads_adapter_down": [_i, _vp, _vp, _vp, _vp, _vp, _vp, _l, _l, _i, _i, _f, _u64, _u64, _vp, _vp, _vp],
@@ -54,7 +55,8 @@ SIGNATURES = {
 }
 # entries that do not return an error code: name -> (restype, argtypes)
 QUERIES = {"irads_wgrad_workspace": (ctypes.c_long, [_i, _i, _i]),
-           "irads_dattn_offset_partials": (ctypes.c_long, [_i] * 8)}
+           "irads_dattn_offset_partials": (ctypes.c_long, [_i] * 8),
+           "irads_wgrad_batched_workspace": (ctypes.c_long, [_i] * 4)}
 CE_WORKSPACE = 2048
 
 _lib = None

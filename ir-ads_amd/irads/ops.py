@@ -555,6 +555,37 @@ def wgrad(A, B, D, colsum_a=None, colsum_b=None, alpha=1.0, accumulate=False):
     return D
 
 
+class _WgradProblem(ctypes.Structure):
+    _fields_ = [("A", ctypes.c_void_p), ("lda", ctypes.c_long), ("B", ctypes.c_void_p), ("ldb", ctypes.c_long),
+                ("D", ctypes.c_void_p), ("colsum_a", ctypes.c_void_p), ("colsum_b", ctypes.c_void_p),
+                ("transpose_out", ctypes.c_int)]
+
+
+def wgrad_batched(problems, alpha=1.0, accumulate=False):
+    """Up to 4 weight-gradient problems of one shape in one launch pair.  Each problem is
+    (A (K, m), B (K, n), D, colsum_a, colsum_b, transpose_out): D receives alpha * A^T B as an
+    (m, n) matrix, or (n, m) with transpose_out; colsum_a (m) / colsum_b (n) the column sums
+    of A / B (or None).  A and B bf16 with unit column stride, D / colsums contiguous fp32."""
+    K, m = problems[0][0].shape
+    n = problems[0][1].shape[1]
+    arr = (_WgradProblem * len(problems))()
+    for q, (A, B, D, sa, sb, tr) in enumerate(problems):
+        if tuple(A.shape) != (K, m) or tuple(B.shape) != (K, n):
+            raise RuntimeError("wgrad_batched: problems must share K, m, n")
+        for t in (A, B):
+            if t.dtype != torch.bfloat16 or t.stride(1) != 1 or not t.is_cuda:
+                raise RuntimeError("wgrad_batched: operands must be CUDA bf16 matrices with unit column stride")
+        want = (n, m) if tr else (m, n)
+        if D.dtype != torch.float32 or D.numel() != m * n or not D.is_contiguous() or D.shape[0] != want[0]:
+            raise RuntimeError("wgrad_batched: D must be a contiguous fp32 %s tensor" % (want,))
+        arr[q] = _WgradProblem(A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), D.data_ptr(),
+                               None if sa is None else sa.data_ptr(), None if sb is None else sb.data_ptr(), int(tr))
+    dev = problems[0][0].device
+    ws = torch.empty((N.load().irads_wgrad_batched_workspace(len(problems), K, m, n),), device=dev,
+                     dtype=torch.float32)
+    N.call("irads_wgrad_batched", len(problems), arr, K, m, n, float(alpha), int(accumulate), N.ptr(ws), N.stream())
+
+
 def wgrad_ok(in_features, out_features):
     return in_features % 8 == 0 and out_features % 8 == 0
 

@@ -284,12 +284,16 @@ class SwinStageFn(torch.autograd.Function):
                 dA = torch.empty((M, R), device=g.device, dtype=_BF16)  # grad of the D_fc1 output
                 N.call("irads_adapter_down", 1, N.ptr(dd), N.ptr(W2t[2 * i]), N.ptr(W2t[2 * i + 1]), None, None,
                        N.ptr(rs), M, Mh, C, R, float(p_drop), 0, 0, None, N.ptr(dA), N.stream())
+                # the four weight gradients of the block (D_fc2, D_fc1 x rgb, dte) in one batched
+                # split-K launch pair, all as (R, C) products: D_fc2's stored transposed
+                probs = []
                 for half in (0, 1):
                     k = 8 * i + 4 * half
                     gwa1, gba1, gwa2, gba2 = gparts[k: k + 4]
                     rows = slice(half * Mh, (half + 1) * Mh)
-                    ops.wgrad(dd[rows], rs[rows], gwa2, colsum_a=gba2)  # dW, db of D_fc2 in fp32 (split-K)
-                    ops.wgrad(dA[rows], X1b[rows], gwa1, colsum_a=gba1)
+                    probs.append((rs[rows], dd[rows], gwa2, None, gba2, True))
+                    probs.append((dA[rows], X1b[rows], gwa1, gba1, None, False))
+                ops.wgrad_batched(probs)
                 N.call("irads_adapter_up", N.ptr(dA), N.ptr(W1t[2 * i]), N.ptr(W1t[2 * i + 1]), None, None, M, Mh,
                        C, R, N.ptr(dX1b), N.stream())
             for half in (() if fast else (0, 1)):

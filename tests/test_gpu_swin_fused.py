@@ -362,3 +362,30 @@ def test_adapter_kernels_match_linear_path(C, Mh):
         assert torch.equal(dA[rows] != 0, dA_ref != 0) or (dA[rows] != 0).ne(dA_ref != 0).float().mean() < 1e-3
         assert _rel(dA[rows], dA_ref) < 4e-3
         assert _rel(dx[rows], torch.mm(dA[rows], W1[h])) < 4e-3
+
+
+def test_wgrad_batched_matches_single():
+    """irads_wgrad_batched: four problems of one shape (the Adapter layout: two transposed
+    stores with column sums of B, two plain with column sums of A) against the fp32 A^T B
+    and column sums of the same bf16 operands (fp32 accumulation order: rtol 1e-5)."""
+    from irads import ops
+    torch.manual_seed(5)
+    K, m, n = 8192, 32, 512
+    probs, refs = [], []
+    for q in range(4):
+        A = (torch.randn(K, m, device=DEV) * 0.3).bfloat16()
+        B = (torch.randn(K, n, device=DEV) * 0.3).bfloat16()
+        tr = q % 2 == 0
+        D = torch.empty((n, m) if tr else (m, n), device=DEV)
+        sa = None if tr else torch.empty(m, device=DEV)
+        sb = torch.empty(n, device=DEV) if tr else None
+        probs.append((A, B, D, sa, sb, tr))
+        ref = A.float().t() @ B.float()
+        refs.append((ref.t() if tr else ref, A.float().sum(0), B.float().sum(0)))
+    ops.wgrad_batched(probs)
+    for (A, B, D, sa, sb, tr), (ref, ca, cb) in zip(probs, refs):
+        torch.testing.assert_close(D, ref, rtol=1e-5, atol=1e-3)
+        if sa is not None:
+            torch.testing.assert_close(sa, ca, rtol=1e-5, atol=1e-3)
+        if sb is not None:
+            torch.testing.assert_close(sb, cb, rtol=1e-5, atol=1e-3)
