@@ -50,9 +50,11 @@ template <int T> struct Tile {
     static constexpr int THREADS = ELEMS / 8 < 256 ? ELEMS / 8 : 256;       // threads that load
 };
 
+// csum: this thread's column-sum accumulators, updated when do_sum (an array reference and
+// a flag rather than a maybe-null pointer, so that the sums stay in registers, not scratch)
 template <int T>
 __device__ __forceinline__ void load_tile(const u16 *__restrict__ g, long ld, int k0, int kend, int c0, int cols,
-                                          u16x8 *reg, float *csum) {
+                                          u16x8 *reg, float (&csum)[Tile<T>::LOADS * 8], bool do_sum) {
     const int t = threadIdx.x;
 #pragma unroll
     for (int s = 0; s < Tile<T>::LOADS; ++s) {
@@ -62,7 +64,7 @@ __device__ __forceinline__ void load_tile(const u16 *__restrict__ g, long ld, in
         if (t < Tile<T>::THREADS && k0 + k < kend && c0 + c < cols)
             v = *reinterpret_cast<const u16x8 *>(g + (long)(k0 + k) * ld + c0 + c);
         reg[s] = v;
-        if (csum) {
+        if (do_sum) {
 #pragma unroll
             for (int j = 0; j < 8; ++j) csum[s * 8 + j] += bf2f(v[j]);
         }
@@ -142,15 +144,15 @@ __global__ __launch_bounds__(256) void wgrad_partial_kernel(WProbs probs, int K,
 #pragma unroll
         for (int b = 0; b < BJ; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
     u16x8 ra[LA], rb[LB];
-    load_tile<TI>(A, lda, k0, kend, i0, m, ra, sum_a ? csa : nullptr);
-    load_tile<TJ>(B, ldb, k0, kend, j0, n, rb, sum_b ? csb : nullptr);
+    load_tile<TI>(A, lda, k0, kend, i0, m, ra, csa, sum_a);
+    load_tile<TJ>(B, ldb, k0, kend, j0, n, rb, csb, sum_b);
     for (int k = k0; k < kend; k += KS) {
         store_tile<TI>(lA, ra);
         store_tile<TJ>(lB, rb);
         __syncthreads();
         if (k + KS < kend) {  // prefetch the next step while this one computes
-            load_tile<TI>(A, lda, k + KS, kend, i0, m, ra, sum_a ? csa : nullptr);
-            load_tile<TJ>(B, ldb, k + KS, kend, j0, n, rb, sum_b ? csb : nullptr);
+            load_tile<TI>(A, lda, k + KS, kend, i0, m, ra, csa, sum_a);
+            load_tile<TJ>(B, ldb, k + KS, kend, j0, n, rb, csb, sum_b);
         }
         bf16x8_t fa[BI], fb[BJ];
 #pragma unroll
@@ -261,14 +263,19 @@ int launch_partial(const WProbs &probs, int count, int K, int m, int n, int nspl
 
 int tile_i(int m) { return m <= 16 ? 16 : (m <= 32 ? 32 : (m <= 64 ? 64 : 128)); }
 
-// K-splits: enough workgroups to fill the chip (~1024 over the batch), but each split covers
-// at least max(256, 4mn/(m+n)) rows so that the fp32 partials it writes stay below ~half of
-// the bf16 operand bytes it reads (partials: 4mn per split; operands: 2(m+n) per row).
+// K-splits: enough workgroups to fill the chip (~1024 over the batch).  A single problem
+// takes splits of >= 64 rows (latency-bound: parallelism first).  A batch (the Adapters'
+// skinny (R, C) gradients) covers at least max(256, 4mn/(m+n)) rows per split so that the
+// fp32 partials stay below ~half of the bf16 operand bytes (partials: 4mn per split;
+// operands: 2(m+n) per row) - measured faster for those shapes.
 void plan(int count, int K, int m, int n, long *nsplit_out, long *chunk_out) {
     const long tiles = (long)((m + tile_i(m) - 1) / tile_i(m)) * ((n + 127) / 128);
     long nsplit = (1024 + tiles * count - 1) / (tiles * count);
-    long rows = 4L * m * n / (m + n);
-    if (rows < 256) rows = 256;
+    long rows = 64;
+    if (count > 1) {
+        rows = 4L * m * n / (m + n);
+        if (rows < 256) rows = 256;
+    }
     const long maxsplit = (K + rows - 1) / rows;
     if (nsplit > maxsplit) nsplit = maxsplit;
     if (nsplit < 1) nsplit = 1;

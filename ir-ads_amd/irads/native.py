@@ -89,11 +89,27 @@ def load(require_gpu=False):
     return _lib
 
 
+_DEBUG_SYNC = bool(os.environ.get("IRADS_DEBUG_SYNC"))
+
+
+def _sync_check(where):
+    if torch.cuda.is_current_stream_capturing():
+        return
+    try:
+        torch.cuda.synchronize()
+    except Exception as e:  # noqa: BLE001 - re-raised with the call site named
+        raise RuntimeError(f"IRADS_DEBUG_SYNC: device error detected {where}") from e
+
+
 def call(name, *args):
     lib = load(require_gpu=True)
+    if _DEBUG_SYNC:  # localise asynchronous device faults: the window is between two native calls
+        _sync_check(f"before {name} (raised by work queued since the previous native call)")
     rc = getattr(lib, name)(*args)
     if rc != 0:
         raise RuntimeError(f"{name} failed (code {rc}): {lib.irads_last_error().decode()}")
+    if _DEBUG_SYNC:
+        _sync_check(f"in {name}")
 
 
 def ptr(t):

@@ -37,6 +37,7 @@ from . import ops
 
 _BF16 = torch.bfloat16
 ADAPTER_DROPOUT = 0.1  # hard-coded in the reference Adapter (swin.py:496)
+_UNBATCHED = bool(__import__("os").environ.get("IRADS_WGRAD_UNBATCHED"))
 
 
 def _frozen_trunk(block):
@@ -293,7 +294,14 @@ class SwinStageFn(torch.autograd.Function):
                     rows = slice(half * Mh, (half + 1) * Mh)
                     probs.append((rs[rows], dd[rows], gwa2, None, gba2, True))
                     probs.append((dA[rows], X1b[rows], gwa1, gba1, None, False))
-                ops.wgrad_batched(probs)
+                if _UNBATCHED:
+                    for A_, B_, D_, sa_, sb_, tr_ in probs:
+                        if tr_:
+                            ops.wgrad(B_, A_, D_, colsum_a=sb_)
+                        else:
+                            ops.wgrad(A_, B_, D_, colsum_a=sa_)
+                else:
+                    ops.wgrad_batched(probs)
                 N.call("irads_adapter_up", N.ptr(dA), N.ptr(W1t[2 * i]), N.ptr(W1t[2 * i + 1]), None, None, M, Mh,
                        C, R, N.ptr(dX1b), N.stream())
             for half in (() if fast else (0, 1)):

@@ -14,6 +14,6 @@ timeout -k 10 ${PROFILE_TIMEOUT:-600} rocprofv3 --kernel-trace --stats --output-
 rc=$?
 echo "rocprofv3 rc=$rc"
 find "$out" -name '*kernel_trace.csv' -exec gzip -f {} \;
-find "$out" -type f \( -name '*.db' -o -size +20M \) -print -delete
+find "$out" -type f \( -name '*.db' -o -size +45M \) -print -delete
 du -sh gpurun_out
 exit $rc
