@@ -124,11 +124,13 @@ int irads_dattn_attn_bwd(const float *q, const float *k, const float *v, const f
  * params_{x,y}: 5 fp32 pointers {dw weight (gc,1,ks,ks), dw bias (gc), LN weight (gc),
  * LN bias (gc), 1x1 weight (2,gc)}; ref: (Hk*Wk, 2) bf16 reference points (y, x);
  * pos_x, pos_y: fp32 (B*G, Hk, Wk, 2), Hk = (H + 2 pad - ks) / stride + 1.  gc <= 32,
- * ks in {3, 5, 7, 9}.  Backward takes the pos gradients and writes dv_{x,y} (B*G*Hk*Wk*gc
- * floats, scratch), partials (irads_dattn_offset_partials(...) floats: per-block sums of the
- * 1x1 weight, LN weight, LN bias and conv bias gradients, layout [m][block][5][gc], to be
- * summed over blocks), dw (2*gc*ks*ks floats: the depthwise weight gradients [m][c][ky][kx])
- * and dx, dy (bf16, the strides of x, y). */
+ * ks in {3, 5, 7, 9}, ks*W*GCP*2 + 32*ks*ks*4 <= 144 KiB, GCP = 16 or 32 >= gc (one key row's
+ * input rows in LDS).
+ * Backward takes the pos gradients and writes dv_{x,y} (B*G*Hk*Wk*gc floats, scratch), dx, dy
+ * (bf16, the strides of x, y) and partials (irads_dattn_offset_partials(...) floats) holding
+ * per-block sums to be added over blocks: [m][block][5][gc] (1x1 weight row 0, row 1, LN
+ * weight, LN bias, conv bias), then [m][block][gc][ks*ks] (depthwise weight); block = (map,
+ * key row), B*G*Hk per modality.  Wk <= 64. */
 int irads_dattn_offset_fwd(const uint16_t *x, const long *x_strides, const uint16_t *y, const long *y_strides,
                            const float *const *params_x, const float *const *params_y, const uint16_t *ref, int B,
                            int G, int gc, int H, int W, int ks, int stride, int pad, float eps, float *pos_x,
@@ -136,7 +138,7 @@ int irads_dattn_offset_fwd(const uint16_t *x, const long *x_strides, const uint1
 int irads_dattn_offset_bwd(const uint16_t *x, const long *x_strides, const uint16_t *y, const long *y_strides,
                            const float *const *params_x, const float *const *params_y, const uint16_t *ref, int B,
                            int G, int gc, int H, int W, int ks, int stride, int pad, float eps, const float *gpos_x,
-                           const float *gpos_y, float *dv_x, float *dv_y, float *partials, float *dw, uint16_t *dx,
+                           const float *gpos_y, float *dv_x, float *dv_y, float *partials, uint16_t *dx,
                            uint16_t *dy, void *stream);
 long irads_dattn_offset_partials(int B, int G, int gc, int H, int W, int ks, int stride, int pad);
 int irads_dattn_sample_index(const float *grid, int N, int H, int W, int32_t *corners, void *stream);

@@ -20,13 +20,16 @@
 // the channel reductions of LayerNorm and the 1x1 conv are in-wave butterflies (their result
 // is broadcast from the group's first lane so every lane uses the same value).
 //
+// A block owns one output row of one map: the ks input rows it reads are staged in LDS
+// channel-fastest (coalesced global reads, conflict-free taps), so each input value is read
+// from HBM once per row instead of once per tap (81x at stride 1).
+//
 // Backward recomputes the forward (cheaper than saving it) and:
 //   k1  per cell/channel: the gradient chain down to the conv output dV (bf16 values, kept as
 //       fp32), plus per-block partial sums of the 1x1 weight, LayerNorm affine and conv bias
-//       gradients (summed in a fixed order; the host adds the block partials);
-//   k2  the depthwise weight gradient dW[c][ky][kx] = sum_{n,cell} dV * x, one block per
-//       (channel, ky), a fixed-order block reduction;
-//   k3  the input gradient, gathered per input pixel from the <= ceil(ks/s)^2 cells covering it.
+//       gradients and of the depthwise weight gradient (dV x the staged taps), in fixed orders;
+//       the host adds the block partials;
+//   k2  the input gradient, gathered per input pixel from the <= ceil(ks/s)^2 cells covering it.
 #include "common.h"
 
 namespace irads {
@@ -66,13 +69,54 @@ __device__ __forceinline__ float group_sum(float v) {
     return __shfl(v, (threadIdx.x & 63) & ~(GCP - 1), 64);
 }
 
-// depthwise weights of both modalities, bf16-rounded, into LDS: wl[m][c][k]
+// depthwise weights of modality m, bf16-rounded, into LDS: wl[c][k]
 template <int KS>
-__device__ __forceinline__ void load_weights(const OffArgs &a, float *wl) {
+__device__ __forceinline__ void load_weights(const OffArgs &a, int m, float *wl) {
     const int per = a.gc * KS * KS;
-    for (int i = threadIdx.x; i < 2 * per; i += blockDim.x) {
-        const int m = i / per;
-        wl[i] = rbf(a.net[m].w[i - m * per]);
+    for (int i = threadIdx.x; i < per; i += blockDim.x) wl[i] = rbf(a.net[m].w[i]);
+}
+
+// The KS input rows output row oy of map n reads, into LDS as [r][ix][c] (channel fastest:
+// the GCP lanes of a cell read one 2*GCP-byte run).  Rows outside the map are zero, so the
+// taps only test the column.  Global reads run along the unit-stride dimension of x.
+template <int GCP, int KS>
+__device__ __forceinline__ void stage_rows(const OffArgs &a, int m, int n, int oy, u16 *rows) {
+    const int b = n / a.G, gi = n - b * a.G;
+    const u16 *xb = a.x[m] + b * a.sb[m] + (long)gi * a.gc * a.sc[m];
+    const int W = a.W, gc = a.gc;
+    const int total = KS * W * gc;
+    const bool cfast = a.sc[m] == 1;  // channels-last memory: read channel-fastest
+    if (!cfast && a.sw[m] == 1 && W % 8 == 0 && (((uintptr_t)xb) & 15) == 0 && a.sh[m] % 8 == 0 &&
+        a.sc[m] % 8 == 0) {
+        // NCHW rows: 16-byte loads of 8 columns, scattered channel-fastest into LDS
+        const int groups = KS * gc * (W / 8);
+        for (int e = threadIdx.x; e < groups; e += blockDim.x) {
+            const int ix0 = (e % (W / 8)) * 8, c = (e / (W / 8)) % gc, r = e / ((W / 8) * gc);
+            const int iy = oy * a.stride - a.pad + r;
+            uint4 v = make_uint4(0u, 0u, 0u, 0u);
+            if (iy >= 0 && iy < a.H) v = *reinterpret_cast<const uint4 *>(xb + c * a.sc[m] + iy * a.sh[m] + ix0);
+            const unsigned w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                rows[(r * W + ix0 + j) * GCP + c] = (u16)(j & 1 ? w4[j >> 1] >> 16 : w4[j >> 1] & 0xffffu);
+        }
+        return;
+    }
+    for (int e = threadIdx.x; e < total; e += blockDim.x) {
+        int r, ix, c;
+        if (cfast) {
+            c = e % gc;
+            ix = (e / gc) % W;
+            r = e / (gc * W);
+        } else {
+            ix = e % W;
+            c = (e / W) % gc;
+            r = e / (W * gc);
+        }
+        const int iy = oy * a.stride - a.pad + r;
+        u16 v = 0;
+        if (iy >= 0 && iy < a.H) v = xb[c * a.sc[m] + iy * a.sh[m] + ix * a.sw[m]];
+        rows[(r * W + ix) * GCP + c] = v;
     }
 }
 
@@ -80,26 +124,22 @@ struct Cell {
     float v, rstd, xhat, ln, gb, r0, r1;
 };
 
-// forward of one (cell, channel); every lane of the group must call it (shuffles)
+// forward of one (cell, channel) from the staged rows; every lane of the group must call it
 template <int GCP, int KS>
-__device__ __forceinline__ Cell cell_forward(const OffArgs &a, int m, bool pv, int n, int oy, int ox, int c,
-                                             const float *wl) {
+__device__ __forceinline__ Cell cell_forward(const OffArgs &a, int m, bool pv, int oy, int ox, int c,
+                                             const float *wl, const u16 *rows) {
     const OffNet &net = a.net[m];
     const bool cv = pv && c < a.gc;
     float acc = 0.f;
     if (cv) {
-        const int b = n / a.G, gi = n - b * a.G;
-        const u16 *xp = a.x[m] + b * a.sb[m] + (long)(gi * a.gc + c) * a.sc[m];
-        const float *w = wl + (m * a.gc + c) * KS * KS;
+        const float *w = wl + c * KS * KS;
 #pragma unroll
         for (int ky = 0; ky < KS; ++ky) {
-            const int iy = oy * a.stride - a.pad + ky;
-            if (iy < 0 || iy >= a.H) continue;
 #pragma unroll
             for (int kx = 0; kx < KS; ++kx) {
                 const int ix = ox * a.stride - a.pad + kx;
                 if (ix < 0 || ix >= a.W) continue;
-                acc += bf2f(xp[iy * a.sh[m] + ix * a.sw[m]]) * w[ky * KS + kx];
+                acc += bf2f(rows[(ky * a.W + ix) * GCP + c]) * w[ky * KS + kx];
             }
         }
     }
@@ -121,138 +161,145 @@ __device__ __forceinline__ Cell cell_forward(const OffArgs &a, int m, bool pv, i
     return s;
 }
 
+// dynamic LDS: staged rows (u16) after the fixed arrays
+template <int GCP, int KS>
+__host__ __device__ constexpr int rows_offset_bytes() {
+    return 32 * KS * KS * 4;
+}
+
+// block = (map n, output row oy), blockIdx.y = modality; cells ox in chunks of 256 / GCP
 template <int GCP, int KS>
 __global__ __launch_bounds__(256) void offset_fwd_kernel(OffArgs a, float *__restrict__ pos0,
                                                          float *__restrict__ pos1) {
-    __shared__ float wl[2 * 32 * KS * KS];
-    load_weights<KS>(a, wl);
-    __syncthreads();
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    float *wl = reinterpret_cast<float *>(smem);
+    u16 *rows = reinterpret_cast<u16 *>(smem + rows_offset_bytes<GCP, KS>());
     constexpr int PPB = 256 / GCP;
-    const int m = blockIdx.y;
-    const long cells = (long)a.B * a.G * a.Hk * a.Wk;
-    const long pix = (long)blockIdx.x * PPB + threadIdx.x / GCP;
-    const int c = threadIdx.x % GCP;
-    const bool pv = pix < cells;
-    const int hw = a.Hk * a.Wk;
-    const int n = pv ? (int)(pix / hw) : 0, p = pv ? (int)(pix % hw) : 0;
-    const Cell s = cell_forward<GCP, KS>(a, m, pv, n, p / a.Wk, p % a.Wk, c, wl);
-    if (pv && c == 0) {
-        float *pos = m ? pos1 : pos0;
-        pos[2 * pix] = fminf(fmaxf(s.r0, -1.f), 1.f);
-        pos[2 * pix + 1] = fminf(fmaxf(s.r1, -1.f), 1.f);
+    const int m = blockIdx.y, n = blockIdx.x / a.Hk, oy = blockIdx.x % a.Hk;
+    load_weights<KS>(a, m, wl);
+    stage_rows<GCP, KS>(a, m, n, oy, rows);
+    __syncthreads();
+    const int pl = threadIdx.x / GCP, c = threadIdx.x % GCP;
+    float *pos = m ? pos1 : pos0;
+    for (int ox0 = 0; ox0 < a.Wk; ox0 += PPB) {
+        const int ox = ox0 + pl;
+        const bool pv = ox < a.Wk;
+        const Cell s = cell_forward<GCP, KS>(a, m, pv, oy, pv ? ox : 0, c, wl, rows);
+        if (pv && c == 0) {
+            const long pix = ((long)n * a.Hk + oy) * a.Wk + ox;
+            pos[2 * pix] = fminf(fmaxf(s.r0, -1.f), 1.f);
+            pos[2 * pix + 1] = fminf(fmaxf(s.r1, -1.f), 1.f);
+        }
     }
 }
 
-// k1: gradient down to the conv output + block partials of (dW2[0], dW2[1], dLNw, dLNb, db)
+// backward, block = (map n, output row oy) as the forward: the gradient chain down to the conv
+// output dV (kept for the input gradient, and in LDS), then this block's partial sums of the
+// 1x1 weight, LN affine and conv bias gradients ([5][gc]) and of the depthwise weight gradient
+// ([gc][KS*KS]: dV x the staged taps, summed over the row's cells).  Fixed summation orders.
 template <int GCP, int KS>
 __global__ __launch_bounds__(256) void offset_bwd_cell_kernel(OffArgs a, const float *__restrict__ gpos0,
                                                               const float *__restrict__ gpos1,
                                                               float *__restrict__ dv0, float *__restrict__ dv1,
-                                                              float *__restrict__ part) {
+                                                              float *__restrict__ part, float *__restrict__ wpart) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    float *wl = reinterpret_cast<float *>(smem);
+    u16 *rows = reinterpret_cast<u16 *>(smem + rows_offset_bytes<GCP, KS>());
     constexpr int PPB = 256 / GCP;
-    __shared__ float wl[2 * 32 * KS * KS];
+    constexpr int MAXW = 64;  // cells per row held in LDS for the weight-gradient pass
     __shared__ float red[5][PPB][GCP];
-    load_weights<KS>(a, wl);
-    __syncthreads();
-    const int m = blockIdx.y;
+    __shared__ float dvl[MAXW][GCP];
+    const int m = blockIdx.y, n = blockIdx.x / a.Hk, oy = blockIdx.x % a.Hk;
     const OffNet &net = a.net[m];
-    const long cells = (long)a.B * a.G * a.Hk * a.Wk;
-    const int pl = threadIdx.x / GCP, c = threadIdx.x % GCP;
-    const long pix = (long)blockIdx.x * PPB + pl;
-    const bool pv = pix < cells, cv = pv && c < a.gc;
-    const int hw = a.Hk * a.Wk;
-    const int n = pv ? (int)(pix / hw) : 0, p = pv ? (int)(pix % hw) : 0;
-    const Cell s = cell_forward<GCP, KS>(a, m, pv, n, p / a.Wk, p % a.Wk, c, wl);
-    const float *gpos = m ? gpos1 : gpos0;
-    // .float() backward -> bf16 gradient; clamp passes it where -1 <= r <= 1
-    const float gp0 = pv ? rbf(gpos[2 * pix]) : 0.f, gp1 = pv ? rbf(gpos[2 * pix + 1]) : 0.f;
-    const float go0 = (s.r0 >= -1.f && s.r0 <= 1.f) ? gp0 : 0.f;
-    const float go1 = (s.r1 >= -1.f && s.r1 <= 1.f) ? gp1 : 0.f;
-    float dgb = 0.f, dln = 0.f;
-    if (cv) {
-        dgb = rbf(go0 * rbf(net.w2[c]) + go1 * rbf(net.w2[a.gc + c]));  // 1x1 conv dgrad (bf16)
-        dln = dgb * gelu_grad(s.ln);
-    }
-    const float t = cv ? dln * net.lg[c] : 0.f;
-    const float inv = 1.f / (float)a.gc;
-    const float mt = group_sum<GCP>(t) * inv;
-    const float mtx = group_sum<GCP>(t * s.xhat) * inv;
-    const float dvb = cv ? rbf(s.rstd * (t - mt - s.xhat * mtx)) : 0.f;  // LN input is bf16
-    if (cv) (m ? dv1 : dv0)[pix * a.gc + c] = dvb;
-    red[0][pl][c] = go0 * s.gb;
-    red[1][pl][c] = go1 * s.gb;
-    red[2][pl][c] = dln * s.xhat;
-    red[3][pl][c] = dln;
-    red[4][pl][c] = dvb;
+    load_weights<KS>(a, m, wl);
+    stage_rows<GCP, KS>(a, m, n, oy, rows);
     __syncthreads();
+    const int pl = threadIdx.x / GCP, c = threadIdx.x % GCP;
+    const float *gpos = m ? gpos1 : gpos0;
+    float *dvg = m ? dv1 : dv0;
+    float acc5[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int ox0 = 0; ox0 < a.Wk; ox0 += PPB) {
+        const int ox = ox0 + pl;
+        const bool pv = ox < a.Wk, cv = pv && c < a.gc;
+        const Cell s = cell_forward<GCP, KS>(a, m, pv, oy, pv ? ox : 0, c, wl, rows);
+        const long pix = ((long)n * a.Hk + oy) * a.Wk + (pv ? ox : 0);
+        // .float() backward -> bf16 gradient; clamp passes it where -1 <= r <= 1
+        const float gp0 = pv ? rbf(gpos[2 * pix]) : 0.f, gp1 = pv ? rbf(gpos[2 * pix + 1]) : 0.f;
+        const float go0 = (s.r0 >= -1.f && s.r0 <= 1.f) ? gp0 : 0.f;
+        const float go1 = (s.r1 >= -1.f && s.r1 <= 1.f) ? gp1 : 0.f;
+        float dgb = 0.f, dln = 0.f;
+        if (cv) {
+            dgb = rbf(go0 * rbf(net.w2[c]) + go1 * rbf(net.w2[a.gc + c]));  // 1x1 conv dgrad (bf16)
+            dln = dgb * gelu_grad(s.ln);
+        }
+        const float t = cv ? dln * net.lg[c] : 0.f;
+        const float inv = 1.f / (float)a.gc;
+        const float mt = group_sum<GCP>(t) * inv;
+        const float mtx = group_sum<GCP>(t * s.xhat) * inv;
+        const float dvb = cv ? rbf(s.rstd * (t - mt - s.xhat * mtx)) : 0.f;  // LN input is bf16
+        if (cv) dvg[pix * a.gc + c] = dvb;
+        if (pv && ox < MAXW) dvl[ox][c] = dvb;
+        acc5[0] += go0 * s.gb;
+        acc5[1] += go1 * s.gb;
+        acc5[2] += dln * s.xhat;
+        acc5[3] += dln;
+        acc5[4] += dvb;
+    }
+#pragma unroll
+    for (int q = 0; q < 5; ++q) red[q][pl][c] = acc5[q];
+    __syncthreads();
+    const long blk = (long)m * gridDim.x + blockIdx.x;
     if (threadIdx.x < 5 * GCP) {
         const int q = threadIdx.x / GCP, cc = threadIdx.x % GCP;
         float acc = 0.f;
         for (int i = 0; i < PPB; ++i) acc += red[q][i][cc];
-        if (cc < a.gc) part[(((long)m * gridDim.x + blockIdx.x) * 5 + q) * a.gc + cc] = acc;
+        if (cc < a.gc) part[(blk * 5 + q) * a.gc + cc] = acc;
     }
-}
-
-// k2: depthwise weight gradient, block (c, ky, m), threads stride over cells
-template <int KS>
-__global__ __launch_bounds__(256) void offset_bwd_weight_kernel(OffArgs a, const float *__restrict__ dv0,
-                                                                const float *__restrict__ dv1,
-                                                                float *__restrict__ dw) {
-    __shared__ float red[4][KS];
-    const int c = blockIdx.x, ky = blockIdx.y, m = blockIdx.z;
-    const float *dv = m ? dv1 : dv0;
-    const long cells = (long)a.B * a.G * a.Hk * a.Wk;
-    const int hw = a.Hk * a.Wk;
-    float acc[KS];
-#pragma unroll
-    for (int k = 0; k < KS; ++k) acc[k] = 0.f;
-    for (long pix = threadIdx.x; pix < cells; pix += blockDim.x) {
-        const int n = (int)(pix / hw), p = (int)(pix % hw);
-        const int oy = p / a.Wk, ox = p % a.Wk;
-        const int iy = oy * a.stride - a.pad + ky;
-        if (iy < 0 || iy >= a.H) continue;
-        const float d = dv[pix * a.gc + c];
-        const int b = n / a.G, gi = n - b * a.G;
-        const u16 *xp = a.x[m] + b * a.sb[m] + (long)(gi * a.gc + c) * a.sc[m] + iy * a.sh[m];
-#pragma unroll
-        for (int kx = 0; kx < KS; ++kx) {
+    // depthwise weight gradient of this row: pair (c, ky, kx) per thread iteration
+    const int KK = KS * KS, pairs = a.gc * KK, wk = min(a.Wk, MAXW);
+    for (int pr = threadIdx.x; pr < pairs; pr += blockDim.x) {
+        const int cc = pr / KK, k = pr - cc * KK, ky = k / KS, kx = k - ky * KS;
+        float acc = 0.f;
+        for (int ox = 0; ox < wk; ++ox) {
             const int ix = ox * a.stride - a.pad + kx;
-            if (ix >= 0 && ix < a.W) acc[kx] += d * bf2f(xp[ix * a.sw[m]]);
+            if (ix >= 0 && ix < a.W) acc += dvl[ox][cc] * bf2f(rows[(ky * a.W + ix) * GCP + cc]);
         }
-    }
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-#pragma unroll
-    for (int k = 0; k < KS; ++k) {
-        const float v = wave_sum(acc[k]);  // butterfly: every lane holds the same bits only up to order;
-        if (lane == 0) red[wave][k] = v;  // lane 0's value is the one kept
-    }
-    __syncthreads();
-    if (threadIdx.x < KS) {
-        const int k = threadIdx.x;
-        dw[(((long)m * a.gc + c) * KS + ky) * KS + k] = ((red[0][k] + red[1][k]) + red[2][k]) + red[3][k];
+        wpart[blk * pairs + pr] = acc;
     }
 }
 
-// k3: input gradient, thread per (m, n, iy, ix, c), channel fastest
+// input gradient, thread per (m, n, c, iy, ix) in the order of x's unit-stride dimension
 template <int KS>
 __global__ __launch_bounds__(256) void offset_bwd_input_kernel(OffArgs a, const float *__restrict__ dv0,
                                                                const float *__restrict__ dv1, u16 *__restrict__ dx0,
                                                                u16 *__restrict__ dx1) {
-    __shared__ float wl[2 * 32 * KS * KS];
-    load_weights<KS>(a, wl);
-    __syncthreads();
+    __shared__ float wl[32 * KS * KS];
     const int m = blockIdx.y;
+    load_weights<KS>(a, m, wl);
+    __syncthreads();
     const long total = (long)a.B * a.G * a.H * a.W * a.gc;
     const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= total) return;
-    const int c = (int)(e % a.gc);
-    long r = e / a.gc;
-    const int ix = (int)(r % a.W);
-    r /= a.W;
-    const int iy = (int)(r % a.H);
-    const int n = (int)(r / a.H);
+    int c, ix, iy, n;
+    // channel fastest when x is channels-last, or at stride 1 (each pixel gathers up to ks^2
+    // cells: coalesced dV reads dominate); else column fastest (coalesced dx stores)
+    if (a.sc[m] == 1 || a.stride == 1) {
+        c = (int)(e % a.gc);
+        long r = e / a.gc;
+        ix = (int)(r % a.W);
+        r /= a.W;
+        iy = (int)(r % a.H);
+        n = (int)(r / a.H);
+    } else {  // NCHW: column fastest
+        ix = (int)(e % a.W);
+        long r = e / a.W;
+        iy = (int)(r % a.H);
+        r /= a.H;
+        c = (int)(r % a.gc);
+        n = (int)(r / a.gc);
+    }
     const float *dv = m ? dv1 : dv0;
-    const float *w = wl + (m * a.gc + c) * KS * KS;
+    const float *w = wl + c * KS * KS;
     // cells with oy*s - pad <= iy <= oy*s - pad + KS - 1
     const int s = a.stride;
     const int oy_lo = max(0, (iy + a.pad - KS + 1 + s - 1 + s * KS) / s - KS), oy_hi = min(a.Hk - 1, (iy + a.pad) / s);
@@ -307,12 +354,46 @@ int fill_args(OffArgs &a, const uint16_t *x, const long *xs, const uint16_t *y, 
 
 using namespace irads;
 
-extern "C" long irads_dattn_offset_partials(int B, int G, int gc, int H, int W, int ks, int stride, int pad) {
-    const long hk = (H + 2 * pad - ks) / stride + 1, wk = (W + 2 * pad - ks) / stride + 1;
-    const long cells = (long)B * G * hk * wk;
-    const int ppb = gc <= 16 ? 16 : 8;
-    return 2 * ((cells + ppb - 1) / ppb) * 5 * gc;
+// dynamic LDS above the 64 KiB default needs the per-kernel opt-in (gfx950: 160 KiB per
+// workgroup, static arrays included; those are < 16 KiB here)
+static int allow_lds(const void *kernel, size_t bytes) {
+    if (bytes <= 64 * 1024) return IRADS_OK;
+    if (bytes > 144 * 1024) return IRADS_EINVAL;
+    return hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) == hipSuccess
+               ? IRADS_OK
+               : IRADS_EINVAL;
 }
+
+template <int GCP, int KS>
+size_t smem_bytes(int W) {
+    return rows_offset_bytes<GCP, KS>() + (size_t)KS * W * GCP * 2;
+}
+
+extern "C" long irads_dattn_offset_partials(int B, int G, int gc, int H, int W, int ks, int stride, int pad) {
+    const long hk = (H + 2 * pad - ks) / stride + 1;
+    const long nblk = (long)B * G * hk;
+    return 2 * nblk * (5 * gc + (long)gc * ks * ks);
+}
+
+#define IRADS_OFF_LAUNCH(KERNEL, ...)                                                                             \
+    do {                                                                                                         \
+        dim3 grid((unsigned)(B * G * a.Hk), 2);                                                                  \
+        if (gc <= 16) {                                                                                          \
+            IRADS_OFF_KS(ks, {                                                                                   \
+                const size_t sm = smem_bytes<16, KS>(W);                                                         \
+                IRADS_REQUIRE(allow_lds((const void *)KERNEL<16, KS>, sm) == IRADS_OK,                             \
+                              "irads_dattn_offset: row tile %zu B exceeds the LDS (W=%d)", sm, W);               \
+                hipLaunchKernelGGL((KERNEL<16, KS>), grid, dim3(256), sm, st, a, __VA_ARGS__);                   \
+            });                                                                                                  \
+        } else {                                                                                                 \
+            IRADS_OFF_KS(ks, {                                                                                   \
+                const size_t sm = smem_bytes<32, KS>(W);                                                         \
+                IRADS_REQUIRE(allow_lds((const void *)KERNEL<32, KS>, sm) == IRADS_OK,                             \
+                              "irads_dattn_offset: row tile %zu B exceeds the LDS (W=%d)", sm, W);               \
+                hipLaunchKernelGGL((KERNEL<32, KS>), grid, dim3(256), sm, st, a, __VA_ARGS__);                   \
+            });                                                                                                  \
+        }                                                                                                        \
+    } while (0)
 
 extern "C" int irads_dattn_offset_fwd(const uint16_t *x, const long *x_strides, const uint16_t *y,
                                       const long *y_strides, const float *const *params_x,
@@ -323,15 +404,8 @@ extern "C" int irads_dattn_offset_fwd(const uint16_t *x, const long *x_strides, 
     int rc = fill_args(a, x, x_strides, y, y_strides, params_x, params_y, ref, B, G, gc, H, W, ks, stride, pad, eps);
     if (rc) return rc;
     IRADS_REQUIRE(pos_x && pos_y, "irads_dattn_offset_fwd: null output");
-    const long cells = (long)B * G * a.Hk * a.Wk;
     hipStream_t st = (hipStream_t)stream;
-    if (gc <= 16) {
-        dim3 grid((unsigned)((cells + 15) / 16), 2);
-        IRADS_OFF_KS(ks, hipLaunchKernelGGL((offset_fwd_kernel<16, KS>), grid, dim3(256), 0, st, a, pos_x, pos_y));
-    } else {
-        dim3 grid((unsigned)((cells + 7) / 8), 2);
-        IRADS_OFF_KS(ks, hipLaunchKernelGGL((offset_fwd_kernel<32, KS>), grid, dim3(256), 0, st, a, pos_x, pos_y));
-    }
+    IRADS_OFF_LAUNCH(offset_fwd_kernel, pos_x, pos_y);
     return check_launch("irads_dattn_offset_fwd");
 }
 
@@ -339,28 +413,18 @@ extern "C" int irads_dattn_offset_bwd(const uint16_t *x, const long *x_strides, 
                                       const long *y_strides, const float *const *params_x,
                                       const float *const *params_y, const uint16_t *ref, int B, int G, int gc, int H,
                                       int W, int ks, int stride, int pad, float eps, const float *gpos_x,
-                                      const float *gpos_y, float *dv_x, float *dv_y, float *partials, float *dw,
-                                      uint16_t *dx, uint16_t *dy, void *stream) {
+                                      const float *gpos_y, float *dv_x, float *dv_y, float *partials, uint16_t *dx,
+                                      uint16_t *dy, void *stream) {
     OffArgs a;
     int rc = fill_args(a, x, x_strides, y, y_strides, params_x, params_y, ref, B, G, gc, H, W, ks, stride, pad, eps);
     if (rc) return rc;
-    IRADS_REQUIRE(gpos_x && gpos_y && dv_x && dv_y && partials && dw && dx && dy, "irads_dattn_offset_bwd: null");
-    const long cells = (long)B * G * a.Hk * a.Wk;
+    IRADS_REQUIRE(gpos_x && gpos_y && dv_x && dv_y && partials && dx && dy, "irads_dattn_offset_bwd: null");
+    IRADS_REQUIRE(a.Wk <= 64, "irads_dattn_offset_bwd: %d key cells per row > 64", a.Wk);
     hipStream_t st = (hipStream_t)stream;
-    if (gc <= 16) {
-        dim3 grid((unsigned)((cells + 15) / 16), 2);
-        IRADS_OFF_KS(ks, hipLaunchKernelGGL((offset_bwd_cell_kernel<16, KS>), grid, dim3(256), 0, st, a, gpos_x,
-                                            gpos_y, dv_x, dv_y, partials));
-    } else {
-        dim3 grid((unsigned)((cells + 7) / 8), 2);
-        IRADS_OFF_KS(ks, hipLaunchKernelGGL((offset_bwd_cell_kernel<32, KS>), grid, dim3(256), 0, st, a, gpos_x,
-                                            gpos_y, dv_x, dv_y, partials));
-    }
+    const long nblk = (long)B * G * a.Hk;
+    float *wpart = partials + 2 * nblk * 5 * gc;
+    IRADS_OFF_LAUNCH(offset_bwd_cell_kernel, gpos_x, gpos_y, dv_x, dv_y, partials, wpart);
     rc = check_launch("irads_dattn_offset_bwd cells");
-    if (rc) return rc;
-    IRADS_OFF_KS(ks, hipLaunchKernelGGL((offset_bwd_weight_kernel<KS>), dim3(gc, KS, 2), dim3(256), 0, st, a, dv_x,
-                                        dv_y, dw));
-    rc = check_launch("irads_dattn_offset_bwd weight");
     if (rc) return rc;
     const long total = (long)B * G * H * W * gc;
     IRADS_OFF_KS(ks, hipLaunchKernelGGL((offset_bwd_input_kernel<KS>), dim3((unsigned)((total + 255) / 256), 2),

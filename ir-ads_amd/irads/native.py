@@ -46,7 +46,7 @@ SIGNATURES = {
     "irads_relu_dropout_bwd": [_vp, _vp, _vp, _l, _f, _vp],
     "irads_wgrad_batched": [_i, _vp, _i, _i, _i, _f, _i, _vp, _vp],
     "irads_dattn_offset_fwd": [_vp] * 7 + [_i] * 8 + [_f] + [_vp] * 3,
-    "irads_dattn_offset_bwd": [_vp] * 7 + [_i] * 8 + [_f] + [_vp] * 9,
+    "irads_dattn_offset_bwd": [_vp] * 7 + [_i] * 8 + [_f] + [_vp] * 8,
     "irads_adapter_down": [_i, _vp, _vp, _vp, _vp, _vp, _vp, _l, _l, _i, _i, _f, _u64, _u64, _vp, _vp, _vp],
     "irads_adapter_up": [_vp, _vp, _vp, _vp, _vp, _l, _l, _i, _i, _vp, _vp],
     "irads_upsample_sum_fwd": [_i, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _vp, _vp],

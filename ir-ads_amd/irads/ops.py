@@ -291,14 +291,14 @@ class DAttnOffsetFn(torch.autograd.Function):
         dv = torch.empty((2, cells * gc), device=dev, dtype=torch.float32)
         parts = torch.empty((N.load().irads_dattn_offset_partials(B, G, gc, H, W, ks, stride, pad),), device=dev,
                             dtype=torch.float32)
-        dw = torch.empty((2, gc, 1, ks, ks), device=dev, dtype=torch.float32)
         dx = torch.empty_strided(x.shape, x.stride(), device=dev, dtype=x.dtype)
         dy = torch.empty_strided(y.shape, y.stride(), device=dev, dtype=y.dtype)
         N.call("irads_dattn_offset_bwd", N.ptr(x), _stride_array(x), N.ptr(y), _stride_array(y),
                _ptr_array(params[:5]), _ptr_array(params[5:]), N.ptr(ref), B, G, gc, H, W, ks, stride, pad, eps,
-               N.ptr(gpx), N.ptr(gpy), N.ptr(dv[0]), N.ptr(dv[1]), N.ptr(parts), N.ptr(dw), N.ptr(dx), N.ptr(dy),
-               N.stream())
-        ps = parts.view(2, -1, 5, gc).sum(1)  # (m, [1x1 w row 0, row 1, LN w, LN b, conv b], gc)
+               N.ptr(gpx), N.ptr(gpy), N.ptr(dv[0]), N.ptr(dv[1]), N.ptr(parts), N.ptr(dx), N.ptr(dy), N.stream())
+        nblk = B * G * Hk
+        ps = parts[:2 * nblk * 5 * gc].view(2, nblk, 5, gc).sum(1)  # (m, [1x1 w row 0, row 1, LN w, LN b, b], gc)
+        dw = parts[2 * nblk * 5 * gc:].view(2, nblk, gc, ks * ks).sum(1).view(2, gc, 1, ks, ks)
         grads = []
         for m in (0, 1):
             grads += [dw[m], ps[m, 4], ps[m, 2], ps[m, 3], ps[m, 0:2].reshape(2, gc, 1, 1)]
