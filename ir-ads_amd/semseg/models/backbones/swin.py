@@ -396,8 +396,53 @@ class DAttentionMM(nn.Module):
         gx = torch.arange(0, W, dtype=dtype, device=device).div(W - 1.0).mul(2.0).sub(1.0)
         return gy, gx
 
+    @staticmethod
+    def _tok_linear(conv, x_tok):
+        """1x1 nn.Conv2d on token-major input (..., Cin) as a Linear: one bf16 GEMM under
+        autocast with the bias in its epilogue, no NCHW <-> NHWC transposes; the weight
+        gradient (K = every token of the batch) on the split-K irads_wgrad kernel."""
+        return ops.linear(x_tok, conv.weight.view(conv.out_channels, conv.in_channels), conv.bias)
+
+    def _forward_amp(self, x, y):
+        """bf16-autocast forward: the reference's 1x1 convolutions as token-major GEMMs, the
+        offset networks and sampling / attention cores as HIP kernels, q cast to fp32 once
+        for both.  Same values as the module path up to GEMM summation order."""
+        B, C, H, W = x.size()
+        g = self.n_groups
+        dtype, device = x.dtype, x.device
+        xy = self.fuse_q(torch.cat([x, y], dim=1))
+        q_tok = self._tok_linear(self.proj_q, xy.flatten(2).transpose(1, 2))  # (B, HW, C) bf16
+        q32 = q_tok.transpose(1, 2).to(torch.float32, memory_format=torch.contiguous_format)  # (B, C, HW)
+        conv = self.conv_offset_x[0]
+        Hk = (H + 2 * conv.padding[0] - conv.kernel_size[0]) // conv.stride[0] + 1
+        Wk = (W + 2 * conv.padding[1] - conv.kernel_size[1]) // conv.stride[1] + 1
+        ref = self._get_ref_points(Hk, Wk, 1, dtype, device)[0].reshape(Hk * Wk, 2)
+        pos_x, pos_y = ops.dattn_offsets(x, y, self.conv_offset_x, self.conv_offset_y, g, ref)
+        n = Hk * Wk
+        xs, ys, qs = ops.DAttnSampleFn.apply(x.float(), y.float(), q32.view(B, C, H, W), pos_x, pos_y, g)
+        # get_sample_weight + softmax over the two modalities, token-major: (B, 2n, 2)
+        sw = self.get_sample_weight
+        w = F.softmax(self._tok_linear(sw[2], sw[1](self._tok_linear(sw[0], qs.transpose(1, 2)))), dim=-1)
+        sampled = xs * w[..., 0].unsqueeze(1) + ys * w[..., 1].unsqueeze(1)  # (B, C, 2n) fp32
+        s_tok = sampled.transpose(1, 2)
+        nH, hc = self.n_heads, self.n_head_channels
+
+        def key_major(conv_):  # (B, 2n, C) bf16 -> (B*nH, 2n, hc) fp32, viewed as (B*nH, hc, 2n)
+            t = self._tok_linear(conv_, s_tok).view(B, 2 * n, nH, hc).permute(0, 2, 1, 3)
+            return t.to(torch.float32, memory_format=torch.contiguous_format).view(B * nH, 2 * n, hc).transpose(1, 2)
+        k, v = key_major(self.proj_k), key_major(self.proj_v)
+        gy, gx = self._q_grid_axes(H, W, dtype, device)
+        out = ops.DAttnAttentionFn.apply(q32.view(B * nH, hc, H * W), k, v, pos_x, pos_y, self.rpe_table.float(),
+                                         gy.float(), gx.float(), B, nH, g, H, W, self.scale)
+        out_tok = self._tok_linear(self.proj_out, out.view(B, C, H * W).transpose(1, 2))  # (B, HW, C) bf16
+        out = out_tok.transpose(1, 2).view(B, C, H, W)  # proj_drop has p == 0 on this path: identity
+        return self.deform_weight[None, :, None, None] * out + self.identity_weight[None, :, None, None] * xy
+
     def forward(self, x, y):
         _require_gpu(x, "DAttentionMM")
+        if (ops.dattn_offset_ok(x, y, self.conv_offset_x) and self.proj_drop.p == 0
+                and all(c.kernel_size == (1, 1) for c in (self.proj_q, self.proj_k, self.proj_v, self.proj_out))):
+            return self._forward_amp(x, y)
         B, C, H, W = x.size()
         g, gc = self.n_groups, self.n_group_channels
         dtype, device = x.dtype, x.device

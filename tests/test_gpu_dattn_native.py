@@ -80,3 +80,50 @@ def test_dattn_offset_kernel_matches_module_path(tag, channels_last):
     for n, a, b in zip(names, g1, g0):
         assert a.shape == b.shape and a.dtype == b.dtype, n
         assert _rel(a, b) < 2e-2, (n, _rel(a, b))
+
+
+@pytest.mark.parametrize("tag", ["s0", "s1", "s2", "s3"])
+def test_dattn_amp_path_matches_module_path(tag):
+    """DAttentionMM under bf16 autocast: the token-major fast path (1x1 convs as GEMMs, offset
+    kernels, one fp32 cast of q) against the module path it replaces (MIOpen convolutions,
+    torch ops), both measured against the same module in fp32 without autocast.  The two bf16
+    paths round every op as autocast does but sum in different orders, so neither equals the
+    other bit for bit; the criterion is that the fast path is as close to fp32 as the module
+    path: error <= 1.5 x the module path's error + 5e-3 (relative L2), on the output and on
+    every gradient.  The offset networks' output layers are zeroed so that positions are the
+    (bf16) reference points in both bf16 paths (the kernels are compared on their own above)."""
+    from irads import ops
+    from semseg.models.backbones import swin
+    dims, stride, g, h, level, H, W, B = CFGS[tag]
+    torch.manual_seed(level + 11)
+    m = swin.DAttentionMM(dims, stride=stride, n_groups=g, n_heads=h, level=level).to(DEV)
+    fill_module(m, seed=17)
+    with torch.no_grad():
+        for net in (m.conv_offset_x, m.conv_offset_y):
+            net[3].weight.zero_()
+    m.train()
+    x = (torch.randn(B, dims, H, W, device=DEV) * 0.7).bfloat16()
+    y = torch.rand(B, dims, H, W, device=DEV).bfloat16()
+    params = [p for _, p in m.named_parameters()]
+    names = ["x", "y"] + [n for n, _ in m.named_parameters()]
+    torch.manual_seed(5)
+    go = torch.randn(B, dims, H, W, device=DEV)
+    orig = ops.dattn_offset_ok
+    res = {}
+    for mode in ("fast", "module", "fp32"):
+        if mode != "fast":
+            ops.dattn_offset_ok = lambda *a, **k: False
+        try:
+            xx = (x.float() if mode == "fp32" else x.clone()).requires_grad_()
+            yy = (y.float() if mode == "fp32" else y.clone()).requires_grad_()
+            with torch.autocast("cuda", dtype=torch.bfloat16, enabled=mode != "fp32"):
+                o = m(xx, yy)
+            grads = torch.autograd.grad(o, [xx, yy] + params, go, allow_unused=True)
+        finally:
+            ops.dattn_offset_ok = orig
+        res[mode] = [o] + list(grads)
+    for n, f, md, r in zip(["out"] + names, res["fast"], res["module"], res["fp32"]):
+        if r is None or r.abs().max() == 0:
+            continue
+        e_fast, e_mod = _rel(f, r), _rel(md, r)
+        assert e_fast <= 1.5 * e_mod + 5e-3, (n, e_fast, e_mod)
