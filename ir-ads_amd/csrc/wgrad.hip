@@ -203,8 +203,8 @@ __global__ __launch_bounds__(256) void wgrad_partial_kernel(WProbs probs, int K,
 
 // sum the per-split partials: out[e] = alpha * sum_s ws[s][e] (+ out[e]), for every problem's
 // weight block and column-sum vectors in one launch (segments by blockIdx).  A workgroup
-// owns 64 consecutive elements (coalesced across lanes); its 4 waves take the splits
-// s = w, w+4, ... and are combined in wave order through LDS: a fixed summation order.
+// owns 64 consecutive elements (coalesced across lanes); its 16 waves take the splits
+// s = w, w+16, ... and are combined in wave order through LDS: a fixed summation order.
 struct Seg {
     const float *ws;
     float *out;
@@ -215,9 +215,10 @@ struct Segs {
     Seg s[3 * kMaxBatch];
     int nseg;
 };
-__global__ __launch_bounds__(256) void wgrad_reduce_kernel(Segs segs, int nsplit, float alpha, int accumulate, int m,
-                                                           int n) {
-    __shared__ float part[4][64];
+constexpr int kRedWaves = 16;  // waves per reduce workgroup: splits s = w, w + 16, ... per wave
+__global__ __launch_bounds__(64 * kRedWaves) void wgrad_reduce_kernel(Segs segs, int nsplit, float alpha,
+                                                                    int accumulate, int m, int n) {
+    __shared__ float part[kRedWaves][64];
     int blk = blockIdx.x;
     Seg sg = segs.s[0];  // segment walk with constant indices (no scratch copy of the argument)
 #pragma unroll
@@ -233,16 +234,18 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(Segs segs, int nsplit
     float acc[4] = {0.f, 0.f, 0.f, 0.f};
     if (e < count) {
         int p = w;
-        for (; p + 12 < nsplit; p += 16) {  // 4 independent loads in flight per lane
+        for (; p + 3 * kRedWaves < nsplit; p += 4 * kRedWaves) {  // 4 independent loads in flight per lane
 #pragma unroll
-            for (int u = 0; u < 4; ++u) acc[u] += sg.ws[(long)(p + 4 * u) * count + e];
+            for (int u = 0; u < 4; ++u) acc[u] += sg.ws[(long)(p + u * kRedWaves) * count + e];
         }
-        for (; p < nsplit; p += 4) acc[0] += sg.ws[(long)p * count + e];
+        for (; p < nsplit; p += kRedWaves) acc[0] += sg.ws[(long)p * count + e];
     }
     part[w][lane] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
     __syncthreads();
     if (w == 0 && e < count) {
-        float t = ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
+        float t = 0.f;
+#pragma unroll
+        for (int i = 0; i < kRedWaves; ++i) t += part[i][lane];  // fixed wave order: deterministic
         t *= alpha;
         long o = e;
         if (sg.transpose) {  // element (i, j) of the m x n result stored at (j, i)
@@ -348,8 +351,8 @@ extern "C" int irads_wgrad_batched(int count, const irads_wgrad_problem *problem
     }
     int blocks = 0;
     for (int i = 0; i < segs.nseg; ++i) blocks += segs.s[i].blocks;
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, segs, (int)nsplit, alpha, accumulate, m,
-                       n);
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(64 * kRedWaves), 0, st, segs, (int)nsplit, alpha,
+                       accumulate, m, n);
     return check_launch("irads_wgrad reduce");
 }
 

@@ -9,6 +9,7 @@ import ctypes
 
 import torch
 
+from . import amp_cache
 from . import native as N
 
 WINDOW = 12
@@ -604,8 +605,14 @@ class LinearFn(torch.autograd.Function):
             xb = torch.empty(shape, device=x.device, dtype=torch.bfloat16)
             xb.copy_(x)
             xb = xb.view(-1, shape[-1])
-        wb = weight.detach().to(torch.bfloat16)
-        bb = None if bias is None else bias.detach().to(torch.bfloat16)
+        wb = amp_cache.lookup(weight)
+        if wb is None:
+            wb = weight.detach().to(torch.bfloat16)
+        bb = None
+        if bias is not None:
+            bb = amp_cache.lookup(bias)
+            if bb is None:
+                bb = bias.detach().to(torch.bfloat16)
         y = torch.nn.functional.linear(xb, wb, bb)
         ctx.save_for_backward(xb, wb)
         ctx.has_bias = bias is not None

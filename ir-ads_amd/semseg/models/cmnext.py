@@ -1,5 +1,7 @@
 """CMNeXt with the two-stream Swin backbone (reference semseg/models/cmnext.py:11-36)."""
-from irads import ops
+import torch
+
+from irads import amp_cache, ops
 from semseg.models.base import BaseModel
 from semseg.models.heads import SegFormerHead
 
@@ -20,6 +22,10 @@ class CMNeXt(BaseModel):
         self.apply(self._init_weights)
 
     def forward(self, x: list):
+        if (self.training and x[0].is_cuda and torch.is_autocast_enabled("cuda")
+                and torch.get_autocast_dtype("cuda") == torch.bfloat16):
+            # all trainable weights cast to bf16 in one pass (irads/amp_cache.py)
+            amp_cache.refresh([p for p in self.parameters() if p.requires_grad])
         y, y_rgb, y_dte = self.backbone(x)
         size = x[0].shape[2:]
         # F.interpolate(..., mode='bilinear', align_corners=False) on the HIP resize kernels
