@@ -234,6 +234,21 @@ int irads_relu_dropout_fwd(const uint16_t *a, uint16_t *r, long n, float p, uint
                            void *stream);
 int irads_relu_dropout_bwd(const uint16_t *r, const uint16_t *dr, uint16_t *da, long n, float p, void *stream);
 
+/* MAPA prompt residual + stream concatenation (MPGBlock.forward, swin.py:1045-1068, and the stage
+ * loop's x_rgb + f_rgb / x_dte + f_dte, :1455-1460):
+ *   out[0:R]  = x_rgb + (x + (x * gamma_rgb + beta_rgb))
+ *   out[R:2R] = x_dte + (x + (x * gamma_dte + beta_dte))       x bf16 (R x C), the rest fp32,
+ * each op an fp32 op rounded on its own.  Backward: grad (2R x C) -> grad_x bf16 =
+ * bf16((g_r + g_r*gamma_rgb) + (g_d + g_d*gamma_dte)) and partials [block][4][C] = (sum g_r*x,
+ * sum g_r, sum g_d*x, sum g_d), irads_mpg_partials(R, C) floats, summed over blocks by the caller.
+ * C a multiple of 8, <= 2048. */
+int irads_mpg_fwd(const uint16_t *x, const float *x_rgb, const float *x_dte, const float *gamma_rgb,
+                  const float *beta_rgb, const float *gamma_dte, const float *beta_dte, long R, int C, float *out,
+                  void *stream);
+int irads_mpg_bwd(const float *grad, const uint16_t *x, const float *gamma_rgb, const float *gamma_dte, long R, int C,
+                  uint16_t *grad_x, float *partials, void *stream);
+long irads_mpg_partials(long R, int C);
+
 /* The two Adapters of a block (MLP_RGB_Adapter / MLP_DTE_Adapter, swin.py:472-502:
  * D_fc2(dropout(ReLU(D_fc1(x)))), D_fc1: C -> R, D_fc2: R -> C) on the rgb+dte row batch:
  * rows [0, Mh) use weights w0 / b0, rows [Mh, M) w1 / b1 (M, Mh multiples of 16, R <= 128).

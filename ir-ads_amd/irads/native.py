@@ -47,6 +47,8 @@ SIGNATURES = {
     "irads_wgrad_batched": [_i, _vp, _i, _i, _i, _f, _i, _vp, _vp],
     "irads_dattn_offset_fwd": [_vp] * 7 + [_i] * 8 + [_f] + [_vp] * 3,
     "irads_dattn_offset_bwd": [_vp] * 7 + [_i] * 8 + [_f] + [_vp] * 8,
+    "irads_mpg_fwd": [_vp] * 7 + [_l, _i, _vp, _vp],
+    "irads_mpg_bwd": [_vp] * 4 + [_l, _i, _vp, _vp, _vp],
     "irads_adapter_down": [_i, _vp, _vp, _vp, _vp, _vp, _vp, _l, _l, _i, _i, _f, _u64, _u64, _vp, _vp, _vp],
     "irads_adapter_up": [_vp, _vp, _vp, _vp, _vp, _l, _l, _i, _i, _vp, _vp],
     "irads_upsample_sum_fwd": [_i, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _vp, _vp],
@@ -56,7 +58,8 @@ SIGNATURES = {
 # entries that do not return an error code: name -> (restype, argtypes)
 QUERIES = {"irads_wgrad_workspace": (ctypes.c_long, [_i, _i, _i]),
            "irads_dattn_offset_partials": (ctypes.c_long, [_i] * 8),
-           "irads_wgrad_batched_workspace": (ctypes.c_long, [_i] * 4)}
+           "irads_wgrad_batched_workspace": (ctypes.c_long, [_i] * 4),
+           "irads_mpg_partials": (ctypes.c_long, [_l, _i])}
 CE_WORKSPACE = 2048
 
 _lib = None

@@ -556,6 +556,45 @@ def wgrad(A, B, D, colsum_a=None, colsum_b=None, alpha=1.0, accumulate=False):
     return D
 
 
+class MPGResidualFn(torch.autograd.Function):
+    """cat[x_rgb + (x + x*g_rgb + b_rgb), x_dte + (x + x*g_dte + b_dte)] (MPGBlock + the stage
+    loop's residual adds + torch.cat, swin.py:1045-1068 / :1455-1460) in one kernel each way."""
+
+    @staticmethod
+    def forward(ctx, x, x_rgb, x_dte, g_rgb, b_rgb, g_dte, b_dte):
+        B, L, C = x_rgb.shape
+        R = B * L
+        xb = N.check(x.contiguous(), "MPG x", torch.bfloat16)
+        xr = N.check(x_rgb.contiguous(), "x_rgb", torch.float32)
+        xd = N.check(x_dte.contiguous(), "x_dte", torch.float32)
+        ps = [N.check(t.detach().contiguous(), "tfts parameter", torch.float32) for t in (g_rgb, b_rgb, g_dte, b_dte)]
+        out = torch.empty((2 * B, L, C), device=x.device, dtype=torch.float32)
+        N.call("irads_mpg_fwd", N.ptr(xb), N.ptr(xr), N.ptr(xd), *[N.ptr(t) for t in ps], R, C, N.ptr(out),
+               N.stream())
+        ctx.save_for_backward(xb, ps[0], ps[2])
+        ctx.cfg = (B, L, C)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        xb, g_rgb, g_dte = ctx.saved_tensors
+        B, L, C = ctx.cfg
+        R = B * L
+        g = g.contiguous().float()
+        gx = torch.empty_like(xb)
+        parts = torch.empty((N.load().irads_mpg_partials(R, C),), device=g.device, dtype=torch.float32)
+        N.call("irads_mpg_bwd", N.ptr(g), N.ptr(xb), N.ptr(g_rgb), N.ptr(g_dte), R, C, N.ptr(gx), N.ptr(parts),
+               N.stream())
+        s = parts.view(-1, 4, C).sum(0)
+        return gx, g[:B], g[B:], s[0], s[1], s[2], s[3]
+
+
+def mpg_residual_ok(x, x_rgb, x_dte):
+    return (x.is_cuda and x.dtype == torch.bfloat16 and x_rgb.dtype == torch.float32
+            and x_dte.dtype == torch.float32 and x_rgb.shape == x_dte.shape == x.shape and x.shape[-1] % 8 == 0
+            and x.shape[-1] <= 2048)
+
+
 class _WgradProblem(ctypes.Structure):
     _fields_ = [("A", ctypes.c_void_p), ("lda", ctypes.c_long), ("B", ctypes.c_void_p), ("ldb", ctypes.c_long),
                 ("D", ctypes.c_void_p), ("colsum_a", ctypes.c_void_p), ("colsum_b", ctypes.c_void_p),

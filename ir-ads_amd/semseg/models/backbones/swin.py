@@ -514,6 +514,18 @@ class MPGBlock(nn.Module):
         p_dte = apply_tfts(x, self.tfts_gamma_dte, self.tfts_beta_dte)
         return x + p_rgb, x + p_dte
 
+    def residual_cat(self, x_rgb, x_dte, H, W):
+        """torch.cat([x_rgb + f_rgb, x_dte + f_dte], 0) with (f_rgb, f_dte) = forward(...): the
+        stage input of the batched streams.  Under bf16 autocast the prompt arithmetic, the
+        residual adds and the concatenation are one HIP kernel (irads_mpg_fwd/bwd)."""
+        x = self.U_fc1(self.P_fc2(torch.cat([self.D_fc1(x_rgb), self.D_fc2(x_dte)], dim=-1)))
+        if ops.mpg_residual_ok(x, x_rgb, x_dte):
+            return ops.MPGResidualFn.apply(x, x_rgb, x_dte, self.tfts_gamma_rgb, self.tfts_beta_rgb,
+                                           self.tfts_gamma_dte, self.tfts_beta_dte)
+        p_rgb = apply_tfts(x, self.tfts_gamma_rgb, self.tfts_beta_rgb)
+        p_dte = apply_tfts(x, self.tfts_gamma_dte, self.tfts_beta_dte)
+        return torch.cat([x_rgb + (x + p_rgb), x_dte + (x + p_dte)], 0)
+
 
 class DeformMPGBlock(nn.Module):
     """DSCF fusion (reference swin.py:1071-1091)."""
@@ -687,15 +699,16 @@ class SwinTransformer(nn.Module):
         outs, outs_rgb, outs_dte = [], [], []
         B = x_rgb.shape[0]
         for i, stage in enumerate(self.stages):
-            f_rgb, f_dte = self.MPGBlocks[i](x_rgb, x_dte, hw_rgb[0], hw_rgb[1])
-            x_rgb = x_rgb + f_rgb
-            x_dte = x_dte + f_dte
             if self.batch_streams and hw_rgb == hw_dte:
-                xd, hw_d, xo, out_hw = stage.forward_pair(torch.cat([x_rgb, x_dte], 0), hw_rgb, B)
+                xcat = self.MPGBlocks[i].residual_cat(x_rgb, x_dte, hw_rgb[0], hw_rgb[1])
+                xd, hw_d, xo, out_hw = stage.forward_pair(xcat, hw_rgb, B)
                 x_rgb, x_dte = xd[:B], xd[B:]
                 x_rgb_out, x_dte_out = xo[:B], xo[B:]
                 hw_rgb = hw_dte = hw_d
             else:
+                f_rgb, f_dte = self.MPGBlocks[i](x_rgb, x_dte, hw_rgb[0], hw_rgb[1])
+                x_rgb = x_rgb + f_rgb
+                x_dte = x_dte + f_dte
                 x_rgb, hw_rgb, x_rgb_out, out_hw = stage(x_rgb, hw_rgb, sub_mode='rgb')
                 x_dte, hw_dte, x_dte_out, out_hw = stage(x_dte, hw_dte, sub_mode='dte')
             if i in self.out_indices:

@@ -389,3 +389,38 @@ def test_wgrad_batched_matches_single():
             torch.testing.assert_close(sa, ca, rtol=1e-5, atol=1e-3)
         if sb is not None:
             torch.testing.assert_close(sb, cb, rtol=1e-5, atol=1e-3)
+
+
+@pytest.mark.parametrize("C,L", [(128, 4096), (256, 1024), (512, 256), (1024, 64), (192, 300)])
+def test_mpg_residual_matches_module_math(C, L):
+    """irads_mpg_fwd/bwd against MPGBlock's prompt arithmetic + the stage loop's residual adds
+    + torch.cat under autocast.  Forward: the same fp32 ops in the same order, bit-exact.
+    Backward: dx_rgb / dx_dte are the halves of the incoming gradient (exact); the tfts
+    gradients are fp32 sums in another order (rtol 1e-5); dx is the exact sum rounded to bf16
+    once (one bf16 rounding + the fp32 rounding of its terms, against fp64)."""
+    from irads import ops
+    from semseg.models.backbones.swin import apply_tfts
+    torch.manual_seed(C)
+    B = 2
+    x = (torch.randn(B, L, C, device=DEV)).bfloat16().requires_grad_()
+    xr = torch.randn(B, L, C, device=DEV, requires_grad=True)
+    xd = torch.randn(B, L, C, device=DEV, requires_grad=True)
+    prm = [(torch.randn(C, device=DEV) * 0.1 + (1.0 if i % 2 == 0 else 0.0)).requires_grad_() for i in range(4)]
+    g = torch.randn(2 * B, L, C, device=DEV)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        ref = torch.cat([xr + (x + apply_tfts(x, prm[0], prm[1])), xd + (x + apply_tfts(x, prm[2], prm[3]))], 0)
+        out = ops.MPGResidualFn.apply(x, xr, xd, *prm)
+    assert out.dtype == ref.dtype == torch.float32 and torch.equal(out, ref)
+    g_ref = torch.autograd.grad(ref, [x, xr, xd] + prm, g)
+    g_out = torch.autograd.grad(out, [x, xr, xd] + prm, g)
+    assert torch.equal(g_out[1], g_ref[1]) and torch.equal(g_out[2], g_ref[2])
+    # dx: one rounding of the exact sum (autograd's four bf16-rounded partial terms can be
+    # several ulps off it under cancellation, so the check is against fp64, not against autograd)
+    gd = g.double()
+    exact = (gd[:B] + gd[:B] * prm[0].double() + gd[B:] + gd[B:] * prm[2].double())
+    # one bf16 rounding of the result + the fp32 rounding of the four terms it sums
+    terms = gd[:B].abs() * (1 + prm[0].double().abs()) + gd[B:].abs() * (1 + prm[2].double().abs())
+    tol = torch.finfo(torch.bfloat16).eps * exact.abs() + 4 * torch.finfo(torch.float32).eps * terms
+    assert ((g_out[0].double() - exact).abs() <= tol).all()
+    for a, b in zip(g_out[3:], g_ref[3:]):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-3)
