@@ -297,6 +297,23 @@ int irads_wgrad(const uint16_t *A, long lda, const uint16_t *B, long ldb, int K,
                 int accumulate, int transpose_out, float *D, float *colsum_a, float *colsum_b, float *workspace,
                 void *stream);
 
+/* SegFormer head tail in training mode (segformer.py:22-48: ConvModule BatchNorm2d (batch
+ * statistics) + ReLU, then Dropout2d) on the fused map held token-major: x (M x E) bf16, M =
+ * B * rows_per_sample.  irads_bnact_stats: per-block partials [block][2][E] of sum (x - x[0]) and
+ * sum (x - x[0])^2 (irads_bnact_partials(M, E) floats; the caller adds them and forms the batch
+ * mean / biased variance).  irads_bnact_fwd: y = bf16(mask[b][c] * bf16(relu(bf16((x - mean) *
+ * invstd * weight + bias)))), mask (B x E) bf16 or NULL.  irads_bnact_bwd pass 1 (partials !=
+ * NULL): partials [block][2][E] of sum d and sum d * xhat with d = relu'(bn) * bf16(dy * mask);
+ * pass 2 (dx != NULL): dx = bf16(weight * invstd * (d - mean_d - xhat * mean_dxhat)).
+ * E a multiple of 8, <= 2048. */
+int irads_bnact_stats(const uint16_t *x, long M, int E, float *partials, void *stream);
+int irads_bnact_fwd(const uint16_t *x, long M, int E, long rows_per_sample, const float *mean, const float *invstd,
+                    const float *weight, const float *bias, const uint16_t *mask, uint16_t *y, void *stream);
+int irads_bnact_bwd(const uint16_t *dy, const uint16_t *x, long M, int E, long rows_per_sample, const float *mean,
+                    const float *invstd, const float *weight, const float *bias, const uint16_t *mask,
+                    float *partials, const float *mean_d, const float *mean_dxhat, uint16_t *dx, void *stream);
+long irads_bnact_partials(long M, int E);
+
 /* Metrics.update (semseg/metrics.py:58-69): hist ((C+1) x C int64, accumulated) += the
  * confusion of target (row; C = valid targets outside [0, C)) and arg-max over the C scores
  * (column; first maximum, NaN maximal as torch.argmax), over pixels whose target !=

@@ -1,0 +1,248 @@
+// SegFormer head tail (reference semseg/models/heads/segformer.py:22-48: ConvModule's BatchNorm2d
+// in training mode + ReLU, then Dropout2d(0.1)) on the fused map z (B, E, H, W) held token-major
+// (M = B*H*W rows of E bf16 channels, channels-last).  The reference runs MIOpen BN (statistics
+// pass, normalise pass), an in-place ReLU and a broadcast multiply, and as many passes backward;
+// here:
+//   bnact_stats  per-channel shifted sums  S1 = sum (x - s), S2 = sum (x - s)^2  (s = row 0), as
+//                per-block partials the host adds (fixed order) -> batch mean / biased variance
+//   bnact_fwd    y = bf16(dropmask[b, c] * bf16(relu(bf16((x - mean) * invstd * w + b))))
+//   bnact_bwd1   d = relu'(y) * bf16(dy * dropmask)   ->  partials of sum d, sum d * xhat
+//   bnact_bwd2   dx = bf16(w * invstd * (d - mean(d) - xhat * mean(d * xhat)))
+// The normalised value, ReLU mask and dropout mask are recomputed in the backward passes from x
+// and the statistics (nothing of size M x E is saved).  Rounding is autocast's op by op: the BN
+// output, the ReLU and the dropout product are each bf16 (the reference's bf16 tensors).
+#include "common.h"
+
+namespace irads {
+namespace {
+
+typedef unsigned short u16;
+typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+
+__device__ __forceinline__ void unpack8(u32x4 w, float *f) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        f[2 * i] = __uint_as_float(w[i] << 16);
+        f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+    }
+}
+__device__ __forceinline__ u32x4 pack8(const float *f) {
+    u32x4 w;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w[i] = (unsigned)f2bf(f[2 * i]) | ((unsigned)f2bf(f[2 * i + 1]) << 16);
+    return w;
+}
+__device__ __forceinline__ float rbf(float v) { return bf2f(f2bf(v)); }
+
+// thread = 8 consecutive channels of a row; rpi = 256 / (E/8) rows per block iteration
+struct Lay {
+    int groups, rpi, cg, rl, c0;
+    bool act;
+};
+__device__ __forceinline__ Lay lay(int E) {
+    Lay l;
+    l.groups = E / 8;
+    l.rpi = 256 / l.groups;
+    l.cg = threadIdx.x % l.groups;
+    l.rl = threadIdx.x / l.groups;
+    l.c0 = l.cg * 8;
+    l.act = l.rl < l.rpi;
+    return l;
+}
+
+// fixed-order sum of per-thread [Q][8] accumulators over the block's row lanes -> part[blk][Q][E]
+template <int Q>
+__device__ __forceinline__ void block_partials(const Lay &l, float (&s)[Q][8], float *red, float *part, int E) {
+    for (int j = 0; j < 8; ++j) {
+#pragma unroll
+        for (int q = 0; q < Q; ++q) red[q * 256 + threadIdx.x] = s[q][j];
+        __syncthreads();
+        for (int qc = threadIdx.x; qc < Q * l.groups; qc += blockDim.x) {
+            const int q = qc / l.groups, cc = qc % l.groups;
+            float t = 0.f;
+            for (int i = 0; i < l.rpi; ++i) t += red[q * 256 + i * l.groups + cc];
+            part[((long)blockIdx.x * Q + q) * E + cc * 8 + j] = t;
+        }
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(256) void bnact_stats_kernel(const u16 *__restrict__ x, long M, int E,
+                                                          float *__restrict__ part) {
+    __shared__ float red[2 * 256];
+    const Lay l = lay(E);
+    float s[2][8], sh[8];
+    unpack8(*reinterpret_cast<const u32x4 *>(x + (l.act ? l.c0 : 0)), sh);  // shift: row 0
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s[0][j] = s[1][j] = 0.f;
+    if (l.act) {
+        for (long r = (long)blockIdx.x * l.rpi + l.rl; r < M; r += (long)gridDim.x * l.rpi) {
+            float v[8];
+            unpack8(*reinterpret_cast<const u32x4 *>(x + r * E + l.c0), v);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float d = v[j] - sh[j];
+                s[0][j] += d;
+                s[1][j] += d * d;
+            }
+        }
+    }
+    block_partials<2>(l, s, red, part, E);
+}
+
+// per-channel affine of the BN output: v = (x - mean) * invstd * w + b
+struct Chan {
+    float mean[8], inv[8], w[8], b[8];
+};
+__device__ __forceinline__ void load_chan(const float *mean, const float *invstd, const float *w, const float *b, int c0,
+                                          Chan &ch) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        ch.mean[j] = mean[c0 + j];
+        ch.inv[j] = invstd[c0 + j];
+        ch.w[j] = w[c0 + j];
+        ch.b[j] = b[c0 + j];
+    }
+}
+
+__global__ __launch_bounds__(256) void bnact_fwd_kernel(const u16 *__restrict__ x, long M, int E, long rps,
+                                                        const float *__restrict__ mean, const float *__restrict__ invstd,
+                                                        const float *__restrict__ w, const float *__restrict__ b,
+                                                        const u16 *__restrict__ mask, u16 *__restrict__ y) {
+    const Lay l = lay(E);
+    if (!l.act) return;
+    Chan ch;
+    load_chan(mean, invstd, w, b, l.c0, ch);
+    for (long r = (long)blockIdx.x * l.rpi + l.rl; r < M; r += (long)gridDim.x * l.rpi) {
+        float v[8], mk[8] = {1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f};
+        unpack8(*reinterpret_cast<const u32x4 *>(x + r * E + l.c0), v);
+        if (mask) unpack8(*reinterpret_cast<const u32x4 *>(mask + (r / rps) * E + l.c0), mk);
+        float o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const float bn = rbf((v[j] - ch.mean[j]) * ch.inv[j] * ch.w[j] + ch.b[j]);
+            const float re = bn > 0.f ? bn : 0.f;
+            o[j] = re * mk[j];  // rounded by pack8
+        }
+        *reinterpret_cast<u32x4 *>(y + r * E + l.c0) = pack8(o);
+    }
+}
+
+// d = relu'(bn) * bf16(dy * mask); partials (sum d, sum d * xhat)
+__global__ __launch_bounds__(256) void bnact_bwd1_kernel(const u16 *__restrict__ dy, const u16 *__restrict__ x,
+                                                         long M, int E, long rps, const float *__restrict__ mean,
+                                                         const float *__restrict__ invstd,
+                                                         const float *__restrict__ w, const float *__restrict__ b,
+                                                         const u16 *__restrict__ mask, float *__restrict__ part) {
+    __shared__ float red[2 * 256];
+    const Lay l = lay(E);
+    Chan ch;
+    float s[2][8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s[0][j] = s[1][j] = 0.f;
+    if (l.act) {
+        load_chan(mean, invstd, w, b, l.c0, ch);
+        for (long r = (long)blockIdx.x * l.rpi + l.rl; r < M; r += (long)gridDim.x * l.rpi) {
+            float v[8], g[8], mk[8] = {1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f};
+            unpack8(*reinterpret_cast<const u32x4 *>(x + r * E + l.c0), v);
+            unpack8(*reinterpret_cast<const u32x4 *>(dy + r * E + l.c0), g);
+            if (mask) unpack8(*reinterpret_cast<const u32x4 *>(mask + (r / rps) * E + l.c0), mk);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float xh = (v[j] - ch.mean[j]) * ch.inv[j];
+                const float bn = rbf(xh * ch.w[j] + ch.b[j]);
+                const float d = bn > 0.f ? rbf(g[j] * mk[j]) : 0.f;
+                s[0][j] += d;
+                s[1][j] += d * xh;
+            }
+        }
+    }
+    block_partials<2>(l, s, red, part, E);
+}
+
+__global__ __launch_bounds__(256) void bnact_bwd2_kernel(const u16 *__restrict__ dy, const u16 *__restrict__ x,
+                                                         long M, int E, long rps, const float *__restrict__ mean,
+                                                         const float *__restrict__ invstd,
+                                                         const float *__restrict__ w, const float *__restrict__ b,
+                                                         const u16 *__restrict__ mask, const float *__restrict__ md,
+                                                         const float *__restrict__ mdx, u16 *__restrict__ dx) {
+    const Lay l = lay(E);
+    if (!l.act) return;
+    Chan ch;
+    load_chan(mean, invstd, w, b, l.c0, ch);
+    float a[8], c1[8], c2[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        a[j] = ch.w[j] * ch.inv[j];
+        c1[j] = md[l.c0 + j];
+        c2[j] = mdx[l.c0 + j];
+    }
+    for (long r = (long)blockIdx.x * l.rpi + l.rl; r < M; r += (long)gridDim.x * l.rpi) {
+        float v[8], g[8], mk[8] = {1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f}, o[8];
+        unpack8(*reinterpret_cast<const u32x4 *>(x + r * E + l.c0), v);
+        unpack8(*reinterpret_cast<const u32x4 *>(dy + r * E + l.c0), g);
+        if (mask) unpack8(*reinterpret_cast<const u32x4 *>(mask + (r / rps) * E + l.c0), mk);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const float xh = (v[j] - ch.mean[j]) * ch.inv[j];
+            const float bn = rbf(xh * ch.w[j] + ch.b[j]);
+            const float d = bn > 0.f ? rbf(g[j] * mk[j]) : 0.f;
+            o[j] = a[j] * (d - c1[j] - xh * c2[j]);
+        }
+        *reinterpret_cast<u32x4 *>(dx + r * E + l.c0) = pack8(o);
+    }
+}
+
+int bn_blocks(long M, int E) {
+    const int rpi = 256 / (E / 8);
+    const long b = (M + rpi - 1) / rpi;
+    return (int)(b < 1024 ? b : 1024);
+}
+
+}  // namespace
+}  // namespace irads
+
+using namespace irads;
+
+#define IRADS_BN_CHECK(fn)                                                                                        \
+    IRADS_REQUIRE(M > 1 && E >= 8 && E % 8 == 0 && E <= 2048, fn ": need M > 1 and E a multiple of 8 in [8, 2048] " \
+                                                               "(M=%ld E=%d)", M, E)
+
+extern "C" long irads_bnact_partials(long M, int E) { return (long)bn_blocks(M, E) * 2 * E; }
+
+extern "C" int irads_bnact_stats(const uint16_t *x, long M, int E, float *partials, void *stream) {
+    IRADS_BN_CHECK("irads_bnact_stats");
+    IRADS_REQUIRE(x && partials, "irads_bnact_stats: null pointer");
+    hipLaunchKernelGGL(bnact_stats_kernel, dim3(bn_blocks(M, E)), dim3(256), 0, (hipStream_t)stream, x, M, E,
+                       partials);
+    return check_launch("irads_bnact_stats");
+}
+
+extern "C" int irads_bnact_fwd(const uint16_t *x, long M, int E, long rows_per_sample, const float *mean,
+                               const float *invstd, const float *weight, const float *bias, const uint16_t *mask,
+                               uint16_t *y, void *stream) {
+    IRADS_BN_CHECK("irads_bnact_fwd");
+    IRADS_REQUIRE(x && mean && invstd && weight && bias && y && rows_per_sample > 0, "irads_bnact_fwd: bad argument");
+    hipLaunchKernelGGL(bnact_fwd_kernel, dim3(bn_blocks(M, E)), dim3(256), 0, (hipStream_t)stream, x, M, E,
+                       rows_per_sample, mean, invstd, weight, bias, mask, y);
+    return check_launch("irads_bnact_fwd");
+}
+
+extern "C" int irads_bnact_bwd(const uint16_t *dy, const uint16_t *x, long M, int E, long rows_per_sample,
+                               const float *mean, const float *invstd, const float *weight, const float *bias,
+                               const uint16_t *mask, float *partials, const float *mean_d, const float *mean_dxhat,
+                               uint16_t *dx, void *stream) {
+    IRADS_BN_CHECK("irads_bnact_bwd");
+    IRADS_REQUIRE(dy && x && mean && invstd && weight && bias && rows_per_sample > 0, "irads_bnact_bwd: bad argument");
+    IRADS_REQUIRE((partials != nullptr) != (dx != nullptr), "irads_bnact_bwd: pass 1 (partials) or pass 2 (dx)");
+    hipStream_t st = (hipStream_t)stream;
+    if (partials) {
+        hipLaunchKernelGGL(bnact_bwd1_kernel, dim3(bn_blocks(M, E)), dim3(256), 0, st, dy, x, M, E, rows_per_sample,
+                           mean, invstd, weight, bias, mask, partials);
+        return check_launch("irads_bnact_bwd pass 1");
+    }
+    IRADS_REQUIRE(mean_d && mean_dxhat, "irads_bnact_bwd: pass 2 needs mean_d, mean_dxhat");
+    hipLaunchKernelGGL(bnact_bwd2_kernel, dim3(bn_blocks(M, E)), dim3(256), 0, st, dy, x, M, E, rows_per_sample, mean,
+                       invstd, weight, bias, mask, mean_d, mean_dxhat, dx);
+    return check_launch("irads_bnact_bwd pass 2");
+}

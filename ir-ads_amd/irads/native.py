@@ -47,6 +47,9 @@ SIGNATURES = {
     "irads_wgrad_batched": [_i, _vp, _i, _i, _i, _f, _i, _vp, _vp],
     "irads_dattn_offset_fwd": [_vp] * 7 + [_i] * 8 + [_f] + [_vp] * 3,
     "irads_dattn_offset_bwd": [_vp] * 7 + [_i] * 8 + [_f] + [_vp] * 8,
+    "irads_bnact_stats": [_vp, _l, _i, _vp, _vp],
+    "irads_bnact_fwd": [_vp, _l, _i, _l] + [_vp] * 7,
+    "irads_bnact_bwd": [_vp, _vp, _l, _i, _l] + [_vp] * 10,
     "irads_mpg_fwd": [_vp] * 7 + [_l, _i, _vp, _vp],
     "irads_mpg_bwd": [_vp] * 4 + [_l, _i, _vp, _vp, _vp],
     "irads_adapter_down": [_i, _vp, _vp, _vp, _vp, _vp, _vp, _l, _l, _i, _i, _f, _u64, _u64, _vp, _vp, _vp],
@@ -59,7 +62,8 @@ SIGNATURES = {
 QUERIES = {"irads_wgrad_workspace": (ctypes.c_long, [_i, _i, _i]),
            "irads_dattn_offset_partials": (ctypes.c_long, [_i] * 8),
            "irads_wgrad_batched_workspace": (ctypes.c_long, [_i] * 4),
-           "irads_mpg_partials": (ctypes.c_long, [_l, _i])}
+           "irads_mpg_partials": (ctypes.c_long, [_l, _i]),
+           "irads_bnact_partials": (ctypes.c_long, [_l, _i])}
 CE_WORKSPACE = 2048
 
 _lib = None

@@ -556,6 +556,71 @@ def wgrad(A, B, D, colsum_a=None, colsum_b=None, alpha=1.0, accumulate=False):
     return D
 
 
+class BNActFn(torch.autograd.Function):
+    """BatchNorm2d (training: batch statistics, running-stat update) + ReLU + Dropout2d of the
+    SegFormer head (segformer.py:22-48) on token-major bf16 x (B, L, E): irads_bnact_*."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, mask, bn):
+        B, L, E = x.shape
+        M = B * L
+        xb = N.check(x.contiguous(), "head map", torch.bfloat16)
+        w = N.check(weight.detach().contiguous(), "bn weight", torch.float32)
+        b = N.check(bias.detach().contiguous(), "bn bias", torch.float32)
+        n_part = N.load().irads_bnact_partials(M, E)
+        parts = torch.empty((n_part,), device=x.device, dtype=torch.float32)
+        N.call("irads_bnact_stats", N.ptr(xb), M, E, N.ptr(parts), N.stream())
+        s = parts.view(-1, 2, E).sum(0)
+        shift = xb.view(M, E)[0].float()
+        m1 = s[0] / M
+        mean = shift + m1
+        var = (s[1] / M - m1 * m1).clamp_min(0.)
+        invstd = torch.rsqrt(var + bn.eps)
+        if bn.track_running_stats and bn.running_mean is not None:
+            with torch.no_grad():
+                mom = bn.momentum
+                bn.running_mean.mul_(1 - mom).add_(mean, alpha=mom)
+                bn.running_var.mul_(1 - mom).add_(var * (M / (M - 1)), alpha=mom)
+                bn.num_batches_tracked.add_(1)
+        y = torch.empty_like(xb)
+        N.call("irads_bnact_fwd", N.ptr(xb), M, E, L, N.ptr(mean), N.ptr(invstd), N.ptr(w), N.ptr(b), N.ptr(mask),
+               N.ptr(y), N.stream())
+        ctx.save_for_backward(xb, mean, invstd, w, b, mask)
+        ctx.cfg = (B, L, E)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        xb, mean, invstd, w, b, mask = ctx.saved_tensors
+        B, L, E = ctx.cfg
+        M = B * L
+        g = gy.contiguous().to(torch.bfloat16)
+        parts = torch.empty((N.load().irads_bnact_partials(M, E),), device=g.device, dtype=torch.float32)
+        N.call("irads_bnact_bwd", N.ptr(g), N.ptr(xb), M, E, L, N.ptr(mean), N.ptr(invstd), N.ptr(w), N.ptr(b),
+               N.ptr(mask), N.ptr(parts), None, None, None, N.stream())
+        s = parts.view(-1, 2, E).sum(0)  # (sum d, sum d * xhat)
+        md, mdx = s[0] / M, s[1] / M
+        dx = torch.empty_like(xb)
+        N.call("irads_bnact_bwd", N.ptr(g), N.ptr(xb), M, E, L, N.ptr(mean), N.ptr(invstd), N.ptr(w), N.ptr(b),
+               N.ptr(mask), None, N.ptr(md), N.ptr(mdx), N.ptr(dx), N.stream())
+        return dx, s[1], s[0], None, None
+
+
+def bn_relu_dropout2d(x, bn, p):
+    """Training-mode BatchNorm2d + ReLU + Dropout2d(p) of token-major bf16 x (B, L, E)."""
+    B, L, E = x.shape
+    mask = None
+    if p > 0:
+        mask = torch.empty((B, E), device=x.device, dtype=torch.bfloat16).bernoulli_(1 - p).div_(1 - p)
+    return BNActFn.apply(x, bn.weight, bn.bias, mask, bn)
+
+
+def bnact_ok(x_tok, bn):
+    return (x_tok.is_cuda and x_tok.dtype == torch.bfloat16 and bn.training and bn.affine
+            and bn.momentum is not None and x_tok.shape[-1] % 8 == 0 and x_tok.shape[-1] <= 2048
+            and x_tok.shape[0] * x_tok.shape[1] > 1)
+
+
 class MPGResidualFn(torch.autograd.Function):
     """cat[x_rgb + (x + x*g_rgb + b_rgb), x_dte + (x + x*g_dte + b_dte)] (MPGBlock + the stage
     loop's residual adds + torch.cat, swin.py:1045-1068 / :1455-1460) in one kernel each way."""

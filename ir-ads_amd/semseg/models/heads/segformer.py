@@ -62,5 +62,14 @@ class SegFormerHead(nn.Module):
             z = ops.linear(f.flatten(2).transpose(1, 2), A, c)  # (B, h*w, E)
             zs.append(z.transpose(1, 2).reshape(B, E, *f.shape[-2:]))  # channels-last (B, E, h, w) view
         seg = ops.upsample_sum(zs[0], zs[1:])
+        if self.training and seg.dtype == torch.bfloat16 and seg.is_cuda:
+            tok = seg.permute(0, 2, 3, 1).reshape(B, H * W, E)  # channels-last memory: a view
+            if ops.bnact_ok(tok, self.linear_fuse.bn):
+                # BN (batch statistics) + ReLU + Dropout2d in one pass each way (csrc/bnact.hip),
+                # then linear_pred as a token-major Linear: logits stay channels-last
+                z = ops.bn_relu_dropout2d(tok, self.linear_fuse.bn, self.dropout.p)
+                pred = self.linear_pred
+                out = ops.linear(z, pred.weight.view(pred.out_channels, E), pred.bias)
+                return out.view(B, H, W, -1).permute(0, 3, 1, 2)
         seg = self.linear_fuse.activate(self.linear_fuse.bn(seg))
         return self.linear_pred(self.dropout(seg))

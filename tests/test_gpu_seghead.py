@@ -205,3 +205,74 @@ def test_mmst_full_size_c2_bf16():
     for i in range(3):
         scale = float(xd[i].grad.abs().max())
         close(xg[i].grad.float(), xd[i].grad, 1e-3 * scale, 2 ** -7, f"MMST C2 grad head {i}")
+
+
+@pytest.mark.parametrize("E", [256, 512])
+def test_head_bnact_tail_matches_module_path(E):
+    """SegFormerHead in training mode under bf16 autocast: the fused BN (batch statistics) +
+    ReLU + Dropout2d kernels + token-major linear_pred against the module path (nn.BatchNorm2d
+    on MIOpen, in-place ReLU, Dropout2d, 1x1 Conv2d).  With Dropout2d at p = 0 the two are the
+    same arithmetic up to the BN normalisation's fp32 formula and GEMM summation order: output
+    and every gradient within relative L2 1e-2 (the MLP biases, whose gradient BatchNorm
+    cancels, only need to be noise-sized), running statistics within 1e-5.  A second pass
+    at p = 0.5 checks the Dropout2d semantics: each (image, channel) of the fused map is either
+    zeroed or scaled by 1 / (1 - p)."""
+    from semseg.models.heads import SegFormerHead
+    from fill import fill_module
+    torch.manual_seed(E)
+    dims = [128, 256, 512, 1024]
+    heads = []
+    for _ in range(2):
+        h = SegFormerHead(dims, E, 40).to(DEV)
+        heads.append(h)
+    fill_module(heads[0], seed=3)
+    heads[1].load_state_dict(heads[0].state_dict())
+    B, sizes = 2, [(64, 64), (32, 32), (16, 16), (8, 8)]
+    feats = [torch.randn(B, c, *hw, device=DEV).contiguous(memory_format=torch.channels_last)
+             for c, hw in zip(dims, sizes)]
+    res = []
+    for k, h in enumerate(heads):
+        h.train()
+        h.dropout.p = 0.0
+        fs = [f.clone().requires_grad_() for f in feats]
+        from irads import ops
+        orig = ops.bnact_ok
+        if k == 1:
+            ops.bnact_ok = lambda *a, **kw: False
+        try:
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                out = h(fs)
+        finally:
+            ops.bnact_ok = orig
+        torch.manual_seed(7)
+        go = torch.randn(out.shape, device=DEV)
+        params = [p for p in h.parameters() if p.requires_grad]
+        grads = torch.autograd.grad(out, fs + params, go)
+        res.append((out, grads, h.linear_fuse.bn.running_mean.clone(), h.linear_fuse.bn.running_var.clone()))
+    (o1, g1, rm1, rv1), (o0, g0, rm0, rv0) = res
+
+    def rel(a, b):
+        return ((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-30)).item()
+    assert o1.shape == o0.shape and rel(o1, o0) < 1e-2
+    names = [f"feat{i}" for i in range(4)] + [n for n, p in heads[0].named_parameters() if p.requires_grad]
+    for n, a, b in zip(names, g1, g0):
+        if n.startswith("linear_c") and n.endswith("proj.bias"):
+            # a per-channel constant ahead of train-mode BatchNorm: the gradient vanishes
+            # analytically and is rounding noise in both paths
+            assert a.abs().max() < 1e-2 * g0[names.index(n[:-4] + "weight")].abs().max() + 1e-3, n
+            continue
+        assert rel(a, b) < 1e-2, (n, rel(a, b))
+    torch.testing.assert_close(rm1, rm0, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(rv1, rv0, rtol=1e-5, atol=1e-5)
+    # Dropout2d semantics on the fused kernels
+    from irads import ops
+    bn = heads[0].linear_fuse.bn
+    x = torch.randn(B, 100, E, device=DEV).bfloat16()
+    with torch.no_grad():
+        torch.manual_seed(1)
+        y0 = ops.bn_relu_dropout2d(x, bn, 0.0).float()
+        y1 = ops.bn_relu_dropout2d(x, bn, 0.5).float()
+    ratio = torch.where(y0 != 0, y1 / y0.where(y0 != 0, torch.ones_like(y0)), torch.zeros_like(y0))
+    per_chan = ratio.abs().amax(1)  # (B, E): 0 (dropped) or 2 (kept)
+    assert ((per_chan == 0) | ((per_chan - 2).abs() < 1e-2)).all()
+    assert 0.2 < (per_chan > 0).float().mean().item() < 0.8
