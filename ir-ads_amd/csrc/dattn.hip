@@ -154,6 +154,82 @@ __global__ void dattn_sample_bwd_kernel(const float *__restrict__ x, const float
     }
 }
 
+// Small maps (the late stages: 16x16 / 32x32 key grids, 512 samples per map) make the global
+// atomics of the kernel above contend on a few hundred addresses.  Here one workgroup owns a
+// whole (b, group) map: the input gradients accumulate in LDS (ds_add_f32) and are written
+// out once; `per_pass` of the three tensors (x, y, q) are accumulated per pass (the launcher
+// uses 3: all in LDS at once), the position gradient stays in registers across passes and is
+// reduced over the GP channel lanes at the end (same accumulation order as the kernel above).
+template <int GP, int SPT, int NT>
+__global__ __launch_bounds__(NT) void dattn_sample_bwd_lds_kernel(
+    const float *__restrict__ x, const float *__restrict__ y, const float *__restrict__ q,
+    const float *__restrict__ px, const float *__restrict__ py, const float *__restrict__ gxs,
+    const float *__restrict__ gys, const float *__restrict__ gqs, int C, int H, int W, int G, int n, int per_pass,
+    float *__restrict__ gx, float *__restrict__ gy, float *__restrict__ gq, float *__restrict__ gpx,
+    float *__restrict__ gpy) {
+    extern __shared__ float acc[];
+    constexpr int SLOTS = NT / GP;
+    const int map = blockIdx.x, b = map / G, gi = map % G, gc = C / G, HW = H * W;
+    const int slot = threadIdx.x / GP, cc = threadIdx.x % GP;
+    const int ns = 2 * n, iters = (ns + SLOTS - 1) / SLOTS;
+    const float *planes[3] = {x, y, q};
+    const float *gouts[3] = {gxs, gys, gqs};
+    float *gins[3] = {gx, gy, gq};
+    float dix[SPT], diy[SPT];
+#pragma unroll
+    for (int it = 0; it < SPT; ++it) dix[it] = diy[it] = 0.f;
+    const long cbase = (long)b * C + gi * gc;  // first channel of this map
+    for (int t0 = 0; t0 < 3; t0 += per_pass) {
+        for (int i = threadIdx.x; i < per_pass * gc * HW; i += NT) acc[i] = 0.f;
+        __syncthreads();
+#pragma unroll
+        for (int it = 0; it < SPT; ++it) {
+            const int j2 = it * SLOTS + slot;
+            if (it >= iters || j2 >= ns || cc >= gc) continue;
+            const int j = j2 % n;
+            const float *pos = (j2 < n ? px : py) + ((long)map * n + j) * 2;
+            const Corner cr = corner_ac(pos[1], pos[0], H, W);
+            const bool xl = cr.x0 >= 0 && cr.x0 < W, xh = cr.x0 + 1 >= 0 && cr.x0 + 1 < W;
+            const bool yl = cr.y0 >= 0 && cr.y0 < H, yh = cr.y0 + 1 >= 0 && cr.y0 + 1 < H;
+            const int o = cr.y0 * W + cr.x0;
+            for (int tt = 0; tt < per_pass; ++tt) {
+                const int t = t0 + tt;
+                const long plane = (cbase + cc) * HW;
+                const float g = gouts[t][(cbase + cc) * ns + j2];
+                dsample(taps(planes[t] + plane, H, W, cr), cr, g, dix[it], diy[it]);
+                float *a = acc + (tt * gc + cc) * HW;
+                if (yl && xl) atomicAdd(a + o, cr.nw * g);
+                if (yl && xh) atomicAdd(a + o + 1, cr.ne * g);
+                if (yh && xl) atomicAdd(a + o + W, cr.sw * g);
+                if (yh && xh) atomicAdd(a + o + W + 1, cr.se * g);
+            }
+        }
+        __syncthreads();
+        for (int i = threadIdx.x; i < per_pass * gc * HW; i += NT) {
+            const int tt = i / (gc * HW), r = i - tt * gc * HW;
+            gins[t0 + tt][cbase * HW + r] = acc[i];
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int it = 0; it < SPT; ++it) {
+        if (it >= iters) continue;  // uniform across the block
+        float dx_ = dix[it], dy_ = diy[it];
+#pragma unroll
+        for (int o = GP / 2; o > 0; o >>= 1) {
+            dx_ += __shfl_xor(dx_, o, GP);
+            dy_ += __shfl_xor(dy_, o, GP);
+        }
+        const int j2 = it * SLOTS + slot;
+        if (cc == 0 && j2 < ns) {
+            const int j = j2 % n;
+            float *gp = (j2 < n ? gpx : gpy) + ((long)map * n + j) * 2;
+            gp[0] = dy_ * (((float)H - 1.0f) / 2.0f);
+            gp[1] = dx_ * (((float)W - 1.0f) / 2.0f);
+        }
+    }
+}
+
 // ---------------------------------------------------------------- fused attention
 struct AttnArgs {
     const float *q, *k, *v, *px, *py, *rpe, *qgy, *qgx;
@@ -667,6 +743,17 @@ extern "C" int irads_dattn_sample_bwd(const float *x, const float *y, const floa
     if (total == 0) return IRADS_OK;
     const unsigned grid = (unsigned)((total + 255) / 256);
     hipStream_t st = (hipStream_t)stream;
+    // small maps: a workgroup per (b, group) map with LDS accumulation (see the kernel)
+    const long plane_bytes = (long)gc * H * W * 4;
+    // (all three tensors' planes in LDS at once; a map too big for that runs faster on the
+    // global-atomic kernel than in three sequential LDS passes - measured at 32x32 x 16 ch)
+    const int per_pass = 3 * plane_bytes <= 64 * 1024 ? 3 : 0;
+    if (per_pass && GP == 16 && (2 * n + 63) / 64 <= 8) {
+        hipLaunchKernelGGL((dattn_sample_bwd_lds_kernel<16, 8, 1024>), dim3(B * G), dim3(1024),
+                           (size_t)per_pass * plane_bytes, st, x, y, q, pos_x, pos_y, gxs, gys, gqs, C, H, W, G, n,
+                           per_pass, grad_x, grad_y, grad_q, grad_pos_x, grad_pos_y);
+        return check_launch("irads_dattn_sample_bwd (LDS)");
+    }
 #define IRADS_SB(P)                                                                                             \
     case P:                                                                                                     \
         dattn_sample_bwd_kernel<P><<<grid, 256, 0, st>>>(x, y, q, pos_x, pos_y, gxs, gys, gqs, B, C, H, W, G, n, \
