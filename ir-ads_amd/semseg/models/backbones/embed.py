@@ -7,6 +7,7 @@ permute copy, and its LayerNorm writes the bf16 operand of `reduction` directly 
 import math
 from typing import Sequence
 
+import torch
 import torch.nn as nn
 import torch.nn.functional as F
 from irads import ops
@@ -73,12 +74,31 @@ class PatchEmbed(nn.Module):
                 (input_size[i] + 2 * padding[i] - dilation[i] * (kernel_size[i] - 1) - 1) // stride[i] + 1
                 for i in range(2))
 
+    def _patchify_ok(self, x):
+        c = self.projection
+        return (x.is_cuda and torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16
+                and c.kernel_size == c.stride and c.padding == (0, 0) and c.dilation == (1, 1) and c.groups == 1
+                and x.shape[2] % c.kernel_size[0] == 0 and x.shape[3] % c.kernel_size[1] == 0)
+
     def forward(self, x):
         if self.adap_padding:
             x = self.adap_padding(x)
-        x = self.projection(x)
-        out_size = (x.shape[2], x.shape[3])
-        x = x.flatten(2).transpose(1, 2)
+        if self._patchify_ok(x):
+            # non-overlapping patches: the convolution is a GEMM over the (c, ky, kx) patch
+            # vectors, gathered and cast in one copy; its output is token-major, so the
+            # LayerNorm reads contiguous rows (no NCHW -> (B, HW, C) transpose)
+            c = self.projection
+            B, Cin, H, W = x.shape
+            kh, kw = c.kernel_size
+            h, w = H // kh, W // kw
+            tok = torch.empty((B, h * w, Cin * kh * kw), device=x.device, dtype=torch.bfloat16)
+            tok.view(B, h, w, Cin, kh, kw).copy_(x.view(B, Cin, h, kh, w, kw).permute(0, 2, 4, 1, 3, 5))
+            x = ops.linear(tok, c.weight.view(c.out_channels, -1), c.bias)
+            out_size = (h, w)
+        else:
+            x = self.projection(x)
+            out_size = (x.shape[2], x.shape[3])
+            x = x.flatten(2).transpose(1, 2)
         if self.norm is not None:
             x = self.norm(x)
         return x, out_size

@@ -147,20 +147,31 @@ def _dp_worker(rank, world, port, q):
 def test_graph_step_gradient_allreduce_gloo():
     """The data-parallel exchange of the graphed step (irads/graph_step.py): pack the
     gradients, all-reduce (sum), unpack scaled by 1/world = DDP's gradient average."""
+    import queue
     import socket
     import torch
     import torch.multiprocessing as mp
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
     ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    procs = [ctx.Process(target=_dp_worker, args=(r, 2, port, q)) for r in range(2)]
-    for p in procs:
-        p.start()
-    res = dict(q.get(timeout=120) for _ in procs)
-    for p in procs:
-        p.join(timeout=60)
+    res = None
+    for attempt in range(3):  # a free port picked here can be taken before the workers bind it
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            port = s.getsockname()[1]
+        q = ctx.Queue()
+        procs = [ctx.Process(target=_dp_worker, args=(r, 2, port, q)) for r in range(2)]
+        for p in procs:
+            p.start()
+        try:
+            res = dict(q.get(timeout=120) for _ in procs)
+        except queue.Empty:
+            res = None
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+        if res is not None and all(p.exitcode == 0 for p in procs):
+            break
+    assert res is not None, "gloo workers did not report"
     for i, shape in enumerate(((3, 4), (5,), (2, 2, 2))):
         base = torch.arange(torch.Size(shape).numel()).view(shape).float()
         want = base * (1.5 if i != 1 else 0.5)  # mean of 1x and 2x (rank 1 lacks grad #1: 0)

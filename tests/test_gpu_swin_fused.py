@@ -424,3 +424,30 @@ def test_mpg_residual_matches_module_math(C, L):
     assert ((g_out[0].double() - exact).abs() <= tol).all()
     for a, b in zip(g_out[3:], g_ref[3:]):
         torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-3)
+
+
+def test_patch_embed_gemm_matches_conv():
+    """PatchEmbed under bf16 autocast: non-overlapping patches as one gather + GEMM (token-major
+    output, contiguous LayerNorm input) against the Conv2d + flatten/transpose path.  Same bf16
+    operands; the conv adds its bias in a second rounding and sums in another order: output and
+    gradients within relative L2 1e-2."""
+    from semseg.models.backbones.embed import PatchEmbed
+    torch.manual_seed(9)
+    pe = PatchEmbed(3, 128, 'Conv2d', 4, 4, 'corner', norm_cfg=dict(type='LN')).to(DEV)
+    fill_module(pe, seed=2)
+    x = torch.randn(2, 3, 64, 96, device=DEV)
+    g = torch.randn(2, 16 * 24, 128, device=DEV)
+    res = []
+    for fast in (True, False):
+        if not fast:
+            pe._patchify_ok = lambda *a, **k: False
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y, hw = pe(x)
+        grads = torch.autograd.grad(y, list(pe.parameters()), g)
+        res.append((y, hw, grads))
+    del pe._patchify_ok
+    (y1, hw1, g1), (y0, hw0, g0) = res
+    assert hw1 == hw0 == (16, 24) and y1.shape == y0.shape and y1.dtype == y0.dtype
+    assert _rel(y1, y0) < 1e-2
+    for a, b in zip(g1, g0):
+        assert _rel(a, b) < 1e-2
