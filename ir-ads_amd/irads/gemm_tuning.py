@@ -13,7 +13,7 @@ import os
 import torch
 
 TUNED_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned")
-TABLE = os.path.join(TUNED_DIR, "tunableop_mi355x0.csv")
+TABLE = os.environ.get("IRADS_GEMM_TABLE", os.path.join(TUNED_DIR, "tunableop_mi355x0.csv"))
 
 
 def use_tuned_gemms(table=TABLE):
