@@ -814,6 +814,64 @@ class LayerNormBF16Fn(torch.autograd.Function):
         return dx.view(ctx.shape).to(ctx.in_dtype), None, None, None
 
 
+class LayerNormPairBF16Fn(torch.autograd.Function):
+    """Two LayerNorms (own weights) on the two stream halves of one (2B, ...) fp32 tensor, as
+    the bf16 operands of the following Linears (see LayerNormBF16Fn).  Taking the whole tensor
+    lets the backward write one full-size gradient: no zero-filled slice gradients and no
+    accumulate kernel, which two separate norms of x[:B] / x[B:] would cost."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2, eps1, eps2, B):
+        shape = x.shape
+        C = shape[-1]
+        x2 = x.reshape(-1, C)
+        if x2.dtype != torch.float32 or not x2.is_contiguous():
+            x2 = x2.float().contiguous()
+        M = x2.shape[0]
+        Mh = M // 2
+        y = torch.empty((M, C), device=x.device, dtype=torch.bfloat16)
+        mean = torch.empty((M,), device=x.device, dtype=torch.float32)
+        rstd = torch.empty_like(mean)
+        for h, (w, b, eps) in enumerate(((w1, b1, eps1), (w2, b2, eps2))):
+            r = slice(h * Mh, (h + 1) * Mh)
+            N.call("irads_resln_fwd", N.ptr(x2[r]), None, None, None, 0.0, Mh, C, max(Mh, 1), N.ptr(w.detach()),
+                   N.ptr(b.detach()), float(eps), None, N.ptr(y[r]), None, N.ptr(mean[r]), N.ptr(rstd[r]),
+                   N.stream())
+        ctx.save_for_backward(x2, w1, w2, mean, rstd)
+        ctx.shape, ctx.in_dtype = shape, x.dtype
+        half = (shape[0] // 2,) + tuple(shape[1:])
+        return y[:Mh].view(half), y[Mh:].view(half)
+
+    @staticmethod
+    def backward(ctx, gy1, gy2):
+        x2, w1, w2, mean, rstd = ctx.saved_tensors
+        M, C = x2.shape
+        Mh = M // 2
+        dx = torch.empty((M, C), device=x2.device, dtype=torch.float32)
+        for h, (gy, w) in enumerate(((gy1, w1), (gy2, w2))):
+            r = slice(h * Mh, (h + 1) * Mh)
+            if gy is None:
+                dx[r].zero_()
+                continue
+            g = gy.reshape(Mh, C)
+            if g.dtype != torch.bfloat16 or not g.is_contiguous():
+                g = g.to(torch.bfloat16).contiguous()
+            N.call("irads_resln_bwd", N.ptr(g), N.ptr(x2[r]), N.ptr(mean[r]), N.ptr(rstd[r]), N.ptr(w.detach()),
+                   None, None, Mh, C, max(Mh, 1), N.ptr(dx[r]), None, None, None, 0.0, N.stream())
+        return dx.view(ctx.shape).to(ctx.in_dtype), None, None, None, None, None, None, None
+
+
+def layer_norm_bf16_pair(x, norm1, norm2):
+    """(norm1(x[:B]), norm2(x[B:])) with B = x.shape[0] // 2, fused (bf16 outputs) when both
+    norms qualify for layer_norm_bf16, else the two module calls."""
+    B = x.shape[0] // 2
+    if x.shape[0] == 2 * B and ln_bf16_ok(x, norm1) and ln_bf16_ok(x, norm2):
+        with torch.autocast("cuda", enabled=False):
+            return LayerNormPairBF16Fn.apply(x, norm1.weight, norm1.bias, norm2.weight, norm2.bias, norm1.eps,
+                                             norm2.eps, B)
+    return layer_norm_bf16(x[:B], norm1), layer_norm_bf16(x[B:], norm2)
+
+
 def layer_norm_bf16(x, norm):
     """norm(x) as the bf16 operand of a following Linear (fused path) or plain norm(x)."""
     if ln_bf16_ok(x, norm):

@@ -676,11 +676,16 @@ class SwinTransformer(nn.Module):
                     sd[key] = t.view(nH2, L2).permute(1, 0).contiguous()
         self.load_state_dict(sd, strict=False)
 
-    def _outputs(self, i, x_rgb_out, x_dte_out, out_hw):
+    def _outputs(self, i, x_rgb_out, x_dte_out, out_hw, xo=None):
         # every consumer of these norms is a Linear (DeformMPG D_fc1/D_fc2, the heads' MLPs):
-        # under bf16 autocast they are produced directly as the bf16 GEMM operand
-        x_rgb_out = ops.layer_norm_bf16(x_rgb_out, getattr(self, f'norm{i}'))
-        x_dte_out = ops.layer_norm_bf16(x_dte_out, getattr(self, f'extra_norm{i}'))
+        # under bf16 autocast they are produced directly as the bf16 GEMM operand; given the
+        # batched stage output xo = cat[x_rgb_out, x_dte_out], both norms run as one op on it
+        if xo is not None:
+            x_rgb_out, x_dte_out = ops.layer_norm_bf16_pair(xo, getattr(self, f'norm{i}'),
+                                                            getattr(self, f'extra_norm{i}'))
+        else:
+            x_rgb_out = ops.layer_norm_bf16(x_rgb_out, getattr(self, f'norm{i}'))
+            x_dte_out = ops.layer_norm_bf16(x_dte_out, getattr(self, f'extra_norm{i}'))
         fused = ops.layer_norm_bf16(self.DeformMPGBlocks[i](x_rgb_out, x_dte_out, *out_hw, i),
                                     getattr(self, f'fuse_norm{i}'))
         c = self.num_features[i]
@@ -699,6 +704,7 @@ class SwinTransformer(nn.Module):
         outs, outs_rgb, outs_dte = [], [], []
         B = x_rgb.shape[0]
         for i, stage in enumerate(self.stages):
+            xo = None
             if self.batch_streams and hw_rgb == hw_dte:
                 xcat = self.MPGBlocks[i].residual_cat(x_rgb, x_dte, hw_rgb[0], hw_rgb[1])
                 xd, hw_d, xo, out_hw = stage.forward_pair(xcat, hw_rgb, B)
@@ -712,7 +718,7 @@ class SwinTransformer(nn.Module):
                 x_rgb, hw_rgb, x_rgb_out, out_hw = stage(x_rgb, hw_rgb, sub_mode='rgb')
                 x_dte, hw_dte, x_dte_out, out_hw = stage(x_dte, hw_dte, sub_mode='dte')
             if i in self.out_indices:
-                o, orgb, odte = self._outputs(i, x_rgb_out, x_dte_out, out_hw)
+                o, orgb, odte = self._outputs(i, x_rgb_out, x_dte_out, out_hw, xo)
                 outs.append(o)
                 outs_rgb.append(orgb)
                 outs_dte.append(odte)

@@ -297,6 +297,37 @@ def test_layer_norm_bf16_matches_autocast(C):
     assert gx1.dtype == torch.float32 and _rel(gx1, gx0) < 1e-3
 
 
+@pytest.mark.parametrize("C", [128, 1024])
+def test_layer_norm_bf16_pair_matches_two_norms(C):
+    """ops.layer_norm_bf16_pair (the two streams' output norms on one batched tensor) gives
+    exactly the two separate layer_norm_bf16 calls on x[:B] and x[B:]: same kernels on the
+    same rows, so outputs and dX are bit-identical, including with one half's grad unused."""
+    from irads import ops
+    torch.manual_seed(C + 1)
+    norms = [torch.nn.LayerNorm(C).to(DEV) for _ in range(2)]
+    for n in norms:
+        with torch.no_grad():
+            n.weight.uniform_(0.5, 1.5)
+            n.bias.uniform_(-0.2, 0.2)
+        n.requires_grad_(False)
+    x = torch.randn(4, 257, C, device=DEV) * 2 + 0.3
+    g = torch.randn(4, 257, C, device=DEV).bfloat16()
+    for use_second in (True, False):
+        outs = []
+        for pair in (False, True):
+            xx = x.clone().requires_grad_()
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                if pair:
+                    y1, y2 = ops.layer_norm_bf16_pair(xx, *norms)
+                else:
+                    y1, y2 = ops.layer_norm_bf16(xx[:2], norms[0]), ops.layer_norm_bf16(xx[2:], norms[1])
+            ys, gs = ([y1, y2], [g[:2], g[2:]]) if use_second else ([y1], [g[:2]])
+            (gx,) = torch.autograd.grad(ys, [xx], gs)
+            outs.append((y1, y2, gx))
+        for a, b in zip(*outs):
+            assert a.dtype == b.dtype and torch.equal(a, b)
+
+
 def test_patch_merging_reshape_matches_unfold():
     """PatchMerging's permute-reshape equals nn.Unfold's 2x2 sampling (same channel order),
     and under AMP the block output matches the unfold + LayerNorm + Linear path."""
