@@ -107,6 +107,86 @@ __global__ void __launch_bounds__(256) msda_fwd_kernel(const T *__restrict__ val
     }
 }
 
+// fp32 forward, D % 4 == 0: V = D/4 lanes own one (b, q, m) row, each lane 4 consecutive
+// channels, so every corner gather is one 16-B load per lane and a wave instruction
+// fetches 64/V whole 128-B value segments (the scalar kernel above moves 4 B per lane and
+// needs 4x the load instructions for the same bytes).  The sample loop over a chunk of V
+// samples is unrolled so the 4·V gathers of a chunk are in flight together.  Per-channel
+// arithmetic is the scalar kernel's, operation for operation (bit-identical output).
+// Blocks are remapped so that each XCD (blockIdx % 8) walks a contiguous range of
+// queries: neighbouring queries sample neighbouring value cells, which then share that
+// XCD's L2 instead of being spread over all eight.
+__device__ __forceinline__ long xcd_block(long bid, long nblk) {
+    const long q = nblk / 8, r = nblk % 8, x = bid % 8;
+    return x * q + min(x, r) + bid / 8;
+}
+
+template <int V>
+__global__ void __launch_bounds__(256) msda_fwd_vec_kernel(const float *__restrict__ value,
+                                                           const int64_t *__restrict__ shapes,
+                                                           const int64_t *__restrict__ lsi,
+                                                           const float *__restrict__ loc,
+                                                           const float *__restrict__ aw, int bs, int S, int M, int D,
+                                                           int L, int Q, int P, float *__restrict__ out) {
+    __shared__ int sH[kMaxLevels], sW[kMaxLevels], sS[kMaxLevels];
+    if (threadIdx.x < L) {
+        sH[threadIdx.x] = (int)shapes[2 * threadIdx.x];
+        sW[threadIdx.x] = (int)shapes[2 * threadIdx.x + 1];
+        sS[threadIdx.x] = (int)lsi[threadIdx.x];
+    }
+    __syncthreads();
+    const long blk = xcd_block(blockIdx.x, gridDim.x);
+    const long gid = (blk * blockDim.x + threadIdx.x) / V;
+    const int lane = threadIdx.x % V;
+    if (gid >= (long)bs * Q * M) return;  // whole group exits together
+    const int m = (int)(gid % M);
+    const int b = (int)(gid / ((long)M * Q));
+    const int LP = L * P;
+    const long cs = (long)M * D;
+    const float *vb = value + (long)b * S * cs + (long)m * D + 4 * lane;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int s0 = 0; s0 < LP; s0 += V) {
+        const int sl = s0 + lane;
+        float lx = 0.f, ly = 0.f, w = 0.f;
+        if (sl < LP) {
+            const long li = gid * LP + sl;
+            lx = loc[2 * li];
+            ly = loc[2 * li + 1];
+            w = aw[li];
+        }
+#pragma unroll
+        for (int k = 0; k < V; ++k) {
+            const float x = __shfl(lx, k, V), y = __shfl(ly, k, V), a = __shfl(w, k, V);
+            if (s0 + k < LP) {  // uniform over the group
+                const int l = (s0 + k) / P;
+                const int H = sH[l], W = sW[l];
+                const Samp<float> s = locate(x, y, H, W);
+                const float *v = vb + (long)sS[l] * cs;
+                const long rs = (long)W * cs;
+                const bool xl = s.x0 >= 0 && s.x0 < W, xh = s.x0 + 1 >= 0 && s.x0 + 1 < W;
+                const bool yl = s.y0 >= 0 && s.y0 < H, yh = s.y0 + 1 >= 0 && s.y0 + 1 < H;
+                const float *r0 = v + s.y0 * rs, *r1 = r0 + rs;
+                float4 v_nw = make_float4(0.f, 0.f, 0.f, 0.f), v_ne = v_nw, v_sw = v_nw, v_se = v_nw;
+                if (yl && xl) v_nw = *(const float4 *)(r0 + s.x0 * cs);
+                if (yl && xh) v_ne = *(const float4 *)(r0 + (s.x0 + 1) * cs);
+                if (yh && xl) v_sw = *(const float4 *)(r1 + s.x0 * cs);
+                if (yh && xh) v_se = *(const float4 *)(r1 + (s.x0 + 1) * cs);
+#define IRADS_MSDA_CH(c)                         \
+    {                                            \
+        float val = v_nw.c * s.nw;               \
+        val = fmaf(v_ne.c, s.ne, val);           \
+        val = fmaf(v_sw.c, s.sw, val);           \
+        val = fmaf(v_se.c, s.se, val);           \
+        acc.c += val * a;                        \
+    }
+                IRADS_MSDA_CH(x) IRADS_MSDA_CH(y) IRADS_MSDA_CH(z) IRADS_MSDA_CH(w)
+#undef IRADS_MSDA_CH
+            }
+        }
+    }
+    *(float4 *)(out + gid * D + 4 * lane) = acc;
+}
+
 template <typename T, int G>
 __device__ __forceinline__ T group_sum(T v) {
 #pragma unroll
@@ -213,6 +293,26 @@ int pick_group(int D) {
 template <typename T>
 int launch_fwd(const void *value, const int64_t *shapes, const int64_t *lsi, const void *loc, const void *aw, int bs,
                int S, int M, int D, int L, int Q, int P, void *out, hipStream_t st) {
+    if constexpr (sizeof(T) == 4) {
+        // 16-B gathers need D = 4·V with V a power of two and 16-B aligned value / out rows
+        const int V = D / 4;
+        const bool aligned = (((uintptr_t)value | (uintptr_t)out) & 15) == 0;
+        if (D % 4 == 0 && V <= 64 && (V & (V - 1)) == 0 && aligned) {
+            const long threads = (long)bs * Q * M * V;
+            dim3 grid((unsigned)((threads + 255) / 256));
+#define IRADS_MSDA_V(VV)                                                                                        \
+    case VV:                                                                                                    \
+        msda_fwd_vec_kernel<VV><<<grid, 256, 0, st>>>((const float *)value, shapes, lsi, (const float *)loc,   \
+                                                      (const float *)aw, bs, S, M, D, L, Q, P, (float *)out); \
+        break;
+            switch (V) {
+                IRADS_MSDA_V(1) IRADS_MSDA_V(2) IRADS_MSDA_V(4) IRADS_MSDA_V(8) IRADS_MSDA_V(16) IRADS_MSDA_V(32)
+                IRADS_MSDA_V(64)
+            }
+#undef IRADS_MSDA_V
+            return check_launch("irads_msda_fwd");
+        }
+    }
     const int G = pick_group(D);
     const long groups = (long)bs * Q * M;
     const long threads = groups * G;
