@@ -85,8 +85,29 @@ def parse(dir_fetch, dir_write):
     print(json.dumps(out, indent=1))
 
 
+SQ_COUNTERS = ("SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU",
+               "SQ_ACTIVE_INST_LDS", "SQ_VALU_MFMA_BUSY_CYCLES", "SQ_BUSY_CYCLES")
+
+
+def parse_sq(dir_sq):
+    """Wave-state breakdown of the 24 launches (one SQ pass, 8 counters): SQ_WAIT_ANY =
+    parked at s_waitcnt / barrier, SQ_WAIT_INST_ANY = issue-stalled, SQ_ACTIVE_INST_ANY =
+    issuing; the three are disjoint and sum to SQ_WAVE_CYCLES (MI355X_MICROARCH.md, PMC
+    slots).  The wave counters are in quad-cycles, SQ_VALU_MFMA_BUSY_CYCLES in cycles."""
+    tot = {c: sum(_values(dir_sq, c)) for c in SQ_COUNTERS}
+    w = tot["SQ_WAVE_CYCLES"]
+    out = {"kernel": "irads_winattn_fwd (bf16)", "launches": 24,
+           "per_launch": {c: round(v / 24) for c, v in tot.items()},
+           "fraction_of_wave_cycles": {c: round(tot[c] / w, 3) for c in SQ_COUNTERS[1:6]},
+           "source": "rocprofv3 --pmc " + " ".join(SQ_COUNTERS) + " --kernel-trace, "
+                     "scripts/pmc_winattn.py run (the 24 launches of one bench step)"}
+    print(json.dumps(out, indent=1))
+
+
 if __name__ == "__main__":
     if sys.argv[1] == "run":
         run()
+    elif sys.argv[1] == "parse_sq":
+        parse_sq(sys.argv[2])
     else:
         parse(sys.argv[2], sys.argv[3])

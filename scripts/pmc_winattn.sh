@@ -9,3 +9,8 @@ timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format cs
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $R/gpurun_out/pmc_write -o run -- python3 $R/scripts/pmc_winattn.py run > gpurun_out/pmc_write.log 2>&1 || { echo "write pass failed"; tail gpurun_out/pmc_write.log; exit 1; }
 python3 scripts/pmc_winattn.py parse gpurun_out/pmc_fetch gpurun_out/pmc_write > gpurun_out/pmc_winattn_fwd.json && cat gpurun_out/pmc_winattn_fwd.json
 find gpurun_out/pmc_fetch gpurun_out/pmc_write -name '*kernel_trace.csv' -delete
+# wave-state pass (8 SQ counters fit one pass)
+rm -rf gpurun_out/pmc_sq
+timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES --kernel-trace --output-format csv -d $R/gpurun_out/pmc_sq -o run -- python3 $R/scripts/pmc_winattn.py run > gpurun_out/pmc_sq.log 2>&1 || { echo "sq pass failed"; tail gpurun_out/pmc_sq.log; exit 1; }
+python3 scripts/pmc_winattn.py parse_sq gpurun_out/pmc_sq > gpurun_out/pmc_winattn_fwd_sq.json && cat gpurun_out/pmc_winattn_fwd_sq.json
+find gpurun_out/pmc_sq -name '*kernel_trace.csv' -delete

@@ -163,3 +163,29 @@ def test_large_dino_encoder_linearity():
     # checksum of checksums against a float64 run of the same kernel
     o64 = ops.MSDAFn.apply(v1.double(), shapes, lsi, loc.double(), aw.double(), 64)
     torch.testing.assert_close(o1.double(), o64, atol=1e-4, rtol=1e-5)
+
+
+@pytest.mark.parametrize("D", [4, 12, 16, 32, 64, 256])
+def test_fp32_vector_path_bitexact_vs_scalar_path(D):
+    """The fp32 forward's 16-B-gather kernel (D = 4·V, V a power of two, 16-B aligned rows)
+    performs the scalar kernel's per-channel operations in the same order: outputs are
+    bit-identical.  A value tensor offset by one float (not 16-B aligned) takes the scalar
+    kernel; D = 12 (V = 3) takes it too, on both sides."""
+    ops = _ops()
+    g = torch.Generator().manual_seed(D)
+    lv = [(13, 17), (7, 9), (4, 5)]
+    shapes = torch.as_tensor(lv, dtype=torch.long, device=DEV)
+    lsi = torch.cat((shapes.new_zeros((1,)), shapes.prod(1).cumsum(0)[:-1]))
+    S, bs, M, Q, L, P = int(shapes.prod(1).sum()), 2, 3, 57, 3, 5
+    value = torch.randn(bs, S, M, D, generator=g).to(DEV)
+    buf = torch.empty(value.numel() + 1, device=DEV)
+    value_unaligned = buf[1:].view(value.shape)
+    value_unaligned.copy_(value)
+    assert value_unaligned.data_ptr() % 16 != 0
+    loc = (torch.rand(bs, Q, M, L, P, 2, generator=g) * 1.1 - 0.05).to(DEV)  # some corners outside
+    aw = torch.rand(bs, Q, M, L, P, generator=g).to(DEV)
+    vec = ops.MSDAFn.apply(value, shapes, lsi, loc, aw, 2)
+    sca = ops.MSDAFn.apply(value_unaligned, shapes, lsi, loc, aw, 2)
+    assert torch.equal(vec, sca), (vec - sca).abs().max().item()
+    ref = ops.MSDAFn.apply(value.double(), shapes, lsi, loc.double(), aw.double(), 2)
+    torch.testing.assert_close(vec.double(), ref, atol=1e-5, rtol=1e-5)
