@@ -220,11 +220,28 @@ class DAttnSampleFn(torch.autograd.Function):
         def g(t):
             return torch.zeros((B, C, 2 * n), device=x.device) if t is None else t.contiguous().float()
         gxs, gys, gqs = g(gxs), g(gys), g(gqs)
-        gx, gy, gq = torch.zeros_like(x), torch.zeros_like(y), torch.zeros_like(q)
+        gx, gy, gq = zeros_like_many(x, y, q)
         gpx, gpy = torch.empty_like(px), torch.empty_like(py)
         N.call("irads_dattn_sample_bwd", N.ptr(x), N.ptr(y), N.ptr(q), N.ptr(px), N.ptr(py), N.ptr(gxs), N.ptr(gys),
                N.ptr(gqs), B, C, H, W, G, n, N.ptr(gx), N.ptr(gy), N.ptr(gq), N.ptr(gpx), N.ptr(gpy), N.stream())
         return gx, gy, gq, gpx, gpy, None
+
+
+def zeros_like_many(*ts):
+    """Zero-filled gradients for several contiguous tensors of one dtype / device as views of
+    ONE buffer (one fill launch instead of one per tensor); segments start on 256-B
+    boundaries so vector loads stay aligned.  Other layouts fall back to zeros_like."""
+    t0 = ts[0]
+    if not all(t.is_contiguous() and t.dtype == t0.dtype and t.device == t0.device for t in ts):
+        return [torch.zeros_like(t) for t in ts]
+    per = 256 // t0.element_size()
+    sizes = [-(-t.numel() // per) * per for t in ts]
+    flat = torch.zeros((sum(sizes),), dtype=t0.dtype, device=t0.device)
+    out, o = [], 0
+    for t, n in zip(ts, sizes):
+        out.append(flat[o:o + t.numel()].view(t.shape))
+        o += n
+    return out
 
 
 def _ptr_array(tensors):
@@ -341,10 +358,9 @@ class DAttnAttentionFn(torch.autograd.Function):
         B, nH, G, hc, H, W, n, Ht, Wt, scale = ctx.cfg
         gout = gout.contiguous().float()
         delta = torch.empty_like(lse)
-        gq = torch.zeros_like(q)  # key splits add into it
-        gk, gv = torch.zeros_like(k), torch.zeros_like(v)  # key-major, like k and v here
-        grpe = torch.zeros_like(rpe)
-        gpx, gpy = torch.zeros_like(px), torch.zeros_like(py)
+        # all six are atomically accumulated: zeroed by one fill (gq: key splits add into it;
+        # gk, gv key-major like k and v here)
+        gq, gk, gv, grpe, gpx, gpy = zeros_like_many(q, k, v, rpe, px, py)
         N.call("irads_dattn_attn_bwd", N.ptr(q), N.ptr(k), N.ptr(v), N.ptr(px), N.ptr(py), N.ptr(rpe), N.ptr(qgy),
                N.ptr(qgx), B, nH, G, hc, H, W, n, Ht, Wt, scale, N.ptr(out), N.ptr(lse), N.ptr(gout), N.ptr(delta),
                N.ptr(gq), N.ptr(gk), N.ptr(gv), N.ptr(grpe), N.ptr(gpx), N.ptr(gpy), N.stream())
