@@ -148,6 +148,7 @@ def msda_inputs(device, bs=2, Q=None, seed=0):
     return [t.to(device) for t in (value, shapes, lsi, loc, aw)]
 
 
+GATHER_PEAK_GBS = 18800.0  # L2-resident random-row gather rate (upper end), MI355X_MICROARCH.md
 ATOMIC_PEAK_GBS = 1300.0  # chip-wide f32 atomic-add rate, MI355X_MICROARCH.md 'Global float atomics'
 
 
@@ -199,6 +200,9 @@ def msda_rooflines(device, reps=20):
             ent = out[f"msda_{tag}_{name}"]
             ent["gathered_bytes_per_launch"] = samp_b
             ent["gather_rate_gbs"] = round(samp_b / (ms * 1e-3) / 1e9, 1)
+            if tag == "fwd":  # ceiling: L2-resident random-row gathers, 16.8-18.8 TB/s (MI355X_MICROARCH.md)
+                ent["gather_peak_gbs"] = GATHER_PEAK_GBS
+                ent["gather_frac"] = round(samp_b / (ms * 1e-3) / 1e9 / GATHER_PEAK_GBS, 4)
             if tag == "bwd":
                 ent["atomic_bytes_per_launch"] = samp_b
                 ent["atomic_rate_gbs"] = ent["gather_rate_gbs"]

@@ -670,6 +670,38 @@ class MPGResidualFn(torch.autograd.Function):
         return gx, g[:B], g[B:], s[0], s[1], s[2], s[3]
 
 
+class SplitStreamsFn(torch.autograd.Function):
+    """(x[:n], x[n:]) of the batched rgb+dte tensor with a backward that concatenates the two
+    gradients (one copy kernel).  Plain slicing makes autograd materialise each half's
+    gradient as a zero-filled full-size tensor plus a copy, then add the two full tensors."""
+
+    @staticmethod
+    def forward(ctx, x, n):
+        ctx.n = n
+        ctx.shape = x.shape
+        return x[:n], x[n:]
+
+    @staticmethod
+    def backward(ctx, g1, g2):
+        n = ctx.n
+        if g1 is None and g2 is None:
+            return None, None
+        ref = g1 if g1 is not None else g2
+        out = torch.empty(ctx.shape, device=ref.device, dtype=ref.dtype)
+        for part, g in ((out[:n], g1), (out[n:], g2)):
+            if g is None:
+                part.zero_()
+            else:
+                part.copy_(g)
+        return out, None
+
+
+def split_streams(x, n):
+    if x.requires_grad and torch.is_grad_enabled():
+        return SplitStreamsFn.apply(x, n)
+    return x[:n], x[n:]
+
+
 def mpg_residual_ok(x, x_rgb, x_dte):
     return (x.is_cuda and x.dtype == torch.bfloat16 and x_rgb.dtype == torch.float32
             and x_dte.dtype == torch.float32 and x_rgb.shape == x_dte.shape == x.shape and x.shape[-1] % 8 == 0
@@ -708,7 +740,9 @@ def wgrad_batched(problems, alpha=1.0, accumulate=False):
 
 
 def wgrad_ok(in_features, out_features):
-    return in_features % 8 == 0 and out_features % 8 == 0
+    # out_features < 8 (DAttn's get_sample_weight 1x1 conv, C -> 2) is padded to 8 in backward:
+    # hipBLASLt's pick for that (2, B*2n) x (B*2n, C) weight-gradient GEMM took ~60 us
+    return in_features % 8 == 0 and (out_features % 8 == 0 or out_features < 8)
 
 
 class LinearFn(torch.autograd.Function):
@@ -749,9 +783,18 @@ class LinearFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             gx = torch.mm(g, wb).view(ctx.shape)
         if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
-            gw = torch.empty(wb.shape, device=g.device, dtype=torch.float32)
-            gb = torch.empty((wb.shape[0],), device=g.device, dtype=torch.float32) if ctx.has_bias else None
-            wgrad(g, xb, gw, colsum_a=gb)
+            o = wb.shape[0]
+            if o % 8:  # narrow output: zero-pad dY to 8 columns (16-B rows for the kernel)
+                g8 = torch.zeros((g.shape[0], 8), device=g.device, dtype=torch.bfloat16)
+                g8[:, :o] = g
+                gw8 = torch.empty((8, wb.shape[1]), device=g.device, dtype=torch.float32)
+                gb8 = torch.empty((8,), device=g.device, dtype=torch.float32) if ctx.has_bias else None
+                wgrad(g8, xb, gw8, colsum_a=gb8)
+                gw, gb = gw8[:o], (gb8[:o] if ctx.has_bias else None)
+            else:
+                gw = torch.empty(wb.shape, device=g.device, dtype=torch.float32)
+                gb = torch.empty((o,), device=g.device, dtype=torch.float32) if ctx.has_bias else None
+                wgrad(g, xb, gw, colsum_a=gb)
         return gx, gw, gb
 
 

@@ -708,7 +708,7 @@ class SwinTransformer(nn.Module):
             if self.batch_streams and hw_rgb == hw_dte:
                 xcat = self.MPGBlocks[i].residual_cat(x_rgb, x_dte, hw_rgb[0], hw_rgb[1])
                 xd, hw_d, xo, out_hw = stage.forward_pair(xcat, hw_rgb, B)
-                x_rgb, x_dte = xd[:B], xd[B:]
+                x_rgb, x_dte = ops.split_streams(xd, B)  # one gradient copy back, no zero-fill + add
                 x_rgb_out, x_dte_out = xo[:B], xo[B:]
                 hw_rgb = hw_dte = hw_d
             else:

@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--rows", type=int, default=60)
     ap.add_argument("--batch", type=int, default=8)
+    ap.add_argument("--stacks", default=None, help="comma-separated aten ops: print their Python call stacks")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.manual_seed(3407)
@@ -31,7 +32,8 @@ def main():
     for _ in range(3):
         bench.train_step(model, opt, sched, loss_fn, batch)
     torch.cuda.synchronize()
-    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True) as prof:
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True,
+                 with_stack=a.stacks is not None) as prof:
         for _ in range(a.steps):
             bench.train_step(model, opt, sched, loss_fn, batch)
         torch.cuda.synchronize()
@@ -59,6 +61,22 @@ def main():
         except Exception:
             pass
         print(f"{us:9.1f} {n:6.1f}  {k:34s} {shp[:150]}{extra}")
+    if a.stacks:
+        want = set(a.stacks.split(","))
+        print("\n# call stacks (GPU us per step, calls per step)")
+        for e in sorted(prof.key_averages(group_by_stack_n=6), key=lambda e: -e.self_device_time_total):
+            if e.key in want and e.self_device_time_total > 0:
+                print(f"{e.self_device_time_total / a.steps:9.1f} {e.count / a.steps:6.1f} {e.key}")
+                for fr in e.stack:
+                    print("          ", fr)
+    # backward nodes: GPU time (self + children) per step, to attribute fills / casts / adds
+    ka2 = prof.key_averages()
+    rows = [(e.device_time_total / a.steps, e.count / a.steps, e.key) for e in ka2
+            if e.key.startswith("autograd::engine::evaluate_function") and e.device_time_total > 0]
+    rows.sort(reverse=True)
+    print("\n# autograd nodes by GPU time per step (us, incl. children), calls per step")
+    for us, n, k in rows[:a.rows]:
+        print(f"{us:9.1f} {n:6.1f}  {k[len('autograd::engine::evaluate_function: '):]}")
 
 
 if __name__ == "__main__":

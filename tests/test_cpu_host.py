@@ -177,3 +177,21 @@ def test_graph_step_gradient_allreduce_gloo():
         want = base * (1.5 if i != 1 else 0.5)  # mean of 1x and 2x (rank 1 lacks grad #1: 0)
         for r in range(2):
             torch.testing.assert_close(torch.from_numpy(res[r][i]), want)
+
+
+def test_split_streams_gradient_matches_slicing():
+    """ops.split_streams: the batched-stream split whose backward concatenates the halves'
+    gradients (one copy) — same gradient as plain slicing, including an unused half."""
+    import torch
+    from irads import ops
+    torch.manual_seed(0)
+    x = torch.randn(6, 5, 4, requires_grad=True)
+    w1, w2 = torch.randn(3, 5, 4), torch.randn(3, 5, 4)
+    a, b = ops.split_streams(x, 3)
+    (ga,) = torch.autograd.grad((a * w1).sum() + (b * w2).sum(), x)
+    x2 = x.detach().clone().requires_grad_()
+    (gb,) = torch.autograd.grad((x2[:3] * w1).sum() + (x2[3:] * w2).sum(), x2)
+    assert torch.equal(ga, gb)
+    a, b = ops.split_streams(x, 3)
+    (gc,) = torch.autograd.grad((b * w2).sum(), x)  # rgb half unused
+    assert torch.equal(gc[:3], torch.zeros(3, 5, 4)) and torch.equal(gc[3:], w2)

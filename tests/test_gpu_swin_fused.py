@@ -244,17 +244,21 @@ def test_wgrad_split_k(K, m, n):
     assert torch.equal(D, D3)
 
 
-def test_linear_fn_matches_autocast_linear():
+@pytest.mark.parametrize("out_features", [16, 2, 5])
+def test_linear_fn_matches_autocast_linear(out_features):
     """ops.linear (trainable weight, bf16 autocast): forward is the autocast GEMM bit for bit;
     dX equals autocast's; dW / db are the fp32 sums autocast rounds to bf16 (tolerance: one
-    bf16 rounding, 2^-8 relative)."""
+    bf16 rounding, 2^-8 relative).  out_features < 8 takes the zero-padded weight-gradient
+    path (DAttn's C -> 2 sample-weight projection)."""
+    from irads import ops
     from semseg.models.layers.common import TrainLinear
     torch.manual_seed(2)
-    lin = torch.nn.Linear(128, 16).to(DEV)
-    tl = TrainLinear(128, 16).to(DEV)
+    lin = torch.nn.Linear(128, out_features).to(DEV)
+    tl = TrainLinear(128, out_features).to(DEV)
     tl.load_state_dict(lin.state_dict())
     x = torch.randn(2, 300, 128, device=DEV)
-    g = torch.randn(2, 300, 16, device=DEV).bfloat16()
+    g = torch.randn(2, 300, out_features, device=DEV).bfloat16()
+    assert ops.wgrad_ok(128, out_features)
     outs = []
     for mod in (lin, tl):
         xx = x.clone().requires_grad_()
