@@ -245,6 +245,11 @@ int irads_relu_dropout_bwd(const uint16_t *r, const uint16_t *dr, uint16_t *da, 
 int irads_mpg_fwd(const uint16_t *x, const float *x_rgb, const float *x_dte, const float *gamma_rgb,
                   const float *beta_rgb, const float *gamma_dte, const float *beta_dte, long R, int C, float *out,
                   void *stream);
+/* Same, with bf16 stream inputs (stages 1-3, where x_rgb / x_dte are PatchMerging's bf16 GEMM
+ * output): each is upcast exactly before the fp32 adds, as torch's type promotion does. */
+int irads_mpg_fwd_bf16(const uint16_t *x, const uint16_t *x_rgb, const uint16_t *x_dte, const float *gamma_rgb,
+                       const float *beta_rgb, const float *gamma_dte, const float *beta_dte, long R, int C,
+                       float *out, void *stream);
 int irads_mpg_bwd(const float *grad, const uint16_t *x, const float *gamma_rgb, const float *gamma_dte, long R, int C,
                   uint16_t *grad_x, float *partials, void *stream);
 long irads_mpg_partials(long R, int C);

@@ -31,8 +31,18 @@ __device__ __forceinline__ void unpack8(u32x4 w, float *f) {
 
 // one thread = 8 consecutive channels of one row; a block walks rows with stride
 // (256 / (C/8)) rows per iteration
-__global__ __launch_bounds__(256) void mpg_fwd_kernel(const u16 *__restrict__ x, const float *__restrict__ xr,
-                                                      const float *__restrict__ xd, const float *__restrict__ gr,
+// 8 consecutive stream values as fp32: fp32 rows (stage 0: the patch embedding's output) or
+// bf16 rows (stages 1-3: PatchMerging's reduction GEMM output), upcast exactly as torch's
+// bf16 + fp32 type promotion does
+__device__ __forceinline__ void load8(const float *p, float *f) {
+    const float4 a = reinterpret_cast<const float4 *>(p)[0], b = reinterpret_cast<const float4 *>(p)[1];
+    f[0] = a.x, f[1] = a.y, f[2] = a.z, f[3] = a.w, f[4] = b.x, f[5] = b.y, f[6] = b.z, f[7] = b.w;
+}
+__device__ __forceinline__ void load8(const u16 *p, float *f) { unpack8(*reinterpret_cast<const u32x4 *>(p), f); }
+
+template <typename TS>
+__global__ __launch_bounds__(256) void mpg_fwd_kernel(const u16 *__restrict__ x, const TS *__restrict__ xr,
+                                                      const TS *__restrict__ xd, const float *__restrict__ gr,
                                                       const float *__restrict__ br, const float *__restrict__ gd,
                                                       const float *__restrict__ bd, long R, int C,
                                                       float *__restrict__ out) {
@@ -47,11 +57,9 @@ __global__ __launch_bounds__(256) void mpg_fwd_kernel(const u16 *__restrict__ x,
     for (long r = (long)blockIdx.x * rpi + rl; r < R; r += (long)gridDim.x * rpi) {
         float xv[8];
         unpack8(*reinterpret_cast<const u32x4 *>(x + r * C + c0), xv);
-        const float4 *pr = reinterpret_cast<const float4 *>(xr + r * C + c0);
-        const float4 *pd = reinterpret_cast<const float4 *>(xd + r * C + c0);
-        const float4 a0 = pr[0], a1 = pr[1], d0 = pd[0], d1 = pd[1];
-        const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-        const float dv[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
+        float av[8], dv[8];
+        load8(xr + r * C + c0, av);
+        load8(xd + r * C + c0, dv);
         float orr[8], odd[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -154,9 +162,19 @@ extern "C" int irads_mpg_fwd(const uint16_t *x, const float *x_rgb, const float 
     IRADS_MPG_CHECK("irads_mpg_fwd");
     IRADS_REQUIRE(x && x_rgb && x_dte && gamma_rgb && beta_rgb && gamma_dte && beta_dte && out,
                   "irads_mpg_fwd: null pointer");
-    hipLaunchKernelGGL(mpg_fwd_kernel, dim3(mpg_blocks(R, C)), dim3(256), 0, (hipStream_t)stream, x, x_rgb, x_dte,
-                       gamma_rgb, beta_rgb, gamma_dte, beta_dte, R, C, out);
+    hipLaunchKernelGGL(mpg_fwd_kernel<float>, dim3(mpg_blocks(R, C)), dim3(256), 0, (hipStream_t)stream, x, x_rgb,
+                       x_dte, gamma_rgb, beta_rgb, gamma_dte, beta_dte, R, C, out);
     return check_launch("irads_mpg_fwd");
+}
+extern "C" int irads_mpg_fwd_bf16(const uint16_t *x, const uint16_t *x_rgb, const uint16_t *x_dte,
+                                  const float *gamma_rgb, const float *beta_rgb, const float *gamma_dte,
+                                  const float *beta_dte, long R, int C, float *out, void *stream) {
+    IRADS_MPG_CHECK("irads_mpg_fwd_bf16");
+    IRADS_REQUIRE(x && x_rgb && x_dte && gamma_rgb && beta_rgb && gamma_dte && beta_dte && out,
+                  "irads_mpg_fwd_bf16: null pointer");
+    hipLaunchKernelGGL(mpg_fwd_kernel<u16>, dim3(mpg_blocks(R, C)), dim3(256), 0, (hipStream_t)stream, x, x_rgb,
+                       x_dte, gamma_rgb, beta_rgb, gamma_dte, beta_dte, R, C, out);
+    return check_launch("irads_mpg_fwd_bf16");
 }
 
 extern "C" int irads_mpg_bwd(const float *grad, const uint16_t *x, const float *gamma_rgb, const float *gamma_dte,

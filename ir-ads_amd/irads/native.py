@@ -51,6 +51,7 @@ SIGNATURES = {
     "irads_bnact_fwd": [_vp, _l, _i, _l] + [_vp] * 7,
     "irads_bnact_bwd": [_vp, _vp, _l, _i, _l] + [_vp] * 10,
     "irads_mpg_fwd": [_vp] * 7 + [_l, _i, _vp, _vp],
+    "irads_mpg_fwd_bf16": [_vp] * 7 + [_l, _i, _vp, _vp],
     "irads_mpg_bwd": [_vp] * 4 + [_l, _i, _vp, _vp, _vp],
     "irads_adapter_down": [_i, _vp, _vp, _vp, _vp, _vp, _vp, _l, _l, _i, _i, _f, _u64, _u64, _vp, _vp, _vp],
     "irads_adapter_up": [_vp, _vp, _vp, _vp, _vp, _l, _l, _i, _i, _vp, _vp],

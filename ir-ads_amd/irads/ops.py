@@ -646,12 +646,13 @@ class MPGResidualFn(torch.autograd.Function):
         B, L, C = x_rgb.shape
         R = B * L
         xb = N.check(x.contiguous(), "MPG x", torch.bfloat16)
-        xr = N.check(x_rgb.contiguous(), "x_rgb", torch.float32)
-        xd = N.check(x_dte.contiguous(), "x_dte", torch.float32)
+        sdt = x_rgb.dtype  # fp32 (stage 0) or bf16 (PatchMerging output, stages 1-3)
+        xr = N.check(x_rgb.contiguous(), "x_rgb", sdt)
+        xd = N.check(x_dte.contiguous(), "x_dte", sdt)
         ps = [N.check(t.detach().contiguous(), "tfts parameter", torch.float32) for t in (g_rgb, b_rgb, g_dte, b_dte)]
         out = torch.empty((2 * B, L, C), device=x.device, dtype=torch.float32)
-        N.call("irads_mpg_fwd", N.ptr(xb), N.ptr(xr), N.ptr(xd), *[N.ptr(t) for t in ps], R, C, N.ptr(out),
-               N.stream())
+        N.call("irads_mpg_fwd" if sdt == torch.float32 else "irads_mpg_fwd_bf16", N.ptr(xb), N.ptr(xr), N.ptr(xd),
+               *[N.ptr(t) for t in ps], R, C, N.ptr(out), N.stream())
         ctx.save_for_backward(xb, ps[0], ps[2])
         ctx.cfg = (B, L, C)
         return out
@@ -703,8 +704,8 @@ def split_streams(x, n):
 
 
 def mpg_residual_ok(x, x_rgb, x_dte):
-    return (x.is_cuda and x.dtype == torch.bfloat16 and x_rgb.dtype == torch.float32
-            and x_dte.dtype == torch.float32 and x_rgb.shape == x_dte.shape == x.shape and x.shape[-1] % 8 == 0
+    return (x.is_cuda and x.dtype == torch.bfloat16 and x_rgb.dtype in (torch.float32, torch.bfloat16)
+            and x_dte.dtype == x_rgb.dtype and x_rgb.shape == x_dte.shape == x.shape and x.shape[-1] % 8 == 0
             and x.shape[-1] <= 2048)
 
 

@@ -1,0 +1,78 @@
+"""Where the bench step's dtype casts and copies come from: one eager training step under a
+TorchDispatchMode that records every aten._to_copy / copy_ / add / fill_ / zero_ with its
+shape and dtype, and the issuing site — the Python frame inside the package for forward
+ops, the autograd node for backward ops.  Prints the sites by bytes moved.
+
+    python scripts/cast_audit.py [--batch 8] [--top 40]
+"""
+import argparse
+import collections
+import os
+import sys
+import traceback
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "ir-ads_amd")]
+
+import torch  # noqa: E402
+from torch.utils._python_dispatch import TorchDispatchMode  # noqa: E402
+
+import bench  # noqa: E402
+
+WATCH = {"aten._to_copy.default", "aten.copy_.default", "aten.add.Tensor", "aten.fill_.Scalar", "aten.zero_.default",
+         "aten.zeros.default", "aten.new_zeros.default", "aten.clone.default", "aten.cat.default",
+         "aten.sum.dim_IntList", "aten.mul.Tensor"}
+
+
+def site():
+    node = torch._C._current_autograd_node()
+    if node is not None:
+        return "bwd " + node.name()
+    for fr in reversed(traceback.extract_stack()[:-3]):
+        if "ir-ads_amd" in fr.filename:
+            return f"fwd {os.path.relpath(fr.filename, ROOT)}:{fr.lineno} {fr.line.strip()[:70]}"
+    return "fwd ?"
+
+
+class Audit(TorchDispatchMode):
+    def __init__(self):
+        super().__init__()
+        self.rows = collections.defaultdict(lambda: [0, 0])
+
+    def __torch_dispatch__(self, func, types, args=(), kwargs=None):
+        out = func(*args, **(kwargs or {}))
+        name = str(func)
+        if name in WATCH:
+            t = out if torch.is_tensor(out) else (args[0] if args and torch.is_tensor(args[0]) else None)
+            if t is not None and t.is_cuda and t.numel() >= 1 << 16:
+                key = (name.replace("aten.", "").replace(".default", ""), site(), tuple(t.shape), str(t.dtype))
+                r = self.rows[key]
+                r[0] += 1
+                r[1] += t.numel() * t.element_size()
+        return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=8)
+    ap.add_argument("--top", type=int, default=40)
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(3407)
+    model, opt, sched, loss_fn = bench.build(dev, 1, 0, 1000)
+    model.train()
+    batch = bench.synthetic_batch(a.batch, 512, dev, 3407)
+    bench.train_step(model, opt, sched, loss_fn, batch)
+    torch.cuda.synchronize()
+    audit = Audit()
+    with audit:
+        bench.train_step(model, opt, sched, loss_fn, batch)
+    torch.cuda.synchronize()
+    rows = sorted(audit.rows.items(), key=lambda kv: -kv[1][1])
+    print(f"{'MB out':>9} {'calls':>5}  op / site / shape / dtype")
+    for (op, st, shape, dt), (n, b) in rows[:a.top]:
+        print(f"{b / 1e6:9.1f} {n:5d}  {op:10s} {st[:90]:90s} {list(shape)} {dt.replace('torch.', '')}")
+
+
+if __name__ == "__main__":
+    main()

@@ -426,8 +426,9 @@ def test_wgrad_batched_matches_single():
             torch.testing.assert_close(sb, cb, rtol=1e-5, atol=1e-3)
 
 
+@pytest.mark.parametrize("sdt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("C,L", [(128, 4096), (256, 1024), (512, 256), (1024, 64), (192, 300)])
-def test_mpg_residual_matches_module_math(C, L):
+def test_mpg_residual_matches_module_math(C, L, sdt):
     """irads_mpg_fwd/bwd against MPGBlock's prompt arithmetic + the stage loop's residual adds
     + torch.cat under autocast.  Forward: the same fp32 ops in the same order, bit-exact.
     Backward: dx_rgb / dx_dte are the halves of the incoming gradient (exact); the tfts
@@ -438,8 +439,9 @@ def test_mpg_residual_matches_module_math(C, L):
     torch.manual_seed(C)
     B = 2
     x = (torch.randn(B, L, C, device=DEV)).bfloat16().requires_grad_()
-    xr = torch.randn(B, L, C, device=DEV, requires_grad=True)
-    xd = torch.randn(B, L, C, device=DEV, requires_grad=True)
+    # stream inputs fp32 (stage 0) or bf16 (stages 1-3: PatchMerging's GEMM output)
+    xr = torch.randn(B, L, C, device=DEV).to(sdt).requires_grad_()
+    xd = torch.randn(B, L, C, device=DEV).to(sdt).requires_grad_()
     prm = [(torch.randn(C, device=DEV) * 0.1 + (1.0 if i % 2 == 0 else 0.0)).requires_grad_() for i in range(4)]
     g = torch.randn(2 * B, L, C, device=DEV)
     with torch.autocast("cuda", dtype=torch.bfloat16):
