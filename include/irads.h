@@ -254,6 +254,18 @@ int irads_mpg_bwd(const float *grad, const uint16_t *x, const float *gamma_rgb, 
                   uint16_t *grad_x, float *partials, void *stream);
 long irads_mpg_partials(long R, int C);
 
+/* Trainable LayerNorm on bf16 rows with an fp32 result (the patch embeddings' norm, PatchEmbed
+ * in semseg/models/backbones/swin.py -> mmcv LN, run by autocast in fp32 on the bf16 projection
+ * output).  Forward: y = (x - mean) * rstd * gamma + beta (fp32, biased variance), mean / rstd
+ * (M fp32) saved.  Backward: dx bf16 = rstd * (dy*g - mean(dy*g) - xhat * mean(dy*g*xhat)) and
+ * partials [block][2][C] = (sum dy*xhat, sum dy), irads_ln_bf16_partials(M, C) floats, summed
+ * over blocks by the caller.  C in {64, 128, 192, 256}. */
+int irads_ln_bf16_fwd(const uint16_t *x, const float *gamma, const float *beta, long M, int C, float eps, float *y,
+                      float *mean, float *rstd, void *stream);
+int irads_ln_bf16_bwd(const float *dy, const uint16_t *x, const float *mean, const float *rstd, const float *gamma,
+                      long M, int C, uint16_t *dx, float *partials, void *stream);
+long irads_ln_bf16_partials(long M, int C);
+
 /* The two Adapters of a block (MLP_RGB_Adapter / MLP_DTE_Adapter, swin.py:472-502:
  * D_fc2(dropout(ReLU(D_fc1(x)))), D_fc1: C -> R, D_fc2: R -> C) on the rgb+dte row batch:
  * rows [0, Mh) use weights w0 / b0, rows [Mh, M) w1 / b1 (M, Mh multiples of 16, R <= 128).

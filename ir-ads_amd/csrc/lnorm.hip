@@ -1,0 +1,150 @@
+// Trainable LayerNorm on bf16 rows with an fp32 result: the patch embeddings' norm
+// (reference semseg/models/backbones/swin.py PatchEmbed -> mmcv build_norm_layer LN, run by
+// autocast in fp32 on the bf16 projection output).  torch runs it as a cast kernel, its
+// generic LayerNorm kernel and three backward kernels (input, partial and final gamma/beta
+// reductions) over 128-wide rows; here it is one pass each way.
+//
+// Forward: one wave per row, C/64 values per lane held in registers; mean and variance in
+//   fp32 (two passes over the registers, biased variance like torch), y = (x - mean) * rstd
+//   * gamma + beta in fp32; mean / rstd saved.
+// Backward: one wave per row again; dx = rstd * (dy*g - mean(dy*g) - xhat * mean(dy*g*xhat))
+//   written as bf16 (the input's dtype), and per-workgroup partial sums of dy*xhat (dgamma)
+//   and dy (dbeta) in a fixed order, summed over workgroups by the caller (deterministic).
+#include "common.h"
+
+namespace irads {
+namespace {
+
+constexpr int kWaves = 4;  // rows in flight per workgroup
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+template <int V>  // V = C / 64 values per lane (lane owns channels lane + 64 k)
+__global__ __launch_bounds__(256) void ln_fwd_kernel(const unsigned short *__restrict__ x, const float *__restrict__ g,
+                                                     const float *__restrict__ b, long M, float eps,
+                                                     float *__restrict__ y, float *__restrict__ mean,
+                                                     float *__restrict__ rstd) {
+    constexpr int C = 64 * V;
+    const int lane = threadIdx.x & 63;
+    float gv[V], bv[V];
+#pragma unroll
+    for (int k = 0; k < V; ++k) gv[k] = g[lane + 64 * k], bv[k] = b[lane + 64 * k];
+    for (long r = (long)blockIdx.x * kWaves + (threadIdx.x >> 6); r < M; r += (long)gridDim.x * kWaves) {
+        float v[V];
+        float s = 0.f;
+#pragma unroll
+        for (int k = 0; k < V; ++k) {
+            v[k] = bf2f(x[r * C + lane + 64 * k]);
+            s += v[k];
+        }
+        const float mu = wave_sum(s) / (float)C;
+        float q = 0.f;
+#pragma unroll
+        for (int k = 0; k < V; ++k) {
+            const float d = v[k] - mu;
+            q += d * d;
+        }
+        const float rs = rsqrtf(wave_sum(q) / (float)C + eps);
+#pragma unroll
+        for (int k = 0; k < V; ++k) y[r * C + lane + 64 * k] = (v[k] - mu) * rs * gv[k] + bv[k];
+        if (lane == 0) {
+            mean[r] = mu;
+            rstd[r] = rs;
+        }
+    }
+}
+
+template <int V>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const float *__restrict__ dy, const unsigned short *__restrict__ x,
+                                                     const float *__restrict__ mean, const float *__restrict__ rstd,
+                                                     const float *__restrict__ g, long M,
+                                                     unsigned short *__restrict__ dx, float *__restrict__ part) {
+    constexpr int C = 64 * V;
+    __shared__ float red[kWaves][2][C];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    float gv[V], sg[V], sb[V];
+#pragma unroll
+    for (int k = 0; k < V; ++k) gv[k] = g[lane + 64 * k], sg[k] = sb[k] = 0.f;
+    for (long r = (long)blockIdx.x * kWaves + wv; r < M; r += (long)gridDim.x * kWaves) {
+        const float mu = mean[r], rs = rstd[r];
+        float xh[V], d[V];
+        float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int k = 0; k < V; ++k) {
+            const long i = r * C + lane + 64 * k;
+            xh[k] = (bf2f(x[i]) - mu) * rs;
+            const float dyk = dy[i];
+            d[k] = dyk * gv[k];
+            s1 += d[k];
+            s2 += d[k] * xh[k];
+            sg[k] += dyk * xh[k];
+            sb[k] += dyk;
+        }
+        const float m1 = wave_sum(s1) / (float)C, m2 = wave_sum(s2) / (float)C;
+#pragma unroll
+        for (int k = 0; k < V; ++k) dx[r * C + lane + 64 * k] = f2bf(rs * (d[k] - m1 - xh[k] * m2));
+    }
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+        red[wv][0][lane + 64 * k] = sg[k];
+        red[wv][1][lane + 64 * k] = sb[k];
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < 2 * C; c += blockDim.x) {
+        const int q = c / C, cc = c % C;
+        float t = 0.f;
+#pragma unroll
+        for (int w = 0; w < kWaves; ++w) t += red[w][q][cc];
+        part[((long)blockIdx.x * 2 + q) * C + cc] = t;
+    }
+}
+
+int ln_blocks(long M) {
+    const long b = (M + kWaves - 1) / kWaves;
+    return (int)(b < 2048 ? b : 2048);  // ~8 workgroups per CU, each walking M / (2048·4) rows
+}
+
+}  // namespace
+}  // namespace irads
+
+using namespace irads;
+
+#define IRADS_LN_CHECK(fn)                                                                                 \
+    IRADS_REQUIRE(M > 0 && (C == 64 || C == 128 || C == 192 || C == 256),                                  \
+                  fn ": need M > 0 and C in {64, 128, 192, 256} (M=%ld C=%d)", M, C)
+
+extern "C" long irads_ln_bf16_partials(long M, int C) { return (long)ln_blocks(M) * 2 * C; }
+
+extern "C" int irads_ln_bf16_fwd(const uint16_t *x, const float *gamma, const float *beta, long M, int C, float eps,
+                                 float *y, float *mean, float *rstd, void *stream) {
+    IRADS_LN_CHECK("irads_ln_bf16_fwd");
+    IRADS_REQUIRE(x && gamma && beta && y && mean && rstd, "irads_ln_bf16_fwd: null pointer");
+    hipStream_t st = (hipStream_t)stream;
+    const dim3 grid(ln_blocks(M));
+    switch (C / 64) {
+        case 1: ln_fwd_kernel<1><<<grid, 256, 0, st>>>(x, gamma, beta, M, eps, y, mean, rstd); break;
+        case 2: ln_fwd_kernel<2><<<grid, 256, 0, st>>>(x, gamma, beta, M, eps, y, mean, rstd); break;
+        case 3: ln_fwd_kernel<3><<<grid, 256, 0, st>>>(x, gamma, beta, M, eps, y, mean, rstd); break;
+        default: ln_fwd_kernel<4><<<grid, 256, 0, st>>>(x, gamma, beta, M, eps, y, mean, rstd); break;
+    }
+    return check_launch("irads_ln_bf16_fwd");
+}
+
+extern "C" int irads_ln_bf16_bwd(const float *dy, const uint16_t *x, const float *mean, const float *rstd,
+                                 const float *gamma, long M, int C, uint16_t *dx, float *partials, void *stream) {
+    IRADS_LN_CHECK("irads_ln_bf16_bwd");
+    IRADS_REQUIRE(dy && x && mean && rstd && gamma && dx && partials, "irads_ln_bf16_bwd: null pointer");
+    hipStream_t st = (hipStream_t)stream;
+    const dim3 grid(ln_blocks(M));
+    switch (C / 64) {
+        case 1: ln_bwd_kernel<1><<<grid, 256, 0, st>>>(dy, x, mean, rstd, gamma, M, dx, partials); break;
+        case 2: ln_bwd_kernel<2><<<grid, 256, 0, st>>>(dy, x, mean, rstd, gamma, M, dx, partials); break;
+        case 3: ln_bwd_kernel<3><<<grid, 256, 0, st>>>(dy, x, mean, rstd, gamma, M, dx, partials); break;
+        default: ln_bwd_kernel<4><<<grid, 256, 0, st>>>(dy, x, mean, rstd, gamma, M, dx, partials); break;
+    }
+    return check_launch("irads_ln_bf16_bwd");
+}

@@ -52,6 +52,8 @@ SIGNATURES = {
     "irads_bnact_bwd": [_vp, _vp, _l, _i, _l] + [_vp] * 10,
     "irads_mpg_fwd": [_vp] * 7 + [_l, _i, _vp, _vp],
     "irads_mpg_fwd_bf16": [_vp] * 7 + [_l, _i, _vp, _vp],
+    "irads_ln_bf16_fwd": [_vp] * 3 + [_l, _i, _f] + [_vp] * 4,
+    "irads_ln_bf16_bwd": [_vp] * 5 + [_l, _i, _vp, _vp, _vp],
     "irads_mpg_bwd": [_vp] * 4 + [_l, _i, _vp, _vp, _vp],
     "irads_adapter_down": [_i, _vp, _vp, _vp, _vp, _vp, _vp, _l, _l, _i, _i, _f, _u64, _u64, _vp, _vp, _vp],
     "irads_adapter_up": [_vp, _vp, _vp, _vp, _vp, _l, _l, _i, _i, _vp, _vp],
@@ -64,6 +66,7 @@ QUERIES = {"irads_wgrad_workspace": (ctypes.c_long, [_i, _i, _i]),
            "irads_dattn_offset_partials": (ctypes.c_long, [_i] * 8),
            "irads_wgrad_batched_workspace": (ctypes.c_long, [_i] * 4),
            "irads_mpg_partials": (ctypes.c_long, [_l, _i]),
+           "irads_ln_bf16_partials": (ctypes.c_long, [_l, _i]),
            "irads_bnact_partials": (ctypes.c_long, [_l, _i])}
 CE_WORKSPACE = 2048
 

@@ -874,6 +874,58 @@ class LayerNormBF16Fn(torch.autograd.Function):
         return dx.view(ctx.shape).to(ctx.in_dtype), None, None, None
 
 
+class LayerNormFromBF16Fn(torch.autograd.Function):
+    """Trainable nn.LayerNorm on a bf16 input under autocast (fp32 math, fp32 result) as one
+    irads_ln_bf16_fwd pass; backward: one irads_ln_bf16_bwd pass (bf16 dx) plus the summed
+    per-workgroup gamma / beta partials."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, eps):
+        shape = x.shape
+        C = shape[-1]
+        x2 = x.reshape(-1, C)
+        if not x2.is_contiguous():
+            x2 = x2.contiguous()
+        M = x2.shape[0]
+        y = torch.empty(shape, device=x.device, dtype=torch.float32)  # not a view: callers modify it in place
+        mean = torch.empty((M,), device=x.device, dtype=torch.float32)
+        rstd = torch.empty_like(mean)
+        w, b = weight.detach().float().contiguous(), bias.detach().float().contiguous()
+        N.call("irads_ln_bf16_fwd", N.ptr(x2), N.ptr(w), N.ptr(b), M, C, float(eps), N.ptr(y), N.ptr(mean),
+               N.ptr(rstd), N.stream())
+        ctx.save_for_backward(x2, w, mean, rstd)
+        ctx.shape = shape
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x2, w, mean, rstd = ctx.saved_tensors
+        M, C = x2.shape
+        g = gy.reshape(M, C)
+        if g.dtype != torch.float32 or not g.is_contiguous():
+            g = g.float().contiguous()
+        dx = torch.empty((M, C), device=x2.device, dtype=torch.bfloat16)
+        parts = torch.empty((N.load().irads_ln_bf16_partials(M, C),), device=g.device, dtype=torch.float32)
+        N.call("irads_ln_bf16_bwd", N.ptr(g), N.ptr(x2), N.ptr(mean), N.ptr(rstd), N.ptr(w), M, C, N.ptr(dx),
+               N.ptr(parts), N.stream())
+        s = parts.view(-1, 2, C).sum(0)
+        return dx.view(ctx.shape), s[0], s[1], None
+
+
+def layer_norm_from_bf16_ok(x, norm):
+    return (x.is_cuda and x.dtype == torch.bfloat16 and torch.is_autocast_enabled("cuda")
+            and isinstance(norm, torch.nn.LayerNorm) and norm.elementwise_affine and norm.bias is not None
+            and len(norm.normalized_shape) == 1 and x.shape[-1] in (64, 128, 192, 256))
+
+
+def layer_norm_from_bf16(x, norm):
+    """norm(x) for a bf16 x under bf16 autocast (fp32 result, as autocast's LayerNorm)."""
+    if layer_norm_from_bf16_ok(x, norm):
+        with torch.autocast("cuda", enabled=False):
+            return LayerNormFromBF16Fn.apply(x, norm.weight, norm.bias, norm.eps)
+    return norm(x)
+
+
 class LayerNormPairBF16Fn(torch.autograd.Function):
     """Two LayerNorms (own weights) on the two stream halves of one (2B, ...) fp32 tensor, as
     the bf16 operands of the following Linears (see LayerNormBF16Fn).  Taking the whole tensor

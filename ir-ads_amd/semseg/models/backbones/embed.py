@@ -100,7 +100,7 @@ class PatchEmbed(nn.Module):
             out_size = (x.shape[2], x.shape[3])
             x = x.flatten(2).transpose(1, 2)
         if self.norm is not None:
-            x = self.norm(x)
+            x = ops.layer_norm_from_bf16(x, self.norm)  # = self.norm(x) under autocast, one kernel
         return x, out_size
 
 

@@ -488,3 +488,34 @@ def test_patch_embed_gemm_matches_conv():
     assert _rel(y1, y0) < 1e-2
     for a, b in zip(g1, g0):
         assert _rel(a, b) < 1e-2
+
+
+@pytest.mark.parametrize("C,M", [(128, 131072), (192, 3000), (64, 77), (256, 1000)])
+def test_layer_norm_from_bf16_matches_autocast(C, M):
+    """irads_ln_bf16_fwd/bwd (PatchEmbed's trainable norm on the bf16 projection output)
+    against nn.LayerNorm under bf16 autocast (fp32 math on the upcast input).  Forward and
+    the gamma / beta gradients are fp32 sums in another order (rtol 1e-5 / 1e-4); dx is one
+    bf16 rounding of the fp32 result."""
+    from irads import ops
+    torch.manual_seed(C + M)
+    norm = torch.nn.LayerNorm(C).to(DEV)
+    with torch.no_grad():
+        norm.weight.copy_(torch.randn(C) * 0.2 + 1)
+        norm.bias.copy_(torch.randn(C) * 0.1)
+    x = (torch.randn(2, M // 2 if M % 2 == 0 else M, C, device=DEV) * 3 + 0.5).bfloat16()
+    g = torch.randn(x.shape, device=DEV)
+    outs = []
+    for fn in (lambda t: norm(t), lambda t: ops.layer_norm_from_bf16(t, norm)):
+        xx = x.clone().requires_grad_()
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = fn(xx)
+        outs.append((y,) + torch.autograd.grad(y, [xx, norm.weight, norm.bias], g))
+    (y0, dx0, dw0, db0), (y1, dx1, dw1, db1) = outs
+    assert y1.dtype == y0.dtype == torch.float32 and dx1.dtype == torch.bfloat16
+    torch.testing.assert_close(y1, y0, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(dx1.float(), dx0.float(), rtol=2 ** -7, atol=1e-3)
+    torch.testing.assert_close(dw1, dw0, rtol=1e-4, atol=1e-2)
+    torch.testing.assert_close(db1, db0, rtol=1e-4, atol=1e-2)
+    with torch.autocast("cuda", dtype=torch.bfloat16):  # the output may be modified in place (apply_mask)
+        y = ops.layer_norm_from_bf16(x.clone().requires_grad_(), norm)
+    y[0].zero_()
