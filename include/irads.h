@@ -266,6 +266,16 @@ int irads_ln_bf16_bwd(const float *dy, const uint16_t *x, const float *mean, con
                       long M, int C, uint16_t *dx, float *partials, void *stream);
 long irads_ln_bf16_partials(long M, int C);
 
+/* PatchMerging's 2x2 unfold + frozen LayerNorm(4C) (mmcv PatchMerging: nn.Unfold(2, stride 2),
+ * norm, reduction) as one gather: x fp32 (Bt, H, W, C) token-major -> y bf16 (Bt, H/2, W/2, 4C)
+ * with row element 4c + 2i + j = LN(x[b, 2oh+i, 2ow+j, c]) (nn.Unfold's order); mean / rstd per
+ * output token.  Backward: dy bf16 -> dx fp32 (Bt, H, W, C), each element written once.
+ * H, W even; C in {128, 192, 256, 384, 512, 768}. */
+int irads_merge_ln_fwd(const float *x, int Bt, int H, int W, int C, const float *gamma, const float *beta, float eps,
+                       uint16_t *y, float *mean, float *rstd, void *stream);
+int irads_merge_ln_bwd(const uint16_t *dy, const float *x, int Bt, int H, int W, int C, const float *mean,
+                       const float *rstd, const float *gamma, float *dx, void *stream);
+
 /* The two Adapters of a block (MLP_RGB_Adapter / MLP_DTE_Adapter, swin.py:472-502:
  * D_fc2(dropout(ReLU(D_fc1(x)))), D_fc1: C -> R, D_fc2: R -> C) on the rgb+dte row batch:
  * rows [0, Mh) use weights w0 / b0, rows [Mh, M) w1 / b1 (M, Mh multiples of 16, R <= 128).

@@ -15,7 +15,7 @@
 namespace irads {
 namespace {
 
-constexpr int kWaves = 4;  // rows in flight per workgroup
+constexpr int kWaves = 4;  // rows in flight per workgroup (one wave per row)
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
@@ -103,6 +103,109 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float *__restrict__ d
     }
 }
 
+// ---------------------------------------------------------------- PatchMerging gather + norm
+// PatchMerging (reference mmcv PatchMerging in semseg/models/backbones/swin.py: nn.Unfold
+// 2x2/2 + LayerNorm(4C) + Linear): the 2x2 unfold as the LayerNorm's read pattern.  Output
+// token (b, oh, ow) is the row p = 4c + 2i + j <- x[b, 2oh+i, 2ow+j, c] (nn.Unfold's
+// channel-major order), normalised in fp32 with the frozen affine and written as the bf16
+// operand of the reduction GEMM.  Lane l owns channels c = l + 64k (k < V) and all four
+// (i, j) of each: every load is a 256-B row segment of one source token, every store 8 B per
+// lane over a contiguous 512-B run.  The backward recomputes xhat from the same gather and
+// scatters dx (fp32) back to the source tokens: each source element is written exactly once.
+template <int V>
+__global__ __launch_bounds__(256) void merge_ln_fwd_kernel(const float *__restrict__ x, int Bt, int H, int W,
+                                                           const float *__restrict__ g, const float *__restrict__ b,
+                                                           float eps, unsigned short *__restrict__ y,
+                                                           float *__restrict__ mean, float *__restrict__ rstd) {
+    constexpr int C = 64 * V, C4 = 4 * C;
+    const int lane = threadIdx.x & 63;
+    const int Ho = H / 2, Wo = W / 2;
+    const long M = (long)Bt * Ho * Wo;
+    for (long r = (long)blockIdx.x * kWaves + (threadIdx.x >> 6); r < M; r += (long)gridDim.x * kWaves) {
+        const int ow = (int)(r % Wo), oh = (int)((r / Wo) % Ho);
+        const long bb = r / ((long)Wo * Ho);
+        const float *src = x + ((bb * H + 2 * oh) * W + 2 * ow) * C + lane;
+        float v[V][4];
+        float s = 0.f;
+#pragma unroll
+        for (int k = 0; k < V; ++k)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {  // q = 2i + j
+                v[k][q] = src[((q >> 1) * W + (q & 1)) * C + 64 * k];
+                s += v[k][q];
+            }
+        const float mu = wave_sum(s) / (float)C4;
+        float ss = 0.f;
+#pragma unroll
+        for (int k = 0; k < V; ++k)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float d = v[k][q] - mu;
+                ss += d * d;
+            }
+        const float rs = rsqrtf(wave_sum(ss) / (float)C4 + eps);
+#pragma unroll
+        for (int k = 0; k < V; ++k) {
+            const int p = 4 * (lane + 64 * k);
+            const float4 gg = *reinterpret_cast<const float4 *>(g + p), be = *reinterpret_cast<const float4 *>(b + p);
+            const float gq[4] = {gg.x, gg.y, gg.z, gg.w}, bq[4] = {be.x, be.y, be.z, be.w};
+            unsigned short o[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) o[q] = f2bf((v[k][q] - mu) * rs * gq[q] + bq[q]);
+            uint2 w;
+            w.x = (unsigned)o[0] | ((unsigned)o[1] << 16);
+            w.y = (unsigned)o[2] | ((unsigned)o[3] << 16);
+            *reinterpret_cast<uint2 *>(y + r * C4 + p) = w;
+        }
+        if (lane == 0) {
+            mean[r] = mu;
+            rstd[r] = rs;
+        }
+    }
+}
+
+template <int V>
+__global__ __launch_bounds__(256) void merge_ln_bwd_kernel(const unsigned short *__restrict__ dy,
+                                                           const float *__restrict__ x, int Bt, int H, int W,
+                                                           const float *__restrict__ mean,
+                                                           const float *__restrict__ rstd,
+                                                           const float *__restrict__ g, float *__restrict__ dx) {
+    constexpr int C = 64 * V, C4 = 4 * C;
+    const int lane = threadIdx.x & 63;
+    const int Ho = H / 2, Wo = W / 2;
+    const long M = (long)Bt * Ho * Wo;
+    for (long r = (long)blockIdx.x * kWaves + (threadIdx.x >> 6); r < M; r += (long)gridDim.x * kWaves) {
+        const int ow = (int)(r % Wo), oh = (int)((r / Wo) % Ho);
+        const long bb = r / ((long)Wo * Ho);
+        const long base = ((bb * H + 2 * oh) * W + 2 * ow) * C + lane;
+        const float mu = mean[r], rs = rstd[r];
+        float xh[V][4], d[V][4];
+        float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int k = 0; k < V; ++k) {
+            const int p = 4 * (lane + 64 * k);
+            const uint2 w = *reinterpret_cast<const uint2 *>(dy + r * C4 + p);
+            const float4 gg = *reinterpret_cast<const float4 *>(g + p);
+            const float dq[4] = {bf2f((unsigned short)(w.x & 0xffffu)), bf2f((unsigned short)(w.x >> 16)),
+                                 bf2f((unsigned short)(w.y & 0xffffu)), bf2f((unsigned short)(w.y >> 16))};
+            const float gq[4] = {gg.x, gg.y, gg.z, gg.w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                xh[k][q] = (x[base + ((q >> 1) * W + (q & 1)) * C + 64 * k] - mu) * rs;
+                d[k][q] = dq[q] * gq[q];
+                s1 += d[k][q];
+                s2 += d[k][q] * xh[k][q];
+            }
+        }
+        const float m1 = wave_sum(s1) / (float)C4, m2 = wave_sum(s2) / (float)C4;
+#pragma unroll
+        for (int k = 0; k < V; ++k)
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                dx[base + ((q >> 1) * W + (q & 1)) * C + 64 * k] = rs * (d[k][q] - m1 - xh[k][q] * m2);
+    }
+}
+
 int ln_blocks(long M) {
     const long b = (M + kWaves - 1) / kWaves;
     return (int)(b < 2048 ? b : 2048);  // ~8 workgroups per CU, each walking M / (2048·4) rows
@@ -147,4 +250,47 @@ extern "C" int irads_ln_bf16_bwd(const float *dy, const uint16_t *x, const float
         default: ln_bwd_kernel<4><<<grid, 256, 0, st>>>(dy, x, mean, rstd, gamma, M, dx, partials); break;
     }
     return check_launch("irads_ln_bf16_bwd");
+}
+
+#define IRADS_MERGE_CHECK(fn)                                                                                     \
+    IRADS_REQUIRE(Bt > 0 && H > 0 && W > 0 && H % 2 == 0 && W % 2 == 0 &&                                         \
+                      (C == 128 || C == 192 || C == 256 || C == 384 || C == 512 || C == 768),                     \
+                  fn ": need even H, W and C in {128, 192, 256, 384, 512, 768} (H=%d W=%d C=%d)", H, W, C)
+
+extern "C" int irads_merge_ln_fwd(const float *x, int Bt, int H, int W, int C, const float *gamma, const float *beta,
+                                  float eps, uint16_t *y, float *mean, float *rstd, void *stream) {
+    IRADS_MERGE_CHECK("irads_merge_ln_fwd");
+    IRADS_REQUIRE(x && gamma && beta && y && mean && rstd, "irads_merge_ln_fwd: null pointer");
+    hipStream_t st = (hipStream_t)stream;
+    const dim3 grid(ln_blocks((long)Bt * (H / 2) * (W / 2)));
+#define IRADS_MF(VV) merge_ln_fwd_kernel<VV><<<grid, 256, 0, st>>>(x, Bt, H, W, gamma, beta, eps, y, mean, rstd)
+    switch (C / 64) {
+        case 2: IRADS_MF(2); break;
+        case 3: IRADS_MF(3); break;
+        case 4: IRADS_MF(4); break;
+        case 6: IRADS_MF(6); break;
+        case 8: IRADS_MF(8); break;
+        default: IRADS_MF(12); break;
+    }
+#undef IRADS_MF
+    return check_launch("irads_merge_ln_fwd");
+}
+
+extern "C" int irads_merge_ln_bwd(const uint16_t *dy, const float *x, int Bt, int H, int W, int C, const float *mean,
+                                  const float *rstd, const float *gamma, float *dx, void *stream) {
+    IRADS_MERGE_CHECK("irads_merge_ln_bwd");
+    IRADS_REQUIRE(dy && x && mean && rstd && gamma && dx, "irads_merge_ln_bwd: null pointer");
+    hipStream_t st = (hipStream_t)stream;
+    const dim3 grid(ln_blocks((long)Bt * (H / 2) * (W / 2)));
+#define IRADS_MB(VV) merge_ln_bwd_kernel<VV><<<grid, 256, 0, st>>>(dy, x, Bt, H, W, mean, rstd, gamma, dx)
+    switch (C / 64) {
+        case 2: IRADS_MB(2); break;
+        case 3: IRADS_MB(3); break;
+        case 4: IRADS_MB(4); break;
+        case 6: IRADS_MB(6); break;
+        case 8: IRADS_MB(8); break;
+        default: IRADS_MB(12); break;
+    }
+#undef IRADS_MB
+    return check_launch("irads_merge_ln_bwd");
 }

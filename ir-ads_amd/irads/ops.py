@@ -926,6 +926,43 @@ def layer_norm_from_bf16(x, norm):
     return norm(x)
 
 
+class PatchMergeNormFn(torch.autograd.Function):
+    """PatchMerging's 2x2 unfold + frozen LayerNorm(4C) under bf16 autocast as one gather pass
+    (irads_merge_ln_fwd): x fp32 (B, H*W, C) -> the bf16 operand (B, H*W/4, 4C) of `reduction`,
+    without the permuted fp32 copy; backward scatters dx straight into (B, H*W, C)."""
+
+    @staticmethod
+    def forward(ctx, x, H, W, weight, bias, eps):
+        B, L, C = x.shape
+        xc = x.contiguous()
+        M = B * (H // 2) * (W // 2)
+        y = torch.empty((B, (H // 2) * (W // 2), 4 * C), device=x.device, dtype=torch.bfloat16)
+        mean = torch.empty((M,), device=x.device, dtype=torch.float32)
+        rstd = torch.empty_like(mean)
+        w, b = weight.detach().float().contiguous(), bias.detach().float().contiguous()
+        N.call("irads_merge_ln_fwd", N.ptr(xc), B, H, W, C, N.ptr(w), N.ptr(b), float(eps), N.ptr(y), N.ptr(mean),
+               N.ptr(rstd), N.stream())
+        ctx.save_for_backward(xc, w, mean, rstd)
+        ctx.cfg = (B, H, W, C)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        xc, w, mean, rstd = ctx.saved_tensors
+        B, H, W, C = ctx.cfg
+        g = gy if gy.dtype == torch.bfloat16 and gy.is_contiguous() else gy.to(torch.bfloat16).contiguous()
+        dx = torch.empty_like(xc)
+        N.call("irads_merge_ln_bwd", N.ptr(g), N.ptr(xc), B, H, W, C, N.ptr(mean), N.ptr(rstd), N.ptr(w), N.ptr(dx),
+               N.stream())
+        return dx, None, None, None, None, None
+
+
+def patch_merge_norm_ok(x, H, W, norm):
+    C = x.shape[-1]
+    return (ln_bf16_ok(x, norm) and x.dtype == torch.float32 and x.dim() == 3 and x.shape[1] == H * W
+            and H % 2 == 0 and W % 2 == 0 and C in (128, 192, 256, 384, 512, 768))
+
+
 class LayerNormPairBF16Fn(torch.autograd.Function):
     """Two LayerNorms (own weights) on the two stream halves of one (2B, ...) fp32 tensor, as
     the bf16 operands of the following Linears (see LayerNormBF16Fn).  Taking the whole tensor

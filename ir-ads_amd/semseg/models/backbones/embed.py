@@ -129,6 +129,14 @@ class PatchMerging(nn.Module):
         assert isinstance(input_size, Sequence), f'Expect input_size is `Sequence` but get {input_size}'
         H, W = input_size
         assert L == H * W, 'input feature has wrong size'
+        s = self.sampler
+        no_pad = not self.adap_padding or tuple(self.adap_padding.get_pad_shape((H, W))) == (0, 0)
+        if (self.norm is not None and no_pad and s.kernel_size == s.stride == (2, 2)
+                and s.padding == (0, 0) and s.dilation == (1, 1) and ops.patch_merge_norm_ok(x, H, W, self.norm)):
+            # the 2x2 unfold as the LayerNorm's gather (one HIP pass each way, no permuted copy)
+            with torch.autocast("cuda", enabled=False):
+                xm = ops.PatchMergeNormFn.apply(x, H, W, self.norm.weight, self.norm.bias, self.norm.eps)
+            return self.reduction(xm), (H // 2, W // 2)
         x = x.view(B, H, W, C).permute([0, 3, 1, 2])
         if self.adap_padding:
             x = self.adap_padding(x)

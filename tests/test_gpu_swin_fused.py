@@ -519,3 +519,31 @@ def test_layer_norm_from_bf16_matches_autocast(C, M):
     with torch.autocast("cuda", dtype=torch.bfloat16):  # the output may be modified in place (apply_mask)
         y = ops.layer_norm_from_bf16(x.clone().requires_grad_(), norm)
     y[0].zero_()
+
+
+@pytest.mark.parametrize("C,H,W", [(128, 64, 64), (256, 32, 32), (512, 16, 16), (192, 12, 20)])
+def test_patch_merge_norm_matches_unfold_path(C, H, W):
+    """irads_merge_ln_fwd/bwd (PatchMerging's 2x2 unfold as the frozen LayerNorm's gather)
+    against nn.Unfold + LayerNorm(4C) under autocast (fp32 math, bf16 operand of the
+    reduction): one bf16 rounding apart in the forward; dx fp32 within the rounding of the
+    bf16 incoming gradient's fp32 LayerNorm backward (rtol 1e-4)."""
+    from irads import ops
+    torch.manual_seed(C + H)
+    B = 3
+    norm = torch.nn.LayerNorm(4 * C).to(DEV).requires_grad_(False)
+    with torch.no_grad():
+        norm.weight.copy_(torch.randn(4 * C) * 0.2 + 1)
+        norm.bias.copy_(torch.randn(4 * C) * 0.1)
+    x = torch.randn(B, H * W, C, device=DEV) * 2 + 0.3
+    g = torch.randn(B, H * W // 4, 4 * C, device=DEV).bfloat16()
+    xa = x.clone().requires_grad_()
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        unf = torch.nn.functional.unfold(xa.view(B, H, W, C).permute(0, 3, 1, 2), 2, stride=2).transpose(1, 2)
+        ya = norm(unf).to(torch.bfloat16)
+    (dxa,) = torch.autograd.grad(ya, xa, g)
+    xb = x.clone().requires_grad_()
+    yb = ops.PatchMergeNormFn.apply(xb, H, W, norm.weight, norm.bias, norm.eps)
+    (dxb,) = torch.autograd.grad(yb, xb, g)
+    assert yb.dtype == torch.bfloat16 and yb.shape == ya.shape
+    torch.testing.assert_close(yb.float(), ya.float(), rtol=2 ** -7, atol=1e-2)
+    torch.testing.assert_close(dxb, dxa, rtol=1e-4, atol=1e-4)
