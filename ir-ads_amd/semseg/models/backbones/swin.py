@@ -396,6 +396,19 @@ class DAttentionMM(nn.Module):
         gx = torch.arange(0, W, dtype=dtype, device=device).div(W - 1.0).mul(2.0).sub(1.0)
         return gy, gx
 
+    def _amp_consts(self, H, W, Hk, Wk, dtype, device):
+        """Reference points (Hk*Wk, 2) and the fp32 query-grid axes of _forward_amp: constants
+        of the shapes, built once (not re-launched every step; a graph captures the cached
+        tensors).  Kept out of the state dict."""
+        cache = self.__dict__.setdefault("_const_cache", {})
+        key = (H, W, Hk, Wk, dtype, device)
+        if key not in cache:
+            with torch.no_grad():
+                ref = self._get_ref_points(Hk, Wk, 1, dtype, device)[0].reshape(Hk * Wk, 2).contiguous()
+                gy, gx = self._q_grid_axes(H, W, dtype, device)
+                cache[key] = (ref, gy.float(), gx.float())
+        return cache[key]
+
     @staticmethod
     def _tok_linear(conv, x_tok):
         """1x1 nn.Conv2d on token-major input (..., Cin) as a Linear: one bf16 GEMM under
@@ -416,7 +429,7 @@ class DAttentionMM(nn.Module):
         conv = self.conv_offset_x[0]
         Hk = (H + 2 * conv.padding[0] - conv.kernel_size[0]) // conv.stride[0] + 1
         Wk = (W + 2 * conv.padding[1] - conv.kernel_size[1]) // conv.stride[1] + 1
-        ref = self._get_ref_points(Hk, Wk, 1, dtype, device)[0].reshape(Hk * Wk, 2)
+        ref, gy, gx = self._amp_consts(H, W, Hk, Wk, dtype, device)
         pos_x, pos_y = ops.dattn_offsets(x, y, self.conv_offset_x, self.conv_offset_y, g, ref)
         n = Hk * Wk
         xs, ys, qs = ops.DAttnSampleFn.apply(x.float(), y.float(), q32.view(B, C, H, W), pos_x, pos_y, g)
@@ -431,9 +444,8 @@ class DAttentionMM(nn.Module):
             t = self._tok_linear(conv_, s_tok).view(B, 2 * n, nH, hc).permute(0, 2, 1, 3)
             return t.to(torch.float32, memory_format=torch.contiguous_format).view(B * nH, 2 * n, hc).transpose(1, 2)
         k, v = key_major(self.proj_k), key_major(self.proj_v)
-        gy, gx = self._q_grid_axes(H, W, dtype, device)
         out = ops.DAttnAttentionFn.apply(q32.view(B * nH, hc, H * W), k, v, pos_x, pos_y, self.rpe_table.float(),
-                                         gy.float(), gx.float(), B, nH, g, H, W, self.scale)
+                                         gy, gx, B, nH, g, H, W, self.scale)
         out_tok = self._tok_linear(self.proj_out, out.view(B, C, H * W).transpose(1, 2))  # (B, HW, C) bf16
         out = out_tok.transpose(1, 2).view(B, C, H, W)  # proj_drop has p == 0 on this path: identity
         return self.deform_weight[None, :, None, None] * out + self.identity_weight[None, :, None, None] * xy

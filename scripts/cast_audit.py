@@ -24,6 +24,13 @@ WATCH = {"aten._to_copy.default", "aten.copy_.default", "aten.add.Tensor", "aten
          "aten.sum.dim_IntList", "aten.mul.Tensor"}
 
 
+# metadata-only ops (no kernel): skipped under --all-ops
+NO_KERNEL = {"view", "_unsafe_view", "slice.Tensor", "select.int", "detach", "empty.memory_format", "empty_strided",
+             "as_strided", "t", "transpose.int", "permute", "expand", "unsqueeze", "squeeze.dim", "alias",
+             "split.Tensor", "split_with_sizes", "unbind.int", "_reshape_alias", "lift_fresh", "set_.source_Storage",
+             "split_with_sizes.default", "_to_copy.noop", "is_same_size", "new_empty", "resize_"}
+
+
 def site():
     node = torch._C._current_autograd_node()
     if node is not None:
@@ -35,16 +42,18 @@ def site():
 
 
 class Audit(TorchDispatchMode):
-    def __init__(self):
+    def __init__(self, min_numel=1 << 16, watch=WATCH):
         super().__init__()
         self.rows = collections.defaultdict(lambda: [0, 0])
+        self.min_numel, self.watch = min_numel, watch
 
     def __torch_dispatch__(self, func, types, args=(), kwargs=None):
         out = func(*args, **(kwargs or {}))
         name = str(func)
-        if name in WATCH:
+        short = name.replace("aten.", "").replace(".default", "")
+        if (self.watch is None and short not in NO_KERNEL) or (self.watch is not None and name in self.watch):
             t = out if torch.is_tensor(out) else (args[0] if args and torch.is_tensor(args[0]) else None)
-            if t is not None and t.is_cuda and t.numel() >= 1 << 16:
+            if t is not None and t.is_cuda and t.numel() >= self.min_numel:
                 key = (name.replace("aten.", "").replace(".default", ""), site(), tuple(t.shape), str(t.dtype))
                 r = self.rows[key]
                 r[0] += 1
@@ -56,6 +65,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--top", type=int, default=40)
+    ap.add_argument("--all-ops", action="store_true", help="every aten op, not just casts / copies / adds / fills")
+    ap.add_argument("--min-numel", type=int, default=1 << 16)
+    ap.add_argument("--by-count", action="store_true", help="sort sites by calls (launch-bound glue)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.manual_seed(3407)
@@ -64,11 +76,11 @@ def main():
     batch = bench.synthetic_batch(a.batch, 512, dev, 3407)
     bench.train_step(model, opt, sched, loss_fn, batch)
     torch.cuda.synchronize()
-    audit = Audit()
+    audit = Audit(a.min_numel, None if a.all_ops else WATCH)
     with audit:
         bench.train_step(model, opt, sched, loss_fn, batch)
     torch.cuda.synchronize()
-    rows = sorted(audit.rows.items(), key=lambda kv: -kv[1][1])
+    rows = sorted(audit.rows.items(), key=lambda kv: -kv[1][0 if a.by_count else 1])
     print(f"{'MB out':>9} {'calls':>5}  op / site / shape / dtype")
     for (op, st, shape, dt), (n, b) in rows[:a.top]:
         print(f"{b / 1e6:9.1f} {n:5d}  {op:10s} {st[:90]:90s} {list(shape)} {dt.replace('torch.', '')}")
