@@ -266,6 +266,14 @@ int irads_ln_bf16_bwd(const float *dy, const uint16_t *x, const float *mean, con
                       long M, int C, uint16_t *dx, float *partials, void *stream);
 long irads_ln_bf16_partials(long M, int C);
 
+/* Frozen LayerNorm, bf16 rows in and out (DeformMPG's fuse_norm on the bf16 U_fc1 output; its
+ * consumers are Linears): fp32 math as autocast runs it, one bf16 rounding of the result.
+ * Backward: bf16 dy -> bf16 dx, no affine gradients.  C / 64 in {1, 2, 3, 4, 8, 16}. */
+int irads_ln_bf16_bf16_fwd(const uint16_t *x, const float *gamma, const float *beta, long M, int C, float eps,
+                           uint16_t *y, float *mean, float *rstd, void *stream);
+int irads_ln_bf16_bf16_bwd(const uint16_t *dy, const uint16_t *x, const float *mean, const float *rstd,
+                           const float *gamma, long M, int C, uint16_t *dx, void *stream);
+
 /* PatchMerging's 2x2 unfold + frozen LayerNorm(4C) (mmcv PatchMerging: nn.Unfold(2, stride 2),
  * norm, reduction) as one gather: x fp32 (Bt, H, W, C) token-major -> y bf16 (Bt, H/2, W/2, 4C)
  * with row element 4c + 2i + j = LN(x[b, 2oh+i, 2ow+j, c]) (nn.Unfold's order); mean / rstd per

@@ -23,10 +23,17 @@ __device__ __forceinline__ float wave_sum(float v) {
     return v;
 }
 
-template <int V>  // V = C / 64 values per lane (lane owns channels lane + 64 k)
+__device__ __forceinline__ void store_out(float *y, long i, float v) { y[i] = v; }
+__device__ __forceinline__ void store_out(unsigned short *y, long i, float v) { y[i] = f2bf(v); }
+__device__ __forceinline__ float load_in(const float *p, long i) { return p[i]; }
+__device__ __forceinline__ float load_in(const unsigned short *p, long i) { return bf2f(p[i]); }
+
+// V = C / 64 values per lane (lane owns channels lane + 64 k); TO = float (PatchEmbed norm)
+// or bf16 storage (a frozen norm on a bf16 tensor whose consumers are Linears)
+template <int V, typename TO>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(const unsigned short *__restrict__ x, const float *__restrict__ g,
                                                      const float *__restrict__ b, long M, float eps,
-                                                     float *__restrict__ y, float *__restrict__ mean,
+                                                     TO *__restrict__ y, float *__restrict__ mean,
                                                      float *__restrict__ rstd) {
     constexpr int C = 64 * V;
     const int lane = threadIdx.x & 63;
@@ -50,7 +57,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const unsigned short *__res
         }
         const float rs = rsqrtf(wave_sum(q) / (float)C + eps);
 #pragma unroll
-        for (int k = 0; k < V; ++k) y[r * C + lane + 64 * k] = (v[k] - mu) * rs * gv[k] + bv[k];
+        for (int k = 0; k < V; ++k) store_out(y, r * C + lane + 64 * k, (v[k] - mu) * rs * gv[k] + bv[k]);
         if (lane == 0) {
             mean[r] = mu;
             rstd[r] = rs;
@@ -58,8 +65,9 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const unsigned short *__res
     }
 }
 
-template <int V>
-__global__ __launch_bounds__(256) void ln_bwd_kernel(const float *__restrict__ dy, const unsigned short *__restrict__ x,
+// TD = dy storage (fp32 / bf16); part == nullptr: frozen affine, no gamma / beta sums
+template <int V, typename TD>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const TD *__restrict__ dy, const unsigned short *__restrict__ x,
                                                      const float *__restrict__ mean, const float *__restrict__ rstd,
                                                      const float *__restrict__ g, long M,
                                                      unsigned short *__restrict__ dx, float *__restrict__ part) {
@@ -77,7 +85,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float *__restrict__ d
         for (int k = 0; k < V; ++k) {
             const long i = r * C + lane + 64 * k;
             xh[k] = (bf2f(x[i]) - mu) * rs;
-            const float dyk = dy[i];
+            const float dyk = load_in(dy, i);
             d[k] = dyk * gv[k];
             s1 += d[k];
             s2 += d[k] * xh[k];
@@ -88,6 +96,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float *__restrict__ d
 #pragma unroll
         for (int k = 0; k < V; ++k) dx[r * C + lane + 64 * k] = f2bf(rs * (d[k] - m1 - xh[k] * m2));
     }
+    if (part == nullptr) return;  // uniform over the grid
 #pragma unroll
     for (int k = 0; k < V; ++k) {
         red[wv][0][lane + 64 * k] = sg[k];
@@ -229,10 +238,10 @@ extern "C" int irads_ln_bf16_fwd(const uint16_t *x, const float *gamma, const fl
     hipStream_t st = (hipStream_t)stream;
     const dim3 grid(ln_blocks(M));
     switch (C / 64) {
-        case 1: ln_fwd_kernel<1><<<grid, 256, 0, st>>>(x, gamma, beta, M, eps, y, mean, rstd); break;
-        case 2: ln_fwd_kernel<2><<<grid, 256, 0, st>>>(x, gamma, beta, M, eps, y, mean, rstd); break;
-        case 3: ln_fwd_kernel<3><<<grid, 256, 0, st>>>(x, gamma, beta, M, eps, y, mean, rstd); break;
-        default: ln_fwd_kernel<4><<<grid, 256, 0, st>>>(x, gamma, beta, M, eps, y, mean, rstd); break;
+        case 1: ln_fwd_kernel<1, float><<<grid, 256, 0, st>>>(x, gamma, beta, M, eps, y, mean, rstd); break;
+        case 2: ln_fwd_kernel<2, float><<<grid, 256, 0, st>>>(x, gamma, beta, M, eps, y, mean, rstd); break;
+        case 3: ln_fwd_kernel<3, float><<<grid, 256, 0, st>>>(x, gamma, beta, M, eps, y, mean, rstd); break;
+        default: ln_fwd_kernel<4, float><<<grid, 256, 0, st>>>(x, gamma, beta, M, eps, y, mean, rstd); break;
     }
     return check_launch("irads_ln_bf16_fwd");
 }
@@ -244,10 +253,10 @@ extern "C" int irads_ln_bf16_bwd(const float *dy, const uint16_t *x, const float
     hipStream_t st = (hipStream_t)stream;
     const dim3 grid(ln_blocks(M));
     switch (C / 64) {
-        case 1: ln_bwd_kernel<1><<<grid, 256, 0, st>>>(dy, x, mean, rstd, gamma, M, dx, partials); break;
-        case 2: ln_bwd_kernel<2><<<grid, 256, 0, st>>>(dy, x, mean, rstd, gamma, M, dx, partials); break;
-        case 3: ln_bwd_kernel<3><<<grid, 256, 0, st>>>(dy, x, mean, rstd, gamma, M, dx, partials); break;
-        default: ln_bwd_kernel<4><<<grid, 256, 0, st>>>(dy, x, mean, rstd, gamma, M, dx, partials); break;
+        case 1: ln_bwd_kernel<1, float><<<grid, 256, 0, st>>>(dy, x, mean, rstd, gamma, M, dx, partials); break;
+        case 2: ln_bwd_kernel<2, float><<<grid, 256, 0, st>>>(dy, x, mean, rstd, gamma, M, dx, partials); break;
+        case 3: ln_bwd_kernel<3, float><<<grid, 256, 0, st>>>(dy, x, mean, rstd, gamma, M, dx, partials); break;
+        default: ln_bwd_kernel<4, float><<<grid, 256, 0, st>>>(dy, x, mean, rstd, gamma, M, dx, partials); break;
     }
     return check_launch("irads_ln_bf16_bwd");
 }
@@ -293,4 +302,49 @@ extern "C" int irads_merge_ln_bwd(const uint16_t *dy, const float *x, int Bt, in
     }
 #undef IRADS_MB
     return check_launch("irads_merge_ln_bwd");
+}
+
+// frozen LayerNorm, bf16 in -> bf16 out (DeformMPG's fuse_norm on the bf16 U_fc1 output, whose
+// consumers are the heads' Linears); backward bf16 dy -> bf16 dx, no affine gradients.
+#define IRADS_LNB_CHECK(fn)                                                                                \
+    IRADS_REQUIRE(M > 0 && C % 64 == 0 && (C / 64 <= 4 || C / 64 == 8 || C / 64 == 16),                    \
+                  fn ": need M > 0 and C / 64 in {1, 2, 3, 4, 8, 16} (M=%ld C=%d)", M, C)
+
+extern "C" int irads_ln_bf16_bf16_fwd(const uint16_t *x, const float *gamma, const float *beta, long M, int C,
+                                      float eps, uint16_t *y, float *mean, float *rstd, void *stream) {
+    IRADS_LNB_CHECK("irads_ln_bf16_bf16_fwd");
+    IRADS_REQUIRE(x && gamma && beta && y && mean && rstd, "irads_ln_bf16_bf16_fwd: null pointer");
+    hipStream_t st = (hipStream_t)stream;
+    const dim3 grid(ln_blocks(M));
+#define IRADS_LF(VV) ln_fwd_kernel<VV, unsigned short><<<grid, 256, 0, st>>>(x, gamma, beta, M, eps, y, mean, rstd)
+    switch (C / 64) {
+        case 1: IRADS_LF(1); break;
+        case 2: IRADS_LF(2); break;
+        case 3: IRADS_LF(3); break;
+        case 4: IRADS_LF(4); break;
+        case 8: IRADS_LF(8); break;
+        default: IRADS_LF(16); break;
+    }
+#undef IRADS_LF
+    return check_launch("irads_ln_bf16_bf16_fwd");
+}
+
+extern "C" int irads_ln_bf16_bf16_bwd(const uint16_t *dy, const uint16_t *x, const float *mean, const float *rstd,
+                                      const float *gamma, long M, int C, uint16_t *dx, void *stream) {
+    IRADS_LNB_CHECK("irads_ln_bf16_bf16_bwd");
+    IRADS_REQUIRE(dy && x && mean && rstd && gamma && dx, "irads_ln_bf16_bf16_bwd: null pointer");
+    hipStream_t st = (hipStream_t)stream;
+    const dim3 grid(ln_blocks(M));
+#define IRADS_LB(VV) \
+    ln_bwd_kernel<VV, unsigned short><<<grid, 256, 0, st>>>(dy, x, mean, rstd, gamma, M, dx, nullptr)
+    switch (C / 64) {
+        case 1: IRADS_LB(1); break;
+        case 2: IRADS_LB(2); break;
+        case 3: IRADS_LB(3); break;
+        case 4: IRADS_LB(4); break;
+        case 8: IRADS_LB(8); break;
+        default: IRADS_LB(16); break;
+    }
+#undef IRADS_LB
+    return check_launch("irads_ln_bf16_bf16_bwd");
 }

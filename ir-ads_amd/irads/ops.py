@@ -849,12 +849,20 @@ class LayerNormBF16Fn(torch.autograd.Function):
         shape = x.shape
         C = shape[-1]
         x2 = x.reshape(-1, C)
-        if x2.dtype != torch.float32 or not x2.is_contiguous():
-            x2 = x2.float().contiguous()
         M = x2.shape[0]
-        y = torch.empty((M, C), device=x.device, dtype=torch.bfloat16)
         mean = torch.empty((M,), device=x.device, dtype=torch.float32)
         rstd = torch.empty_like(mean)
+        y = torch.empty((M, C), device=x.device, dtype=torch.bfloat16)
+        ctx.bf16_in = x.dtype == torch.bfloat16 and C % 64 == 0 and C // 64 in (1, 2, 3, 4, 8, 16)
+        if ctx.bf16_in:  # bf16 rows in and out: no fp32 copy of the input, bf16 dx in backward
+            x2 = x2.contiguous()
+            N.call("irads_ln_bf16_bf16_fwd", N.ptr(x2), N.ptr(weight.detach()), N.ptr(bias.detach()), M, C,
+                   float(eps), N.ptr(y), N.ptr(mean), N.ptr(rstd), N.stream())
+            ctx.save_for_backward(x2, weight, mean, rstd)
+            ctx.shape, ctx.in_dtype = shape, x.dtype
+            return y.view(*shape)
+        if x2.dtype != torch.float32 or not x2.is_contiguous():
+            x2 = x2.float().contiguous()
         N.call("irads_resln_fwd", N.ptr(x2), None, None, None, 0.0, M, C, max(M, 1), N.ptr(weight.detach()),
                N.ptr(bias.detach()), float(eps), None, N.ptr(y), None, N.ptr(mean), N.ptr(rstd), N.stream())
         ctx.save_for_backward(x2, weight, mean, rstd)
@@ -868,6 +876,11 @@ class LayerNormBF16Fn(torch.autograd.Function):
         g = gy.reshape(M, C)
         if g.dtype != torch.bfloat16 or not g.is_contiguous():
             g = g.to(torch.bfloat16).contiguous()
+        if ctx.bf16_in:
+            dxb = torch.empty((M, C), device=x2.device, dtype=torch.bfloat16)
+            N.call("irads_ln_bf16_bf16_bwd", N.ptr(g), N.ptr(x2), N.ptr(mean), N.ptr(rstd), N.ptr(weight.detach()),
+                   M, C, N.ptr(dxb), N.stream())
+            return dxb.view(ctx.shape), None, None, None
         dx = torch.empty((M, C), device=x2.device, dtype=torch.float32)
         N.call("irads_resln_bwd", N.ptr(g), N.ptr(x2), N.ptr(mean), N.ptr(rstd), N.ptr(weight.detach()), None, None,
                M, C, max(M, 1), N.ptr(dx), None, None, None, 0.0, N.stream())

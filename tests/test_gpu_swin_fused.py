@@ -272,11 +272,13 @@ def test_linear_fn_matches_autocast_linear(out_features):
     assert _rel(gw1, gw0) < 4e-3 and _rel(gb1, gb0) < 4e-3
 
 
+@pytest.mark.parametrize("in_dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("C", [128, 512, 1024, 2048, 3072])
-def test_layer_norm_bf16_matches_autocast(C):
+def test_layer_norm_bf16_matches_autocast(C, in_dtype):
     """ops.layer_norm_bf16 (frozen affine LN feeding a Linear): the bf16 output is autocast's
     fp32 LayerNorm rounded to bf16 (1 ulp on a few elements: reduction order), and dX is
-    autograd's through that cast (relative L2 1e-3)."""
+    autograd's through that cast (relative L2 1e-3).  A bf16 input (DeformMPG's fuse_norm
+    on the U_fc1 output) takes the bf16-in / bf16-out kernels where C / 64 allows."""
     from irads import ops
     torch.manual_seed(C)
     norm = torch.nn.LayerNorm(C).to(DEV)
@@ -284,7 +286,7 @@ def test_layer_norm_bf16_matches_autocast(C):
         norm.weight.uniform_(0.5, 1.5)
         norm.bias.uniform_(-0.2, 0.2)
     norm.requires_grad_(False)
-    x = (torch.randn(2, 333, C, device=DEV) * 2 + 0.3)
+    x = (torch.randn(2, 333, C, device=DEV) * 2 + 0.3).to(in_dtype)
     g = torch.randn(2, 333, C, device=DEV).bfloat16()
     outs = []
     for fused in (False, True):
@@ -298,7 +300,7 @@ def test_layer_norm_bf16_matches_autocast(C):
     assert y1.dtype == torch.bfloat16 and y1.shape == y0.shape
     d = (y1.float() - y0.float()).abs()
     assert (d <= y0.float().abs() * 2 ** -7 + 1e-6).all()
-    assert gx1.dtype == torch.float32 and _rel(gx1, gx0) < 1e-3
+    assert gx1.dtype == in_dtype and _rel(gx1.float(), gx0.float()) < 1e-3
 
 
 @pytest.mark.parametrize("C", [128, 1024])
