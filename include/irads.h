@@ -277,12 +277,13 @@ int irads_ln_bf16_bf16_bwd(const uint16_t *dy, const uint16_t *x, const float *m
 /* PatchMerging's 2x2 unfold + frozen LayerNorm(4C) (mmcv PatchMerging: nn.Unfold(2, stride 2),
  * norm, reduction) as one gather: x fp32 (Bt, H, W, C) token-major -> y bf16 (Bt, H/2, W/2, 4C)
  * with row element 4c + 2i + j = LN(x[b, 2oh+i, 2ow+j, c]) (nn.Unfold's order); mean / rstd per
- * output token.  Backward: dy bf16 -> dx fp32 (Bt, H, W, C), each element written once.
+ * output token.  Backward: dy bf16 -> dx fp32 (Bt, H, W, C), each element written once (added to
+ * dx when accumulate != 0: the stage output's other gradient, written first).
  * H, W even; C in {128, 192, 256, 384, 512, 768}. */
 int irads_merge_ln_fwd(const float *x, int Bt, int H, int W, int C, const float *gamma, const float *beta, float eps,
                        uint16_t *y, float *mean, float *rstd, void *stream);
 int irads_merge_ln_bwd(const uint16_t *dy, const float *x, int Bt, int H, int W, int C, const float *mean,
-                       const float *rstd, const float *gamma, float *dx, void *stream);
+                       const float *rstd, const float *gamma, float *dx, int accumulate, void *stream);
 
 /* The two Adapters of a block (MLP_RGB_Adapter / MLP_DTE_Adapter, swin.py:472-502:
  * D_fc2(dropout(ReLU(D_fc1(x)))), D_fc1: C -> R, D_fc2: R -> C) on the rgb+dte row batch:

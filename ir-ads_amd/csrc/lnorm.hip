@@ -173,7 +173,7 @@ __global__ __launch_bounds__(256) void merge_ln_fwd_kernel(const float *__restri
     }
 }
 
-template <int V>
+template <int V, bool ACC>  // ACC: add into dx (the stage output's other consumers already wrote it)
 __global__ __launch_bounds__(256) void merge_ln_bwd_kernel(const unsigned short *__restrict__ dy,
                                                            const float *__restrict__ x, int Bt, int H, int W,
                                                            const float *__restrict__ mean,
@@ -211,7 +211,11 @@ __global__ __launch_bounds__(256) void merge_ln_bwd_kernel(const unsigned short 
         for (int k = 0; k < V; ++k)
 #pragma unroll
             for (int q = 0; q < 4; ++q)
-                dx[base + ((q >> 1) * W + (q & 1)) * C + 64 * k] = rs * (d[k][q] - m1 - xh[k][q] * m2);
+            {
+                const long i = base + ((q >> 1) * W + (q & 1)) * C + 64 * k;
+                const float v = rs * (d[k][q] - m1 - xh[k][q] * m2);
+                dx[i] = ACC ? __fadd_rn(dx[i], v) : v;  // separately rounded: the fp32 sum autograd would form
+            }
     }
 }
 
@@ -286,12 +290,14 @@ extern "C" int irads_merge_ln_fwd(const float *x, int Bt, int H, int W, int C, c
 }
 
 extern "C" int irads_merge_ln_bwd(const uint16_t *dy, const float *x, int Bt, int H, int W, int C, const float *mean,
-                                  const float *rstd, const float *gamma, float *dx, void *stream) {
+                                  const float *rstd, const float *gamma, float *dx, int accumulate, void *stream) {
     IRADS_MERGE_CHECK("irads_merge_ln_bwd");
     IRADS_REQUIRE(dy && x && mean && rstd && gamma && dx, "irads_merge_ln_bwd: null pointer");
     hipStream_t st = (hipStream_t)stream;
     const dim3 grid(ln_blocks((long)Bt * (H / 2) * (W / 2)));
-#define IRADS_MB(VV) merge_ln_bwd_kernel<VV><<<grid, 256, 0, st>>>(dy, x, Bt, H, W, mean, rstd, gamma, dx)
+#define IRADS_MB(VV)                                                                                    \
+    (accumulate ? merge_ln_bwd_kernel<VV, true><<<grid, 256, 0, st>>>(dy, x, Bt, H, W, mean, rstd, gamma, dx) \
+                : merge_ln_bwd_kernel<VV, false><<<grid, 256, 0, st>>>(dy, x, Bt, H, W, mean, rstd, gamma, dx))
     switch (C / 64) {
         case 2: IRADS_MB(2); break;
         case 3: IRADS_MB(3); break;

@@ -57,7 +57,7 @@ SIGNATURES = {
     "irads_ln_bf16_bf16_fwd": [_vp] * 3 + [_l, _i, _f] + [_vp] * 4,
     "irads_ln_bf16_bf16_bwd": [_vp] * 5 + [_l, _i, _vp, _vp],
     "irads_merge_ln_fwd": [_vp, _i, _i, _i, _i, _vp, _vp, _f, _vp, _vp, _vp, _vp],
-    "irads_merge_ln_bwd": [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp],
+    "irads_merge_ln_bwd": [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _i, _vp],
     "irads_mpg_bwd": [_vp] * 4 + [_l, _i, _vp, _vp, _vp],
     "irads_adapter_down": [_i, _vp, _vp, _vp, _vp, _vp, _vp, _l, _l, _i, _i, _f, _u64, _u64, _vp, _vp, _vp],
     "irads_adapter_up": [_vp, _vp, _vp, _vp, _vp, _l, _l, _i, _i, _vp, _vp],

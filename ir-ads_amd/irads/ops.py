@@ -966,8 +966,77 @@ class PatchMergeNormFn(torch.autograd.Function):
         g = gy if gy.dtype == torch.bfloat16 and gy.is_contiguous() else gy.to(torch.bfloat16).contiguous()
         dx = torch.empty_like(xc)
         N.call("irads_merge_ln_bwd", N.ptr(g), N.ptr(xc), B, H, W, C, N.ptr(mean), N.ptr(rstd), N.ptr(w), N.ptr(dx),
-               N.stream())
+               0, N.stream())
         return dx, None, None, None, None, None
+
+
+class StageTailFn(torch.autograd.Function):
+    """The batched stage output xo (2B, H*W, C) fp32 has two consumers: the output norms of the
+    two streams (norm_i / extra_norm_i, swin.py:1440-1470) and PatchMerging's unfold + norm.
+    As one node, the backward writes the norms' gradient and then ADDS the PatchMerging
+    gradient into it (irads_merge_ln_bwd accumulate) — no separate full-size gradient add."""
+
+    @staticmethod
+    def forward(ctx, xo, H, W, mw, mb, meps, w1, b1, w2, b2, eps1, eps2):
+        S, L, C = xo.shape
+        xc = xo.contiguous()
+        x2 = xc.view(-1, C)
+        M = x2.shape[0]
+        Mh = M // 2
+        Mm = S * (H // 2) * (W // 2)
+        ym = torch.empty((S, (H // 2) * (W // 2), 4 * C), device=xo.device, dtype=torch.bfloat16)
+        stats = torch.empty((2 * Mm + 2 * M,), device=xo.device, dtype=torch.float32)
+        mm_, mr, mean, rstd = stats[:Mm], stats[Mm:2 * Mm], stats[2 * Mm:2 * Mm + M], stats[2 * Mm + M:]
+        mwf, mbf = mw.detach().float().contiguous(), mb.detach().float().contiguous()
+        N.call("irads_merge_ln_fwd", N.ptr(xc), S, H, W, C, N.ptr(mwf), N.ptr(mbf), float(meps), N.ptr(ym),
+               N.ptr(mm_), N.ptr(mr), N.stream())
+        y = torch.empty((M, C), device=xo.device, dtype=torch.bfloat16)
+        for h, (w, b, eps) in enumerate(((w1, b1, eps1), (w2, b2, eps2))):
+            r = slice(h * Mh, (h + 1) * Mh)
+            N.call("irads_resln_fwd", N.ptr(x2[r]), None, None, None, 0.0, Mh, C, max(Mh, 1), N.ptr(w.detach()),
+                   N.ptr(b.detach()), float(eps), None, N.ptr(y[r]), None, N.ptr(mean[r]), N.ptr(rstd[r]),
+                   N.stream())
+        ctx.save_for_backward(xc, mwf, w1, w2, stats)
+        ctx.cfg = (S, H, W, C, Mm, M)
+        half = (S // 2, L, C)
+        return ym, y[:Mh].view(half), y[Mh:].view(half)
+
+    @staticmethod
+    def backward(ctx, gm, g1, g2):
+        xc, mwf, w1, w2, stats = ctx.saved_tensors
+        S, H, W, C, Mm, M = ctx.cfg
+        Mh = M // 2
+        mm_, mr, mean, rstd = stats[:Mm], stats[Mm:2 * Mm], stats[2 * Mm:2 * Mm + M], stats[2 * Mm + M:]
+        x2 = xc.view(-1, C)
+        dx = torch.empty_like(xc)
+        d2 = dx.view(-1, C)
+        for h, (gy, w) in enumerate(((g1, w1), (g2, w2))):
+            r = slice(h * Mh, (h + 1) * Mh)
+            if gy is None:
+                d2[r].zero_()
+                continue
+            g = gy.reshape(Mh, C)
+            if g.dtype != torch.bfloat16 or not g.is_contiguous():
+                g = g.to(torch.bfloat16).contiguous()
+            N.call("irads_resln_bwd", N.ptr(g), N.ptr(x2[r]), N.ptr(mean[r]), N.ptr(rstd[r]), N.ptr(w.detach()),
+                   None, None, Mh, C, max(Mh, 1), N.ptr(d2[r]), None, None, None, 0.0, N.stream())
+        if gm is not None:
+            g = gm if gm.dtype == torch.bfloat16 and gm.is_contiguous() else gm.to(torch.bfloat16).contiguous()
+            N.call("irads_merge_ln_bwd", N.ptr(g), N.ptr(xc), S, H, W, C, N.ptr(mm_), N.ptr(mr), N.ptr(mwf),
+                   N.ptr(dx), 1, N.stream())
+        return dx, None, None, None, None, None, None, None, None, None, None, None
+
+
+def stage_tail_ok(xo, H, W, merge_norm, norm1, norm2):
+    return (xo.dim() == 3 and xo.shape[0] % 2 == 0 and patch_merge_norm_ok(xo, H, W, merge_norm)
+            and ln_bf16_ok(xo, norm1) and ln_bf16_ok(xo, norm2))
+
+
+def stage_tail(xo, H, W, merge_norm, norm1, norm2):
+    """(PatchMerging unfold+norm of xo as the bf16 reduction operand, norm1(xo[:B]), norm2(xo[B:]))."""
+    with torch.autocast("cuda", enabled=False):
+        return StageTailFn.apply(xo, H, W, merge_norm.weight, merge_norm.bias, merge_norm.eps, norm1.weight,
+                                 norm1.bias, norm2.weight, norm2.bias, norm1.eps, norm2.eps)
 
 
 def patch_merge_norm_ok(x, H, W, norm):

@@ -124,15 +124,20 @@ class PatchMerging(nn.Module):
         self.norm = nn.LayerNorm(sample_dim) if norm_cfg is not None else None
         self.reduction = Linear(sample_dim, out_channels, bias=bias)
 
+    def gather_shape_ok(self, H, W):
+        """The 2x2 / stride-2 unfold with a norm and no padding: the gather-norm kernels apply."""
+        s = self.sampler
+        no_pad = not self.adap_padding or tuple(self.adap_padding.get_pad_shape((H, W))) == (0, 0)
+        return (self.norm is not None and no_pad and s.kernel_size == s.stride == (2, 2) and s.padding == (0, 0)
+                and s.dilation == (1, 1))
+
     def forward(self, x, input_size, sub_mode=None):
         B, L, C = x.shape
         assert isinstance(input_size, Sequence), f'Expect input_size is `Sequence` but get {input_size}'
         H, W = input_size
         assert L == H * W, 'input feature has wrong size'
         s = self.sampler
-        no_pad = not self.adap_padding or tuple(self.adap_padding.get_pad_shape((H, W))) == (0, 0)
-        if (self.norm is not None and no_pad and s.kernel_size == s.stride == (2, 2)
-                and s.padding == (0, 0) and s.dilation == (1, 1) and ops.patch_merge_norm_ok(x, H, W, self.norm)):
+        if self.gather_shape_ok(H, W) and ops.patch_merge_norm_ok(x, H, W, self.norm):
             # the 2x2 unfold as the LayerNorm's gather (one HIP pass each way, no permuted copy)
             with torch.autocast("cuda", enabled=False):
                 xm = ops.PatchMergeNormFn.apply(x, H, W, self.norm.weight, self.norm.bias, self.norm.eps)

@@ -18,6 +18,7 @@ What changed under the hood (MI355X-first):
 There is no CPU path: the HIP library and a GPU are required (CPU tensors raise).
 """
 import math
+import os
 import warnings
 from copy import deepcopy
 
@@ -27,6 +28,8 @@ import torch.nn.functional as F
 import torch.utils.checkpoint as cp
 
 from irads import ops, swin_fused
+
+_NO_STAGE_TAIL = os.environ.get("IRADS_NO_STAGE_TAIL") == "1"  # A/B switch: separate output norms + PatchMerging
 
 from ..layers.common import DropPath, Linear, TrainLinear
 from .embed import PatchEmbed, PatchMerging
@@ -297,7 +300,7 @@ class SwinBlockSequence(nn.Module):
             return x_down, hw_down, x, hw_shape
         return x, hw_shape, x, hw_shape
 
-    def forward_pair(self, x, hw_shape, n_rgb):
+    def forward_pair(self, x, hw_shape, n_rgb, downsample=True):
         if self.fused and 2 * n_rgb == x.shape[0] and swin_fused.usable(self, x):
             # frozen trunk under bf16 autocast: the whole stage is one hand-scheduled
             # autograd node (irads/swin_fused.py); results follow the module path below
@@ -305,7 +308,7 @@ class SwinBlockSequence(nn.Module):
         else:
             for block in self.blocks:
                 x = block.forward_pair(x, hw_shape, n_rgb)
-        if self.downsample:
+        if self.downsample and downsample:
             x_down, hw_down = self.downsample(x, hw_shape, None)
             return x_down, hw_down, x, hw_shape
         return x, hw_shape, x, hw_shape
@@ -688,11 +691,13 @@ class SwinTransformer(nn.Module):
                     sd[key] = t.view(nH2, L2).permute(1, 0).contiguous()
         self.load_state_dict(sd, strict=False)
 
-    def _outputs(self, i, x_rgb_out, x_dte_out, out_hw, xo=None):
+    def _outputs(self, i, x_rgb_out, x_dte_out, out_hw, xo=None, normed=None):
         # every consumer of these norms is a Linear (DeformMPG D_fc1/D_fc2, the heads' MLPs):
         # under bf16 autocast they are produced directly as the bf16 GEMM operand; given the
         # batched stage output xo = cat[x_rgb_out, x_dte_out], both norms run as one op on it
-        if xo is not None:
+        if normed is not None:  # computed with the PatchMerging gather (ops.stage_tail)
+            x_rgb_out, x_dte_out = normed
+        elif xo is not None:
             x_rgb_out, x_dte_out = ops.layer_norm_bf16_pair(xo, getattr(self, f'norm{i}'),
                                                             getattr(self, f'extra_norm{i}'))
         else:
@@ -716,10 +721,22 @@ class SwinTransformer(nn.Module):
         outs, outs_rgb, outs_dte = [], [], []
         B = x_rgb.shape[0]
         for i, stage in enumerate(self.stages):
-            xo = None
+            xo = normed = None
             if self.batch_streams and hw_rgb == hw_dte:
                 xcat = self.MPGBlocks[i].residual_cat(x_rgb, x_dte, hw_rgb[0], hw_rgb[1])
-                xd, hw_d, xo, out_hw = stage.forward_pair(xcat, hw_rgb, B)
+                ds = stage.downsample
+                tail = (i in self.out_indices and ds is not None and hasattr(ds, "gather_shape_ok")
+                        and not _NO_STAGE_TAIL)
+                xd, hw_d, xo, out_hw = stage.forward_pair(xcat, hw_rgb, B, downsample=not tail)
+                if tail:
+                    H_, W_ = out_hw
+                    n1, n2 = getattr(self, f'norm{i}'), getattr(self, f'extra_norm{i}')
+                    if ds.gather_shape_ok(H_, W_) and ops.stage_tail_ok(xo, H_, W_, ds.norm, n1, n2):
+                        # output norms + PatchMerging's gather-norm as one node (one gradient write)
+                        ym, y1, y2 = ops.stage_tail(xo, H_, W_, ds.norm, n1, n2)
+                        xd, hw_d, normed = ds.reduction(ym), (H_ // 2, W_ // 2), (y1, y2)
+                    else:
+                        xd, hw_d = ds(xo, out_hw, None)
                 x_rgb, x_dte = ops.split_streams(xd, B)  # one gradient copy back, no zero-fill + add
                 x_rgb_out, x_dte_out = xo[:B], xo[B:]
                 hw_rgb = hw_dte = hw_d
@@ -730,7 +747,7 @@ class SwinTransformer(nn.Module):
                 x_rgb, hw_rgb, x_rgb_out, out_hw = stage(x_rgb, hw_rgb, sub_mode='rgb')
                 x_dte, hw_dte, x_dte_out, out_hw = stage(x_dte, hw_dte, sub_mode='dte')
             if i in self.out_indices:
-                o, orgb, odte = self._outputs(i, x_rgb_out, x_dte_out, out_hw, xo)
+                o, orgb, odte = self._outputs(i, x_rgb_out, x_dte_out, out_hw, xo, normed)
                 outs.append(o)
                 outs_rgb.append(orgb)
                 outs_dte.append(odte)

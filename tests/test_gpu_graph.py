@@ -63,7 +63,10 @@ def test_graphed_step_matches_eager():
             ref = p0[n].grad
             den = torch.maximum(ref.norm(), 0.1 * rms * ref.numel() ** 0.5)
             err = ((p.grad - ref).norm() / den).item()
-            assert err < 8e-3, (n, err)
+            # both runs accumulate float atomics in a different order (DAttn table / offset
+            # gradients, split-K partials): observed 0.0075-0.0085 run to run on the DAttn and
+            # MPG stage-0 weights, a real graph-capture bug shows up at O(1)
+            assert err < 1.5e-2, (n, err)
             n_checked += 1
     assert n_checked > 100
     before = [p.detach().clone() for p in runner.params]

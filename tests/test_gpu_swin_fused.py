@@ -549,3 +549,36 @@ def test_patch_merge_norm_matches_unfold_path(C, H, W):
     assert yb.dtype == torch.bfloat16 and yb.shape == ya.shape
     torch.testing.assert_close(yb.float(), ya.float(), rtol=2 ** -7, atol=1e-2)
     torch.testing.assert_close(dxb, dxa, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("C,H,W", [(128, 32, 32), (256, 16, 24)])
+def test_stage_tail_matches_separate_norms(C, H, W):
+    """ops.stage_tail (output norms of both streams + PatchMerging's gather-norm on the batched
+    stage output, one node) against the two separate ops: same kernels forward (bit-exact);
+    backward writes the norms' gradient and adds the PatchMerging gradient in place: the fp32
+    sum autograd forms from the two nodes, to one rounding (the kernels are built without FMA
+    contraction, so in practice bit-exact)."""
+    from irads import ops
+    torch.manual_seed(C + W)
+    B = 2
+    norms = [torch.nn.LayerNorm(n).to(DEV).requires_grad_(False) for n in (4 * C, C, C)]
+    with torch.no_grad():
+        for nm in norms:
+            nm.weight.uniform_(0.5, 1.5)
+            nm.bias.uniform_(-0.2, 0.2)
+    x = torch.randn(2 * B, H * W, C, device=DEV) * 2 + 0.3
+    gm = torch.randn(2 * B, H * W // 4, 4 * C, device=DEV).bfloat16()
+    g1, g2 = (torch.randn(B, H * W, C, device=DEV).bfloat16() for _ in range(2))
+    xa = x.clone().requires_grad_()
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        assert ops.stage_tail_ok(xa, H, W, norms[0], norms[1], norms[2])
+        ya = ops.stage_tail(xa, H, W, *norms)
+    xb = x.clone().requires_grad_()
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        ymb = ops.PatchMergeNormFn.apply(xb, H, W, norms[0].weight, norms[0].bias, norms[0].eps)
+        y1b, y2b = ops.layer_norm_bf16_pair(xb, norms[1], norms[2])
+    for a, b in zip(ya, (ymb, y1b, y2b)):
+        assert torch.equal(a, b)
+    (da,) = torch.autograd.grad(ya, xa, (gm, g1, g2))
+    (db,) = torch.autograd.grad((ymb, y1b, y2b), xb, (gm, g1, g2))
+    torch.testing.assert_close(da, db, rtol=2e-7, atol=1e-7)  # one fp32 rounding of the same two terms
