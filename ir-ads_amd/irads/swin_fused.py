@@ -26,8 +26,9 @@ stage is a single torch.autograd.Function whose forward and backward are hand-sc
 
 Rounding is the autocast reference's op by op (see csrc/swinblock.hip); the GEMMs are the
 same hipBLASLt calls F.linear makes under autocast.  Used only when the stage is frozen
-(no trunk parameter requires grad), not checkpointed, and autocast runs in bf16; any other
-configuration takes the module-by-module path.
+(no trunk parameter requires grad) and autocast runs in bf16; any other configuration takes
+the module-by-module path.  Gradient checkpointing (with_cp, Swin-L) is numerically neutral
+and is not re-enacted: the fused stage keeps its activations.
 """
 import torch
 import torch.nn.functional as F
@@ -53,7 +54,9 @@ def usable(seq, x):
             and torch.get_autocast_dtype("cuda") == _BF16):
         return False
     for blk in seq.blocks:
-        if blk.with_cp or not _frozen_trunk(blk):
+        # with_cp (Swin-L, base.py:43-50) only trades memory for recompute: the fused stage keeps
+        # its activations (a few GB at Swin-L 480x640, B=4, well inside 288 GB) and serves it
+        if not _frozen_trunk(blk):
             return False
         w = blk.attn.w_msa
         if w.attn_drop.p > 0 and blk.training:
@@ -188,8 +191,8 @@ class SwinStageFn(torch.autograd.Function):
         dev = x.device
         x = x.contiguous().view(M, C)
         dp = _droppath_scales(seq, S, dev)
-        train = blocks[0].training
-        p_drop = ADAPTER_DROPOUT if train else 0.
+        # the Adapter's F.dropout(p=0.1, training=self.training) (swin.py:496)
+        p_drop = ADAPTER_DROPOUT if blocks[0].MLP_RGB_Adapter.training else 0.
         # dropout seed drawn on the device by torch's generator: graph-capturable, fresh per replay
         seed = torch.randint(0, 2 ** 62, (1,), device=dev, dtype=torch.int64) if p_drop > 0 else None
         # all adapter weights of the stage cast to bf16 in two launches (autocast casts each per
@@ -294,7 +297,20 @@ class SwinStageFn(torch.autograd.Function):
                     rows = slice(half * Mh, (half + 1) * Mh)
                     probs.append((rs[rows], dd[rows], gwa2, None, gba2, True))
                     probs.append((dA[rows], X1b[rows], gwa1, gba1, None, False))
-                if _UNBATCHED:
+                if R % 8:
+                    # Swin-L (C = 192: R = 12): the split-K kernel takes 16-B rows (R % 8 == 0);
+                    # these four skinny products go to hipBLASLt in bf16 with fp32 column sums
+                    # (autocast's own rounding of a bf16 Linear's weight gradient)
+                    for A_, B_, D_, sa_, sb_, tr_ in probs:
+                        if tr_:
+                            D_.copy_(torch.mm(B_.t(), A_))
+                        else:
+                            D_.copy_(torch.mm(A_.t(), B_))
+                        if sa_ is not None:
+                            torch.sum(A_, 0, dtype=torch.float32, out=sa_)
+                        if sb_ is not None:
+                            torch.sum(B_, 0, dtype=torch.float32, out=sb_)
+                elif _UNBATCHED:
                     for A_, B_, D_, sa_, sb_, tr_ in probs:
                         if tr_:
                             ops.wgrad(B_, A_, D_, colsum_a=sb_)

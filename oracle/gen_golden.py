@@ -357,6 +357,103 @@ def gen_cmnext(ref):
     save("cmnext_swinb512_checksums.npz", **cs)
 
 
+# --------------------------------------------------------------------------- CMNeXt training step
+# Fixture definition, deterministic training mode and inputs: oracle/train_fixture.py
+def _train_step(model, rgb, dep, lbl, amp):
+    """One reference training step (train_mm.py:133-150); amp: CPU bf16 autocast."""
+    for p in model.parameters():
+        p.grad = None
+    with torch.autocast("cpu", dtype=torch.bfloat16, enabled=amp):
+        y, yr, yd = model([t(rgb), t(dep)])
+        lf = nn.CrossEntropyLoss(ignore_index=255)
+        lb = t(lbl)
+        pred = y.softmax(dim=1).argmax(dim=1)
+        mask_lbl = lb.clone()
+        mask_lbl[pred != lb] = 255
+        l1, l4, l5 = lf(y, lb), lf(yr, mask_lbl), lf(yd, mask_lbl)
+        loss = l1 + 0.01 * l4 + 0.01 * l5
+    loss.backward()  # (.backward, not autograd.grad: Swin-L's with_cp checkpoints are reentrant)
+    named = [(n, p) for n, p in model.named_parameters() if p.requires_grad]
+    return (loss, l1, l4, l5), (y.float(), yr.float(), yd.float()), named, [p.grad.detach().clone() for _, p in named]
+
+
+def _rel_l2(a, b):
+    a, b = a.double().flatten(), b.double().flatten()
+    return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+
+def gen_cmnext_train(ref, tags=None):
+    """Reference training-step fixtures (oracle/train_fixture.py).  The reference is run twice:
+    in fp32 (the values the product is compared with) and under CPU bf16 autocast, whose
+    deviation from its own fp32 run is stored per quantity: the bf16 noise envelope the
+    product's bf16 path is judged against (tests/test_gpu_train_parity.py)."""
+    from train_fixture import (FULL_GRAD_KEYS, N_PROJ, TRAIN_FIXTURES, adapter_trainable, deterministic_train_mode,
+                               projection, train_inputs)
+    for tag, (bb, n_cls, B, H, W, fseed, iseed) in TRAIN_FIXTURES.items():
+        if tags and tag not in tags:
+            continue
+        model = ref.cmnext.CMNeXt(bb, n_cls, ["img", "depth"])
+        fill_module(model, seed=fseed)
+        for n, p in model.named_parameters():
+            p.requires_grad_(adapter_trainable(n))
+        deterministic_train_mode(model)
+        rgb, dep, lbl = train_inputs(B, H, W, n_cls, iseed)
+        bn = model.decode_head.linear_fuse.bn
+        rm0 = bn.running_mean.detach().clone()
+        losses, (y, yr, yd), named, grads = _train_step(model, rgb, dep, lbl, amp=False)
+        rm1 = bn.running_mean.detach().clone()
+        res = {"cfg": np.array([B, H, W, n_cls, fseed, iseed]), "backbone": np.array(bb),
+               "loss": np.array([l.item() for l in losses])}
+        for name, f in (("y", y), ("y_rgb", yr), ("y_dte", yd)):
+            fd = f.detach().double()
+            res[name + "_cs"] = np.array([fd.mean().item(), fd.abs().mean().item(), fd.pow(2).mean().sqrt().item()])
+            res[name + "_sub"] = f.detach()[:, :, ::8, ::8].numpy().astype(np.float32)
+            res[name + "_argmax_hist"] = torch.bincount(f.argmax(1).flatten(), minlength=n_cls).numpy()
+        # top-2 margin of the fused logits at full resolution: argmax agreement is judged where it is
+        # decided by more than bf16 noise
+        top2 = y.detach().topk(2, dim=1).values
+        res["y_argmax"] = y.detach().argmax(1).numpy().astype(np.uint8)
+        res["y_margin"] = (top2[:, 0] - top2[:, 1]).numpy().astype(np.float16)
+        names, norms, projs = [], [], []
+        for (n, p), gp in zip(named, grads):
+            g64 = gp.double().numpy()
+            names.append(n)
+            norms.append(np.sqrt((g64 * g64).sum()))
+            projs.append([projection(n, g64, j) for j in range(N_PROJ)])
+            if n in FULL_GRAD_KEYS:
+                res["g." + n] = gp
+        res["grad_names"] = np.array(names)
+        res["grad_norms"] = np.array(norms)
+        res["grad_projs"] = np.array(projs)
+        res["bn_rm.decode_head"] = rm1
+        res["state_keys"] = np.array(sorted(model.state_dict().keys()))
+        # the same step under bf16 autocast: the reference's own bf16 deviation from fp32
+        with torch.no_grad():
+            bn.running_mean.copy_(rm0)
+        lb16, (y16, yr16, yd16), _, g16 = _train_step(model, rgb, dep, lbl, amp=True)
+        res["bf16_loss_rel"] = np.array(abs(lb16[0].item() - losses[0].item()) / abs(losses[0].item()))
+        for name, a16, a32 in (("y", y16, y), ("y_rgb", yr16, yr), ("y_dte", yd16, yd)):
+            res[f"bf16_{name}_rel_l2"] = np.array(_rel_l2(a16.detach()[:, :, ::8, ::8], a32.detach()[:, :, ::8, ::8]))
+        res["bf16_argmax_agree"] = np.array(float((y16.argmax(1) == y.argmax(1)).double().mean()))
+        floor = 1e-5 * float(max(norms))
+        errs, num, den = [], 0.0, 0.0
+        for k, (n, g) in enumerate(zip(names, g16)):
+            g64 = g.double().numpy()
+            d = [projection(n, g64, j) - projs[k][j] for j in range(N_PROJ)]
+            dn = float(np.sqrt((g64 * g64).sum())) - norms[k]
+            errs.append(max(abs(x) for x in d + [dn]) / (norms[k] + floor))
+            num += sum(x * x for x in d) / N_PROJ
+            den += norms[k] ** 2
+            if n in FULL_GRAD_KEYS:
+                res["bf16_full_rel." + n] = np.array(_rel_l2(g, grads[k]))
+        res["bf16_grad_err"] = np.array(errs)
+        res["bf16_grad_agg_rel"] = np.array(np.sqrt(num / den))
+        print(tag, "loss", [round(l.item(), 5) for l in losses], "y rms", res["y_cs"][2],
+              "bf16: y rel", float(res["bf16_y_rel_l2"]), "agg grad", float(res["bf16_grad_agg_rel"]),
+              "worst", max(errs), names[int(np.argmax(errs))])
+        save(f"train_{tag}.npz", **res)
+
+
 # --------------------------------------------------------------------------- LightSB
 def gen_sb(ref):
     sbm = ref.sb.LightSB(dim=512, n_potentials=10, epsilon=0.1, is_diagonal=True)
@@ -414,10 +511,11 @@ def gen_metrics_loss(ref):
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["msda", "swin", "block", "dattn", "fusion", "cmnext", "sb", "metrics"]
+    which = sys.argv[1:] or ["msda", "swin", "block", "dattn", "fusion", "cmnext", "sb", "metrics", "train"]
     ref = load_reference()
     torch.manual_seed(0)
     fns = {"msda": gen_msda, "swin": gen_swin_wmsa, "block": gen_swin_block, "dattn": gen_dattn,
-           "fusion": gen_fusion_small, "cmnext": gen_cmnext, "sb": gen_sb, "metrics": gen_metrics_loss}
+           "fusion": gen_fusion_small, "cmnext": gen_cmnext, "sb": gen_sb, "metrics": gen_metrics_loss,
+           "train": gen_cmnext_train}
     for w in which:
         fns[w](ref)

@@ -295,3 +295,36 @@ def test_metrics_and_mmst_oracle():
     assert [a + b for a, b in zip(fn, fn2)] == fx["fn"].tolist()
     loss = R.mmst_loss(logits, fx.t("logits_rgb"), fx.t("logits_dte"), gt)
     close(loss, fx["mmst_loss"], 1e-6, 1e-6, "MMST loss (train_mm.py:137-148)")
+
+
+# ------------------------------------------------------------------- training step (C2 geometry)
+def test_oracle_train_step_c2():
+    """The oracle's CMNeXt Swin-B training step (deterministic training mode, MMST loss,
+    Adapter-mode gradients) against the reference's fixture at 512², B=2 (fp32 both sides)."""
+    from train_fixture import TRAIN_FIXTURES, adapter_trainable, deterministic_train_mode, projection, train_inputs
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    fx = Fixture("train_c2_swinb_512.npz")
+    bb, n_cls, B, H, W, fseed, iseed = TRAIN_FIXTURES["c2_swinb_512"]
+    m = R.CMNeXt(bb, n_cls, ["img", "depth"])
+    assert sorted(m.state_dict().keys()) == fx["state_keys"].tolist()
+    fill_module(m, seed=fseed)
+    for n, p in m.named_parameters():
+        p.requires_grad_(adapter_trainable(n))
+    deterministic_train_mode(m)
+    rgb, dep, lbl = (torch.from_numpy(a) for a in train_inputs(B, H, W, n_cls, iseed))
+    y, yr, yd = m([rgb, dep])
+    loss = R.mmst_loss(y, yr, yd, lbl)
+    loss.backward()
+    assert abs(loss.item() - fx["loss"][0]) <= 1e-4 * abs(fx["loss"][0])
+    for name, t in (("y", y), ("y_rgb", yr), ("y_dte", yd)):
+        close(t.detach()[:, :, ::8, ::8], fx[name + "_sub"], 1e-4 * float(np.abs(fx[name + "_sub"]).max()), 1e-4, name)
+    names = fx["grad_names"].tolist()
+    params = dict(m.named_parameters())
+    # conv biases ahead of a training-mode BatchNorm (DAttn fuse_q) have a mathematically zero
+    # gradient: rounding noise on both sides, judged against an absolute floor
+    floor = 1e-6 * float(fx["grad_norms"].max())
+    for k, n in enumerate(names):
+        g64 = params[n].grad.double().numpy()
+        nr = float(fx["grad_norms"][k])
+        assert abs(np.sqrt((g64 * g64).sum()) - nr) <= 1e-3 * nr + floor, n
+        assert abs(projection(n, g64, 0) - fx["grad_projs"][k][0]) <= 1e-3 * nr + floor, n
