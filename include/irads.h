@@ -68,17 +68,24 @@ int irads_msda_corner_index(int dtype, const void *loc, const int64_t *shapes, i
  *   mask  (n_mask, 144, 144) fp32 or NULL: explicit WindowMSA mask (swin.py:107-111);
  *         NULL => the shift-region mask computed in-kernel when shift > 0
  *   out   (B, H, W, C) same dtype      lse (B*nW, nH, 144) fp32 workspace for backward
- * window = 12, head_dim = 32 (every Swin-B/L stage).  scale = qk_scale or 32^-0.5. */
+ * window = 12, head_dim = 32 (every Swin-B/L stage).  scale = qk_scale or 32^-0.5.
+ *   bias_quads (nH, 8, 532) fp32 from irads_winattn_bias_quads (required for BF16, ignored for
+ *         F32): the table re-laid so that every 4-key (forward) / 4-query (backward) bias
+ *         group of a window row is one aligned 16-byte LDS read; recompute when rel_table
+ *         changes (a pure function of it; the frozen trunk's is built once). */
+long irads_winattn_bias_quads_size(int nH);
+int irads_winattn_bias_quads(const float *rel_table, int nH, float *bias_quads, void *stream);
 int irads_winattn_fwd(int dtype, const void *qkv, const float *qkv_bias, const float *rel_table,
-                      const float *mask, int n_mask, int B, int H, int W, int C, int nH, int shift,
+                      const float *bias_quads, const float *mask, int n_mask, int B, int H, int W, int C, int nH, int shift,
                       float scale, void *out, float *lse, void *stream);
 /* grad_qkv (B, H, W, 3C) fully written.  Optional accumulators (zero-filled by the
  * caller, fp32, or NULL to skip): grad_table (529, nH); grad_bias_pad (3C) = the qkv-bias
  * gradient carried by the pad tokens (the real tokens' share flows through the Linear). */
 int irads_winattn_bwd(int dtype, const void *qkv, const float *qkv_bias, const float *rel_table,
-                      const float *mask, int n_mask, int B, int H, int W, int C, int nH, int shift,
-                      float scale, const void *out, const float *lse, const void *grad_out,
-                      void *grad_qkv, float *grad_table, float *grad_bias_pad, void *stream);
+                      const float *bias_quads, const float *mask, int n_mask, int B, int H, int W, int C,
+                      int nH, int shift, float scale, const void *out, const float *lse,
+                      const void *grad_out, void *grad_qkv, float *grad_table, float *grad_bias_pad,
+                      void *stream);
 
 /* ------------------------------------------------------------------ DSCF / DAttentionMM
  * Replaces the grid_sample / einsum / softmax core of DAttentionMM.forward

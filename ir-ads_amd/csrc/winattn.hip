@@ -247,6 +247,7 @@ __device__ __forceinline__ f32x4 mfma16(const bf16x8_t &a, const bf16x8_t &b, co
 __device__ __forceinline__ bf16x8_t as_bf(u16x8 v) { return __builtin_bit_cast(bf16x8_t, v); }
 
 typedef __attribute__((ext_vector_type(4))) short i16x4;
+typedef __attribute__((ext_vector_type(4))) short s16x4;
 typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
 
 // 4 rows x 16 columns block, column-major per lane (cdna_hip_programming.md T10)
@@ -318,111 +319,164 @@ __device__ __forceinline__ int token_of(const Geo &g, int bw, int t) {
 __device__ __forceinline__ bool hi_row(const Geo &g, int t) { return t / WS >= WS - g.shift; }
 __device__ __forceinline__ bool hi_col(const Geo &g, int t) { return t % WS >= WS - g.shift; }
 
+// Window origin of one (image, window) work item, decoded once per workgroup (the runtime
+// divisions by nW / nWw are the expensive part of token_of); tok() is then divide-free per token.
+struct WinOrigin {
+    int r0, c0, base;  // rolled-frame row / column of the window's first token, image token offset
+    __device__ __forceinline__ WinOrigin(const Geo &g, int bw) {
+        const int b = bw / g.nW, w = bw - b * g.nW;
+        const int wr = w / g.nWw;
+        r0 = wr * WS;
+        c0 = (w - wr * g.nWw) * WS;
+        base = b * g.H * g.W;
+    }
+    __device__ __forceinline__ int tok(const Geo &g, int t) const {
+        const int tr = t / WS;  // constant divisor: multiply-shift
+        int oh = r0 + tr + g.shift, ow = c0 + (t - tr * WS) + g.shift;
+        if (oh >= g.Hp) oh -= g.Hp;
+        if (ow >= g.Wp) ow -= g.Wp;
+        return (oh < g.H && ow < g.W) ? base + oh * g.W + ow : -1;
+    }
+};
+
+// ---------------------------------------------------------------------------------------------
+// Forward, one workgroup per (window, head): 3 waves, wave w owns query tiles 3w..3w+2.
+//
+// The chunked kernel above ties each wave to one query tile of every window so that its 36
+// biases can live in registers (158 VGPRs): one 9-wave workgroup per CU, a 3-2-2-2 wave split
+// over the SIMDs and a per-window barrier that every wave waits at.  Here the biases come
+// from LDS instead, as the MFMA accumulator seed itself: for a lane's query and its 4
+// consecutive keys (one row of the window, since 4 | 12) the 4 biases are 4 consecutive
+// entries of the reversed 23x23 table, stored 4 times at the 4 alignments so that each seed
+// is ONE ds_read_b128.  That frees the wave from any fixed query tile: a workgroup is one
+// (window, head), all of its loads are issued up front, and 5 workgroups share a CU (LDS
+// 31.7 KB, <= 128 VGPRs), so one workgroup's load latency and barrier are covered by the
+// others' MFMA / softmax work instead of by a register pipeline inside one workgroup.
+constexpr int BQ = 532;  // floats per aligned copy of the reversed table (529 + pad)
+
+// quads (nH, 8, BQ): copies c = 0..3 of the reversed table shifted by c (forward: a query's 4
+// consecutive keys), c = 4..7 of the table itself shifted by c - 4 (backward: a key's 4
+// consecutive queries).  One launch per table version; the caller caches the result.
+__global__ void winattn_bias_quads_kernel(const float *__restrict__ table, int nH, float *__restrict__ quads) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nH * 8 * BQ) return;
+    const int h = i / (8 * BQ), c = (i / BQ) % 8, j = i % BQ;
+    const int idx = c < 4 ? TBL - 1 - (j + c) : j + (c - 4);
+    quads[i] = (idx >= 0 && idx < TBL) ? table[idx * nH + h] : 0.f;
+}
+
 template <int MM>
-__global__ void __launch_bounds__(576) winattn_fwd_bf16(const unsigned short *__restrict__ qkv,
-                                                         const float *__restrict__ qbias,
-                                                         const float *__restrict__ table,
-                                                         const float *__restrict__ mask, Geo g, int cw,
-                                                         unsigned short *__restrict__ out, float *__restrict__ lse) {
-    // K/V tiles double-buffered: window w stages into buffer w&1 while other waves may
-    // still be reading w-1, so one barrier per window suffices
-    __shared__ __attribute__((aligned(16))) unsigned short Ks[2][NT * RS];
-    __shared__ __attribute__((aligned(16))) unsigned short Vs[2][NR * RS];
-    __shared__ __attribute__((aligned(16))) unsigned short padS[3 * HD];  // pad-token q, k, v (bf16)
-    const Chunk ck = decode_chunk(g, cw);
-    const int h = ck.h;
+__global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(4))) winattn_fwd_bf16_wg(const unsigned short *__restrict__ qkv,
+                                                            const float *__restrict__ qbias,
+                                                            const float *__restrict__ quads,
+                                                            const float *__restrict__ mask, Geo g,
+                                                            unsigned short *__restrict__ out, float *__restrict__ lse) {
+    __shared__ __attribute__((aligned(16))) unsigned short Ks[NT * RS];
+    __shared__ __attribute__((aligned(16))) unsigned short Vs[NT * RS];
+    __shared__ __attribute__((aligned(16))) float Bq[4 * BQ];  // copy c: Bq[c*BQ + i] = T[528 - (i + c)]
+    __shared__ __attribute__((aligned(16))) unsigned short padS[3 * HD];
+    const int lid = xcd_remap(blockIdx.x, gridDim.x);  // the heads of one window on one XCD
+    const int h = lid % g.nH, bw = lid / g.nH;
+    const WinOrigin wo(g, bw);
     const long C3 = 3 * g.C;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int l16 = lane & 15, grp = lane >> 4;
-    for (int i = tid; i < (NR - NT) * RS; i += 576) {
-        Vs[0][NT * RS + i] = 0;
-        Vs[1][NT * RS + i] = 0;
-    }
+    // ---- issue every global load of the workgroup first
     if (tid < 3 * HD) padS[tid] = qbias ? f2bf(qbias[(tid / HD) * g.C + h * HD + tid % HD]) : (unsigned short)0;
-    // per-lane biases, log2 domain: query qi = 16 wave + l16, key = 16 kt + 4 grp + r
-    const int qi = wave * 16 + l16;
-    // bias in natural units, rounded through fp16(b·log2 e) exactly as the backward sees it;
-    // it seeds the MFMA accumulator, so S + B costs no VALU op per window
-    f32x4 bias4[9];
+    u16x8 kreg[3], vreg[3], qreg[3];
+    int ktok[3], qtok[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {  // staging: chunk e = tid + 192 j of 576 = (token e / 4, 16-B column e % 4)
+        const int e = tid + 192 * j, t = e >> 2, ch = e & 3;
+        ktok[j] = wo.tok(g, t);
+        const long row = (long)(ktok[j] >= 0 ? ktok[j] : 0) * C3;
+        kreg[j] = *(const u16x8 *)(qkv + row + g.C + h * HD + ch * 8);
+        vreg[j] = *(const u16x8 *)(qkv + row + 2 * g.C + h * HD + ch * 8);
+    }
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        const int qi = (3 * wave + j) * 16 + l16;
+        qtok[j] = wo.tok(g, qi);
+        qreg[j] = *(const u16x8 *)(qkv + (long)(qtok[j] >= 0 ? qtok[j] : 0) * C3 + h * HD + grp * 8);
+    }
+    {  // the head's 4 reversed copies (irads_winattn_bias_quads), 16-B loads
+        const f32x4 *src = (const f32x4 *)(quads + (long)h * 8 * BQ);
+        for (int i = tid; i < BQ; i += 192) ((f32x4 *)Bq)[i] = src[i];
+    }
+    __syncthreads();  // padS
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        const int e = tid + 192 * j, t = e >> 2, ch = e & 3;
+        const u16x8 kp = *(const u16x8 *)(padS + HD + ch * 8), vp = *(const u16x8 *)(padS + 2 * HD + ch * 8);
+        *(u16x8 *)(Ks + t * RS + ch * 8) = ktok[j] >= 0 ? kreg[j] : kp;
+        *(u16x8 *)(Vs + t * RS + ch * 8) = ktok[j] >= 0 ? vreg[j] : vp;
+    }
+    __syncthreads();
+    // ---- per-lane constants: key group of every key tile (keys kt*16 + 4 grp + r, one window row)
+    int kofs[9];  // 23 * row + col of the group's first key
     unsigned long long hb = 0, wb = 0;  // key class bits (MM == 1)
 #pragma unroll
-    for (int kt = 0; kt < 9; ++kt)
+    for (int kt = 0; kt < 9; ++kt) {
+        const int k0 = kt * 16 + grp * 4;
+        kofs[kt] = 23 * (k0 / WS) + k0 % WS;
+        if (MM == 1)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int ki = kt * 16 + grp * 4 + r;
-            bias4[kt][r] = (float)(_Float16)(table[rel_idx(qi, ki) * g.nH + h] * LOG2E) * (1.0f / LOG2E);
-            if (MM == 1) {
-                hb |= (unsigned long long)hi_row(g, ki) << (kt * 4 + r);
-                wb |= (unsigned long long)hi_col(g, ki) << (kt * 4 + r);
+            for (int r = 0; r < 4; ++r) {
+                hb |= (unsigned long long)hi_row(g, k0 + r) << (kt * 4 + r);
+                wb |= (unsigned long long)hi_col(g, k0 + r) << (kt * 4 + r);
             }
-        }
-    const bool q_hr = hi_row(g, qi), q_hc = hi_col(g, qi);
+    }
+    bool lastH = false, lastW = false;
+    if (MM == 1) {
+        const int wi = bw % g.nW;
+        lastH = wi / g.nWw == g.nWh - 1;
+        lastW = wi % g.nWw == g.nWw - 1;
+    }
     const bf16x8_t ones = as_bf(u16x8{0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80});
-    // staging map: thread -> (token t, 16-B chunk ch) of K and V
-    const int st_t = tid >> 2, st_ch = tid & 3;
-    __syncthreads();  // padS
-    // Two register stages: the loads for window w+2 are issued while w computes, so a
-    // window's HBM latency is covered by two windows of work.
-    struct Stage {
-        u16x8 k, v, q;
-        int qtok;
-    };
-    auto load = [&](int bw, Stage &sg) {
-        const int tok = token_of(g, bw, st_t);
-        sg.k = load_frag_sel(qkv, *(const u16x8 *)(padS + HD + st_ch * 8), tok, C3, g.C + h * HD + st_ch * 8);
-        sg.v = load_frag_sel(qkv, *(const u16x8 *)(padS + 2 * HD + st_ch * 8), tok, C3,
-                             2 * g.C + h * HD + st_ch * 8);
-        sg.qtok = token_of(g, bw, qi);
-        sg.q = load_frag_sel(qkv, *(const u16x8 *)(padS + grp * 8), sg.qtok, C3, h * HD + grp * 8);
-    };
-    auto step = [&](int bw, int buf, Stage &sg) {
-        unsigned short *Kb = Ks[buf], *Vb = Vs[buf];
-        *(u16x8 *)(Kb + st_t * RS + st_ch * 8) = sg.k;
-        *(u16x8 *)(Vb + st_t * RS + st_ch * 8) = sg.v;
-        const bf16x8_t qf = scale_q(sg.q, g.scale);
-        const int qtok = sg.qtok;
-        __syncthreads();
-        if (bw + 2 < ck.w_end) load(bw + 2, sg);
+    const int tr_row = (l16 >> 2), tr_col = 4 * (l16 & 3);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        const int qt = 3 * wave + j, qi = qt * 16 + l16;
+        // (selects, not a dynamic index: a runtime index into these arrays would put them in scratch)
+        const int qtk = j == 0 ? qtok[0] : (j == 1 ? qtok[1] : qtok[2]);
+        const u16x8 qsel = j == 0 ? qreg[0] : (j == 1 ? qreg[1] : qreg[2]);
+        const u16x8 qraw = qtk >= 0 ? qsel : *(const u16x8 *)(padS + grp * 8);
+        const bf16x8_t qf = scale_q(qraw, g.scale);
+        const int aq = 264 - (23 * (qi / WS) + qi % WS);  // reversed-table index = aq + kofs
         f32x4 s[9];
 #pragma unroll
         for (int kt = 0; kt < 9; ++kt) {
-            const bf16x8_t kf = as_bf(*(const u16x8 *)(Kb + (kt * 16 + l16) * RS + grp * 8));
-            s[kt] = mfma16(kf, qf, bias4[kt]);  // Sᵀ + B (key rows, query on the lane)
+            const int si = aq + kofs[kt];
+            const f32x4 b4 = ((const f32x4 *)Bq)[(si & 3) * (BQ / 4) + (si >> 2)];  // copy si & 3, aligned
+            const bf16x8_t kf = as_bf(*(const u16x8 *)(Ks + (kt * 16 + l16) * RS + grp * 8));
+            s[kt] = mfma16(kf, qf, b4);  // Sᵀ + B (key rows, query on the lane)
             if (MM == 2) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
                     s[kt][r] += mask[((long)(bw % g.n_mask) * NT + qi) * NT + kt * 16 + grp * 4 + r];
             }
         }
-        if (MM == 1) {  // only windows on the last row / column of the shifted grid carry a mask (uniform branch)
-            const int wi = bw % g.nW;
-            const bool lastH = wi / g.nWw == g.nWh - 1, lastW = wi % g.nWw == g.nWw - 1;
-            if (lastH || lastW) {
-                unsigned long long mbits = 0;
-                if (lastH) mbits |= q_hr ? ~hb : hb;
-                if (lastW) mbits |= q_hc ? ~wb : wb;
+        if (MM == 1 && (lastH || lastW)) {  // uniform branch: only edge windows of the shifted grid
+            unsigned long long mbits = 0;
+            if (lastH) mbits |= hi_row(g, qi) ? ~hb : hb;
+            if (lastW) mbits |= hi_col(g, qi) ? ~wb : wb;
 #pragma unroll
-                for (int kt = 0; kt < 9; ++kt)
+            for (int kt = 0; kt < 9; ++kt)
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) s[kt][r] += ((mbits >> (kt * 4 + r)) & 1ull) ? -100.0f : 0.0f;
-            }
+                for (int r = 0; r < 4; ++r) s[kt][r] += ((mbits >> (kt * 4 + r)) & 1ull) ? -100.0f : 0.0f;
         }
         float mx = -INFINITY;
 #pragma unroll
         for (int kt = 0; kt < 9; ++kt)
 #pragma unroll
             for (int r = 0; r < 4; ++r) mx = fmaxf(mx, s[kt][r]);
-        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        mx = max_xor16_32(mx);
         const float mneg = -mx * LOG2E;
 #pragma unroll
         for (int kt = 0; kt < 9; ++kt)
 #pragma unroll
             for (int r = 0; r < 4; ++r) s[kt][r] = fast_exp2(fmaf(s[kt][r], LOG2E, mneg));
-        // Oᵀ = Vᵀ·Pᵀ over 5 k-steps of 32 keys (key order permuted identically in A and B);
-        // a third MFMA with an all-ones A gives the row sums of the bf16 P actually used
         f32x4 o0 = {0.f, 0.f, 0.f, 0.f}, o1 = o0, os = o0;
-        const int tr_row = (l16 >> 2), tr_col = 4 * (l16 & 3);
 #pragma unroll
         for (int ks = 0; ks < 5; ++ks) {
             bf16x8_t pb;
@@ -431,46 +485,46 @@ __global__ void __launch_bounds__(576) winattn_fwd_bf16(const unsigned short *__
                 pb[r] = (__bf16)s[2 * ks][r];
                 pb[4 + r] = (2 * ks + 1 < 9) ? (__bf16)s[2 * ks + 1][r] : (__bf16)0.f;
             }
-            const unsigned short *v0 = Vb + (32 * ks + 4 * grp + tr_row) * RS + tr_col;
-            const unsigned short *v1 = v0 + 16 * RS;
+            const unsigned short *v0 = Vs + (32 * ks + 4 * grp + tr_row) * RS + tr_col;
+            // keys 144..159 do not exist: their P is 0, so any finite rows serve (tile 8 again)
+            const unsigned short *v1 = ks < 4 ? v0 + 16 * RS : v0;
             const u16x8 a0 = cat4(tr_read(v0), tr_read(v1));
             const u16x8 a1 = cat4(tr_read(v0 + 16), tr_read(v1 + 16));
             o0 = mfma16(as_bf(a0), pb, o0);
             o1 = mfma16(as_bf(a1), pb, o1);
             os = mfma16(ones, pb, os);
         }
-        const float sum = os[0];
-        const float inv = 1.f / sum;
-        if (qtok >= 0) {
+        const float inv = 1.f / os[0];
+        if (qtk >= 0) {
             u16x4 w0, w1;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 w0[r] = f2bf(o0[r] * inv);
                 w1[r] = f2bf(o1[r] * inv);
             }
-            unsigned short *op = out + (long)qtok * g.C + h * HD;
+            unsigned short *op = out + (long)qtk * g.C + h * HD;
             *(u16x4 *)(op + grp * 4) = w0;
             *(u16x4 *)(op + 16 + grp * 4) = w1;
         }
-        if (grp == 0) lse[((long)bw * g.nH + h) * NT + qi] = fmaf(mx, LOG2E, __log2f(sum));  // base-2 LSE
-    };
-    Stage sa, sb;
-    if (ck.w_begin < ck.w_end) load(ck.w_begin, sa);
-    if (ck.w_begin + 1 < ck.w_end) load(ck.w_begin + 1, sb);
-    for (int bw = ck.w_begin; bw < ck.w_end; bw += 2) {
-        step(bw, 0, sa);
-        if (bw + 1 < ck.w_end) step(bw + 1, 1, sb);
+        if (grp == 0) lse[((long)bw * g.nH + h) * NT + qi] = fmaf(mx, LOG2E, __log2f(os[0]));  // base-2 LSE
     }
 }
 
+// Backward: persistent-chunk workgroups of 9 waves (one head x a contiguous chunk of windows,
+// ~one workgroup per CU), phase 1 key-on-lane (S = Q'·Kᵀ + B, dP = dO·Vᵀ - δ; dVᵀ += dOᵀ·P and
+// dKᵀ += Q'ᵀ·dS straight from the accumulators; dS to LDS), phase 2 dQᵀ = Kᵀ·dSᵀ.  The biases are
+// the forward's fp32 values, seeded into the S accumulator as there: for a key and 4 consecutive
+// queries of one window row they are 4 consecutive table entries, one ds_read_b128 from the
+// head's bias quads (copies 4..7) staged once per workgroup.
 // EX: support the optional rel-table / pad-bias gradient accumulators (frozen in IR-ADS's
 // Adapter training, so the default instantiation compiles them out)
 template <int MM, bool EX>
 __global__ void __launch_bounds__(576) winattn_bwd_bf16(
-    const unsigned short *__restrict__ qkv, const float *__restrict__ qbias, const float *__restrict__ table,
+    const unsigned short *__restrict__ qkv, const float *__restrict__ qbias, const float *__restrict__ quads,
     const float *__restrict__ mask, Geo g, int cw, const unsigned short *__restrict__ out, const float *__restrict__ lse,
     const unsigned short *__restrict__ gout, unsigned short *__restrict__ gqkv, float *__restrict__ gtable,
     float *__restrict__ gbias) {
+    __shared__ __attribute__((aligned(16))) float Bf[4 * BQ];  // copy c: Bf[c*BQ + i] = T[i + c]
     __shared__ __attribute__((aligned(16))) unsigned short Qs[NR * RS];
     __shared__ __attribute__((aligned(16))) unsigned short dOs[NR * RS];
     __shared__ __attribute__((aligned(16))) unsigned short Ks[NR * RS];
@@ -478,6 +532,7 @@ __global__ void __launch_bounds__(576) winattn_bwd_bf16(
     __shared__ __attribute__((aligned(16))) unsigned short dSt[NR * DSR];  // dSᵀ: [key][query], keys >= 144 zero
     __shared__ __attribute__((aligned(16))) float lseS[NT], dltS[NT];
     __shared__ int tokS[NT];
+    __shared__ float tgS[EX ? TBL : 1];  // EX: this workgroup's rel-table gradient, flushed once
     const Chunk ck = decode_chunk(g, cw);
     const int h = ck.h;
     const long C3 = 3 * g.C;
@@ -489,27 +544,25 @@ __global__ void __launch_bounds__(576) winattn_bwd_bf16(
         Ks[NT * RS + i] = 0;
     }
     for (int i = tid; i < (NR - NT) * DSR; i += 576) dSt[NT * DSR + i] = 0;
-    // per-lane biases (key on the lane): key = 16 wave + l16, query = 16 qt + 4 grp + r
+    if (EX)
+        for (int i = tid; i < TBL; i += 576) tgS[i] = 0.f;
+    {  // the head's bias quads, copies 4..7 (key on the lane), 16-B loads
+        const f32x4 *src = (const f32x4 *)(quads + (long)h * 8 * BQ + 4 * BQ);
+        for (int i = tid; i < BQ; i += 576) ((f32x4 *)Bf)[i] = src[i];
+    }
+    // key = 16 wave + l16 on the lane, queries 16 qt + 4 grp + r
     const int kkey = wave * 16 + l16;
-    unsigned bias[18];  // fp16 pairs
+    const int bk = 23 * (kkey / WS) + kkey % WS;  // bias table index = 264 + 23 * row(q) + col(q) - bk
     unsigned long long hb = 0, wb = 0;  // query class bits (MM == 1)
+    if (MM == 1)
 #pragma unroll
-    for (int qt = 0; qt < 9; ++qt)
+        for (int qt = 0; qt < 9; ++qt)
 #pragma unroll
-        for (int r = 0; r < 4; r += 2) {
-            const int q = qt * 16 + grp * 4 + r;
-            h2 pr;
-            pr[0] = (_Float16)(table[rel_idx(q, kkey) * g.nH + h] * LOG2E);
-            pr[1] = (_Float16)(table[rel_idx(q + 1, kkey) * g.nH + h] * LOG2E);
-            bias[qt * 2 + r / 2] = __builtin_bit_cast(unsigned, pr);
-            asm volatile("" : "+v"(bias[qt * 2 + r / 2]));  // opaque: no re-packing from f32 in the loop
-            if (MM == 1) {
+            for (int r = 0; r < 4; ++r) {
+                const int q = qt * 16 + grp * 4 + r;
                 hb |= (unsigned long long)hi_row(g, q) << (qt * 4 + r);
                 wb |= (unsigned long long)hi_col(g, q) << (qt * 4 + r);
-                hb |= (unsigned long long)hi_row(g, q + 1) << (qt * 4 + r + 1);
-                wb |= (unsigned long long)hi_col(g, q + 1) << (qt * 4 + r + 1);
             }
-        }
     const bool k_hr = hi_row(g, kkey), k_hc = hi_col(g, kkey);
     const int st_t = tid >> 2, st_ch = tid & 3;
     u16x8 qreg, oreg, dreg, kreg, vreg;
@@ -553,8 +606,6 @@ __global__ void __launch_bounds__(576) winattn_bwd_bf16(
             }
             if (tid < NT) lseS[tid] = lreg;
         }
-#pragma unroll
-        for (int i = 0; i < 18; ++i) asm volatile("" : "+v"(bias[i]));  // keep biases packed (no LICM unpack)
         __syncthreads();
         if (bw + 1 < ck.w_end) prefetch(bw + 1);
         unsigned long long mbits = 0;
@@ -591,19 +642,20 @@ __global__ void __launch_bounds__(576) winattn_bwd_bf16(
                 const bf16x8_t da = as_bf(*(const u16x8 *)(dOs + (qt * 16 + l16) * RS + grp * 8));
                 const f32x4 l4 = *(const f32x4 *)(lseS + qt * 16 + grp * 4);
                 const f32x4 nd4 = *(const f32x4 *)(dltS + qt * 16 + grp * 4);
-                const f32x4 sa = mfma16(qa, kb, f32x4{0.f, 0.f, 0.f, 0.f});  // S[q][key] (Q' pre-scaled)
+                const int q0 = qt * 16 + grp * 4, si = 264 + 23 * (q0 / WS) + q0 % WS - bk;
+                const f32x4 b4 = ((const f32x4 *)Bf)[(si & 3) * (BQ / 4) + (si >> 2)];
+                const f32x4 sa = mfma16(qa, kb, b4);  // S[q][key] + B (Q' pre-scaled), as the forward's Sᵀ
                 const f32x4 dpa = mfma16(da, vb, nd4);                       // dP[q][key] - delta_q
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    float v = fmaf(sa[r], LOG2E, (float)__builtin_bit_cast(h2, bias[qt * 2 + r / 2])[r & 1]);
-                    if (MASKED) v += ((mbits >> (qt * 4 + r)) & 1ull) ? -100.0f * LOG2E : 0.0f;
-                    if (MM == 2)
-                        v += LOG2E * mask[((long)(bw % g.n_mask) * NT + qt * 16 + grp * 4 + r) * NT + kkey];
-                    const float p = fast_exp2(v - l4[r]);
+                    float v = sa[r];
+                    if (MASKED) v += ((mbits >> (qt * 4 + r)) & 1ull) ? -100.0f : 0.0f;
+                    if (MM == 2) v += mask[((long)(bw % g.n_mask) * NT + qt * 16 + grp * 4 + r) * NT + kkey];
+                    const float p = fast_exp2(fmaf(v, LOG2E, -l4[r]));
                     const float ds = p * dpa[r];
                     pb[4 * half + r] = (__bf16)p;
                     sb[4 * half + r] = (__bf16)ds;
-                    if (EX && gtable) atomicAdd(&gtable[rel_idx(qt * 16 + grp * 4 + r, kkey) * g.nH + h], ds);
+                    if (EX && gtable) atomicAdd(&tgS[rel_idx(qt * 16 + grp * 4 + r, kkey)], ds);  // LDS atomic
                 }
                 const u16x8 sbits = __builtin_bit_cast(u16x8, sb);
                 *(u16x4 *)(dSt + kkey * DSR + qt * 16 + grp * 4) =
@@ -691,6 +743,10 @@ __global__ void __launch_bounds__(576) winattn_bwd_bf16(
             }
         }
     }
+    if (EX && gtable) {
+        __syncthreads();
+        for (int i = tid; i < TBL; i += 576) atomicAdd(&gtable[i * g.nH + h], tgS[i]);
+    }
 }
 
 int chunk_windows(int total_windows, int nH) {
@@ -728,8 +784,17 @@ int make_geo(Geo &g, int dtype, int B, int H, int W, int C, int nH, int shift, f
 
 using namespace irads;
 
+extern "C" int irads_winattn_bias_quads(const float *rel_table, int nH, float *quads, void *stream) {
+    IRADS_REQUIRE(rel_table && quads && nH > 0, "irads_winattn_bias_quads: null pointer / nH=%d", nH);
+    const int n = nH * 8 * BQ;
+    winattn_bias_quads_kernel<<<(n + 255) / 256, 256, 0, (hipStream_t)stream>>>(rel_table, nH, quads);
+    return check_launch("irads_winattn_bias_quads");
+}
+
+extern "C" long irads_winattn_bias_quads_size(int nH) { return (long)nH * 8 * BQ; }
+
 extern "C" int irads_winattn_fwd(int dtype, const void *qkv, const float *qkv_bias, const float *rel_table,
-                                 const float *mask, int n_mask, int B, int H, int W, int C, int nH, int shift,
+                                 const float *bias_quads, const float *mask, int n_mask, int B, int H, int W, int C, int nH, int shift,
                                  float scale, void *out, float *lse, void *stream) {
     Geo g;
     if (int e = make_geo(g, dtype, B, H, W, C, nH, shift, scale, mask, n_mask)) return e;
@@ -741,10 +806,9 @@ extern "C" int irads_winattn_fwd(int dtype, const void *qkv, const float *qkv_bi
     else
     {
         const int mm = mask ? 2 : (shift > 0 ? 1 : 0);
-        const int cw = chunk_windows(B * g.nW, nH);
-        const unsigned nwg = (unsigned)(((B * g.nW + cw - 1) / cw) * nH);
-#define IRADS_WF(M) winattn_fwd_bf16<M><<<nwg, 576, 0, st>>>((const unsigned short *)qkv, qkv_bias, rel_table, mask, \
-                                                             g, cw, (unsigned short *)out, lse)
+        IRADS_REQUIRE(bias_quads, "irads_winattn_fwd: bf16 needs bias_quads (irads_winattn_bias_quads)");
+#define IRADS_WF(M) winattn_fwd_bf16_wg<M><<<nblk, 192, 0, st>>>((const unsigned short *)qkv, qkv_bias, bias_quads, \
+                                                                  mask, g, (unsigned short *)out, lse)
         if (mm == 0) IRADS_WF(0); else if (mm == 1) IRADS_WF(1); else IRADS_WF(2);
 #undef IRADS_WF
     }
@@ -752,26 +816,27 @@ extern "C" int irads_winattn_fwd(int dtype, const void *qkv, const float *qkv_bi
 }
 
 extern "C" int irads_winattn_bwd(int dtype, const void *qkv, const float *qkv_bias, const float *rel_table,
-                                 const float *mask, int n_mask, int B, int H, int W, int C, int nH, int shift,
-                                 float scale, const void *out, const float *lse, const void *grad_out, void *grad_qkv,
-                                 float *grad_table, float *grad_bias_pad, void *stream) {
+                                 const float *bias_quads, const float *mask, int n_mask, int B, int H, int W, int C,
+                                 int nH, int shift, float scale, const void *out, const float *lse,
+                                 const void *grad_out, void *grad_qkv, float *grad_table, float *grad_bias_pad,
+                                 void *stream) {
     Geo g;
     if (int e = make_geo(g, dtype, B, H, W, C, nH, shift, scale, mask, n_mask)) return e;
     if (B == 0) return IRADS_OK;
     hipStream_t st = (hipStream_t)stream;
     const unsigned nblk = (unsigned)(B * g.nW * nH);
-    if (dtype == IRADS_F32)
+    const int mm = mask ? 2 : (shift > 0 ? 1 : 0);
+    const bool ex = grad_table || grad_bias_pad;
+    if (dtype == IRADS_F32) {
         winattn_bwd_f32<<<nblk, 256, 0, st>>>((const float *)qkv, qkv_bias, rel_table, mask, g, (const float *)out,
                                               lse, (const float *)grad_out, (float *)grad_qkv, grad_table,
                                               grad_bias_pad);
-    else
-    {
-        const int mm = mask ? 2 : (shift > 0 ? 1 : 0);
+    } else {
+        IRADS_REQUIRE(bias_quads, "irads_winattn_bwd: bf16 needs bias_quads (irads_winattn_bias_quads)");
         const int cw = chunk_windows(B * g.nW, nH);
         const unsigned nwg = (unsigned)(((B * g.nW + cw - 1) / cw) * nH);
-        const bool ex = grad_table || grad_bias_pad;
 #define IRADS_WB(M, X)                                                                                            \
-    winattn_bwd_bf16<M, X><<<nwg, 576, 0, st>>>((const unsigned short *)qkv, qkv_bias, rel_table, mask, g, cw,    \
+    winattn_bwd_bf16<M, X><<<nwg, 576, 0, st>>>((const unsigned short *)qkv, qkv_bias, bias_quads, mask, g, cw,   \
                                                 (const unsigned short *)out, lse, (const unsigned short *)grad_out, \
                                                 (unsigned short *)grad_qkv, grad_table, grad_bias_pad)
         if (ex) {

@@ -22,8 +22,9 @@ SIGNATURES = {
     "irads_msda_fwd": [_i, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp, _vp],
     "irads_msda_bwd": [_i, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp],
     "irads_msda_corner_index": [_i, _vp, _vp, _i, _i, _i, _i, _i, _vp, _vp],
-    "irads_winattn_fwd": [_i, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _f, _vp, _vp, _vp],
-    "irads_winattn_bwd": [_i, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _f, _vp, _vp, _vp, _vp, _vp, _vp,
+    "irads_winattn_bias_quads": [_vp, _i, _vp, _vp],
+    "irads_winattn_fwd": [_i, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _f, _vp, _vp, _vp],
+    "irads_winattn_bwd": [_i, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _f, _vp, _vp, _vp, _vp, _vp, _vp,
                           _vp],
     "irads_dattn_sample_fwd": [_vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp],
     "irads_dattn_sample_bwd": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp,
@@ -71,7 +72,8 @@ QUERIES = {"irads_wgrad_workspace": (ctypes.c_long, [_i, _i, _i]),
            "irads_wgrad_batched_workspace": (ctypes.c_long, [_i] * 4),
            "irads_mpg_partials": (ctypes.c_long, [_l, _i]),
            "irads_ln_bf16_partials": (ctypes.c_long, [_l, _i]),
-           "irads_bnact_partials": (ctypes.c_long, [_l, _i])}
+           "irads_bnact_partials": (ctypes.c_long, [_l, _i]),
+           "irads_winattn_bias_quads_size": (ctypes.c_long, [_i])}
 CE_WORKSPACE = 2048
 
 _lib = None

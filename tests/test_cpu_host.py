@@ -55,8 +55,8 @@ def test_version_and_error_strings(lib):
     f = lib.irads_msda_fwd
     rc = f(7, None, None, None, None, None, 1, 1, 1, 1, 1, 1, 1, None, None)
     assert rc != 0 and b"dtype" in lib.irads_last_error()
-    rc = lib.irads_winattn_fwd(0, None, None, None, None, 0, 1, 12, 12, 100, 4, 0, ctypes.c_float(1.0), None, None,
-                               None)
+    rc = lib.irads_winattn_fwd(0, None, None, None, None, None, 0, 1, 12, 12, 100, 4, 0, ctypes.c_float(1.0), None,
+                               None, None)
     assert rc != 0 and b"head_dim" in lib.irads_last_error()
 
 
