@@ -37,13 +37,13 @@ N_CLASSES = 40  # NYU-Depth-v2 (nyu.py:20-23)
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--steps", type=int, default=50)   # >= 50 timed
+    p.add_argument("--warmup", type=int, default=10)  # 10 warm-up iterations
     p.add_argument("--batch", type=int, default=8, help="images per GPU (C2: 8)")
     p.add_argument("--size", type=int, default=512)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-batch", type=int, default=4, help="apply_mask needs >= 4 (swin.py:1098-1103)")
-    p.add_argument("--cpu-steps", type=int, default=1)
+    p.add_argument("--cpu-steps", type=int, default=3, help="SURVEY §8(d): 1 warmup + 3 timed")
     p.add_argument("--profile-only", action="store_true", help="run warmup + steps, print nothing extra")
     p.add_argument("--eager", action="store_true", help="launch op by op (default: replay a captured HIP graph)")
     p.add_argument("--no-tuned-gemms", action="store_true", help="hipBLASLt default picks (ignore irads/tuned/)")
@@ -148,6 +148,8 @@ def msda_inputs(device, bs=2, Q=None, seed=0):
     return [t.to(device) for t in (value, shapes, lsi, loc, aw)]
 
 
+TIMED_KERNELS = ("winattn_fwd", "winattn_bwd", "dattn_fwd", "dattn_bwd")
+FP32_PEAK_TFLOPS = 157.3  # MI355X fp32 vector peak (MI355X_MICROARCH.md)
 GATHER_PEAK_GBS = 18800.0  # L2-resident random-row gather rate (upper end), MI355X_MICROARCH.md
 ATOMIC_PEAK_GBS = 1300.0  # chip-wide f32 atomic-add rate, MI355X_MICROARCH.md 'Global float atomics'
 
@@ -212,7 +214,7 @@ def msda_rooflines(device, reps=20):
 
 
 def traffic_from_profile():
-    path = os.path.join(ROOT, "profiles", "pmc_winattn_fwd.json")
+    path = os.path.join(ROOT, "profiles", "r02_pmc_winattn_fwd.json")
     if not os.path.exists(path):
         return None
     with open(path) as f:
@@ -250,7 +252,7 @@ def main():
         def arm_timer():  # per-launch HIP events captured around the window-attention kernels
             if timer_in_graph:
                 ops.TIMER.records.clear()
-                ops.TIMER.enabled = {"winattn_fwd", "winattn_bwd"}
+                ops.TIMER.enabled = set(TIMED_KERNELS)
         runner = GraphedTrainStep(model.parameters(), lambda: fwd_bwd(model, loss_fn, batch), opt, world=world,
                                   warmup=max(args.warmup, 1), before_capture=arm_timer)
         ops.TIMER.enabled = set()
@@ -268,7 +270,7 @@ def main():
     if world > 1:
         dist.barrier()
     if not graph:
-        ops.TIMER.enabled = {"winattn_fwd", "winattn_bwd"}
+        ops.TIMER.enabled = set(TIMED_KERNELS)
     if not timer_in_graph:
         ops.TIMER.records.clear()
     torch.cuda.synchronize()
@@ -284,7 +286,7 @@ def main():
     if graph and not timer_in_graph:
         # HIP events cannot be captured on this stack: time the same kernels in one eager step
         ops.TIMER.records.clear()
-        ops.TIMER.enabled = {"winattn_fwd", "winattn_bwd"}
+        ops.TIMER.enabled = set(TIMED_KERNELS)
         fwd_bwd(model, loss_fn, batch)  # gradients land in the graph's buffer, re-zeroed by the next replay
         ops.TIMER.enabled = set()
     if world > 1:
@@ -338,6 +340,18 @@ def main():
                                       "avg_launch_ms": round(bwd["total_ms"] / bwd["launches"], 5),
                                       "share_of_step": round(bwd["total_ms"] / timer_steps / (1e3 * elapsed / args.steps), 4)}
             result["roofline"]["share_of_step"] = round(fwd["total_ms"] / timer_steps / (1e3 * elapsed / args.steps), 4)
+    for tag in ("fwd", "bwd"):
+        d = ops.TIMER.summary(f"dattn_{tag}")
+        if d:
+            tf = d["flops"] / (d["total_ms"] * 1e-3) / 1e12
+            result[f"roofline_dattn_{tag}"] = {
+                "kernel": f"irads_dattn_attn_{tag} (DSCF deformable attention core, fp32, 4 stages)",
+                "bound": "fp32-valu", "achieved": round(tf, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(tf / FP32_PEAK_TFLOPS, 4), "launches": d["launches"],
+                "avg_launch_ms": round(d["total_ms"] / d["launches"], 5),
+                "flops_definition": "SURVEY §8(d): 44 FLOP per (query, key) pair forward, 88 backward; "
+                                    "pairs = B·heads·H·W·2n per stage",
+                "share_of_step": round(d["total_ms"] / timer_steps / (1e3 * elapsed / args.steps), 4)}
     if rank == 0 and not args.no_kernels:
         try:
             result["kernels"] = msda_rooflines(device)

@@ -367,8 +367,14 @@ class DAttnAttentionFn(torch.autograd.Function):
         Ht, Wt = rpe_table.shape[1], rpe_table.shape[2]
         out = torch.empty_like(ts[0])
         lse = torch.empty((B * n_heads, H * W), device=q.device, dtype=torch.float32)
+        ev = TIMER.start("dattn_fwd")
         N.call("irads_dattn_attn_fwd", *[N.ptr(t) for t in ts], B, n_heads, groups, hc, H, W, n, Ht, Wt,
                float(scale), N.ptr(out), N.ptr(lse), N.stream())
+        # algorithmic work: B·h·HW·2n (query, key) pairs at 44 FLOP each (4·hc for
+        # q·k and p·v with hc = 8, plus 12 for the bilinear rpe bias); bytes: q, out, k, v, pos, table
+        pairs = B * n_heads * H * W * 2 * n
+        TIMER.stop("dattn_fwd", ev, 4 * (2 * q.numel() + 2 * k.numel() + 2 * pos_x.numel() + rpe_table.numel()),
+                   44 * pairs)
         ctx.save_for_backward(*ts, out, lse)
         ctx.cfg = (B, n_heads, groups, hc, H, W, n, Ht, Wt, float(scale))
         return out
@@ -382,9 +388,12 @@ class DAttnAttentionFn(torch.autograd.Function):
         # all six are atomically accumulated: zeroed by one fill (gq: key splits add into it;
         # gk, gv key-major like k and v here)
         gq, gk, gv, grpe, gpx, gpy = zeros_like_many(q, k, v, rpe, px, py)
+        ev = TIMER.start("dattn_bwd")
         N.call("irads_dattn_attn_bwd", N.ptr(q), N.ptr(k), N.ptr(v), N.ptr(px), N.ptr(py), N.ptr(rpe), N.ptr(qgy),
                N.ptr(qgx), B, nH, G, hc, H, W, n, Ht, Wt, scale, N.ptr(out), N.ptr(lse), N.ptr(gout), N.ptr(delta),
                N.ptr(gq), N.ptr(gk), N.ptr(gv), N.ptr(grpe), N.ptr(gpx), N.ptr(gpy), N.stream())
+        TIMER.stop("dattn_bwd", ev, 8 * (2 * q.numel() + 2 * k.numel() + 2 * px.numel() + rpe.numel()),
+                   88 * B * nH * H * W * 2 * n)  # backward = 2x the forward's 44 FLOP / pair
         return (gq, gk.transpose(1, 2), gv.transpose(1, 2), gpx, gpy, grpe, None, None, None, None, None, None, None,
                 None)
 
