@@ -39,8 +39,11 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=50)   # >= 50 timed
     p.add_argument("--warmup", type=int, default=10)  # 10 warm-up iterations
-    p.add_argument("--batch", type=int, default=8, help="images per GPU (C2: 8)")
-    p.add_argument("--size", type=int, default=512)
+    p.add_argument("--workload", choices=("c2", "c4"), default="c2",
+                   help="c2: the headline C2 step (default); c4: BASELINE config C4 (MFNet RGB-T, Swin-L, "
+                        "480x640, B=4 per GPU, SB hook on) as a separate line")
+    p.add_argument("--batch", type=int, default=None, help="images per GPU (C2: 8, C4: 4)")
+    p.add_argument("--size", type=int, default=None, help="square side (C2: 512); C4 is 480x640")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-batch", type=int, default=4, help="apply_mask needs >= 4 (swin.py:1098-1103)")
     p.add_argument("--cpu-steps", type=int, default=3, help="SURVEY §8(d): 1 warmup + 3 timed")
@@ -51,21 +54,36 @@ def parse():
     return p.parse_args()
 
 
-def synthetic_batch(B, size, device, seed):
+WORKLOADS = {
+    # BASELINE.json configs: C2 (headline) and C4; per-GPU batch, (H, W), classes, backbone, SB hook
+    "c2": dict(batch=8, hw=(512, 512), n_cls=N_CLASSES, backbone="SwinTransformer-B", modals=["img", "depth"],
+               sb=None, desc="C2: NYU-Depth-v2 RGB-D CMNeXt(SwinTransformer-B) 512x512 train step "
+                             "(fwd+bwd+AdamW, TRAIN_TYPE Adapter, MMST loss)"),
+    "c4": dict(batch=4, hw=(480, 640), n_cls=9, backbone="SwinTransformer-L", modals=["img", "thermal"],
+               sb={"weight": 0.01, "n_potentials": 10, "epsilon": 0.1},
+               desc="C4: MFNet RGB-T CMNeXt(SwinTransformer-L) 480x640 train step (fwd+bwd+AdamW, TRAIN_TYPE "
+                    "Adapter, MMST loss) with the build-defined SB hook on (LightSB on the 512-d fused head "
+                    "feature, 120x160 rows per image)"),
+}
+
+
+def synthetic_batch(B, hw, device, seed, n_cls=N_CLASSES):
+    H, W = (hw, hw) if isinstance(hw, int) else hw
     g = torch.Generator(device="cpu").manual_seed(seed)
-    rgb = torch.randn(B, 3, size, size, generator=g)                # post-Normalize RGB
-    dep = torch.rand(B, 3, size, size, generator=g)                 # depth / HHA: /255 only
-    lbl = torch.randint(0, N_CLASSES, (B, size, size), generator=g)
-    lbl[torch.rand(B, size, size, generator=g) < 0.1] = 255
+    rgb = torch.randn(B, 3, H, W, generator=g)                # post-Normalize RGB
+    dep = torch.rand(B, 3, H, W, generator=g)                 # depth / HHA / thermal: /255 only
+    lbl = torch.randint(0, n_cls, (B, H, W), generator=g)
+    lbl[torch.rand(B, H, W, generator=g) < 0.1] = 255
     return rgb.to(device), dep.to(device), lbl.to(device)
 
 
-def build(device, world, local_rank, iters, graph=False):
+def build(device, world, local_rank, iters, graph=False, wl=None):
     from semseg.models import CMNeXt
     from semseg.optimizers import get_optimizer
     from semseg.schedulers import get_scheduler
     from semseg.losses import get_loss
-    model = CMNeXt("SwinTransformer-B", N_CLASSES, ["img", "depth"]).to(device)
+    wl = wl or WORKLOADS["c2"]
+    model = CMNeXt(wl["backbone"], wl["n_cls"], wl["modals"], sb=wl["sb"]).to(device)
     opt = get_optimizer(model, "adamw", 4e-4, "Adapter", 0.01, lr_on_device=graph)  # nyu_rgbd.yaml:31-35
     sched = get_scheduler("warmuppolylr", opt, iters, 0.9, 10, 0.1)
     if world > 1 and not graph:
@@ -82,6 +100,9 @@ def fwd_bwd(model, loss_fn, batch):
     with torch.autocast("cuda", dtype=torch.bfloat16):
         logits, logits_rgb, logits_dte = model([rgb, dep])
         loss = mmst_loss(loss_fn, logits, logits_rgb, logits_dte, lbl)
+        m = model.module if hasattr(model, "module") else model
+        if m.sb_cfg:
+            loss = loss + m.sb_loss()
     loss.backward()
     return loss
 
@@ -111,7 +132,8 @@ def cpu_baseline(args):
     opt = torch.optim.AdamW(params, 4e-4, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01)
     model.train()
     B = args.cpu_batch
-    rgb, dep, lbl = synthetic_batch(B, args.size, "cpu", 3407)
+    size = args.size or 512
+    rgb, dep, lbl = synthetic_batch(B, size, "cpu", 3407)
     batch = (rgb[:B], dep[:B], lbl[:B])
 
     def step():
@@ -125,7 +147,7 @@ def cpu_baseline(args):
         step()
     dt = time.perf_counter() - t0
     return {"value": round(B * args.cpu_steps / dt, 4), "unit": "images/s", "cores": threads, "kind": "port",
-            "sample": f"oracle CPU restatement (fp32 PyTorch), same train step at batch {B}, {args.size}x{args.size}, "
+            "sample": f"oracle CPU restatement (fp32 PyTorch), same train step at batch {B}, {size}x{size}, "
                       f"1 warmup + {args.cpu_steps} timed steps, {dt:.1f} s"}
 
 
@@ -237,9 +259,15 @@ def main():
     graph = not args.eager
     from irads.gemm_tuning import use_tuned_gemms
     tuned = False if args.no_tuned_gemms else use_tuned_gemms()
-    model, opt, sched, loss_fn = build(device, world, local_rank, 100000, graph=graph)
+    wl = dict(WORKLOADS[args.workload])
+    if args.batch:
+        wl["batch"] = args.batch
+    if args.size:
+        wl["hw"] = (args.size, args.size)
+    args.batch = wl["batch"]
+    model, opt, sched, loss_fn = build(device, world, local_rank, 100000, graph=graph, wl=wl)
     model.train()
-    batch = synthetic_batch(args.batch, args.size, device, 3407 + rank)
+    batch = synthetic_batch(args.batch, wl["hw"], device, 3407 + rank, wl["n_cls"])
 
     from irads import ops
     timer_in_graph = False
@@ -308,10 +336,9 @@ def main():
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 3),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
         "data": "synthetic (RGB N(0,1), depth U[0,1), labels U{0..39} with 10% ignore=255; random-init weights)",
-        "config": {"workload": "C2: NYU-Depth-v2 RGB-D CMNeXt(SwinTransformer-B) 512x512 train step "
-                               "(fwd+bwd+AdamW, TRAIN_TYPE Adapter, MMST loss)",
+        "config": {"workload": wl["desc"],
                    "per_gpu_batch": args.batch, "global_batch": args.batch * world,
-                   "image_size": [args.size, args.size], "parallelism": f"dp{world}",
+                   "image_size": list(wl["hw"]), "parallelism": f"dp{world}",
                    "execution": "hip-graph replay" if graph else "eager",
                    "gemm_selection": "TunableOp table irads/tuned" if tuned else "hipBLASLt heuristic"},
         "loss": round(loss_val, 5),
@@ -352,12 +379,17 @@ def main():
                 "flops_definition": "SURVEY §8(d): 44 FLOP per (query, key) pair forward, 88 backward; "
                                     "pairs = B·heads·H·W·2n per stage",
                 "share_of_step": round(d["total_ms"] / timer_steps / (1e3 * elapsed / args.steps), 4)}
-    if rank == 0 and not args.no_kernels:
+    if args.workload != "c2":  # a separate line for another BASELINE config, not the headline metric
+        result["metric"] = ("train images/sec @480x640 RGB-T Swin-L, SB hook on (BASELINE.json config C4), "
+                            "1 MI355X" if args.workload == "c4" else f"train images/sec ({args.workload})")
+        result["data"] = ("synthetic (RGB N(0,1), thermal U[0,1), labels U{0..%d} with 10%% ignore=255; random-init "
+                          "weights)" % (wl["n_cls"] - 1))
+    if rank == 0 and not args.no_kernels and args.workload == "c2":
         try:
             result["kernels"] = msda_rooflines(device)
         except Exception as e:  # report, never fake
             result["kernels"] = {"error": repr(e)[:200]}
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == "c2":
         try:
             result["cpu_baseline"] = cpu_baseline(args)
         except Exception as e:  # report, never fake

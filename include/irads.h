@@ -168,6 +168,12 @@ int irads_sb_em(int dtype, const void *x0, const void *noise, int n_steps, const
 int irads_sb_logits(int dtype, const void *x, const void *r, const void *S_log_diag,
                     const void *log_alpha_raw, double epsilon, int rows, int D, int K, void *logits,
                     void *log_C, void *stream);
+/* get_log_potential (sb.py:183-204), diagonal: log_v (rows) = logsumexp_k arg_k with
+ * arg_k = log_alpha_raw_k/eps - ½Σ_d [(x_d - r_kd)²/(eps S_kd) + log(2π eps S_kd)]; logits
+ * (rows, K) = arg, optional (the closed-form backward uses it). */
+int irads_sb_log_potential(int dtype, const void *x, const void *r, const void *S_log_diag,
+                           const void *log_alpha_raw, double epsilon, int rows, int D, int K, void *logits,
+                           void *log_v, void *stream);
 
 /* ------------------------------------------------------------------ segmentation head tail
  * Bilinear resize, align_corners=False, explicit output size: the F.interpolate calls of

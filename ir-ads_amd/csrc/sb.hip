@@ -177,6 +177,62 @@ __global__ void __launch_bounds__(256) sb_logits_kernel(const T *__restrict__ x,
     }
 }
 
+// get_log_potential (sb.py:183-204), diagonal: log Σ_k alpha_k N(x; r_k, eps S_k) + logsumexp(log alpha)
+// = logsumexp_k arg_k with arg_k = log_alpha_raw_k/eps - ½Σ_d [(x_d - r_kd)²/(eps S_kd) + log(2π eps S_kd)]
+// (the mixture's log_softmax and the added logsumexp cancel).  One wave per row, x in registers,
+// 1/(eps S), r and the per-component constants staged once per workgroup in LDS; the squared
+// differences are formed directly (no x² - 2xr + r² expansion, which cancels at eps S = 0.01).
+template <typename T>
+__global__ void __launch_bounds__(256) sb_potential_kernel(const T *__restrict__ x, const T *__restrict__ r,
+                                                           const T *__restrict__ Sl, const T *__restrict__ la, T eps,
+                                                           int rows, int D, int K, T *__restrict__ logits,
+                                                           T *__restrict__ logv) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    T *ise = (T *)smem, *rr = ise + K * D, *kc = rr + K * D;
+    for (int i = threadIdx.x; i < K * D; i += blockDim.x) {
+        ise[i] = exp(-Sl[i]) / eps;
+        rr[i] = r[i];
+    }
+    const int wave = threadIdx.x / 64, lane = threadIdx.x % 64;
+    for (int k = wave; k < K; k += blockDim.x / 64) {
+        T s = 0;
+        for (int d = lane; d < D; d += 64) s += log((T)6.283185307179586 * eps) + Sl[k * D + d];
+        s = wsum(s);
+        if (lane == 0) kc[k] = la[k] / eps - (T)0.5 * s;
+    }
+    __syncthreads();
+    const int nper = (D + 63) / 64;
+    for (int row = blockIdx.x * (blockDim.x / 64) + wave; row < rows; row += gridDim.x * (blockDim.x / 64)) {
+        T xv[kMaxPerLane];
+        for (int j = 0; j < nper; ++j) {
+            const int d = lane + 64 * j;
+            xv[j] = d < D ? x[(long)row * D + d] : (T)0;
+        }
+        T arg[kMaxK];
+        for (int k = 0; k < K; ++k) {
+            T q = 0;
+            for (int j = 0; j < nper; ++j) {
+                const int d = lane + 64 * j;
+                if (d < D) {
+                    const T df = xv[j] - rr[k * D + d];
+                    q += df * df * ise[k * D + d];
+                }
+            }
+            arg[k] = kc[k] - (T)0.5 * wsum(q);
+        }
+        if (lane == 0) {
+            T mx = arg[0];
+            for (int k = 1; k < K; ++k) mx = arg[k] > mx ? arg[k] : mx;
+            T s = 0;
+            for (int k = 0; k < K; ++k) {
+                if (logits) logits[(long)row * K + k] = arg[k];
+                s += exp(arg[k] - mx);
+            }
+            logv[row] = mx + log(s);
+        }
+    }
+}
+
 int check(int dtype, int rows, int D, int K) {
     IRADS_REQUIRE(dtype == IRADS_F32 || dtype == IRADS_F64, "sb: dtype must be float32 or float64");
     IRADS_REQUIRE(rows >= 0 && D > 0 && D <= 64 * kMaxPerLane, "sb: dim must be in [1, %d]", 64 * kMaxPerLane);
@@ -256,4 +312,26 @@ extern "C" int irads_sb_logits(int dtype, const void *x, const void *r, const vo
                                                                   (const double *)log_alpha_raw, epsilon, rows, D, K,
                                                                   (double *)logits, (double *)log_C);
     return check_launch("irads_sb_logits");
+}
+
+extern "C" int irads_sb_log_potential(int dtype, const void *x, const void *r, const void *S_log_diag,
+                                      const void *log_alpha_raw, double epsilon, int rows, int D, int K, void *logits,
+                                      void *log_v, void *stream) {
+    if (int e = check(dtype, rows, D, K)) return e;
+    IRADS_REQUIRE(log_v != nullptr, "sb_log_potential: null output");
+    if (rows == 0) return IRADS_OK;
+    hipStream_t st = (hipStream_t)stream;
+    if (dtype == IRADS_F32) {
+        size_t sh = (2 * (size_t)K * D + K) * sizeof(float);
+        sb_potential_kernel<float><<<grid_for(rows), 256, sh, st>>>(
+            (const float *)x, (const float *)r, (const float *)S_log_diag, (const float *)log_alpha_raw,
+            (float)epsilon, rows, D, K, (float *)logits, (float *)log_v);
+    } else {
+        size_t sh = (2 * (size_t)K * D + K) * sizeof(double);
+        IRADS_REQUIRE(sh <= 160 * 1024, "sb: float64 parameters exceed LDS (K*D too large)");
+        sb_potential_kernel<double><<<grid_for(rows), 256, sh, st>>>(
+            (const double *)x, (const double *)r, (const double *)S_log_diag, (const double *)log_alpha_raw, epsilon,
+            rows, D, K, (double *)logits, (double *)log_v);
+    }
+    return check_launch("irads_sb_log_potential");
 }

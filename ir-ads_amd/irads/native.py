@@ -35,6 +35,7 @@ SIGNATURES = {
     "irads_sb_drift": [_i, _vp, _vp, _vp, _vp, _vp, _d, _i, _i, _i, _vp, _vp],
     "irads_sb_em": [_i, _vp, _vp, _i, _vp, _vp, _vp, _d, _i, _i, _i, _vp, _vp],
     "irads_sb_logits": [_i, _vp, _vp, _vp, _vp, _d, _i, _i, _i, _vp, _vp, _vp],
+    "irads_sb_log_potential": [_i, _vp, _vp, _vp, _vp, _d, _i, _i, _i, _vp, _vp, _vp],
     "irads_resize_fwd": [_i, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _vp],
     "irads_resize_bwd": [_i, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _vp, _vp],
     "irads_ce_fwd": [_i, _vp, _vp, _i, _i, _i, _i, _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp],

@@ -449,6 +449,85 @@ def sb_logits(x, r, S_log_diag, log_alpha_raw, epsilon, want_logits=True, want_l
     return logits, log_c
 
 
+class SBLogCFn(torch.autograd.Function):
+    """LightSB.get_log_C (sb.py:206-224, diagonal S), differentiable in x, r, S_log_diagonal_matrix
+    and log_alpha_raw as the reference's autograd graph is.  Forward: the GMM logits per row
+    a_k = (xᵀS_k x + 2 xᵀr_k) / (2 eps) + log_alpha_raw_k / eps and log C = logsumexp_k a_k on the
+    irads_sb_logits kernel.  Backward, closed form with w = g · softmax_k(a):
+        dx = (w r + x ⊙ (w S)) / eps       dr = wᵀx / eps
+        dS_log = S ⊙ (wᵀ x²) / (2 eps)     dlog_alpha_raw = Σ_rows w / eps
+    (K = n_potentials columns: thin GEMMs on hipBLASLt)."""
+
+    @staticmethod
+    def forward(ctx, x, r, S_log_diag, log_alpha_raw, epsilon):
+        logits, log_c = sb_logits(x, r, S_log_diag, log_alpha_raw, epsilon)
+        ctx.save_for_backward(x, r, S_log_diag, logits, log_c)
+        ctx.eps, ctx.la_dtype = float(epsilon), log_alpha_raw.dtype
+        return log_c
+
+    @staticmethod
+    def backward(ctx, g):
+        x, r, S_log_diag, logits, log_c = ctx.saved_tensors
+        eps, dt = ctx.eps, x.dtype
+        w = torch.exp(logits - log_c[:, None]) * g.to(dt)[:, None]  # (rows, K)
+        S = torch.exp(S_log_diag.detach().to(dt))
+        need = ctx.needs_input_grad
+        dx = (w @ r.detach().to(dt) + x * (w @ S)) / eps if need[0] else None
+        dr = (w.t() @ x / eps).to(r.dtype) if need[1] else None
+        dS = (S * (w.t() @ (x * x)) / (2 * eps)).to(S_log_diag.dtype) if need[2] else None
+        da = (w.sum(0) / eps).to(ctx.la_dtype) if need[3] else None
+        return dx, dr, dS, da, None
+
+
+class SBLogPotentialFn(torch.autograd.Function):
+    """LightSB.get_log_potential (sb.py:183-204, diagonal S) on irads_sb_log_potential:
+    log v(x) = logsumexp_k arg_k, arg_k = log_alpha_raw_k/eps - ½Σ_d [(x_d - r_kd)²/(eps S_kd)
+    + log(2π eps S_kd)].  Backward, closed form with w = g · softmax_k(arg), U = 1/(eps S):
+        dx = w (U ⊙ r) - x ⊙ (w U)          dr = U ⊙ (wᵀx) - U ⊙ r ⊙ Σ_rows w
+        dS_log = ½ [U ⊙ (wᵀx² - 2 r ⊙ wᵀx + r² ⊙ Σ_rows w) - Σ_rows w]   dlog_alpha_raw = Σ_rows w / eps"""
+
+    @staticmethod
+    def forward(ctx, x, r, S_log_diag, log_alpha_raw, epsilon):
+        x = N.check(x.detach().contiguous(), "x")
+        code, (r_, s_, a_) = _sb_params(x, r, S_log_diag, log_alpha_raw)
+        rows, D = x.shape
+        K = r_.shape[0]
+        logits = torch.empty((rows, K), device=x.device, dtype=x.dtype)
+        log_v = torch.empty((rows,), device=x.device, dtype=x.dtype)
+        N.call("irads_sb_log_potential", code, N.ptr(x), N.ptr(r_), N.ptr(s_), N.ptr(a_), float(epsilon), rows, D,
+               K, N.ptr(logits), N.ptr(log_v), N.stream())
+        ctx.save_for_backward(x, r_, s_, logits, log_v)
+        ctx.eps, ctx.dtypes = float(epsilon), (r.dtype, S_log_diag.dtype, log_alpha_raw.dtype)
+        return log_v
+
+    @staticmethod
+    def backward(ctx, g):
+        x, r, Sl, logits, log_v = ctx.saved_tensors
+        eps = ctx.eps
+        w = torch.exp(logits - log_v[:, None]) * g.to(x.dtype)[:, None]  # (rows, K)
+        U = torch.exp(-Sl) / eps
+        cw = w.sum(0)  # (K,)
+        need = ctx.needs_input_grad
+        wx = w.t() @ x if (need[1] or need[2]) else None
+        dx = w @ (U * r) - x * (w @ U) if need[0] else None
+        dr = (U * wx - U * r * cw[:, None]).to(ctx.dtypes[0]) if need[1] else None
+        dS = (0.5 * (U * (w.t() @ (x * x) - 2 * r * wx + r * r * cw[:, None]) - cw[:, None])).to(ctx.dtypes[1]) \
+            if need[2] else None
+        da = (cw / eps).to(ctx.dtypes[2]) if need[3] else None
+        return dx, dr, dS, da, None
+
+
+def sb_log_c(x, r, S_log_diag, log_alpha_raw, epsilon):
+    """get_log_C: differentiable when any input requires grad, a plain launch otherwise."""
+    if torch.is_grad_enabled() and any(t.requires_grad for t in (x, r, S_log_diag, log_alpha_raw)):
+        return SBLogCFn.apply(x, r, S_log_diag, log_alpha_raw, epsilon)
+    return sb_logits(x, r, S_log_diag, log_alpha_raw, epsilon, want_logits=False)[1]
+
+
+def sb_log_potential(x, r, S_log_diag, log_alpha_raw, epsilon):
+    return SBLogPotentialFn.apply(x, r, S_log_diag, log_alpha_raw, epsilon)
+
+
 # ------------------------------------------------------------------ segmentation head tail
 def _layout(x):
     """(tensor, int64[4] strides) in one of the two dense layouts the kernels take."""

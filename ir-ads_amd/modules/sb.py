@@ -7,13 +7,15 @@ path's hot loops run in libirads.so:
   * ``sample_euler_maruyama``: every step inside one kernel launch with the row kept in
     registers (``irads_sb_em``);
   * ``forward`` / ``get_log_C``: GMM logits per row (``irads_sb_logits``), vectorised over
-    rows instead of the reference's ``sampling_batch_size`` Python loop.
+    rows instead of the reference's ``sampling_batch_size`` Python loop;
+  * ``get_log_potential``: the mixture log-density per row (``irads_sb_log_potential``);
+  * ``get_log_C`` and ``get_log_potential`` are differentiable in x and every parameter, as the
+    reference's autograd graphs are (closed-form backwards, irads/ops.py), so LightSB's
+    training objective E[log C(x0)] - E[log v(x1)] trains on this path.
 The reference has no caller for this module; the full-covariance path
 needs geotorch's orthogonal parametrisation, which is not available, so
 ``is_diagonal=False`` raises NotImplementedError.
 """
-import math
-
 import torch
 from torch import nn
 from torch.distributions.categorical import Categorical
@@ -35,7 +37,8 @@ class LightSB(nn.Module):
         self.log_alpha_raw = nn.Parameter(self.epsilon * torch.log(torch.ones(n_potentials) / n_potentials))
         self.r = nn.Parameter(torch.randn(n_potentials, dim))
         self.S_log_diagonal_matrix = nn.Parameter(torch.log(S_diagonal_init * torch.ones(n_potentials, self.dim)))
-        self.S_rotation_matrix = nn.Parameter(torch.randn(n_potentials, self.dim, self.dim))
+        # kept for state-dict parity; the diagonal path never reads it (no gradient, frozen)
+        self.S_rotation_matrix = nn.Parameter(torch.randn(n_potentials, self.dim, self.dim), requires_grad=False)
 
     def init_r_by_samples(self, samples):
         assert samples.shape[0] == self.r.shape[0]
@@ -51,7 +54,15 @@ class LightSB(nn.Module):
         return (1 / self.epsilon) * self.log_alpha_raw
 
     def _eps(self):
-        return float(self.epsilon)
+        """epsilon as a host float for the kernel launches, read from the buffer once per value
+        (a device read inside a captured HIP graph is not allowed; set_epsilon / load_state_dict
+        move the buffer's version and refresh it)."""
+        key = (self.epsilon.data_ptr(), self.epsilon._version)
+        c = self.__dict__.get("_eps_cache")
+        if c is None or c[0] != key:
+            c = (key, float(self.epsilon))
+            self.__dict__["_eps_cache"] = c
+        return c[1]
 
     @torch.no_grad()
     def forward(self, x):
@@ -78,19 +89,14 @@ class LightSB(nn.Module):
         return t * y + (1 - t) * x + torch.sqrt(t * (1 - t) * self.epsilon) * torch.randn_like(x)
 
     def get_log_potential(self, x):
-        """log Σ_k alpha_k N(x; r_k, eps S_k) + logsumexp(log alpha) (sb.py:183-204)."""
-        S = self.get_S().to(x.dtype)
-        r = self.r.to(x.dtype)
-        var = self.epsilon.to(x.dtype) * S
-        log_alpha = self.get_log_alpha().to(x.dtype)
-        comp = -0.5 * (((x[:, None, :] - r[None]) ** 2) / var[None] + torch.log(2 * math.pi * var)[None]).sum(-1)
-        mix = torch.log_softmax(log_alpha, -1)
-        return torch.logsumexp(comp + mix[None], -1) + torch.logsumexp(log_alpha, -1)
+        """log Σ_k alpha_k N(x; r_k, eps S_k) + logsumexp(log alpha) (sb.py:183-204), one wave per
+        row on irads_sb_log_potential, differentiable (closed-form backward)."""
+        return ops.sb_log_potential(x, self.r, self.S_log_diagonal_matrix, self.log_alpha_raw, self._eps())
 
     def get_log_C(self, x):
-        _, log_c = ops.sb_logits(x, self.r, self.S_log_diagonal_matrix, self.log_alpha_raw, self._eps(),
-                                 want_logits=False)
-        return log_c
+        """logsumexp_k of the GMM logits (sb.py:206-224); differentiable in x, r, S and alpha as
+        the reference's (irads.ops.SBLogCFn: closed-form backward)."""
+        return ops.sb_log_c(x, self.r, self.S_log_diagonal_matrix, self.log_alpha_raw, self._eps())
 
     def set_epsilon(self, new_epsilon):
         self.epsilon = torch.tensor(new_epsilon, device=self.epsilon.device)

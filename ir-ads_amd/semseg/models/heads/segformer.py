@@ -37,6 +37,8 @@ class SegFormerHead(nn.Module):
         self.linear_fuse = ConvModule(embed_dim * 4, embed_dim)
         self.linear_pred = nn.Conv2d(embed_dim, num_classes, 1)
         self.dropout = nn.Dropout2d(0.1)
+        self.keep_feature = False  # CMNeXt's SB hook reads the fused E-dim feature (tokens) of the last call
+        self.feature, self.feature_hw = None, None
 
     def forward(self, features: Tuple[Tensor, Tensor, Tensor, Tensor]) -> Tensor:
         """Reference (segformer.py:37-48):
@@ -68,8 +70,12 @@ class SegFormerHead(nn.Module):
                 # BN (batch statistics) + ReLU + Dropout2d in one pass each way (csrc/bnact.hip),
                 # then linear_pred as a token-major Linear: logits stay channels-last
                 z = ops.bn_relu_dropout2d(tok, self.linear_fuse.bn, self.dropout.p)
+                if self.keep_feature:
+                    self.feature, self.feature_hw = z, (H, W)
                 pred = self.linear_pred
                 out = ops.linear(z, pred.weight.view(pred.out_channels, E), pred.bias)
                 return out.view(B, H, W, -1).permute(0, 3, 1, 2)
         seg = self.linear_fuse.activate(self.linear_fuse.bn(seg))
+        if self.keep_feature:
+            self.feature, self.feature_hw = seg.permute(0, 2, 3, 1).reshape(B, H * W, E), (H, W)
         return self.linear_pred(self.dropout(seg))

@@ -12,15 +12,22 @@ def adapter_trainable(name: str) -> bool:
     return ("Adapter" in name) or ("extra_patch_embed" in name) or ("head" in name) or ("MPG" in name)
 
 
+def sb_trainable(name: str) -> bool:
+    """The build-defined SB hook's LightSB (CMNeXt(..., sb=...)): trained alongside the Adapters."""
+    return name.startswith("sb.") and "S_rotation_matrix" not in name
+
+
 def get_optimizer(model: nn.Module, optimizer: str, lr: float, train_type: str, weight_decay: float = 0.01,
                   verbose: bool = False, lr_on_device: bool = False):
     """lr_on_device: keep the learning rate as a device tensor (fused AdamW reads it on the GPU,
     the scheduler fills it in place), which makes the optimizer step graph-capturable."""
     fused = {}
     if 'Adapter' in train_type:
-        params = [p for n, p in model.named_parameters() if adapter_trainable(n) and p.requires_grad]
+        params = [p for n, p in model.named_parameters()
+                  if (adapter_trainable(n) or sb_trainable(n)) and p.requires_grad]
         for n, p in model.named_parameters():
-            if "Adap" not in n and "extra_patch_embed" not in n and "head" not in n and "MPG" not in n:
+            if "Adap" not in n and "extra_patch_embed" not in n and "head" not in n and "MPG" not in n \
+                    and not sb_trainable(n):
                 p.requires_grad = False
             elif verbose:
                 print(n)

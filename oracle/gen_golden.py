@@ -461,7 +461,7 @@ def gen_sb(ref):
     with torch.no_grad():
         sbm.S_log_diagonal_matrix.copy_(torch.log(torch.tensor(0.1)) +
                                         0.3 * t(seeded((10, 512), 120, "uniform", lo=-1, hi=1)))
-        sbm.log_alpha_raw.copy_(0.1 * t(seeded((10,), 121)))
+        sbm.log_alpha_raw.copy_(0.1 * t(seeded((10,), 121)))  # log alpha = raw / eps: N(0, 1)
         sbm.r.copy_(t(seeded((10, 512), 122)))
     rows = 128
     x = t(seeded((rows, 512), 123))
@@ -473,6 +473,28 @@ def gen_sb(ref):
         sbm.float()
     res["log_C"] = sbm.get_log_C(x)
     res["log_potential"] = sbm.get_log_potential(x)
+    # gradients of both objectives (LightSB trains on E[log C(x0)] - E[log v(x1)]): the reference's
+    # autograd graph, weighted by a seeded cotangent, wrt x and every diagonal-path parameter
+    params = [sbm.r, sbm.S_log_diagonal_matrix, sbm.log_alpha_raw]
+    for name, fn in (("logC", sbm.get_log_C), ("logV", sbm.get_log_potential)):
+        for dtype in (torch.float32, torch.float64):
+            sbm.to(dtype)
+            xg = x.to(dtype).clone().requires_grad_()
+            g = t(seeded((rows,), 125), dtype)
+            grads = torch.autograd.grad((fn(xg) * g).sum(), [xg] + params)
+            tag = name + ("64" if dtype == torch.float64 else "")
+            for gname, gv in zip(("x", "r", "S_log_diag", "log_alpha_raw"), grads):
+                res[f"{tag}_g{gname}"] = gv.detach()
+        sbm.float()
+    # forward sampling (sb.py:57-104): rows near the origin so that the component draw is spread
+    # over several components; the fixture holds the reference's mixture logits (exp_argument)
+    with torch.no_grad():
+        xs = t(seeded((4, 512), 126)) * 0.002
+        S, r = sbm.get_S(), sbm.get_r()
+        x_S_x = (xs[:, None, :] * S[None] * xs[:, None, :]).sum(-1)
+        x_r = (xs[:, None, :] * r[None]).sum(-1)
+        res["fwd_x"] = xs
+        res["fwd_logits"] = (x_S_x + 2 * x_r) / (2 * sbm.epsilon) + sbm.get_log_alpha()[None]
     # Euler–Maruyama with injected noise (sb.py:163-175 draws torch.randn_like each step)
     n_steps = 10
     noise = t(seeded((n_steps, rows, 512), 124))

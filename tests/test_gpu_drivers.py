@@ -96,3 +96,51 @@ def test_train_and_val_drivers(tmp_path, graph):
     (miou,) = val_mm.main(cfg)
     assert 0.0 <= miou <= 100.0
     assert any(p.startswith("eval_") for p in os.listdir(save))
+
+
+@pytest.mark.gpu
+def test_sb_hook_step():
+    """The build-defined SB hook (CMNeXt(..., sb=...)): in one bf16 training step the
+    hook's loss equals LightSB's objective E[log C(x)] - E[log v(x)] recomputed by the oracle in
+    fp64 on the same fused head feature rows, and its parameter gradients equal the oracle's
+    autograd gradients (relative 1e-3; the kernels run in fp32)."""
+    import irads_ref as R
+    from semseg.models import CMNeXt
+    from semseg.losses import get_loss, mmst_loss
+    from semseg.optimizers import get_optimizer
+    torch.manual_seed(0)
+    dev = torch.device("cuda", 0)
+    m = CMNeXt("SwinTransformer-B", 5, ["img", "depth"], sb={"weight": 0.5, "n_potentials": 10, "epsilon": 0.1})
+    m = m.to(dev)
+    opt = get_optimizer(m, "adamw", 1e-4, "Adapter", 0.01)
+    names = {id(p): n for n, p in m.named_parameters()}
+    assert {names[id(p)] for g in opt.param_groups for p in g["params"] if names[id(p)].startswith("sb.")} == \
+        {"sb.r", "sb.S_log_diagonal_matrix", "sb.log_alpha_raw"}
+    m.train()
+    rgb = torch.randn(4, 3, 128, 128, device=dev)
+    dep = torch.rand(4, 3, 128, 128, device=dev)
+    lbl = torch.randint(0, 5, (4, 128, 128), device=dev)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y, yr, yd = m([rgb, dep])
+        seg = mmst_loss(get_loss("CrossEntropy", 255), y, yr, yd, lbl)
+        sbl = m.sb_loss()
+    (seg + sbl).backward()
+    x = m._sb_rows().double().cpu()
+    assert x.shape == (4 * 32 * 32, 512)
+    r = m.sb.r.detach().double().cpu().requires_grad_()
+    Sl = m.sb.S_log_diagonal_matrix.detach().double().cpu().requires_grad_()
+    la = m.sb.log_alpha_raw.detach().double().cpu().requires_grad_()
+    eps = float(m.sb.epsilon)
+    log_c = R.lightsb_log_C(x, r, Sl, la, eps)
+    var = eps * torch.exp(Sl)
+    comp = -0.5 * (((x[:, None, :] - r[None]) ** 2) / var[None] + torch.log(2 * np.pi * var)[None]).sum(-1)
+    log_v = torch.logsumexp(comp + la[None] / eps, -1)  # log_softmax(log alpha) + logsumexp(log alpha)
+    ref = 0.5 * (log_c.mean() - log_v.mean())
+    assert abs(float(sbl) - float(ref)) <= 1e-3 * abs(float(ref)) + 1e-4, (float(sbl), float(ref))
+    gr = torch.autograd.grad(ref, [r, Sl, la])
+    for got, want, nm in zip((m.sb.r.grad, m.sb.S_log_diagonal_matrix.grad, m.sb.log_alpha_raw.grad), gr,
+                             ("r", "S_log", "log_alpha_raw")):
+        e = float((got.double().cpu() - want).norm() / want.norm())
+        assert e < 1e-3, (nm, e)
+    amap = m.sb_anomaly_map()
+    assert amap.shape == (4, 32, 32) and torch.isfinite(amap).all()

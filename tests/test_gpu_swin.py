@@ -299,3 +299,63 @@ def test_lightsb():
     close(traj.double(), traj64, 2e-3, 1e-4, "EM fp32 vs fp64")
     s = m(x)
     assert s.shape == x.shape and torch.isfinite(s).all()
+
+
+def _sb_from_fixture(fx):
+    from modules.sb import LightSB
+    m = LightSB(dim=512, n_potentials=10, epsilon=0.1).to(DEV)
+    with torch.no_grad():
+        m.r.copy_(fx.regen("r", (10, 512), 122))
+        m.S_log_diagonal_matrix.copy_(fx.t("S_log_diag"))
+        m.log_alpha_raw.copy_(fx.t("log_alpha_raw"))
+    return m
+
+
+def test_lightsb_objective_gradients():
+    """get_log_C and get_log_potential are differentiable in x and every diagonal-path parameter,
+    as the reference's autograd graphs (sb.py:183-224): gradients of (f(x)·g).sum() against the
+    reference's, fp64 to 1e-9 relative, fp32 to 2e-3 relative (the fp32 reference itself carries
+    cancellation error at eps S = 0.01, see test_lightsb)."""
+    fx = Fixture("lightsb.npz")
+    x = fx.regen("x", (128, 512), 123)
+    g = torch.from_numpy(seeded((128,), 125))
+    for name, attr in (("logC", "get_log_C"), ("logV", "get_log_potential")):
+        for dtype, tag, tol in ((torch.float64, "64", 1e-9), (torch.float32, "", 2e-3)):
+            m = _sb_from_fixture(fx).to(dtype)
+            xg = x.to(DEV, dtype).requires_grad_()
+            params = [m.r, m.S_log_diagonal_matrix, m.log_alpha_raw]
+            grads = torch.autograd.grad((getattr(m, attr)(xg) * g.to(DEV, dtype)).sum(), [xg] + params)
+            for gname, gv in zip(("x", "r", "S_log_diag", "log_alpha_raw"), grads):
+                ref = fx[f"{name}{tag}_g{gname}"]
+                scale = float(np.abs(ref).max())
+                close(gv, ref, tol * scale, tol, f"{name}{tag} d/d{gname}")
+
+
+def test_lightsb_forward_sampling():
+    """LightSB.forward (sb.py:57-104): the component draw k ~ Categorical(logits) and the sample
+    r_k + S_k x + sqrt(eps S_k) ξ.  Each of 4 rows is repeated 40 000 times; the component of
+    every sample is recovered by maximum likelihood (components are ~30 noise-stds apart), the
+    frequencies are compared with softmax of the reference's mixture logits (5 sigma), and the
+    standardised residuals with N(0, 1) (mean and variance to 1e-2)."""
+    fx = Fixture("lightsb.npz")
+    m = _sb_from_fixture(fx)
+    xs = torch.from_numpy(fx["fwd_x"]).to(DEV)
+    n = 40000
+    torch.manual_seed(7)
+    probs = torch.from_numpy(fx["fwd_logits"]).double().softmax(-1)
+    S = m.get_S().detach().double()
+    r = m.r.detach().double()
+    eps = float(m.epsilon)
+    for i in range(xs.shape[0]):
+        xi = xs[i:i + 1].expand(n, -1).contiguous()
+        y = m(xi).double()
+        mean_k = r + S * xi[:1].double()  # (K, D)
+        var_k = eps * S
+        ll = -0.5 * (((y[:, None, :] - mean_k[None]) ** 2) / var_k[None]).sum(-1) - 0.5 * torch.log(var_k).sum(-1)
+        k = ll.argmax(-1)
+        freq = torch.bincount(k, minlength=10).double().cpu() / n
+        p = probs[i]
+        sigma = (p * (1 - p) / n).sqrt()
+        assert ((freq - p).abs() <= 5 * sigma + 1e-3).all(), (i, freq, p)
+        z = (y - mean_k[k]) / var_k[k].sqrt()
+        assert abs(float(z.mean())) < 1e-2 and abs(float(z.var()) - 1) < 1e-2, (float(z.mean()), float(z.var()))

@@ -284,6 +284,20 @@ def test_lightsb_oracle():
     close(traj[:, [1, 5, 10]], fx["em_traj_sel"], 4e-3, 1e-4, "EM trajectory")
 
 
+def test_lightsb_oracle_log_c_gradients():
+    """The oracle's log C (autograd) against the reference's gradients, fp64."""
+    fx = Fixture("lightsb.npz")
+    x = fx.regen("x", (128, 512), 123).double().requires_grad_()
+    r = fx.regen("r", (10, 512), 122).double().requires_grad_()
+    Sl = fx.t("S_log_diag").double().requires_grad_()
+    la = fx.t("log_alpha_raw").double().requires_grad_()
+    g = torch.from_numpy(seeded((128,), 125)).double()
+    grads = torch.autograd.grad((R.lightsb_log_C(x, r, Sl, la, float(fx["epsilon"])) * g).sum(), [x, r, Sl, la])
+    for gname, gv in zip(("x", "r", "S_log_diag", "log_alpha_raw"), grads):
+        ref = fx[f"logC64_g{gname}"]
+        close(gv, ref, 1e-9 * float(np.abs(ref).max()), 1e-9, f"log C d/d{gname}")
+
+
 # ------------------------------------------------------------------- metrics / MMST
 def test_metrics_and_mmst_oracle():
     fx = Fixture("metrics_loss.npz")
