@@ -281,6 +281,9 @@ def main():
             if timer_in_graph:
                 ops.TIMER.records.clear()
                 ops.TIMER.enabled = set(TIMED_KERNELS)
+        if world > 1:  # DDP's construction broadcast (the graph path has no DDP wrapper)
+            from irads.graph_step import broadcast_module
+            broadcast_module(model)
         runner = GraphedTrainStep(model.parameters(), lambda: fwd_bwd(model, loss_fn, batch), opt, world=world,
                                   warmup=max(args.warmup, 1), before_capture=arm_timer)
         ops.TIMER.enabled = set()
@@ -340,6 +343,10 @@ def main():
                    "per_gpu_batch": args.batch, "global_batch": args.batch * world,
                    "image_size": list(wl["hw"]), "parallelism": f"dp{world}",
                    "execution": "hip-graph replay" if graph else "eager",
+                   "grad_exchange": ({"none": "none (1 rank)", "overlap": "RCCL all-reduce in 8 MB buckets overlapped "
+                                      "with the backward, inside the graph", "split": "one flat all-reduce between "
+                                      "backward and optimizer graphs"}[runner.comm] if graph else
+                                     ("DDP buckets" if world > 1 else "none (1 rank)")),
                    "gemm_selection": "TunableOp table irads/tuned" if tuned else "hipBLASLt heuristic"},
         "loss": round(loss_val, 5),
     }

@@ -15,10 +15,20 @@ What makes the step capturable (all in this package):
     (fused AdamW reads it on the device);
   * gradients are allocated by the captured backward itself (no .grad before capture, so
     autograd hands each parameter its freshly computed gradient instead of adding it into a
-    zeroed one: no per-parameter add kernels); with several ranks they are packed into one
-    flat fp32 buffer inside the backward graph, all-reduced (RCCL sum, then 1/world) between the backward
-    graph and the optimizer graph, and unpacked by the optimizer graph: one 30 MB bucket
-    instead of DDP's per-bucket hooks (data-parallel semantics of train_mm.py:94 unchanged).
+    zeroed one: no per-parameter add kernels).
+
+Data parallel (world > 1; train_mm.py:94 / DDP semantics: gradients averaged over ranks):
+  * comm="overlap" (default with the RCCL backend): the trainable parameters are split into
+    buckets of ~bucket_mb in reverse registration order (the order their gradients become
+    final in backward, as DDP's buckets).  A post-accumulate-grad hook copies each gradient
+    into its slot of a flat fp32 buffer; when a bucket's last gradient lands, the bucket's
+    all-reduce (RCCL sum) is issued on a side stream that waits on an event recorded at that
+    point of the backward, so the exchange of bucket k overlaps the backward of the layers
+    below it.  The optimizer waits for the side stream, unpacks with the 1/world scale and
+    steps.  Hooks, events, collectives and the optimizer are captured into the one graph.
+  * comm="split": the backward graph packs the gradients, one all-reduce of the flat buffer
+    runs between the backward graph and the optimizer graph (no overlap; the collective is
+    not captured).  Used with the gloo backend (CPU-side tests), which cannot be captured.
 """
 import torch
 import torch.distributed as dist
@@ -26,28 +36,38 @@ import torch.distributed as dist
 
 class GraphedTrainStep:
     """restore: tensors (parameters, BN buffers) to snapshot before the warm-up iterations and
-    put back after capture, together with a zeroed optimizer state, so that the warm-up
-    leaves no trace on the training run (train_mm.py); the bench keeps its warm-up updates."""
+    put back after capture, together with the optimizer state as it was before the warm-up
+    (a resumed run keeps its Adam moments and step counts; a fresh one starts from zero), so
+    that the warm-up leaves no trace on the training run (train_mm.py); the bench keeps its
+    warm-up updates."""
 
-    def __init__(self, params, fwd_bwd, optimizer, world=1, warmup=3, before_capture=None, restore=None):
+    def __init__(self, params, fwd_bwd, optimizer, world=1, warmup=3, before_capture=None, restore=None,
+                 comm=None, bucket_mb=8.0):
         self.params = [p for p in params if p.requires_grad]
-        snap = None if restore is None else [(t, t.detach().clone()) for t in restore]
         self.world = world
         self.opt = optimizer
         dev = self.params[0].device
+        snap = None if restore is None else [(t, t.detach().clone()) for t in restore]
+        opt_snap = _snapshot_optimizer(optimizer) if restore is not None else None
+        if comm is None:
+            comm = "none" if world == 1 else ("overlap" if dist.get_backend() == "nccl" else "split")
+        self.comm = comm  # an explicit "overlap" / "split" also runs at world == 1 (tests)
         self.flat = None
-        if world > 1:
+        if self.comm != "none":
             self.flat = torch.zeros((sum(p.numel() for p in self.params),), device=dev, dtype=torch.float32)
+            self._offsets = []
+            o = 0
+            for p in self.params:
+                self._offsets.append(o)
+                o += p.numel()
+            if self.comm == "overlap":
+                self._make_buckets(bucket_mb)
         side = torch.cuda.Stream(device=dev)
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):  # warm-up (kernel selection, allocator pools) off the capture
             for _ in range(warmup):
                 optimizer.zero_grad(set_to_none=True)
-                fwd_bwd()
-                if world > 1:
-                    self._pack()
-                    dist.all_reduce(self.flat)
-                    self._unpack()
+                self._run(fwd_bwd, capture=False)
                 optimizer.step()
         torch.cuda.current_stream(dev).wait_stream(side)
         torch.cuda.synchronize(dev)
@@ -55,40 +75,152 @@ class GraphedTrainStep:
         if before_capture is not None:
             before_capture()
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
-            self.loss = fwd_bwd()
-            if world == 1:
-                optimizer.step()
-            else:
-                self._pack()
         self.opt_graph = None
-        if world > 1:
+        if self.comm == "split":
+            with torch.cuda.graph(self.graph):
+                self.loss = fwd_bwd()
+                pack_grads(self.params, self.flat)
             self.opt_graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.opt_graph, pool=self.graph.pool()):
-                self._unpack()
+                unpack_grads(self.params, self.flat, 1.0 / self.world)
+                optimizer.step()
+        else:
+            with torch.cuda.graph(self.graph):
+                self.loss = self._run(fwd_bwd, capture=True)
                 optimizer.step()
         if snap is not None:
             with torch.no_grad():
                 for t, v in snap:
                     t.copy_(v)
-                for st in optimizer.state.values():  # in place: the graph holds these addresses
-                    for v in st.values():
-                        if torch.is_tensor(v):
-                            v.zero_()
+                _restore_optimizer(optimizer, opt_snap)
             torch.cuda.synchronize(dev)
 
-    def _pack(self):
-        pack_grads(self.params, self.flat)
+    # ------------------------------------------------------------------ overlapped exchange
+    def _make_buckets(self, bucket_mb):
+        """Buckets of consecutive params in reverse registration order, ~bucket_mb each."""
+        limit = int(bucket_mb * (1 << 20) / 4)
+        order = list(range(len(self.params)))[::-1]
+        self._bucket_of = {}
+        self._buckets = []  # (lo, hi) element range of the flat buffer, param indices
+        cur, size = [], 0
+        for i in order:
+            cur.append(i)
+            size += self.params[i].numel()
+            if size >= limit:
+                self._buckets.append(cur)
+                cur, size = [], 0
+        if cur:
+            self._buckets.append(cur)
+        for b, idx in enumerate(self._buckets):
+            for i in idx:
+                self._bucket_of[i] = b
+        self._comm_stream = torch.cuda.Stream(device=self.params[0].device)
 
-    def _unpack(self):
+    def _run(self, fwd_bwd, capture):
+        """fwd + bwd, with the bucketed all-reduces issued as buckets complete (overlap) or one
+        flat all-reduce after the backward (split, eager warm-up only)."""
+        if self.comm == "none":
+            return fwd_bwd()
+        if self.comm == "split":
+            loss = fwd_bwd()
+            pack_grads(self.params, self.flat)
+            _all_reduce(self.flat)
+            unpack_grads(self.params, self.flat, 1.0 / self.world)
+            return loss
+        main = torch.cuda.current_stream()
+        remaining = [len(b) for b in self._buckets]
+        handles = []
+
+        def make_hook(i):
+            def hook(p):
+                lo = self._offsets[i]
+                self.flat[lo:lo + p.numel()].copy_(p.grad.reshape(-1))
+                b = self._bucket_of[i]
+                remaining[b] -= 1
+                if remaining[b] == 0:
+                    idx = self._buckets[b]
+                    a = min(self._offsets[j] for j in idx)
+                    z = max(self._offsets[j] + self.params[j].numel() for j in idx)
+                    ev = torch.cuda.Event()
+                    ev.record()  # on the stream the backward (and this hook's copy) runs on
+                    self._comm_stream.wait_event(ev)
+                    with torch.cuda.stream(self._comm_stream):
+                        dist.all_reduce(self.flat[a:z])  # RCCL sum over xGMI, overlapping the backward
+            return hook
+        for i, p in enumerate(self.params):
+            handles.append(p.register_post_accumulate_grad_hook(make_hook(i)))
+        try:
+            loss = fwd_bwd()
+        finally:
+            for h in handles:
+                h.remove()
+        # a parameter without a gradient this step (none in Adapter training) still joins its bucket
+        for i, p in enumerate(self.params):
+            if p.grad is None:
+                p.grad = torch.zeros_like(p)
+                make_hook(i)(p)
+        main.wait_stream(self._comm_stream)
         unpack_grads(self.params, self.flat, 1.0 / self.world)
+        return loss
 
     def step(self):
         self.graph.replay()
         if self.opt_graph is not None:
-            dist.all_reduce(self.flat)  # RCCL sum over xGMI; the optimizer graph scales by 1/world
+            _all_reduce(self.flat)  # RCCL / gloo sum; the optimizer graph scales by 1/world
             self.opt_graph.replay()
         return self.loss
+
+
+def _all_reduce(flat):
+    """Sum over ranks; gloo (tests) reduces a host copy."""
+    if dist.get_backend() == "gloo" and flat.is_cuda:
+        h = flat.cpu()
+        dist.all_reduce(h)
+        flat.copy_(h)
+    else:
+        dist.all_reduce(flat)
+
+
+def _snapshot_optimizer(opt):
+    """Clones of the optimizer's state tensors (empty for a fresh optimizer)."""
+    return {id(p): {k: (v.detach().clone() if torch.is_tensor(v) else v) for k, v in st.items()}
+            for p, st in opt.state.items()}
+
+
+def _restore_optimizer(opt, snap):
+    """Put the state back IN PLACE (the captured graph holds these addresses); state created by
+    the warm-up for a parameter that had none is zeroed (a fresh optimizer's start)."""
+    for p, st in opt.state.items():
+        old = snap.get(id(p))
+        for k, v in st.items():
+            if not torch.is_tensor(v):
+                if old is not None and k in old:
+                    st[k] = old[k]
+                continue
+            if old is not None and k in old and torch.is_tensor(old[k]):
+                v.copy_(old[k].to(v.device, v.dtype))
+            else:
+                v.zero_()
+
+
+def lr_to_device(optimizer, device):
+    """After load_state_dict, a graph-mode optimizer's learning rate must be a device tensor at a
+    stable address (the captured fused AdamW reads it; the scheduler fills it in place)."""
+    for g in optimizer.param_groups:
+        lr = g["lr"]
+        val = float(lr.detach().cpu()) if torch.is_tensor(lr) else float(lr)
+        if torch.is_tensor(lr) and lr.device == device:
+            lr.fill_(val)
+        else:
+            g["lr"] = torch.tensor(val, device=device)
+
+
+def broadcast_module(module, src=0):
+    """Parameters and buffers from rank `src` to every rank (DDP does this at construction;
+    the graph path has no DDP wrapper)."""
+    with torch.no_grad():
+        for t in list(module.parameters()) + list(module.buffers()):
+            dist.broadcast(t.data, src)
 
 
 def pack_grads(params, flat):

@@ -155,8 +155,15 @@ class WindowAttentionFn(torch.autograd.Function):
 
 
 def window_attention(qkv, qkv_bias, table, mask, H, W, num_heads, shift, scale):
+    if qkv.dtype == torch.float16:
+        # fp16 autocast (the reference's AMP + GradScaler path, train_mm.py:109-152): the bf16
+        # MFMA kernels on a bf16 copy (same exponent range as fp32: a scaled loss cannot overflow
+        # them), the result handed back in fp16 as autocast's matmuls would produce it
+        out = WindowAttentionFn.apply(qkv.to(torch.bfloat16).contiguous(), qkv_bias, table, mask, H, W, num_heads,
+                                      shift, scale)
+        return out.to(torch.float16)
     if qkv.dtype not in (torch.float32, torch.bfloat16):
-        raise RuntimeError(f"window attention: dtype {qkv.dtype} not supported (float32 / bfloat16)")
+        raise RuntimeError(f"window attention: dtype {qkv.dtype} not supported (float32 / bfloat16 / float16)")
     return WindowAttentionFn.apply(qkv.contiguous(), qkv_bias, table, mask, H, W, num_heads, shift, scale)
 
 
@@ -579,6 +586,8 @@ def _resize_bwd(go, code, B, C, h, w, H, W, nchw):
 
 
 def resize(x, size):
+    if x.dtype == torch.float16:  # fp16 autocast: the fp32 kernel (F.interpolate's upcast precision)
+        x = x.float()
     return ResizeFn.apply(x, tuple(size))
 
 
@@ -612,6 +621,8 @@ class UpsampleSumFn(torch.autograd.Function):
 
 
 def upsample_sum(base, srcs):
+    if base.dtype == torch.float16:  # fp16 autocast: summed in the fp32 kernel
+        base, srcs = base.float(), [s_.float() for s_ in srcs]
     return UpsampleSumFn.apply(base, *srcs)
 
 
@@ -619,7 +630,11 @@ class CrossEntropyFn(torch.autograd.Function):
     """nn.CrossEntropyLoss(weight, ignore_index)(logits, target), mean reduction
     (losses.py:6-19), one fused HIP pass each way; fp32 arithmetic on fp32 or bf16 logits
     (the AMP-cast input of the reference).  Optionally also returns the MMST target of
-    train_mm.py:137-141 computed in the same pass (no gradient)."""
+    train_mm.py:137-141 computed in the same pass (no gradient).  Deviation (documented, pinned
+    by test_gpu_seghead.py::test_cross_entropy_edges): a target outside [0, C) other than
+    ignore_index is treated as ignored — the reference's nn.CrossEntropyLoss raises a device-side
+    assert instead; raising here would need a host sync per step (or a fault inside a captured
+    graph)."""
 
     @staticmethod
     def forward(ctx, logits, target, ignore_index, weight, want_match):
@@ -657,6 +672,8 @@ class CrossEntropyFn(torch.autograd.Function):
 
 
 def cross_entropy(logits, target, ignore_index=255, weight=None, return_match=False):
+    if logits.dtype == torch.float16:  # autocast runs cross-entropy in fp32
+        logits = logits.float()
     return CrossEntropyFn.apply(logits, target, ignore_index, weight, bool(return_match))
 
 
@@ -922,6 +939,8 @@ def linear(x, weight, bias=None):
 def confusion_update(scores, target, ignore_index, hist):
     """hist ((C+1)*C int64) += confusion(target, argmax_c scores) over non-ignored pixels."""
     N.check_device(scores, "metrics scores")
+    if scores.dtype == torch.float16:
+        scores = scores.float()
     code = N.dtype_code(scores, (N.F32, N.BF16), "metrics scores")
     scores, st = _layout(scores)
     B, C, H, W = scores.shape

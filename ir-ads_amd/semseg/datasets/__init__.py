@@ -60,6 +60,39 @@ class NYU(Dataset):
         return [sample[k] for k in self.modals], label
 
 
+class MFNet(Dataset):
+    """MFNet RGB-T, num_classes 9 (reference semseg/datasets/mfnet.py: rgb/<name>.png,
+    ther/<name>.png, labels/<name>.png; the file list is <split>.txt under ROOT)."""
+    CLASSES = ['unlabeled', 'car', 'person', 'bike', 'curve', 'car_stop', 'guardrail', 'color_cone', 'bump']
+    PALETTE = None
+
+    def __init__(self, root='data/MFNet', split='train', transform=None, modals=('img', 'thermal'), case=None):
+        super().__init__()
+        assert split in ['train', 'val']
+        self.root, self.transform, self.modals = root, transform, list(modals)
+        self.n_classes = len(self.CLASSES)
+        self.ignore_label = 255
+        lst = os.path.join(root, f'{split}.txt')
+        self.files = [ln.strip() for ln in open(lst)] if os.path.isfile(lst) else []
+        if not self.files:
+            raise Exception(f"No images found in {root}")
+
+    def __len__(self):
+        return len(self.files)
+
+    def __getitem__(self, index):
+        name = self.files[index]
+        sample = {'img': _read(os.path.join(self.root, 'rgb', name + '.png'))[:3]}
+        if 'thermal' in self.modals:
+            t = _read(os.path.join(self.root, 'ther', name + '.png'))
+            sample['thermal'] = t[:3] if t.shape[0] >= 3 else t[:1].repeat(3, 1, 1)
+        sample['mask'] = _read(os.path.join(self.root, 'labels', name + '.png'))[:1].long()
+        if self.transform:
+            sample = self.transform(sample)
+        label = sample.pop('mask').squeeze(0).long()
+        return [sample[k] for k in self.modals], label
+
+
 class Synthetic(Dataset):
     """Synthetic RGB-D batches with the NYU label space (the bench's data: RGB N(0,1) after
     Normalize, depth U[0,1), labels U{0..n-1} with ~10 % ignore)."""
@@ -83,4 +116,4 @@ class Synthetic(Dataset):
         return xs, lbl
 
 
-__all__ = ['NYU', 'Synthetic']
+__all__ = ['NYU', 'MFNet', 'Synthetic']

@@ -527,9 +527,17 @@ def gen_metrics_loss(ref):
     mask_lbl = gt.clone()
     mask_lbl[pred != gt] = 255
     loss = lf(logits, gt) + 0.01 * lf(lr_, mask_lbl) + 0.01 * lf(ld_, mask_lbl)
+    # the same logits rounded to bf16 (exactly representable): a bf16 input to the product's metrics
+    # kernel then carries the very values the reference scored, ties included
+    lb = logits.bfloat16().float()
+    m2 = ref.metrics.Metrics(n_cls, 255, "cpu")
+    m2.update(lb, gt)
+    m2.update(lb.flip(-1), gt)
+    ious2, miou2 = m2.compute_iou()
     save("metrics_loss.npz", logits=logits, gt=gt, ious=np.array(ious), miou=np.array(miou),
          tp=np.array(m.tp), fp=np.array(m.fp), fn=np.array(m.fn), logits_rgb=lr_, logits_dte=ld_,
-         mmst_loss=loss)
+         mmst_loss=loss, bf16_tp=np.array(m2.tp), bf16_fp=np.array(m2.fp), bf16_fn=np.array(m2.fn),
+         bf16_ious=np.array(ious2), bf16_miou=np.array(miou2))
 
 
 if __name__ == "__main__":

@@ -1,0 +1,69 @@
+"""Worker of test_gpu_drivers.py::test_dp_two_ranks_gradients (one process per rank, both on the
+one GPU of the box): the graph-captured training step of irads/graph_step.py with world = 2 over
+gloo (comm="split"), on this rank's half of a 4-image batch.  Writes rank 0's averaged gradients."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (os.path.join(ROOT, "ir-ads_amd"), os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")):
+    sys.path.insert(0, p)
+
+
+def batch(dev):
+    import torch
+    g = torch.Generator().manual_seed(11)
+    rgb = torch.randn(4, 3, 64, 96, generator=g)
+    dep = torch.rand(4, 3, 64, 96, generator=g)
+    lbl = torch.randint(0, 5, (4, 64, 96), generator=g)  # no ignore pixels: per-rank means average exactly
+    return rgb.to(dev), dep.to(dev), lbl.to(dev)
+
+
+def model(dev):
+    from fill import fill_module
+    from test_gpu_drivers import _tiny_model
+    m = _tiny_model().to(dev)
+    fill_module(m, seed=4)
+    for n, p in m.named_parameters():
+        p.requires_grad_(("Adapter" in n) or ("extra_patch_embed" in n) or ("head" in n) or ("MPG" in n))
+    m.eval()  # deterministic (BN running stats, no dropout / DropPath / apply_mask): per-image independent
+    return m
+
+
+def fwd_bwd_fn(m, rgb, dep, lbl):
+    import torch
+
+    def fwd_bwd():
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = m([rgb, dep])[0]
+            loss = torch.nn.functional.cross_entropy(y.float(), lbl)
+        loss.backward()
+        return loss
+    return fwd_bwd
+
+
+def main():
+    rank, world, port, out = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4]
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = port
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from irads.graph_step import GraphedTrainStep
+    dev = torch.device("cuda", 0)
+    m = model(dev)
+    rgb, dep, lbl = batch(dev)
+    half = slice(rank * 2, rank * 2 + 2)
+    opt = torch.optim.SGD([p for p in m.parameters() if p.requires_grad], lr=0.0)
+    step = GraphedTrainStep(m.parameters(), fwd_bwd_fn(m, rgb[half], dep[half], lbl[half]), opt, world=world,
+                            warmup=1)
+    assert step.comm == "split"
+    step.step()
+    torch.cuda.synchronize()
+    if rank == 0:
+        torch.save({n: p.grad.detach().cpu() for n, p in m.named_parameters() if p.requires_grad}, out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -126,11 +126,11 @@ def test_unsupported_configs_raise():
         w(torch.randn(1, 144, 96))
 
 
-def _dp_worker(rank, world, port, q):
+def _dp_worker(rank, world, init_file, q):
     import torch
     import torch.distributed as dist
     from irads.graph_step import pack_grads, unpack_grads
-    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=f"file://{init_file}", rank=rank, world_size=world)
     torch.manual_seed(0)
     params = [torch.nn.Parameter(torch.randn(s)) for s in ((3, 4), (5,), (2, 2, 2))]
     for p in params:
@@ -144,34 +144,22 @@ def _dp_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_graph_step_gradient_allreduce_gloo():
+def test_graph_step_gradient_allreduce_gloo(tmp_path):
     """The data-parallel exchange of the graphed step (irads/graph_step.py): pack the
-    gradients, all-reduce (sum), unpack scaled by 1/world = DDP's gradient average."""
-    import queue
-    import socket
+    gradients, all-reduce (sum), unpack scaled by 1/world = DDP's gradient average.  World size 2
+    over gloo, rendezvous through a file store (no port to race for)."""
     import torch
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
-    res = None
-    for attempt in range(3):  # a free port picked here can be taken before the workers bind it
-        with socket.socket() as s:
-            s.bind(("127.0.0.1", 0))
-            port = s.getsockname()[1]
-        q = ctx.Queue()
-        procs = [ctx.Process(target=_dp_worker, args=(r, 2, port, q)) for r in range(2)]
-        for p in procs:
-            p.start()
-        try:
-            res = dict(q.get(timeout=120) for _ in procs)
-        except queue.Empty:
-            res = None
-        for p in procs:
-            p.join(timeout=60)
-            if p.is_alive():
-                p.kill()
-        if res is not None and all(p.exitcode == 0 for p in procs):
-            break
-    assert res is not None, "gloo workers did not report"
+    q = ctx.Queue()
+    init_file = str(tmp_path / "pg_init")
+    procs = [ctx.Process(target=_dp_worker, args=(r, 2, init_file, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
     for i, shape in enumerate(((3, 4), (5,), (2, 2, 2))):
         base = torch.arange(torch.Size(shape).numel()).view(shape).float()
         want = base * (1.5 if i != 1 else 0.5)  # mean of 1x and 2x (rank 1 lacks grad #1: 0)
@@ -195,3 +183,29 @@ def test_split_streams_gradient_matches_slicing():
     a, b = ops.split_streams(x, 3)
     (gc,) = torch.autograd.grad((b * w2).sum(), x)  # rgb half unused
     assert torch.equal(gc[:3], torch.zeros(3, 5, 4)) and torch.equal(gc[3:], w2)
+
+
+def test_reference_driver_import_surface():
+    """Every name the reference drivers import from semseg.* (train_mm.py:16-23, val_mm.py:12-22)
+    and from val_mm (train_mm.py:23) resolves on this package."""
+    import importlib
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    names = {
+        "semseg.augmentations_mm": ["get_train_augmentation", "get_val_augmentation"],
+        "semseg.losses": ["get_loss"],
+        "semseg.schedulers": ["get_scheduler"],
+        "semseg.optimizers": ["get_optimizer"],
+        "semseg.metrics": ["Metrics"],
+        "semseg.utils.utils": ["fix_seeds", "setup_cudnn", "cleanup_ddp", "setup_ddp", "get_logger", "cal_flops",
+                               "print_iou"],
+        "val_mm": ["evaluate", "evaluate_msf", "pad_image", "sliding_predict"],
+    }
+    for mod, attrs in names.items():
+        m = importlib.import_module(mod)
+        for a in attrs:
+            assert hasattr(m, a), f"{mod}.{a}"
+    models = importlib.import_module("semseg.models")
+    assert "CMNeXt" in models.__all__  # `from semseg.models import *` + eval(MODEL.NAME)
+    datasets = importlib.import_module("semseg.datasets")
+    assert {"NYU", "MFNet"} <= set(datasets.__all__)  # `from semseg.datasets import *` + eval(DATASET.NAME)

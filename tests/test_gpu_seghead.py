@@ -169,6 +169,23 @@ def test_cross_entropy_edges():
         ops.cross_entropy(_rand((1, 129, 2, 2), 52).to(DEV), torch.zeros(1, 2, 2, dtype=torch.int64, device=DEV))
     with pytest.raises(RuntimeError):
         ops.cross_entropy(_rand((1, 3, 2, 2), 53).to(DEV), torch.zeros(1, 2, 3, dtype=torch.int64, device=DEV))
+    # documented deviation: a target outside [0, C) that is not ignore_index counts as
+    # an ignored pixel (no loss, zero gradient, MMST target = ignore) where nn.CrossEntropyLoss raises
+    # a device-side assert; the loss equals the reference's on the same pixels marked ignored
+    x = _rand((2, 5, 4, 4), 54).to(DEV).requires_grad_()
+    t = torch.randint(0, 5, (2, 4, 4), device=DEV)
+    t[0, 1, 2], t[1, 3, 0] = 7, -3
+    loss, match = ops.cross_entropy(x, t, 255, return_match=True)
+    t_ref = t.clone()
+    t_ref[(t_ref < 0) | (t_ref >= 5)] = 255
+    xr = x.detach().clone().requires_grad_()
+    ref = F.cross_entropy(xr, t_ref, ignore_index=255)
+    close(loss, ref, 1e-6, 1e-6, "CE with out-of-range targets")
+    (gx,) = torch.autograd.grad(loss, x)
+    (gr,) = torch.autograd.grad(ref, xr)
+    close(gx, gr, 1e-7, 1e-6, "CE grad with out-of-range targets")
+    assert gx[0, :, 1, 2].abs().max() == 0 and gx[1, :, 3, 0].abs().max() == 0
+    assert match[0, 1, 2] == 255 and match[1, 3, 0] == 255
 
 
 def test_mmst_target_and_loss_golden():

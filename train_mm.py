@@ -1,10 +1,17 @@
 """Training driver (reference train_mm.py): same --cfg YAML schema, model initialisation,
 TRAIN_TYPE optimiser, warm-up poly LR, MMST objective, evaluation schedule, checkpoint
-dicts and logs.  MI355X-first differences:
-  * AMP is bf16 autocast (no GradScaler: bf16 has fp32's exponent range);
-  * with TRAIN.GRAPH (default on) the iteration is captured once into a HIP graph and
-    replayed (irads/graph_step.py); with DDP the gradients are all-reduced over RCCL as one
-    flat bucket between the backward and optimizer graphs;
+dicts and logs.  Numerics follow the YAML as the reference's do:
+  * TRAIN.AMP false: fp32 training (the reference's configs, e.g. nyu_rgbd.yaml:24);
+    TRAIN.AMP true: autocast + GradScaler in fp16 as the reference (train_mm.py:109,133,150-152),
+    or in bf16 without a scaler when TRAIN.AMP_DTYPE is 'bf16' (a build extension: the fast
+    fused-stage path and the one bench.py times);
+  * iters_per_epoch uses the reference's hard-coded gpus = 1 (train_mm.py:37,85): under DDP the
+    warm-up and poly horizon are stretched by the world size exactly as in the reference.
+MI355X-first differences:
+  * with TRAIN.GRAPH (default on; not with the fp16 GradScaler, whose step syncs the host) the
+    iteration is captured once into a HIP graph and replayed (irads/graph_step.py); with DDP
+    the gradients are all-reduced over RCCL in buckets overlapped with the backward, inside the
+    graph; parameters and buffers are broadcast from rank 0 first (DDP's construction does it);
   * the loss is accumulated on the device and read once per epoch (the reference syncs
     every iteration, train_mm.py:154,160).
 
@@ -34,6 +41,7 @@ from semseg.models import CMNeXt  # noqa: E402,F401
 from semseg.optimizers import get_optimizer  # noqa: E402
 from semseg.schedulers import get_scheduler  # noqa: E402
 from semseg.utils.utils import cleanup_ddp, fix_seeds, get_logger, print_iou, setup_cudnn, setup_ddp  # noqa: E402
+from semseg.utils.utils import cal_flops  # noqa: E402
 from val_mm import evaluate, make_dataset  # noqa: E402
 
 
@@ -73,12 +81,17 @@ def main(cfg, gpu, save_dir, logger):
     dataset_cfg, model_cfg = cfg['DATASET'], cfg['MODEL']
     loss_cfg, optim_cfg, sched_cfg = cfg['LOSS'], cfg['OPTIMIZER'], cfg['SCHEDULER']
     epochs, lr = train_cfg['EPOCHS'], optim_cfg['LR']
-    use_graph = bool(train_cfg.get('GRAPH', True))
+    amp = bool(train_cfg['AMP'])
+    amp_dtype = torch.float16 if str(train_cfg.get('AMP_DTYPE', 'fp16')).lower() in ('fp16', 'float16') \
+        else torch.bfloat16
+    scaled = amp and amp_dtype == torch.float16  # the reference's GradScaler path
+    use_graph = bool(train_cfg.get('GRAPH', True)) and not scaled
     trainset = make_dataset(cfg, 'train', get_train_augmentation(train_cfg['IMAGE_SIZE'],
                                                                  seg_fill=dataset_cfg['IGNORE_LABEL']))
     valset = make_dataset(cfg, 'val', get_val_augmentation(eval_cfg['IMAGE_SIZE']))
     class_names = trainset.CLASSES
-    model = globals()[model_cfg['NAME']](model_cfg['BACKBONE'], trainset.n_classes, dataset_cfg['MODALS'])
+    extra = {'sb': model_cfg['SB']} if model_cfg.get('SB') else {}  # build-defined SB hook
+    model = globals()[model_cfg['NAME']](model_cfg['BACKBONE'], trainset.n_classes, dataset_cfg['MODALS'], **extra)
     resume = None
     if os.path.isfile(model_cfg['RESUME']):
         resume = torch.load(model_cfg['RESUME'], map_location='cpu', weights_only=True)
@@ -87,7 +100,8 @@ def main(cfg, gpu, save_dir, logger):
         model.init_pretrained(model_cfg['PRETRAINED'])
     init_extra(model)
     model = model.to(device)
-    iters_per_epoch = len(trainset) // train_cfg['BATCH_SIZE'] // world
+    gpus = 1  # reference train_mm.py:37 (`gpus = 1#int(os.environ['WORLD_SIZE'])`), kept for schedule parity
+    iters_per_epoch = len(trainset) // train_cfg['BATCH_SIZE'] // gpus
     loss_fn = get_loss(loss_cfg['NAME'], trainset.ignore_label, None)
     optimizer = get_optimizer(model, optim_cfg['NAME'], lr, optim_cfg['TRAIN_TYPE'], optim_cfg['WEIGHT_DECAY'],
                               lr_on_device=use_graph)
@@ -104,11 +118,19 @@ def main(cfg, gpu, save_dir, logger):
         optimizer.load_state_dict(resume['optimizer_state_dict'])
         scheduler.load_state_dict(resume['scheduler_state_dict'])
         best_mIoU = resume['best_miou']
+        if use_graph:  # the captured AdamW reads lr from the device (a checkpoint may carry a CPU tensor)
+            from irads.graph_step import lr_to_device
+            lr_to_device(optimizer, device)
+    if ddp and use_graph:
+        from irads.graph_step import broadcast_module
+        broadcast_module(model)
     trainloader = DataLoader(trainset, batch_size=train_cfg['BATCH_SIZE'], num_workers=train_cfg.get('WORKERS', 4),
                              drop_last=True, pin_memory=True, sampler=sampler)
     valloader = DataLoader(valset, batch_size=eval_cfg['BATCH_SIZE'], num_workers=2, pin_memory=True)
-    amp = bool(train_cfg['AMP']) or use_graph  # the HIP path's fast kernels are the bf16 ones
+    scaler = torch.amp.GradScaler("cuda", enabled=scaled)
     if rank0:
+        logger.info('================== model complexity =====================')
+        cal_flops(model, dataset_cfg['MODALS'], logger)
         logger.info('================== training config =====================')
         logger.info(cfg)
 
@@ -118,10 +140,12 @@ def main(cfg, gpu, save_dir, logger):
 
     def fwd_bwd():
         xs, lbl = static
-        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
+        with torch.autocast("cuda", dtype=amp_dtype, enabled=amp):
             logits, logits_rgb, logits_dte = train_model(xs)
             loss = mmst_loss(loss_fn, logits, logits_rgb, logits_dte, lbl)
-        loss.backward()
+            if getattr(model, 'sb_cfg', None):
+                loss = loss + model.sb_loss()
+        scaler.scale(loss).backward()
         return loss
 
     train_loss = torch.zeros((), device=device)
@@ -152,7 +176,8 @@ def main(cfg, gpu, save_dir, logger):
             else:
                 optimizer.zero_grad(set_to_none=True)
                 loss = fwd_bwd()
-                optimizer.step()
+                scaler.step(optimizer)
+                scaler.update()
             scheduler.step()
             train_loss += loss.detach()
             n_iter += 1

@@ -1,6 +1,8 @@
 """Evaluation driver (reference val_mm.py): same --cfg YAML schema and outputs (mIoU, the
 per-class table written next to the checkpoint).  Metrics accumulate on the GPU
-(semseg/metrics.py); the forward runs under bf16 autocast on the HIP path.
+(semseg/metrics.py).  The forward runs in fp32 as the reference's evaluate / evaluate_msf do
+(val_mm.py:64-120), the precision the mIoU comparison is defined at; EVAL.AMP: bf16 (a build
+extension) runs it under bf16 autocast on the fused fast path.
 
     python val_mm.py --cfg configs/nyu_rgbd.yaml
 """
@@ -21,14 +23,51 @@ from tabulate import tabulate  # noqa: E402
 from torch.utils.data import DataLoader  # noqa: E402
 
 from semseg.augmentations_mm import get_val_augmentation  # noqa: E402
-from semseg.datasets import NYU, Synthetic  # noqa: E402,F401
+from semseg.datasets import *  # noqa: E402,F401,F403  (resolved by name: DATASET.NAME)
 from semseg.metrics import Metrics  # noqa: E402
-from semseg.models import CMNeXt  # noqa: E402,F401
+from semseg.models import *  # noqa: E402,F401,F403  (resolved by name: MODEL.NAME)
 from semseg.utils.utils import setup_cudnn  # noqa: E402
 
 
+_AMP = {"dtype": None}  # None: fp32 (reference); torch.bfloat16 with EVAL.AMP: bf16
+
+
 def _amp():
-    return torch.autocast("cuda", dtype=torch.bfloat16)
+    dt = _AMP["dtype"]
+    return torch.autocast("cuda", dtype=dt if dt is not None else torch.bfloat16, enabled=dt is not None)
+
+
+def pad_image(img, target_size):
+    """Zero-pad (B, C, H, W) at the bottom / right to target_size (reference val_mm.py:24-28)."""
+    rows_to_pad = max(target_size[0] - img.shape[2], 0)
+    cols_to_pad = max(target_size[1] - img.shape[3], 0)
+    return F.pad(img, (0, cols_to_pad, 0, rows_to_pad), "constant", 0)
+
+
+@torch.no_grad()
+def sliding_predict(model, image, num_classes, flip=True):
+    """Tiled prediction with 1/3 overlap (reference val_mm.py:30-62; unused by evaluate, as there).
+    Tiles the size of the image itself, so one tile, as the reference's tile_size = image size."""
+    H, W = image[0].shape[2], image[0].shape[3]
+    tile = (H, W)
+    stride = math.ceil(tile[0] * (1 - 1 / 3))
+    rows = int(math.ceil((H - tile[0]) / stride) + 1)
+    cols = int(math.ceil((W - tile[1]) / stride) + 1)
+    dev = image[0].device
+    total = torch.zeros((num_classes, H, W), device=dev)
+    count = torch.zeros((H, W), device=dev)
+    for r in range(rows):
+        for c in range(cols):
+            x0, y0 = int(c * stride), int(r * stride)
+            x1, y1 = min(x0 + tile[1], W), min(y0 + tile[0], H)
+            img = [m[:, :, y0:y1, x0:x1] for m in image]
+            padded = [pad_image(m, tile) for m in img]
+            pred = model(padded)[0]
+            if flip:
+                pred = pred + model([m.flip(-1) for m in padded])[0].flip(-1)
+            count[y0:y1, x0:x1] += 1
+            total[:, y0:y1, x0:x1] += pred[:, :, :img[0].shape[2], :img[0].shape[3]].squeeze(0)
+    return total.unsqueeze(0)
 
 
 @torch.no_grad()
@@ -98,6 +137,7 @@ def make_dataset(cfg, split, transform, case=None):
 def main(cfg):
     device = torch.device(cfg['DEVICE'])
     eval_cfg = cfg['EVAL']
+    _AMP["dtype"] = torch.bfloat16 if str(eval_cfg.get('AMP', '')).lower() in ('bf16', 'bfloat16', 'true') else None
     transform = get_val_augmentation(eval_cfg['IMAGE_SIZE'])
     model_path = Path(eval_cfg['MODEL_PATH'])
     if not model_path.exists():
