@@ -69,12 +69,12 @@ int irads_msda_corner_index(int dtype, const void *loc, const int64_t *shapes, i
  *         NULL => the shift-region mask computed in-kernel when shift > 0
  *   out   (B, H, W, C) same dtype      lse (B*nW, nH, 144) fp32 workspace for backward
  * window = 12, head_dim = 32 (every Swin-B/L stage).  scale = qk_scale or 32^-0.5.
- *   bias_quads (nH, 8, 532) fp32 from irads_winattn_bias_quads (required for BF16, ignored for
- *         F32): the table re-laid so that every 4-key (forward) / 4-query (backward) bias
- *         group of a window row is one aligned 16-byte LDS read; recompute when rel_table
- *         changes (a pure function of it; the frozen trunk's is built once). */
+ *   bias_quads (nH, 2, 532, 4) fp32 from irads_winattn_bias_quads (required for BF16, ignored for
+ *         F32): the table divided by scale and re-laid so that every 4-key (forward) / 4-query
+ *         (backward) bias group of a window row is one 16-byte LDS read; recompute when rel_table
+ *         or scale changes (a pure function of both; the frozen trunk's is built once). */
 long irads_winattn_bias_quads_size(int nH);
-int irads_winattn_bias_quads(const float *rel_table, int nH, float *bias_quads, void *stream);
+int irads_winattn_bias_quads(const float *rel_table, int nH, float scale, float *bias_quads, void *stream);
 int irads_winattn_fwd(int dtype, const void *qkv, const float *qkv_bias, const float *rel_table,
                       const float *bias_quads, const float *mask, int n_mask, int B, int H, int W, int C, int nH, int shift,
                       float scale, void *out, float *lse, void *stream);

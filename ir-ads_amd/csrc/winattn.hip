@@ -259,14 +259,6 @@ __device__ __forceinline__ u16x8 cat4(u16x4 a, u16x4 b) {
     return u16x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
 }
 
-// bf16(q · scale): the reference's `q = q * self.scale` (swin.py:95), rounded as AMP rounds it
-__device__ __forceinline__ bf16x8_t scale_q(const u16x8 &q, float scale) {
-    bf16x8_t r;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) r[j] = (__bf16)(bf2f(q[j]) * scale);
-    return r;
-}
-
 __device__ __forceinline__ u16x8 bias_frag(const float *qbias, int c0) {
     u16x8 r;
 #pragma unroll
@@ -342,140 +334,185 @@ struct WinOrigin {
 // ---------------------------------------------------------------------------------------------
 // Forward, one workgroup per (window, head): 3 waves, wave w owns query tiles 3w..3w+2.
 //
-// The chunked kernel above ties each wave to one query tile of every window so that its 36
-// biases can live in registers (158 VGPRs): one 9-wave workgroup per CU, a 3-2-2-2 wave split
-// over the SIMDs and a per-window barrier that every wave waits at.  Here the biases come
-// from LDS instead, as the MFMA accumulator seed itself: for a lane's query and its 4
-// consecutive keys (one row of the window, since 4 | 12) the 4 biases are 4 consecutive
-// entries of the reversed 23x23 table, stored 4 times at the 4 alignments so that each seed
-// is ONE ds_read_b128.  That frees the wave from any fixed query tile: a workgroup is one
-// (window, head), all of its loads are issued up front, and 5 workgroups share a CU (LDS
-// 31.7 KB, <= 128 VGPRs), so one workgroup's load latency and barrier are covered by the
-// others' MFMA / softmax work instead of by a register pipeline inside one workgroup.
-constexpr int BQ = 532;  // floats per aligned copy of the reversed table (529 + pad)
+// The relative-position biases come from LDS as the MFMA accumulator seed itself: for a lane's
+// query and its 4 consecutive keys (one row of the window, since 4 | 12) the 4 biases are 4
+// consecutive entries of the reversed 23x23 table, so the head's table is staged as QS 16-byte
+// quads F[si] = (R[si], R[si+1], R[si+2], R[si+3]) and each seed is ONE ds_read_b128 at a
+// per-lane byte offset.  A workgroup is one (window, head); all of its global loads are issued
+// up front and retire behind one wait (no load waits on another), 5 workgroups share a CU (LDS
+// 31.5 KB, <= 128 VGPRs), so one workgroup's load latency is covered by the others' MFMA /
+// softmax work.
+//
+// Scale folding: the MFMA computes s' = q·k + b / scale on the raw bf16 q (the quads hold the
+// table divided by scale), and the softmax runs in base 2 on s'·(scale·log2 e): one fma per
+// score turns s' into the exponent, no per-element q·scale pass.  (The reference's AMP rounds
+// q·scale to bf16 before the product; here q·k is accumulated in fp32 from the unscaled bf16 q,
+// one bf16 rounding closer to the fp32 module.)
+constexpr int QS = 532;  // quads per head and direction (si <= 525 is ever read)
 
-// quads (nH, 8, BQ): copies c = 0..3 of the reversed table shifted by c (forward: a query's 4
-// consecutive keys), c = 4..7 of the table itself shifted by c - 4 (backward: a key's 4
-// consecutive queries).  One launch per table version; the caller caches the result.
-__global__ void winattn_bias_quads_kernel(const float *__restrict__ table, int nH, float *__restrict__ quads) {
+// quads (nH, 2, QS, 4) fp32, pre-divided by scale: direction 0 (forward, a query's 4 consecutive
+// keys) F[si][r] = T[528 - (si + r)]; direction 1 (backward, a key's 4 consecutive queries)
+// F[si][r] = T[si + r]; 0 outside the table.  One launch per (table version, scale).
+__global__ void winattn_bias_quads_kernel(const float *__restrict__ table, int nH, float inv_scale,
+                                          float *__restrict__ quads) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= nH * 8 * BQ) return;
-    const int h = i / (8 * BQ), c = (i / BQ) % 8, j = i % BQ;
-    const int idx = c < 4 ? TBL - 1 - (j + c) : j + (c - 4);
-    quads[i] = (idx >= 0 && idx < TBL) ? table[idx * nH + h] : 0.f;
+    if (i >= nH * 2 * QS * 4) return;
+    const int h = i / (2 * QS * 4), dir = (i / (QS * 4)) % 2, si = (i / 4) % QS, r = i % 4;
+    const int idx = dir == 0 ? TBL - 1 - (si + r) : si + r;
+    quads[i] = (idx >= 0 && idx < TBL) ? table[idx * nH + h] * inv_scale : 0.f;
+}
+
+// Shift-region class bits of a lane's 36 keys (key tiles kt, keys kt*16 + 4 grp + r, bit kt*4 + r):
+// hbits = key row in the second region (k / 12 >= 12 - shift, a threshold on k: the low n bits
+// clear), wbits = key column in the second region ((k % 12) >= 12 - shift: the 4 keys of a group
+// are one row segment starting at column 4 ((kt + grp) % 3), so the pattern repeats every 3 tiles).
+__device__ __forceinline__ void key_class_bits(int shift, int grp, unsigned long long &hbits,
+                                               unsigned long long &wbits) {
+    const int u = WS * (WS - shift) - 4 * grp;  // keys below the row threshold, counted from this group
+    const int n = u <= 0 ? 0 : min(36, 4 * (u >> 4) + min(u & 15, 4));
+    hbits = (n >= 64 ? 0ull : (~0ull << n)) & ((1ull << 36) - 1);
+    unsigned m[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) m[c] = 0xFu & (0xFu << min(4, max(0, WS - shift - 4 * c)));
+    const int g3 = grp % 3;
+    const unsigned long long P = m[g3] | (m[(g3 + 1) % 3] << 4) | (m[(g3 + 2) % 3] << 8);
+    wbits = P | (P << 12) | (P << 24);
+}
+
+// mneg100 where bit j of the mask is set, else 0: sign-extended one-bit field ANDed with the value
+__device__ __forceinline__ float mask_term(unsigned long long mbits, int j, float mneg100) {
+    const unsigned w = j < 32 ? (unsigned)mbits : (unsigned)(mbits >> 32);
+    const int all = __builtin_amdgcn_sbfe((int)w, j & 31, 1);
+    return __uint_as_float((unsigned)all & __float_as_uint(mneg100));
+}
+
+// wave-uniform "any lane true"
+__device__ __forceinline__ bool wave_any(bool p) { return __builtin_amdgcn_ballot_w64(p) != 0ull; }
+
+// bf16 pad-token fragment (the qkv bias, swin.py:186-190) of 8 channels starting at c0
+__device__ __forceinline__ u16x8 pad_frag(const float *qbias, int c0) {
+    if (!qbias) return u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    const f32x4 a = *(const f32x4 *)(qbias + c0), b = *(const f32x4 *)(qbias + c0 + 4);
+    u16x8 r;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        r[j] = f2bf(a[j]);
+        r[4 + j] = f2bf(b[j]);
+    }
+    return r;
 }
 
 template <int MM>
 __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(4))) winattn_fwd_bf16_wg(const unsigned short *__restrict__ qkv,
                                                             const float *__restrict__ qbias,
                                                             const float *__restrict__ quads,
-                                                            const float *__restrict__ mask, Geo g,
+                                                            const float *__restrict__ mask, Geo g, float c2,
                                                             unsigned short *__restrict__ out, float *__restrict__ lse) {
     __shared__ __attribute__((aligned(16))) unsigned short Ks[NT * RS];
     __shared__ __attribute__((aligned(16))) unsigned short Vs[NT * RS];
-    __shared__ __attribute__((aligned(16))) float Bq[4 * BQ];  // copy c: Bq[c*BQ + i] = T[528 - (i + c)]
-    __shared__ __attribute__((aligned(16))) unsigned short padS[3 * HD];
-    const int lid = xcd_remap(blockIdx.x, gridDim.x);  // the heads of one window on one XCD
+    __shared__ __attribute__((aligned(16))) f32x4 Bq[QS];  // forward quads of this head
+    const int lid = xcd_remap(blockIdx.x, gridDim.x);      // the heads of one window on one XCD
     const int h = lid % g.nH, bw = lid / g.nH;
     const WinOrigin wo(g, bw);
-    const long C3 = 3 * g.C;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int l16 = lane & 15, grp = lane >> 4;
-    // ---- issue every global load of the workgroup first
-    if (tid < 3 * HD) padS[tid] = qbias ? f2bf(qbias[(tid / HD) * g.C + h * HD + tid % HD]) : (unsigned short)0;
-    u16x8 kreg[3], vreg[3], qreg[3];
-    int ktok[3], qtok[3];
+    // ---- every global load of the workgroup first.  Thread (wave, l16, grp) owns tokens
+    // t_j = (3 wave + j) 16 + l16 and 16-B chunk grp of their q, k and v: its q rows are exactly
+    // its MFMA B fragments, its k / v chunks are staged to LDS.  32-bit byte offsets (< 4 GiB).
+    const char *base = (const char *)qkv;
+    const unsigned rowb = 6u * (unsigned)g.C, cb = 2u * (unsigned)g.C, hb = (unsigned)(h * HD + grp * 8) * 2u;
+    int tok[3];
+    u16x8 qreg[3], kreg[3], vreg[3];
 #pragma unroll
-    for (int j = 0; j < 3; ++j) {  // staging: chunk e = tid + 192 j of 576 = (token e / 4, 16-B column e % 4)
-        const int e = tid + 192 * j, t = e >> 2, ch = e & 3;
-        ktok[j] = wo.tok(g, t);
-        const long row = (long)(ktok[j] >= 0 ? ktok[j] : 0) * C3;
-        kreg[j] = *(const u16x8 *)(qkv + row + g.C + h * HD + ch * 8);
-        vreg[j] = *(const u16x8 *)(qkv + row + 2 * g.C + h * HD + ch * 8);
+    for (int j = 0; j < 3; ++j) {
+        tok[j] = wo.tok(g, (3 * wave + j) * 16 + l16);
+        const unsigned off = (unsigned)max(tok[j], 0) * rowb + hb;
+        qreg[j] = *(const u16x8 *)(base + off);
+        kreg[j] = *(const u16x8 *)(base + off + cb);
+        vreg[j] = *(const u16x8 *)(base + off + 2 * cb);
+    }
+    f32x4 bq[3];
+    const f32x4 *qsrc = (const f32x4 *)quads + (long)h * 2 * QS;
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+        if (tid + 192 * j < QS) bq[j] = qsrc[tid + 192 * j];
+    if (wave_any(tok[0] < 0 || tok[1] < 0 || tok[2] < 0)) {  // uniform: only waves holding pad tokens
+        const int c0 = h * HD + grp * 8;
+        const u16x8 qp = pad_frag(qbias, c0), kp = pad_frag(qbias, g.C + c0), vp = pad_frag(qbias, 2 * g.C + c0);
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+            if (tok[j] < 0) {
+                qreg[j] = qp;
+                kreg[j] = kp;
+                vreg[j] = vp;
+            }
     }
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
-        const int qi = (3 * wave + j) * 16 + l16;
-        qtok[j] = wo.tok(g, qi);
-        qreg[j] = *(const u16x8 *)(qkv + (long)(qtok[j] >= 0 ? qtok[j] : 0) * C3 + h * HD + grp * 8);
-    }
-    {  // the head's 4 reversed copies (irads_winattn_bias_quads), 16-B loads
-        const f32x4 *src = (const f32x4 *)(quads + (long)h * 8 * BQ);
-        for (int i = tid; i < BQ; i += 192) ((f32x4 *)Bq)[i] = src[i];
-    }
-    __syncthreads();  // padS
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-        const int e = tid + 192 * j, t = e >> 2, ch = e & 3;
-        const u16x8 kp = *(const u16x8 *)(padS + HD + ch * 8), vp = *(const u16x8 *)(padS + 2 * HD + ch * 8);
-        *(u16x8 *)(Ks + t * RS + ch * 8) = ktok[j] >= 0 ? kreg[j] : kp;
-        *(u16x8 *)(Vs + t * RS + ch * 8) = ktok[j] >= 0 ? vreg[j] : vp;
+        const int t = (3 * wave + j) * 16 + l16;
+        *(u16x8 *)(Ks + t * RS + grp * 8) = kreg[j];
+        *(u16x8 *)(Vs + t * RS + grp * 8) = vreg[j];
+        if (tid + 192 * j < QS) Bq[tid + 192 * j] = bq[j];
     }
     __syncthreads();
-    // ---- per-lane constants: key group of every key tile (keys kt*16 + 4 grp + r, one window row)
-    int kofs[9];  // 23 * row + col of the group's first key
-    unsigned long long hb = 0, wb = 0;  // key class bits (MM == 1)
+    // ---- per-lane constants: byte offset of the key group of every key tile (keys kt*16 + 4 grp + r,
+    // one window row) in the quads, and the key class bits (MM == 1)
+    int kofs[9];
 #pragma unroll
     for (int kt = 0; kt < 9; ++kt) {
         const int k0 = kt * 16 + grp * 4;
-        kofs[kt] = 23 * (k0 / WS) + k0 % WS;
-        if (MM == 1)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                hb |= (unsigned long long)hi_row(g, k0 + r) << (kt * 4 + r);
-                wb |= (unsigned long long)hi_col(g, k0 + r) << (kt * 4 + r);
-            }
+        kofs[kt] = (23 * (k0 / WS) + k0 % WS) * 16;
     }
+    unsigned long long hbits = 0, wbits = 0;
+    if (MM == 1) key_class_bits(g.shift, grp, hbits, wbits);
     bool lastH = false, lastW = false;
     if (MM == 1) {
         const int wi = bw % g.nW;
         lastH = wi / g.nWw == g.nWh - 1;
         lastW = wi % g.nWw == g.nWw - 1;
     }
+    const float mneg100 = -100.0f / g.scale;  // the region mask in s' units
     const bf16x8_t ones = as_bf(u16x8{0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80});
     const int tr_row = (l16 >> 2), tr_col = 4 * (l16 & 3);
+    const char *bqb = (const char *)Bq;
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
-        const int qt = 3 * wave + j, qi = qt * 16 + l16;
-        // (selects, not a dynamic index: a runtime index into these arrays would put them in scratch)
-        const int qtk = j == 0 ? qtok[0] : (j == 1 ? qtok[1] : qtok[2]);
-        const u16x8 qsel = j == 0 ? qreg[0] : (j == 1 ? qreg[1] : qreg[2]);
-        const u16x8 qraw = qtk >= 0 ? qsel : *(const u16x8 *)(padS + grp * 8);
-        const bf16x8_t qf = scale_q(qraw, g.scale);
-        const int aq = 264 - (23 * (qi / WS) + qi % WS);  // reversed-table index = aq + kofs
+        const int qi = (3 * wave + j) * 16 + l16;
+        const bf16x8_t qf = as_bf(qreg[j]);
+        const char *bq_q = bqb + (264 - (23 * (qi / WS) + qi % WS)) * 16;  // reversed-table index aq + key offset
         f32x4 s[9];
 #pragma unroll
         for (int kt = 0; kt < 9; ++kt) {
-            const int si = aq + kofs[kt];
-            const f32x4 b4 = ((const f32x4 *)Bq)[(si & 3) * (BQ / 4) + (si >> 2)];  // copy si & 3, aligned
+            const f32x4 b4 = *(const f32x4 *)(bq_q + kofs[kt]);
             const bf16x8_t kf = as_bf(*(const u16x8 *)(Ks + (kt * 16 + l16) * RS + grp * 8));
-            s[kt] = mfma16(kf, qf, b4);  // Sᵀ + B (key rows, query on the lane)
+            s[kt] = mfma16(kf, qf, b4);  // s'ᵀ (key rows, query on the lane), bias seeded
             if (MM == 2) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
-                    s[kt][r] += mask[((long)(bw % g.n_mask) * NT + qi) * NT + kt * 16 + grp * 4 + r];
+                    s[kt][r] = fmaf(mask[((long)(bw % g.n_mask) * NT + qi) * NT + kt * 16 + grp * 4 + r], 1.0f / g.scale,
+                                    s[kt][r]);
             }
         }
         if (MM == 1 && (lastH || lastW)) {  // uniform branch: only edge windows of the shifted grid
             unsigned long long mbits = 0;
-            if (lastH) mbits |= hi_row(g, qi) ? ~hb : hb;
-            if (lastW) mbits |= hi_col(g, qi) ? ~wb : wb;
+            if (lastH) mbits |= hi_row(g, qi) ? ~hbits : hbits;
+            if (lastW) mbits |= hi_col(g, qi) ? ~wbits : wbits;
 #pragma unroll
             for (int kt = 0; kt < 9; ++kt)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) s[kt][r] += ((mbits >> (kt * 4 + r)) & 1ull) ? -100.0f : 0.0f;
+                for (int r = 0; r < 4; ++r) s[kt][r] += mask_term(mbits, kt * 4 + r, mneg100);
         }
-        float mx = -INFINITY;
+        float mx = s[0][0];
 #pragma unroll
         for (int kt = 0; kt < 9; ++kt)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) mx = fmaxf(mx, s[kt][r]);
+            for (int r = (kt == 0); r < 4; ++r) mx = fmaxf(mx, s[kt][r]);
         mx = max_xor16_32(mx);
-        const float mneg = -mx * LOG2E;
+        const float mneg = -mx * c2;
 #pragma unroll
         for (int kt = 0; kt < 9; ++kt)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) s[kt][r] = fast_exp2(fmaf(s[kt][r], LOG2E, mneg));
+            for (int r = 0; r < 4; ++r) s[kt][r] = fast_exp2(fmaf(s[kt][r], c2, mneg));
         f32x4 o0 = {0.f, 0.f, 0.f, 0.f}, o1 = o0, os = o0;
 #pragma unroll
         for (int ks = 0; ks < 5; ++ks) {
@@ -494,19 +531,19 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(4))) w
             o1 = mfma16(as_bf(a1), pb, o1);
             os = mfma16(ones, pb, os);
         }
-        const float inv = 1.f / os[0];
-        if (qtk >= 0) {
+        const float inv = __builtin_amdgcn_rcpf(os[0]);
+        if (tok[j] >= 0) {
             u16x4 w0, w1;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 w0[r] = f2bf(o0[r] * inv);
                 w1[r] = f2bf(o1[r] * inv);
             }
-            unsigned short *op = out + (long)qtk * g.C + h * HD;
+            unsigned short *op = out + (long)tok[j] * g.C + h * HD;
             *(u16x4 *)(op + grp * 4) = w0;
             *(u16x4 *)(op + 16 + grp * 4) = w1;
         }
-        if (grp == 0) lse[((long)bw * g.nH + h) * NT + qi] = fmaf(mx, LOG2E, __log2f(os[0]));  // base-2 LSE
+        if (grp == 0) lse[((long)bw * g.nH + h) * NT + qi] = mx * c2 + __log2f(os[0]);  // base-2 LSE of s'·scale
     }
 }
 
@@ -521,10 +558,11 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(4))) w
 template <int MM, bool EX>
 __global__ void __launch_bounds__(576) winattn_bwd_bf16(
     const unsigned short *__restrict__ qkv, const float *__restrict__ qbias, const float *__restrict__ quads,
-    const float *__restrict__ mask, Geo g, int cw, const unsigned short *__restrict__ out, const float *__restrict__ lse,
+    const float *__restrict__ mask, Geo g, int cw, float c2, const unsigned short *__restrict__ out,
+    const float *__restrict__ lse,
     const unsigned short *__restrict__ gout, unsigned short *__restrict__ gqkv, float *__restrict__ gtable,
     float *__restrict__ gbias) {
-    __shared__ __attribute__((aligned(16))) float Bf[4 * BQ];  // copy c: Bf[c*BQ + i] = T[i + c]
+    __shared__ __attribute__((aligned(16))) f32x4 Bf[QS];  // backward quads: Bf[si] = T[si .. si + 3] / scale
     __shared__ __attribute__((aligned(16))) unsigned short Qs[NR * RS];
     __shared__ __attribute__((aligned(16))) unsigned short dOs[NR * RS];
     __shared__ __attribute__((aligned(16))) unsigned short Ks[NR * RS];
@@ -535,6 +573,7 @@ __global__ void __launch_bounds__(576) winattn_bwd_bf16(
     __shared__ float tgS[EX ? TBL : 1];  // EX: this workgroup's rel-table gradient, flushed once
     const Chunk ck = decode_chunk(g, cw);
     const int h = ck.h;
+    const float mneg100 = -100.0f / g.scale;  // the region mask in s' units
     const long C3 = 3 * g.C;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int l16 = lane & 15, grp = lane >> 4;
@@ -547,8 +586,8 @@ __global__ void __launch_bounds__(576) winattn_bwd_bf16(
     if (EX)
         for (int i = tid; i < TBL; i += 576) tgS[i] = 0.f;
     {  // the head's bias quads, copies 4..7 (key on the lane), 16-B loads
-        const f32x4 *src = (const f32x4 *)(quads + (long)h * 8 * BQ + 4 * BQ);
-        for (int i = tid; i < BQ; i += 576) ((f32x4 *)Bf)[i] = src[i];
+        const f32x4 *src = (const f32x4 *)quads + (long)h * 2 * QS + QS;
+        for (int i = tid; i < QS; i += 576) Bf[i] = src[i];
     }
     // key = 16 wave + l16 on the lane, queries 16 qt + 4 grp + r
     const int kkey = wave * 16 + l16;
@@ -590,7 +629,7 @@ __global__ void __launch_bounds__(576) winattn_bwd_bf16(
     const int tr_row = (l16 >> 2), tr_col = 4 * (l16 & 3);
     for (int bw = ck.w_begin; bw < ck.w_end; ++bw) {
         __syncthreads();
-        *(bf16x8_t *)(Qs + st_t * RS + st_ch * 8) = scale_q(qreg, g.scale);  // Q' = bf16(q·scale), as forward
+        *(u16x8 *)(Qs + st_t * RS + st_ch * 8) = qreg;  // raw q: the scale is folded into c2, as forward
         *(u16x8 *)(dOs + st_t * RS + st_ch * 8) = dreg;
         *(u16x8 *)(Ks + st_t * RS + st_ch * 8) = kreg;
         *(u16x8 *)(Vs + st_t * RS + st_ch * 8) = vreg;
@@ -643,15 +682,16 @@ __global__ void __launch_bounds__(576) winattn_bwd_bf16(
                 const f32x4 l4 = *(const f32x4 *)(lseS + qt * 16 + grp * 4);
                 const f32x4 nd4 = *(const f32x4 *)(dltS + qt * 16 + grp * 4);
                 const int q0 = qt * 16 + grp * 4, si = 264 + 23 * (q0 / WS) + q0 % WS - bk;
-                const f32x4 b4 = ((const f32x4 *)Bf)[(si & 3) * (BQ / 4) + (si >> 2)];
-                const f32x4 sa = mfma16(qa, kb, b4);  // S[q][key] + B (Q' pre-scaled), as the forward's Sᵀ
+                const f32x4 b4 = Bf[si];
+                const f32x4 sa = mfma16(qa, kb, b4);  // s'[q][key] = q·k + b / scale, as the forward's s'ᵀ
                 const f32x4 dpa = mfma16(da, vb, nd4);                       // dP[q][key] - delta_q
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     float v = sa[r];
-                    if (MASKED) v += ((mbits >> (qt * 4 + r)) & 1ull) ? -100.0f : 0.0f;
-                    if (MM == 2) v += mask[((long)(bw % g.n_mask) * NT + qt * 16 + grp * 4 + r) * NT + kkey];
-                    const float p = fast_exp2(fmaf(v, LOG2E, -l4[r]));
+                    if (MASKED) v += ((mbits >> (qt * 4 + r)) & 1ull) ? mneg100 : 0.0f;
+                    if (MM == 2)
+                        v = fmaf(mask[((long)(bw % g.n_mask) * NT + qt * 16 + grp * 4 + r) * NT + kkey], 1.0f / g.scale, v);
+                    const float p = fast_exp2(fmaf(v, c2, -l4[r]));
                     const float ds = p * dpa[r];
                     pb[4 * half + r] = (__bf16)p;
                     sb[4 * half + r] = (__bf16)ds;
@@ -686,8 +726,8 @@ __global__ void __launch_bounds__(576) winattn_bwd_bf16(
                 u16x4 k0, k1, v0, v1;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    k0[r] = f2bf(dk0[r]);  // dK = dSᵀ·Q' (Q' already carries the scale)
-                    k1[r] = f2bf(dk1[r]);
+                    k0[r] = f2bf(dk0[r] * g.scale);  // dK = scale · dSᵀ·q
+                    k1[r] = f2bf(dk1[r] * g.scale);
                     v0[r] = f2bf(dv0[r]);
                     v1[r] = f2bf(dv1[r]);
                 }
@@ -699,8 +739,8 @@ __global__ void __launch_bounds__(576) winattn_bwd_bf16(
             } else if (EX && gbias) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    atomicAdd(&gbias[g.C + c0 + r], dk0[r]);
-                    atomicAdd(&gbias[g.C + c0 + 16 + r], dk1[r]);
+                    atomicAdd(&gbias[g.C + c0 + r], dk0[r] * g.scale);
+                    atomicAdd(&gbias[g.C + c0 + 16 + r], dk1[r] * g.scale);
                     atomicAdd(&gbias[2 * g.C + c0 + r], dv0[r]);
                     atomicAdd(&gbias[2 * g.C + c0 + 16 + r], dv1[r]);
                 }
@@ -784,14 +824,15 @@ int make_geo(Geo &g, int dtype, int B, int H, int W, int C, int nH, int shift, f
 
 using namespace irads;
 
-extern "C" int irads_winattn_bias_quads(const float *rel_table, int nH, float *quads, void *stream) {
+extern "C" int irads_winattn_bias_quads(const float *rel_table, int nH, float scale, float *quads, void *stream) {
     IRADS_REQUIRE(rel_table && quads && nH > 0, "irads_winattn_bias_quads: null pointer / nH=%d", nH);
-    const int n = nH * 8 * BQ;
-    winattn_bias_quads_kernel<<<(n + 255) / 256, 256, 0, (hipStream_t)stream>>>(rel_table, nH, quads);
+    IRADS_REQUIRE(scale > 0.f, "irads_winattn_bias_quads: scale must be positive (%g)", scale);
+    const int n = nH * 2 * QS * 4;
+    winattn_bias_quads_kernel<<<(n + 255) / 256, 256, 0, (hipStream_t)stream>>>(rel_table, nH, 1.0f / scale, quads);
     return check_launch("irads_winattn_bias_quads");
 }
 
-extern "C" long irads_winattn_bias_quads_size(int nH) { return (long)nH * 8 * BQ; }
+extern "C" long irads_winattn_bias_quads_size(int nH) { return (long)nH * 2 * QS * 4; }
 
 extern "C" int irads_winattn_fwd(int dtype, const void *qkv, const float *qkv_bias, const float *rel_table,
                                  const float *bias_quads, const float *mask, int n_mask, int B, int H, int W, int C, int nH, int shift,
@@ -807,8 +848,10 @@ extern "C" int irads_winattn_fwd(int dtype, const void *qkv, const float *qkv_bi
     {
         const int mm = mask ? 2 : (shift > 0 ? 1 : 0);
         IRADS_REQUIRE(bias_quads, "irads_winattn_fwd: bf16 needs bias_quads (irads_winattn_bias_quads)");
+        IRADS_REQUIRE(scale > 0.f, "irads_winattn_fwd: scale must be positive (%g)", scale);
+        const float c2 = scale * LOG2E;
 #define IRADS_WF(M) winattn_fwd_bf16_wg<M><<<nblk, 192, 0, st>>>((const unsigned short *)qkv, qkv_bias, bias_quads, \
-                                                                  mask, g, (unsigned short *)out, lse)
+                                                                  mask, g, c2, (unsigned short *)out, lse)
         if (mm == 0) IRADS_WF(0); else if (mm == 1) IRADS_WF(1); else IRADS_WF(2);
 #undef IRADS_WF
     }
@@ -833,10 +876,12 @@ extern "C" int irads_winattn_bwd(int dtype, const void *qkv, const float *qkv_bi
                                               grad_bias_pad);
     } else {
         IRADS_REQUIRE(bias_quads, "irads_winattn_bwd: bf16 needs bias_quads (irads_winattn_bias_quads)");
+        IRADS_REQUIRE(scale > 0.f, "irads_winattn_bwd: scale must be positive (%g)", scale);
         const int cw = chunk_windows(B * g.nW, nH);
         const unsigned nwg = (unsigned)(((B * g.nW + cw - 1) / cw) * nH);
 #define IRADS_WB(M, X)                                                                                            \
     winattn_bwd_bf16<M, X><<<nwg, 576, 0, st>>>((const unsigned short *)qkv, qkv_bias, bias_quads, mask, g, cw,   \
+                                                scale * LOG2E,                                                    \
                                                 (const unsigned short *)out, lse, (const unsigned short *)grad_out, \
                                                 (unsigned short *)grad_qkv, grad_table, grad_bias_pad)
         if (ex) {

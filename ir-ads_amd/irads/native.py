@@ -22,7 +22,7 @@ SIGNATURES = {
     "irads_msda_fwd": [_i, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp, _vp],
     "irads_msda_bwd": [_i, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp],
     "irads_msda_corner_index": [_i, _vp, _vp, _i, _i, _i, _i, _i, _vp, _vp],
-    "irads_winattn_bias_quads": [_vp, _i, _vp, _vp],
+    "irads_winattn_bias_quads": [_vp, _i, _f, _vp, _vp],
     "irads_winattn_fwd": [_i, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _f, _vp, _vp, _vp],
     "irads_winattn_bwd": [_i, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _f, _vp, _vp, _vp, _vp, _vp, _vp,
                           _vp],

@@ -62,15 +62,15 @@ def _winattn_geometry(H, W):
 _QUADS = {}  # (table data_ptr, version, nH) -> (table, quads): the table is held so its address stays its own
 
 
-def bias_quads(table_f, nH):
-    """irads_winattn_bias_quads of a (529, nH) fp32 table, cached per table version (the frozen
-    trunk's tables are re-laid once; a trainable table is re-laid after each update)."""
-    key = (table_f.data_ptr(), table_f._version, nH, table_f.device)
+def bias_quads(table_f, nH, scale):
+    """irads_winattn_bias_quads of a (529, nH) fp32 table (divided by scale), cached per table
+    version (the frozen trunk's tables are re-laid once; a trainable table after each update)."""
+    key = (table_f.data_ptr(), table_f._version, nH, float(scale), table_f.device)
     hit = _QUADS.get(key)
     if hit is not None:
         return hit[1]
     q = torch.empty((N.load().irads_winattn_bias_quads_size(nH),), device=table_f.device, dtype=torch.float32)
-    N.call("irads_winattn_bias_quads", N.ptr(table_f), nH, N.ptr(q), N.stream())
+    N.call("irads_winattn_bias_quads", N.ptr(table_f), nH, float(scale), N.ptr(q), N.stream())
     if len(_QUADS) >= 256:
         _QUADS.clear()
     _QUADS[key] = (table_f, q)
@@ -89,7 +89,7 @@ def winattn_fwd(qkv, bias_f, table_f, mask_f, H, W, num_heads, shift, scale):
     out = torch.empty((B, L, C), device=qkv.device, dtype=qkv.dtype)
     Hp, Wp, nW = _winattn_geometry(H, W)
     lse = torch.empty((B * nW * num_heads * WINDOW * WINDOW,), device=qkv.device, dtype=torch.float32)
-    quads = bias_quads(table_f, num_heads) if code == N.BF16 else None
+    quads = bias_quads(table_f, num_heads, scale) if code == N.BF16 else None
     ev = TIMER.start("winattn_fwd")
     N.call("irads_winattn_fwd", code, N.ptr(qkv), N.ptr(bias_f), N.ptr(table_f), N.ptr(quads), N.ptr(mask_f), n_mask,
            B, H, W,
@@ -113,7 +113,7 @@ def winattn_bwd(qkv, bias_f, table_f, mask_f, H, W, nH, shift, scale, out, lse, 
     gqkv = torch.empty_like(qkv)
     gtable = torch.zeros_like(table_f) if need_table else None
     gbias = torch.zeros((3 * C,), device=qkv.device, dtype=torch.float32) if need_bias else None
-    quads = bias_quads(table_f, nH) if code == N.BF16 else None
+    quads = bias_quads(table_f, nH, scale) if code == N.BF16 else None
     ev = TIMER.start("winattn_bwd")
     N.call("irads_winattn_bwd", code, N.ptr(qkv), N.ptr(bias_f), N.ptr(table_f), N.ptr(quads), N.ptr(mask_f), n_mask,
            B, H, W, C, nH, shift, float(scale), N.ptr(out), N.ptr(lse), N.ptr(gout), N.ptr(gqkv), N.ptr(gtable),

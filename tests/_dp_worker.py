@@ -60,7 +60,8 @@ def main():
     step.step()
     torch.cuda.synchronize()
     if rank == 0:
-        torch.save({n: p.grad.detach().cpu() for n, p in m.named_parameters() if p.requires_grad}, out)
+        torch.save({n: (p.grad if p.grad is not None else torch.zeros_like(p)).detach().cpu()
+                    for n, p in m.named_parameters() if p.requires_grad}, out)
     dist.barrier()
     dist.destroy_process_group()
 
