@@ -315,11 +315,14 @@ def main():
     ops.TIMER.enabled = set()
     timer_steps = 1 if graph else args.steps  # steps the recorded launches cover
     if graph and not timer_in_graph:
-        # HIP events cannot be captured on this stack: time the same kernels in one eager step
+        # HIP events cannot be captured on this stack: time the same kernels in one eager step, each
+        # timed launch behind a GPU spin so that its event pair brackets the kernel alone
         ops.TIMER.records.clear()
         ops.TIMER.enabled = set(TIMED_KERNELS)
+        ops.TIMER.lead_cycles = 200_000
         fwd_bwd(model, loss_fn, batch)  # gradients land in the graph's buffer, re-zeroed by the next replay
         ops.TIMER.enabled = set()
+        ops.TIMER.lead_cycles = 0
     if world > 1:
         t = torch.tensor([elapsed], device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -363,7 +366,8 @@ def main():
             "launches": fwd["launches"], "avg_launch_ms": round(avg_ms, 5),
             "algorithmic_bytes_per_launch": round(per_launch_bytes),
             "timing": ("HIP events captured in the graph, last timed replay" if timer_in_graph else
-                       "HIP events on the launch stream" + (" (eager step after the timed region)" if graph else "")),
+                       "HIP events on the launch stream" + (" (eager step after the timed region, each launch "
+                                                            "queued behind a GPU spin)" if graph else "")),
             "bytes_definition": "SURVEY §8(d): read q,k,v + write o per padded token (8·Np·C bytes, bf16)",
             "achieved_real_tokens_gbs": round(achieved_real, 1),
             "mfma_tflops": round(fwd["flops"] / (fwd["total_ms"] * 1e-3) / 1e12, 2)}

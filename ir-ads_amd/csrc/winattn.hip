@@ -259,29 +259,7 @@ __device__ __forceinline__ u16x8 cat4(u16x4 a, u16x4 b) {
     return u16x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
 }
 
-__device__ __forceinline__ u16x8 bias_frag(const float *qbias, int c0) {
-    u16x8 r;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) r[j] = qbias ? f2bf(qbias[c0 + j]) : (unsigned short)0;
-    return r;
-}
-
-__device__ __forceinline__ u16x8 load_frag(const unsigned short *qkv, const float *qbias, int tok, long C3, int c0) {
-    if (tok >= 0) return *(const u16x8 *)(qkv + (long)tok * C3 + c0);
-    return bias_frag(qbias, c0);
-}
-
-// branch-free variant for the staging loops: the pad-token value (the qkv bias, bf16)
-// is precomputed once per workgroup and selected
-__device__ __forceinline__ u16x8 load_frag_sel(const unsigned short *qkv, const u16x8 &padv, int tok, long C3,
-                                               int c0) {
-    const u16x8 v = *(const u16x8 *)(qkv + (long)(tok >= 0 ? tok : 0) * C3 + c0);
-    return tok >= 0 ? v : padv;
-}
-
-constexpr int RS = 40;    // LDS row stride (bf16) of the row-major tiles: 80 B
 constexpr int NR = 160;   // rows incl. zero padding to 5 k-steps of 32
-constexpr int DSR = 152;  // dSᵀ row stride in bf16 (144 queries + 8 pad: 304-B rows)
 constexpr float LOG2E = 1.4426950408889634f;
 // Relative-position biases live in registers as fp16 pairs (pre-scaled by log2 e): abs
 // error <= 2^-11 |b|, far below the bf16 rounding the reference's AMP applies to the
@@ -301,18 +279,13 @@ __device__ __forceinline__ Chunk decode_chunk(const Geo &g, int cw) {
     return c;
 }
 
-__device__ __forceinline__ int token_of(const Geo &g, int bw, int t) {
-    int tok, reg;
-    token_info(g, bw % g.nW, t, bw / g.nW, tok, reg);
-    return tok;
-}
 
 // class bits of token t inside a boundary window: row / column in the second shift region
 __device__ __forceinline__ bool hi_row(const Geo &g, int t) { return t / WS >= WS - g.shift; }
 __device__ __forceinline__ bool hi_col(const Geo &g, int t) { return t % WS >= WS - g.shift; }
 
 // Window origin of one (image, window) work item, decoded once per workgroup (the runtime
-// divisions by nW / nWw are the expensive part of token_of); tok() is then divide-free per token.
+// divisions by nW / nWw are the expensive part); tok() is then divide-free per token.
 struct WinOrigin {
     int r0, c0, base;  // rolled-frame row / column of the window's first token, image token offset
     __device__ __forceinline__ WinOrigin(const Geo &g, int bw) {
@@ -336,7 +309,7 @@ struct WinOrigin {
 //
 // The relative-position biases come from LDS as the MFMA accumulator seed itself: for a lane's
 // query and its 4 consecutive keys (one row of the window, since 4 | 12) the 4 biases are 4
-// consecutive entries of the reversed 23x23 table, so the head's table is staged as QS 16-byte
+// consecutive entries of the reversed 23x23 table, so the head's table is staged as 16-byte
 // quads F[si] = (R[si], R[si+1], R[si+2], R[si+3]) and each seed is ONE ds_read_b128 at a
 // per-lane byte offset.  A workgroup is one (window, head); all of its global loads are issued
 // up front and retire behind one wait (no load waits on another), 5 workgroups share a CU (LDS
@@ -348,19 +321,41 @@ struct WinOrigin {
 // score turns s' into the exponent, no per-element q·scale pass.  (The reference's AMP rounds
 // q·scale to bf16 before the product; here q·k is accumulated in fp32 from the unscaled bf16 q,
 // one bf16 rounding closer to the fp32 module.)
-constexpr int QS = 532;  // quads per head and direction (si <= 525 is ever read)
+constexpr int QF_STRIDE = 28;  // row stride of the (dr, dc) quad grids (23 x 28)
+constexpr int QF = 23 * QF_STRIDE;
+constexpr int QH = 2 * QF;     // quads per head: forward grid, then backward grid
 
-// quads (nH, 2, QS, 4) fp32, pre-divided by scale: direction 0 (forward, a query's 4 consecutive
-// keys) F[si][r] = T[528 - (si + r)]; direction 1 (backward, a key's 4 consecutive queries)
-// F[si][r] = T[si + r]; 0 outside the table.  One launch per (table version, scale).
+// quads (nH, QH, 4) fp32, pre-divided by scale.
+//   forward, a query's 4 consecutive keys of one window row: F[28 (dr + 11) + (dc + 11)][r] =
+//     T[(11 - dr) * 23 + (11 - dc - r)] with dr = row(k) - row(q), dc = col(k0) - col(q).  The row
+//     stride 28 (not 23) spreads the 16 lanes of each ds_read_b128 group over the LDS bank slots
+//     (1.4-way on average instead of 2.1-way for the 81 (query tile, key tile) pairs).
+//   backward (offset QF), a key's 4 consecutive queries of one window row: B[28 (dr + 11) + (dc + 11)][r]
+//     = T[(dr + 11) * 23 + (dc + r + 11)] with dr = row(q) - row(k), dc = col(q0) - col(k).
+// 0 outside the table.  One launch per (table version, scale).
 __global__ void winattn_bias_quads_kernel(const float *__restrict__ table, int nH, float inv_scale,
                                           float *__restrict__ quads) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= nH * 2 * QS * 4) return;
-    const int h = i / (2 * QS * 4), dir = (i / (QS * 4)) % 2, si = (i / 4) % QS, r = i % 4;
-    const int idx = dir == 0 ? TBL - 1 - (si + r) : si + r;
+    if (i >= nH * QH * 4) return;
+    const int h = i / (QH * 4), e = (i / 4) % QH, r = i % 4;
+    const int eg = e < QF ? e : e - QF;
+    const int dr = eg / QF_STRIDE - 11, dc = eg % QF_STRIDE - 11;
+    int idx;
+    if (e < QF) {
+        const int tc = 11 - dc - r;
+        idx = (dc <= 11 && tc >= 0 && tc < 23) ? (11 - dr) * 23 + tc : -1;
+    } else {
+        const int tc = dc + r + 11;
+        idx = (dc <= 11 && tc >= 0 && tc < 23) ? (dr + 11) * 23 + tc : -1;
+    }
     quads[i] = (idx >= 0 && idx < TBL) ? table[idx * nH + h] * inv_scale : 0.f;
 }
+
+// K / V tiles of the bf16 forward: 144 rows x 64 B, the four 16-B chunks of row t stored at chunk
+// position c ^ kv_swz(t), kv_swz = {0, 2, 3, 1}[(t >> 2) & 3]: conflict-free for the ds_read_b128
+// K-fragment reads (each 16-lane group covers all 16 slots of a 256-B bank row) and for the
+// ds_read_b64_tr_b16 Vᵀ reads (the 8 rows a half-wave reads land on disjoint 32-B bank spans).
+__device__ __forceinline__ int kv_swz(int t) { return (0x78 >> (2 * ((t >> 2) & 3))) & 3; }
 
 // Shift-region class bits of a lane's 36 keys (key tiles kt, keys kt*16 + 4 grp + r, bit kt*4 + r):
 // hbits = key row in the second region (k / 12 >= 12 - shift, a threshold on k: the low n bits
@@ -408,9 +403,9 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(4))) w
                                                             const float *__restrict__ quads,
                                                             const float *__restrict__ mask, Geo g, float c2,
                                                             unsigned short *__restrict__ out, float *__restrict__ lse) {
-    __shared__ __attribute__((aligned(16))) unsigned short Ks[NT * RS];
-    __shared__ __attribute__((aligned(16))) unsigned short Vs[NT * RS];
-    __shared__ __attribute__((aligned(16))) f32x4 Bq[QS];  // forward quads of this head
+    __shared__ __attribute__((aligned(16))) unsigned short Ks[NT * HD];  // swizzled 64-B rows (kv_swz)
+    __shared__ __attribute__((aligned(16))) unsigned short Vs[NT * HD];
+    __shared__ __attribute__((aligned(16))) f32x4 Bq[QF];  // forward quads of this head
     const int lid = xcd_remap(blockIdx.x, gridDim.x);      // the heads of one window on one XCD
     const int h = lid % g.nH, bw = lid / g.nH;
     const WinOrigin wo(g, bw);
@@ -432,10 +427,11 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(4))) w
         vreg[j] = *(const u16x8 *)(base + off + 2 * cb);
     }
     f32x4 bq[3];
-    const f32x4 *qsrc = (const f32x4 *)quads + (long)h * 2 * QS;
+    f32x4 bq4 = {0.f, 0.f, 0.f, 0.f};
+    const f32x4 *qsrc = (const f32x4 *)quads + (long)h * QH;
 #pragma unroll
-    for (int j = 0; j < 3; ++j)
-        if (tid + 192 * j < QS) bq[j] = qsrc[tid + 192 * j];
+    for (int j = 0; j < 3; ++j) bq[j] = qsrc[tid + 192 * j];  // QF = 644 >= 3 * 192
+    if (tid < QF - 576) bq4 = qsrc[576 + tid];
     if (wave_any(tok[0] < 0 || tok[1] < 0 || tok[2] < 0)) {  // uniform: only waves holding pad tokens
         const int c0 = h * HD + grp * 8;
         const u16x8 qp = pad_frag(qbias, c0), kp = pad_frag(qbias, g.C + c0), vp = pad_frag(qbias, 2 * g.C + c0);
@@ -447,21 +443,23 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(4))) w
                 vreg[j] = vp;
             }
     }
+    const int swz_l = kv_swz(l16);  // rows t = 16 n + l16 all have the swizzle of l16
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
         const int t = (3 * wave + j) * 16 + l16;
-        *(u16x8 *)(Ks + t * RS + grp * 8) = kreg[j];
-        *(u16x8 *)(Vs + t * RS + grp * 8) = vreg[j];
-        if (tid + 192 * j < QS) Bq[tid + 192 * j] = bq[j];
+        *(u16x8 *)(Ks + t * HD + (grp ^ swz_l) * 8) = kreg[j];
+        *(u16x8 *)(Vs + t * HD + (grp ^ swz_l) * 8) = vreg[j];
+        Bq[tid + 192 * j] = bq[j];
     }
+    if (tid < QF - 576) Bq[576 + tid] = bq4;
     __syncthreads();
     // ---- per-lane constants: byte offset of the key group of every key tile (keys kt*16 + 4 grp + r,
     // one window row) in the quads, and the key class bits (MM == 1)
-    int kofs[9];
+    int kofs[9];  // (28 row(k0) + col(k0)) * 16 B
 #pragma unroll
     for (int kt = 0; kt < 9; ++kt) {
         const int k0 = kt * 16 + grp * 4;
-        kofs[kt] = (23 * (k0 / WS) + k0 % WS) * 16;
+        kofs[kt] = (QF_STRIDE * (k0 / WS) + k0 % WS) * 16;
     }
     unsigned long long hbits = 0, wbits = 0;
     if (MM == 1) key_class_bits(g.shift, grp, hbits, wbits);
@@ -473,18 +471,24 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(4))) w
     }
     const float mneg100 = -100.0f / g.scale;  // the region mask in s' units
     const bf16x8_t ones = as_bf(u16x8{0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80});
-    const int tr_row = (l16 >> 2), tr_col = 4 * (l16 & 3);
+    // Vᵀ transposed reads: rows 32 ks + 4 grp + (l16 >> 2) (+16), all with the swizzle of grp; elements
+    // 4 (l16 & 3) .. +3 of d-half 0 (chunk (l16 & 3) >> 1) and of d-half 1 (that chunk ^ 2)
+    const int vsw = kv_swz(4 * grp), vch = ((l16 & 3) >> 1), vin = (l16 & 1) * 4;
+    const int vrow = 4 * grp + (l16 >> 2);
+    const unsigned short *vb0 = Vs + vrow * HD + ((vch ^ vsw) * 8) + vin;
+    const unsigned short *vb1 = Vs + vrow * HD + (((vch ^ 2) ^ vsw) * 8) + vin;
+    const unsigned short *kb = Ks + l16 * HD + (grp ^ swz_l) * 8;
     const char *bqb = (const char *)Bq;
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
         const int qi = (3 * wave + j) * 16 + l16;
         const bf16x8_t qf = as_bf(qreg[j]);
-        const char *bq_q = bqb + (264 - (23 * (qi / WS) + qi % WS)) * 16;  // reversed-table index aq + key offset
+        const char *bq_q = bqb + (QF_STRIDE * 11 + 11 - (QF_STRIDE * (qi / WS) + qi % WS)) * 16;  // + key offset
         f32x4 s[9];
 #pragma unroll
         for (int kt = 0; kt < 9; ++kt) {
             const f32x4 b4 = *(const f32x4 *)(bq_q + kofs[kt]);
-            const bf16x8_t kf = as_bf(*(const u16x8 *)(Ks + (kt * 16 + l16) * RS + grp * 8));
+            const bf16x8_t kf = as_bf(*(const u16x8 *)(kb + kt * 16 * HD));
             s[kt] = mfma16(kf, qf, b4);  // s'ᵀ (key rows, query on the lane), bias seeded
             if (MM == 2) {
 #pragma unroll
@@ -522,11 +526,10 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(4))) w
                 pb[r] = (__bf16)s[2 * ks][r];
                 pb[4 + r] = (2 * ks + 1 < 9) ? (__bf16)s[2 * ks + 1][r] : (__bf16)0.f;
             }
-            const unsigned short *v0 = Vs + (32 * ks + 4 * grp + tr_row) * RS + tr_col;
             // keys 144..159 do not exist: their P is 0, so any finite rows serve (tile 8 again)
-            const unsigned short *v1 = ks < 4 ? v0 + 16 * RS : v0;
-            const u16x8 a0 = cat4(tr_read(v0), tr_read(v1));
-            const u16x8 a1 = cat4(tr_read(v0 + 16), tr_read(v1 + 16));
+            const int r0 = 32 * ks * HD, r1 = ks < 4 ? r0 + 16 * HD : r0;
+            const u16x8 a0 = cat4(tr_read(vb0 + r0), tr_read(vb0 + r1));
+            const u16x8 a1 = cat4(tr_read(vb1 + r0), tr_read(vb1 + r1));
             o0 = mfma16(as_bf(a0), pb, o0);
             o1 = mfma16(as_bf(a1), pb, o1);
             os = mfma16(ones, pb, os);
@@ -548,13 +551,20 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(4))) w
 }
 
 // Backward: persistent-chunk workgroups of 9 waves (one head x a contiguous chunk of windows,
-// ~one workgroup per CU), phase 1 key-on-lane (S = Q'·Kᵀ + B, dP = dO·Vᵀ - δ; dVᵀ += dOᵀ·P and
-// dKᵀ += Q'ᵀ·dS straight from the accumulators; dS to LDS), phase 2 dQᵀ = Kᵀ·dSᵀ.  The biases are
-// the forward's fp32 values, seeded into the S accumulator as there: for a key and 4 consecutive
-// queries of one window row they are 4 consecutive table entries, one ds_read_b128 from the
-// head's bias quads (copies 4..7) staged once per workgroup.
+// ~one workgroup per CU), phase 1 key-on-lane (s' = q·kᵀ + b/scale, dP = dO·Vᵀ - δ; dVᵀ += dOᵀ·P and
+// dKᵀ += qᵀ·dS straight from the accumulators; dS to LDS), phase 2 dQᵀ = Kᵀ·dSᵀ.  The biases are the
+// forward's values, seeded into the s' accumulator as there: for a key and 4 consecutive queries of
+// one window row they are 4 consecutive table entries, one ds_read_b128 from the head's backward
+// quads (the stride-28 (dr, dc) grid) staged once per workgroup.  Q, dO, K and V tiles are 64-B rows
+// swizzled as the forward's (kv_swz), dSᵀ rows are 160 bf16 with 8-B pieces XOR-placed by
+// ds_swz(row): conflict-free both for the dS stores (key on the lane) and for phase 2's transposed
+// reads.  The next window's q, k, v, dO, O and LSE are prefetched into registers while this one
+// computes.
 // EX: support the optional rel-table / pad-bias gradient accumulators (frozen in IR-ADS's
 // Adapter training, so the default instantiation compiles them out)
+constexpr int DST = 160;  // dSᵀ row stride (bf16)
+__device__ __forceinline__ int ds_swz(int row) { return 4 * ((row >> 1) & 7); }
+
 template <int MM, bool EX>
 __global__ void __launch_bounds__(576) winattn_bwd_bf16(
     const unsigned short *__restrict__ qkv, const float *__restrict__ qbias, const float *__restrict__ quads,
@@ -562,77 +572,103 @@ __global__ void __launch_bounds__(576) winattn_bwd_bf16(
     const float *__restrict__ lse,
     const unsigned short *__restrict__ gout, unsigned short *__restrict__ gqkv, float *__restrict__ gtable,
     float *__restrict__ gbias) {
-    __shared__ __attribute__((aligned(16))) f32x4 Bf[QS];  // backward quads: Bf[si] = T[si .. si + 3] / scale
-    __shared__ __attribute__((aligned(16))) unsigned short Qs[NR * RS];
-    __shared__ __attribute__((aligned(16))) unsigned short dOs[NR * RS];
-    __shared__ __attribute__((aligned(16))) unsigned short Ks[NR * RS];
-    __shared__ __attribute__((aligned(16))) unsigned short Vs[NT * RS];
-    __shared__ __attribute__((aligned(16))) unsigned short dSt[NR * DSR];  // dSᵀ: [key][query], keys >= 144 zero
+    __shared__ __attribute__((aligned(16))) f32x4 Bf[QF];  // backward quads (stride-28 grid) of this head
+    __shared__ __attribute__((aligned(16))) unsigned short Qs[NT * HD];
+    __shared__ __attribute__((aligned(16))) unsigned short dOs[NT * HD];
+    __shared__ __attribute__((aligned(16))) unsigned short Ks[NT * HD];
+    __shared__ __attribute__((aligned(16))) unsigned short Vs[NT * HD];
+    __shared__ __attribute__((aligned(16))) unsigned short dSt[NR * DST];  // dSᵀ: [key][query], keys >= 144 zero
     __shared__ __attribute__((aligned(16))) float lseS[NT], dltS[NT];
     __shared__ int tokS[NT];
+    __shared__ __attribute__((aligned(16))) unsigned short padS[3 * HD];  // pad-token q, k, v (bf16)
     __shared__ float tgS[EX ? TBL : 1];  // EX: this workgroup's rel-table gradient, flushed once
     const Chunk ck = decode_chunk(g, cw);
     const int h = ck.h;
     const float mneg100 = -100.0f / g.scale;  // the region mask in s' units
-    const long C3 = 3 * g.C;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int l16 = lane & 15, grp = lane >> 4;
-    for (int i = tid; i < (NR - NT) * RS; i += 576) {
-        Qs[NT * RS + i] = 0;
-        dOs[NT * RS + i] = 0;
-        Ks[NT * RS + i] = 0;
+    {  // the head's backward quads (16-B loads, both issued before either store)
+        const f32x4 *src = (const f32x4 *)quads + (long)h * QH + QF;
+        const f32x4 b0 = src[tid];
+        f32x4 b1 = {0.f, 0.f, 0.f, 0.f};
+        if (tid < QF - 576) b1 = src[576 + tid];
+        Bf[tid] = b0;
+        if (tid < QF - 576) Bf[576 + tid] = b1;
     }
-    for (int i = tid; i < (NR - NT) * DSR; i += 576) dSt[NT * DSR + i] = 0;
+    for (int i = tid; i < (NR - NT) * DST; i += 576) dSt[NT * DST + i] = 0;
     if (EX)
         for (int i = tid; i < TBL; i += 576) tgS[i] = 0.f;
-    {  // the head's bias quads, copies 4..7 (key on the lane), 16-B loads
-        const f32x4 *src = (const f32x4 *)quads + (long)h * 2 * QS + QS;
-        for (int i = tid; i < QS; i += 576) Bf[i] = src[i];
-    }
-    // key = 16 wave + l16 on the lane, queries 16 qt + 4 grp + r
-    const int kkey = wave * 16 + l16;
-    const int bk = 23 * (kkey / WS) + kkey % WS;  // bias table index = 264 + 23 * row(q) + col(q) - bk
-    unsigned long long hb = 0, wb = 0;  // query class bits (MM == 1)
-    if (MM == 1)
-#pragma unroll
-        for (int qt = 0; qt < 9; ++qt)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int q = qt * 16 + grp * 4 + r;
-                hb |= (unsigned long long)hi_row(g, q) << (qt * 4 + r);
-                wb |= (unsigned long long)hi_col(g, q) << (qt * 4 + r);
-            }
-    const bool k_hr = hi_row(g, kkey), k_hc = hi_col(g, kkey);
-    const int st_t = tid >> 2, st_ch = tid & 3;
-    u16x8 qreg, oreg, dreg, kreg, vreg;
-    __shared__ __attribute__((aligned(16))) unsigned short padS[3 * HD];  // pad-token q, k, v (bf16)
     if (tid < 3 * HD) padS[tid] = qbias ? f2bf(qbias[(tid / HD) * g.C + h * HD + tid % HD]) : (unsigned short)0;
-    __syncthreads();
+    // ---- lane constants.  Key kkey = 16 wave + l16 on the lane; queries 16 qt + 4 grp + r.
+    const int kkey = wave * 16 + l16;
+    const int swz_l = kv_swz(l16);
+    // bias quad of (kkey, q0 = 16 qt + 4 grp) at 28 (row(q0) - row(k) + 11) + (col(q0) - col(k) + 11);
+    // q0 + 48 is 4 rows further, so qt and qt + 3 differ by the constant 4 * 28 quads
+    const char *bbase = (const char *)Bf + (QF_STRIDE * 11 + 11 - (QF_STRIDE * (kkey / WS) + kkey % WS)) * 16;
+    int qpart[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        const int q0 = 16 * j + 4 * grp;
+        qpart[j] = (QF_STRIDE * (q0 / WS) + q0 % WS) * 16;
+    }
+    unsigned long long hb = 0, wb = 0;  // query class bits (MM == 1): the forward's key pattern
+    if (MM == 1) key_class_bits(g.shift, grp, hb, wb);
+    const bool k_hr = kkey >= WS * (WS - g.shift), k_hc = kkey % WS >= WS - g.shift;
+    // row-fragment bases (row 16 n + l16, chunk grp) and transposed-read bases (rows 4 grp + (l16 >> 2),
+    // 4 elements at 4 (l16 & 3) of d-half 0 / 1), as the forward's
+    const int rfrag = l16 * HD + (grp ^ swz_l) * 8;
+    const int vsw = kv_swz(4 * grp), vch = ((l16 & 3) >> 1), vin = (l16 & 1) * 4;
+    const int trow = (4 * grp + (l16 >> 2)) * HD;
+    const int tc0 = ((vch ^ vsw) * 8) + vin, tc1 = (((vch ^ 2) ^ vsw) * 8) + vin;
+    const int dsx = ds_swz(kkey);  // this lane's dS row placement
+    // phase 2: rows k0 + (l16 >> 2) and + 4 with k0 = 32 ks + 8 grp; dSᵀ columns 16 wave + 4 (l16 & 3)
+    const int p2c = wave * 16 + 4 * (l16 & 3);
+    const int p2r = 8 * grp + (l16 >> 2);
+    const int dsc0 = p2c ^ ds_swz(p2r), dsc1 = p2c ^ ds_swz(p2r + 4);
+    const int ksw0 = kv_swz(8 * grp), ksw1 = kv_swz(8 * grp + 4);
+    const int kc00 = ((vch ^ ksw0) * 8) + vin, kc01 = (((vch ^ 2) ^ ksw0) * 8) + vin;
+    const int kc10 = ((vch ^ ksw1) * 8) + vin, kc11 = (((vch ^ 2) ^ ksw1) * 8) + vin;
+    // staging: thread = (token tid / 4, chunk tid % 4)
+    const int st_t = tid >> 2, st_ch = tid & 3;
+    const int st_off = st_t * HD + (st_ch ^ kv_swz(st_t)) * 8;
+    const char *qkvb = (const char *)qkv;
+    const unsigned rowb = 6u * (unsigned)g.C, cb = 2u * (unsigned)g.C, orow = 2u * (unsigned)g.C;
+    const unsigned hcb = (unsigned)(h * HD + st_ch * 8) * 2u;
+    u16x8 qreg, oreg, dreg, kreg, vreg;
+    __syncthreads();  // padS, Bf
     float lreg = 0.f;
     int tok_next = -1;
     auto prefetch = [&](int bw) {
-        const int tok = token_of(g, bw, st_t);
+        const WinOrigin wo(g, bw);
+        const int tok = wo.tok(g, st_t);
         tok_next = tok;
-        qreg = load_frag_sel(qkv, *(const u16x8 *)(padS + st_ch * 8), tok, C3, h * HD + st_ch * 8);
-        kreg = load_frag_sel(qkv, *(const u16x8 *)(padS + HD + st_ch * 8), tok, C3, g.C + h * HD + st_ch * 8);
-        vreg = load_frag_sel(qkv, *(const u16x8 *)(padS + 2 * HD + st_ch * 8), tok, C3,
-                             2 * g.C + h * HD + st_ch * 8);
-        // branch-free: pad tokens read token 0 and are zeroed (cropped tokens carry no gradient)
-        const long so = (long)(tok >= 0 ? tok : 0) * g.C + h * HD + st_ch * 8;
-        const u16x8 dz = *(const u16x8 *)(gout + so), oz = *(const u16x8 *)(out + so);
-        const u16x8 zero = {0, 0, 0, 0, 0, 0, 0, 0};
-        dreg = tok >= 0 ? dz : zero;
-        oreg = tok >= 0 ? oz : zero;
+        const unsigned off = (unsigned)max(tok, 0) * rowb + hcb;
+        qreg = *(const u16x8 *)(qkvb + off);
+        kreg = *(const u16x8 *)(qkvb + off + cb);
+        vreg = *(const u16x8 *)(qkvb + off + 2 * cb);
+        // pad / cropped tokens read token 0 and are replaced (their dO and O by zero: no gradient)
+        const unsigned so = (unsigned)max(tok, 0) * orow + hcb;
+        dreg = *(const u16x8 *)((const char *)gout + so);
+        oreg = *(const u16x8 *)((const char *)out + so);
         if (tid < NT) lreg = lse[((long)bw * g.nH + h) * NT + tid];
     };
     if (ck.w_begin < ck.w_end) prefetch(ck.w_begin);
-    const int tr_row = (l16 >> 2), tr_col = 4 * (l16 & 3);
     for (int bw = ck.w_begin; bw < ck.w_end; ++bw) {
+        if (wave_any(tok_next < 0)) {  // uniform: only waves staging pad tokens
+            const u16x8 zero = {0, 0, 0, 0, 0, 0, 0, 0};
+            if (tok_next < 0) {
+                qreg = *(const u16x8 *)(padS + st_ch * 8);
+                kreg = *(const u16x8 *)(padS + HD + st_ch * 8);
+                vreg = *(const u16x8 *)(padS + 2 * HD + st_ch * 8);
+                dreg = zero;
+                oreg = zero;
+            }
+        }
         __syncthreads();
-        *(u16x8 *)(Qs + st_t * RS + st_ch * 8) = qreg;  // raw q: the scale is folded into c2, as forward
-        *(u16x8 *)(dOs + st_t * RS + st_ch * 8) = dreg;
-        *(u16x8 *)(Ks + st_t * RS + st_ch * 8) = kreg;
-        *(u16x8 *)(Vs + st_t * RS + st_ch * 8) = vreg;
+        *(u16x8 *)(Qs + st_off) = qreg;  // raw q: the scale is folded into c2, as forward
+        *(u16x8 *)(dOs + st_off) = dreg;
+        *(u16x8 *)(Ks + st_off) = kreg;
+        *(u16x8 *)(Vs + st_off) = vreg;
         {
             float part = 0.f;  // delta_q = dO_q · O_q, 4 lanes per token (stored negated)
 #pragma unroll
@@ -657,8 +693,8 @@ __global__ void __launch_bounds__(576) winattn_bwd_bf16(
             if (lastW) mbits |= k_hc ? ~wb : wb;
         }
         // ---------------- phase 1: key tile = wave (key on the lane)
-        const bf16x8_t kb = as_bf(*(const u16x8 *)(Ks + kkey * RS + grp * 8));
-        const bf16x8_t vb = as_bf(*(const u16x8 *)(Vs + kkey * RS + grp * 8));
+        const bf16x8_t kb = as_bf(*(const u16x8 *)(Ks + wave * 16 * HD + rfrag));
+        const bf16x8_t vb = as_bf(*(const u16x8 *)(Vs + wave * 16 * HD + rfrag));
         f32x4 dv0 = {0.f, 0.f, 0.f, 0.f}, dv1 = dv0, dk0 = dv0, dk1 = dv0;
         // two copies of the phase, picked by a uniform branch, so interior windows skip the mask test
         auto phase1 = [&](auto masked) {
@@ -677,18 +713,17 @@ __global__ void __launch_bounds__(576) winattn_bwd_bf16(
                     }
                     continue;
                 }
-                const bf16x8_t qa = as_bf(*(const u16x8 *)(Qs + (qt * 16 + l16) * RS + grp * 8));
-                const bf16x8_t da = as_bf(*(const u16x8 *)(dOs + (qt * 16 + l16) * RS + grp * 8));
+                const bf16x8_t qa = as_bf(*(const u16x8 *)(Qs + qt * 16 * HD + rfrag));
+                const bf16x8_t da = as_bf(*(const u16x8 *)(dOs + qt * 16 * HD + rfrag));
                 const f32x4 l4 = *(const f32x4 *)(lseS + qt * 16 + grp * 4);
                 const f32x4 nd4 = *(const f32x4 *)(dltS + qt * 16 + grp * 4);
-                const int q0 = qt * 16 + grp * 4, si = 264 + 23 * (q0 / WS) + q0 % WS - bk;
-                const f32x4 b4 = Bf[si];
-                const f32x4 sa = mfma16(qa, kb, b4);  // s'[q][key] = q·k + b / scale, as the forward's s'ᵀ
-                const f32x4 dpa = mfma16(da, vb, nd4);                       // dP[q][key] - delta_q
+                const f32x4 b4 = *(const f32x4 *)(bbase + qpart[qt % 3] + (qt / 3) * (4 * QF_STRIDE * 16));
+                const f32x4 sa = mfma16(qa, kb, b4);   // s'[q][key] = q·k + b / scale, as the forward's s'ᵀ
+                const f32x4 dpa = mfma16(da, vb, nd4);  // dP[q][key] - delta_q
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     float v = sa[r];
-                    if (MASKED) v += ((mbits >> (qt * 4 + r)) & 1ull) ? mneg100 : 0.0f;
+                    if (MASKED) v += mask_term(mbits, qt * 4 + r, mneg100);
                     if (MM == 2)
                         v = fmaf(mask[((long)(bw % g.n_mask) * NT + qt * 16 + grp * 4 + r) * NT + kkey], 1.0f / g.scale, v);
                     const float p = fast_exp2(fmaf(v, c2, -l4[r]));
@@ -698,16 +733,16 @@ __global__ void __launch_bounds__(576) winattn_bwd_bf16(
                     if (EX && gtable) atomicAdd(&tgS[rel_idx(qt * 16 + grp * 4 + r, kkey)], ds);  // LDS atomic
                 }
                 const u16x8 sbits = __builtin_bit_cast(u16x8, sb);
-                *(u16x4 *)(dSt + kkey * DSR + qt * 16 + grp * 4) =
+                *(u16x4 *)(dSt + kkey * DST + ((qt * 16 + grp * 4) ^ dsx)) =
                     u16x4{sbits[4 * half], sbits[4 * half + 1], sbits[4 * half + 2], sbits[4 * half + 3]};
             }
-            // dVᵀ += dOᵀ·P ; dKᵀ += Qᵀ·dS   (k = 32 queries; A via transposed LDS reads)
-            const int r0 = (32 * ks + 4 * grp + tr_row) * RS + tr_col;
-            const int r1 = r0 + 16 * RS;
-            const u16x8 ao0 = cat4(tr_read(dOs + r0), tr_read(dOs + r1));
-            const u16x8 ao1 = cat4(tr_read(dOs + r0 + 16), tr_read(dOs + r1 + 16));
-            const u16x8 aq0 = cat4(tr_read(Qs + r0), tr_read(Qs + r1));
-            const u16x8 aq1 = cat4(tr_read(Qs + r0 + 16), tr_read(Qs + r1 + 16));
+            // dVᵀ += dOᵀ·P ; dKᵀ += qᵀ·dS   (k = 32 queries; A via transposed LDS reads; queries
+            // 144..159 carry P = dS = 0, so ks = 4 re-reads rows 128..143 for them)
+            const int r0 = 32 * ks * HD + trow, r1 = ks < 4 ? r0 + 16 * HD : r0;
+            const u16x8 ao0 = cat4(tr_read(dOs + r0 + tc0), tr_read(dOs + r1 + tc0));
+            const u16x8 ao1 = cat4(tr_read(dOs + r0 + tc1), tr_read(dOs + r1 + tc1));
+            const u16x8 aq0 = cat4(tr_read(Qs + r0 + tc0), tr_read(Qs + r1 + tc0));
+            const u16x8 aq1 = cat4(tr_read(Qs + r0 + tc1), tr_read(Qs + r1 + tc1));
             dv0 = mfma16(as_bf(ao0), pb, dv0);
             dv1 = mfma16(as_bf(ao1), pb, dv1);
             dk0 = mfma16(as_bf(aq0), sb, dk0);
@@ -731,7 +766,7 @@ __global__ void __launch_bounds__(576) winattn_bwd_bf16(
                     v0[r] = f2bf(dv0[r]);
                     v1[r] = f2bf(dv1[r]);
                 }
-                unsigned short *gp = gqkv + (long)tk * C3;
+                unsigned short *gp = gqkv + (long)tk * 3 * g.C;
                 *(u16x4 *)(gp + g.C + c0) = k0;
                 *(u16x4 *)(gp + g.C + c0 + 16) = k1;
                 *(u16x4 *)(gp + 2 * g.C + c0) = v0;
@@ -747,19 +782,19 @@ __global__ void __launch_bounds__(576) winattn_bwd_bf16(
             }
         }
         __syncthreads();
-        // ---------------- phase 2: dQᵀ = Kᵀ·dSᵀ for query tile = wave
+        // ---------------- phase 2: dQᵀ = Kᵀ·dSᵀ for query tile = wave (keys >= 144: dSᵀ rows are zero,
+        // K rows 32 lower are read in their place)
         {
             const int qq = wave * 16 + l16;
             f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0;
 #pragma unroll
             for (int ks = 0; ks < 5; ++ks) {
-                const int k0 = 32 * ks + 8 * grp;
-                const int d0 = (k0 + tr_row) * DSR + wave * 16 + tr_col;
-                const u16x8 bs = cat4(tr_read(dSt + d0), tr_read(dSt + d0 + 4 * DSR));
-                const int r0 = (k0 + tr_row) * RS + tr_col;
-                const int r1 = r0 + 4 * RS;
-                const u16x8 ak0 = cat4(tr_read(Ks + r0), tr_read(Ks + r1));
-                const u16x8 ak1 = cat4(tr_read(Ks + r0 + 16), tr_read(Ks + r1 + 16));
+                const int kr0 = 32 * ks + p2r, kr1 = kr0 + 4;
+                const u16x8 bs = cat4(tr_read(dSt + kr0 * DST + dsc0), tr_read(dSt + kr1 * DST + dsc1));
+                const int kk0 = (ks == 4 && kr0 >= NT) ? kr0 - 32 : kr0;
+                const int kk1 = (ks == 4 && kr1 >= NT) ? kr1 - 32 : kr1;
+                const u16x8 ak0 = cat4(tr_read(Ks + kk0 * HD + kc00), tr_read(Ks + kk1 * HD + kc10));
+                const u16x8 ak1 = cat4(tr_read(Ks + kk0 * HD + kc01), tr_read(Ks + kk1 * HD + kc11));
                 a0 = mfma16(as_bf(ak0), as_bf(bs), a0);
                 a1 = mfma16(as_bf(ak1), as_bf(bs), a1);
             }
@@ -772,8 +807,8 @@ __global__ void __launch_bounds__(576) winattn_bwd_bf16(
                     w0[r] = f2bf(a0[r] * g.scale);
                     w1[r] = f2bf(a1[r] * g.scale);
                 }
-                *(u16x4 *)(gqkv + (long)qtok * C3 + c0) = w0;
-                *(u16x4 *)(gqkv + (long)qtok * C3 + c0 + 16) = w1;
+                *(u16x4 *)(gqkv + (long)qtok * 3 * g.C + c0) = w0;
+                *(u16x4 *)(gqkv + (long)qtok * 3 * g.C + c0 + 16) = w1;
             } else if (EX && gbias) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
@@ -827,12 +862,12 @@ using namespace irads;
 extern "C" int irads_winattn_bias_quads(const float *rel_table, int nH, float scale, float *quads, void *stream) {
     IRADS_REQUIRE(rel_table && quads && nH > 0, "irads_winattn_bias_quads: null pointer / nH=%d", nH);
     IRADS_REQUIRE(scale > 0.f, "irads_winattn_bias_quads: scale must be positive (%g)", scale);
-    const int n = nH * 2 * QS * 4;
+    const int n = nH * QH * 4;
     winattn_bias_quads_kernel<<<(n + 255) / 256, 256, 0, (hipStream_t)stream>>>(rel_table, nH, 1.0f / scale, quads);
     return check_launch("irads_winattn_bias_quads");
 }
 
-extern "C" long irads_winattn_bias_quads_size(int nH) { return (long)nH * 2 * QS * 4; }
+extern "C" long irads_winattn_bias_quads_size(int nH) { return (long)nH * QH * 4; }
 
 extern "C" int irads_winattn_fwd(int dtype, const void *qkv, const float *qkv_bias, const float *rel_table,
                                  const float *bias_quads, const float *mask, int n_mask, int B, int H, int W, int C, int nH, int shift,

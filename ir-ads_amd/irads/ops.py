@@ -20,15 +20,23 @@ class LaunchTimer:
     """Brackets selected kernel launches with HIP events on the launch stream (the
     current torch stream, which is where every irads kernel is enqueued).  bench.py
     enables it over its timed region to report per-launch durations of the dominant
-    kernel; disabled it costs one attribute check per launch."""
+    kernel; disabled it costs one attribute check per launch.
+
+    lead_cycles > 0 enqueues a GPU spin of that many cycles before the start event, so the stream
+    is still busy when the host enqueues the launch: the event pair then brackets the kernel alone
+    (no host-side enqueue latency inside the interval), which is what rocprofv3's kernel trace
+    reports for the same launch."""
 
     def __init__(self):
         self.enabled = set()
         self.records = []  # (name, start_event, end_event, algorithmic_bytes, flops, real_token_bytes)
+        self.lead_cycles = 0
 
     def start(self, name):
         if name not in self.enabled:
             return None
+        if self.lead_cycles:
+            torch.cuda._sleep(self.lead_cycles)
         ev = torch.cuda.Event(enable_timing=True)
         ev.record()
         return ev

@@ -89,18 +89,24 @@ SQ_COUNTERS = ("SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_I
                "SQ_ACTIVE_INST_LDS", "SQ_VALU_MFMA_BUSY_CYCLES", "SQ_BUSY_CYCLES")
 
 
-def parse_sq(dir_sq):
+def parse_sq(dir_sq, *counters):
     """Wave-state breakdown of the 24 launches (one SQ pass, 8 counters): SQ_WAIT_ANY =
     parked at s_waitcnt / barrier, SQ_WAIT_INST_ANY = issue-stalled, SQ_ACTIVE_INST_ANY =
     issuing; the three are disjoint and sum to SQ_WAVE_CYCLES (MI355X_MICROARCH.md, PMC
     slots).  The wave counters are in quad-cycles, SQ_VALU_MFMA_BUSY_CYCLES in cycles."""
-    tot = {c: sum(_values(dir_sq, c)) for c in SQ_COUNTERS}
-    w = tot["SQ_WAVE_CYCLES"]
+    names = counters or SQ_COUNTERS
+    vals = {c: _values(dir_sq, c) for c in names}
+    tot = {c: sum(v) for c, v in vals.items()}
     out = {"kernel": "irads_winattn_fwd (bf16)", "launches": 24,
            "per_launch": {c: round(v / 24) for c, v in tot.items()},
-           "fraction_of_wave_cycles": {c: round(tot[c] / w, 3) for c in SQ_COUNTERS[1:6]},
-           "source": "rocprofv3 --pmc " + " ".join(SQ_COUNTERS) + " --kernel-trace, "
+           # dispatch order: stage 0 x2, stage 1 x2, stage 2 x18, stage 3 x2 (shift 0 / 6 alternating)
+           "per_stage_sum": {c: [round(sum(v[a:b])) for a, b in ((0, 2), (2, 4), (4, 22), (22, 24))]
+                             for c, v in vals.items()},
+           "source": "rocprofv3 --pmc " + " ".join(names) + " --kernel-trace, "
                      "scripts/pmc_winattn.py run (the 24 launches of one bench step)"}
+    if "SQ_WAVE_CYCLES" in tot:
+        w = tot["SQ_WAVE_CYCLES"]
+        out["fraction_of_wave_cycles"] = {c: round(tot[c] / w, 3) for c in SQ_COUNTERS[1:6] if c in tot}
     print(json.dumps(out, indent=1))
 
 
@@ -108,6 +114,6 @@ if __name__ == "__main__":
     if sys.argv[1] == "run":
         run()
     elif sys.argv[1] == "parse_sq":
-        parse_sq(sys.argv[2])
+        parse_sq(sys.argv[2], *sys.argv[3:])
     else:
         parse(sys.argv[2], sys.argv[3])

@@ -14,3 +14,8 @@ rm -rf gpurun_out/pmc_sq
 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES --kernel-trace --output-format csv -d $R/gpurun_out/pmc_sq -o run -- python3 $R/scripts/pmc_winattn.py run > gpurun_out/pmc_sq.log 2>&1 || { echo "sq pass failed"; tail gpurun_out/pmc_sq.log; exit 1; }
 python3 scripts/pmc_winattn.py parse_sq gpurun_out/pmc_sq > gpurun_out/pmc_winattn_fwd_sq.json && cat gpurun_out/pmc_winattn_fwd_sq.json
 find gpurun_out/pmc_sq -name '*kernel_trace.csv' -delete
+# LDS bank-conflict / instruction-count pass
+rm -rf gpurun_out/pmc_lds
+timeout -s KILL 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU SQ_WAVES --kernel-trace --output-format csv -d $R/gpurun_out/pmc_lds -o run -- python3 $R/scripts/pmc_winattn.py run > gpurun_out/pmc_lds.log 2>&1 || { echo "lds pass failed"; tail gpurun_out/pmc_lds.log; exit 1; }
+python3 scripts/pmc_winattn.py parse_sq gpurun_out/pmc_lds SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU SQ_WAVES > gpurun_out/pmc_winattn_fwd_lds.json && cat gpurun_out/pmc_winattn_fwd_lds.json
+find gpurun_out/pmc_lds -name '*kernel_trace.csv' -delete
