@@ -173,7 +173,6 @@ def msda_inputs(device, bs=2, Q=None, seed=0):
 TIMED_KERNELS = ("winattn_fwd", "winattn_bwd", "dattn_fwd", "dattn_bwd")
 FP32_PEAK_TFLOPS = 157.3  # MI355X fp32 vector peak (MI355X_MICROARCH.md)
 GATHER_PEAK_GBS = 18800.0  # L2-resident random-row gather rate (upper end), MI355X_MICROARCH.md
-ATOMIC_PEAK_GBS = 1300.0  # chip-wide f32 atomic-add rate, MI355X_MICROARCH.md 'Global float atomics'
 
 
 def msda_rooflines(device, reps=20):
@@ -190,15 +189,17 @@ def msda_rooflines(device, reps=20):
         bwd_b = 4 * bs * (2 * S * M * D + 2 * Qn * M * L * P * 3 + Qn * M * D)
         o = ops.MSDAFn.apply(value, shapes, lsi, loc, aw, 64)
         go = torch.randn_like(o)
-        gv, gl, ga = torch.zeros_like(value), torch.empty_like(loc), torch.empty_like(aw)
+        gv, gl, ga = torch.empty_like(value), torch.empty_like(loc), torch.empty_like(aw)
+        ws_bytes = ops.msda_gather_workspace_bytes(value, go, loc)
+        ws = torch.empty((ws_bytes,), device=device, dtype=torch.uint8)
 
         def fwd():
             ops.MSDAFn.apply(value, shapes, lsi, loc, aw, 64)
 
-        def bwd():
-            gv.zero_()
-            N.call("irads_msda_bwd", N.F32, N.ptr(value), N.ptr(shapes), N.ptr(lsi), N.ptr(loc), N.ptr(aw),
-                   N.ptr(go), bs, S, M, D, L, Qn, P, N.ptr(gv), N.ptr(gl), N.ptr(ga), N.stream())
+        def bwd():  # the product's fp32 backward (MSDAFn.backward): bucket + gather, no float atomics
+            N.call("irads_msda_bwd_gather", N.ptr(value), N.ptr(shapes), N.ptr(lsi), N.ptr(loc), N.ptr(aw),
+                   N.ptr(go), bs, S, M, D, L, Qn, P, N.ptr(gv), N.ptr(gl), N.ptr(ga), N.ptr(ws), ws_bytes,
+                   N.stream())
         for fn, tag, nbytes in ((fwd, "fwd", fwd_b), (bwd, "bwd", bwd_b)):
             for _ in range(3):
                 fn()
@@ -214,24 +215,20 @@ def msda_rooflines(device, reps=20):
             out[f"msda_{tag}_{name}"] = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
                                          "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
                                          "avg_launch_ms": round(ms, 4), "algorithmic_bytes_per_launch": nbytes,
-                                         "shape": f"bs={bs} Q={Qn} S={S} M={M} D={D} L={L} P={P} fp32"
-                                                  + (" (incl. grad_value zero-fill)" if tag == "bwd" else "")}
-            # The sampling itself moves 4 corners x D floats per sample: gathered (fwd, mostly
-            # L2 / Infinity-Cache hits) and, in bwd, also atomically added into grad_value.
-            # Float atomics run at ~1.3 TB/s of added bytes chip-wide (MI355X_MICROARCH.md
-            # "Global float atomics"), which is the bound of the reference's scatter backward.
-            samp_b = 4 * D * 4 * bs * Qn * M * L * P
+                                         "shape": f"bs={bs} Q={Qn} S={S} M={M} D={D} L={L} P={P} fp32"}
+            # The sampling itself moves 4 corners x D floats per sample through L2 / Infinity Cache:
+            # forward = the value corners; backward = the value corners again (grad_loc / grad_aw)
+            # plus the grad_out row once per corner in the grad_value gather (the reference adds the
+            # same bytes with float atomics instead, ~1.3 TB/s chip-wide).
+            samp_b = 4 * D * 4 * bs * Qn * M * L * P * (2 if tag == "bwd" else 1)
             ent = out[f"msda_{tag}_{name}"]
             ent["gathered_bytes_per_launch"] = samp_b
             ent["gather_rate_gbs"] = round(samp_b / (ms * 1e-3) / 1e9, 1)
-            if tag == "fwd":  # ceiling: L2-resident random-row gathers, 16.8-18.8 TB/s (MI355X_MICROARCH.md)
-                ent["gather_peak_gbs"] = GATHER_PEAK_GBS
-                ent["gather_frac"] = round(samp_b / (ms * 1e-3) / 1e9 / GATHER_PEAK_GBS, 4)
+            # ceiling: L2-resident random-row gathers, 16.8-18.8 TB/s (MI355X_MICROARCH.md)
+            ent["gather_peak_gbs"] = GATHER_PEAK_GBS
+            ent["gather_frac"] = round(samp_b / (ms * 1e-3) / 1e9 / GATHER_PEAK_GBS, 4)
             if tag == "bwd":
-                ent["atomic_bytes_per_launch"] = samp_b
-                ent["atomic_rate_gbs"] = ent["gather_rate_gbs"]
-                ent["atomic_peak_gbs"] = ATOMIC_PEAK_GBS
-                ent["atomic_frac"] = round(samp_b / (ms * 1e-3) / 1e9 / ATOMIC_PEAK_GBS, 4)
+                ent["kernel"] = "irads_msda_bwd_gather (bucket count/scan/fill + grad_value gather + grad_loc/aw)"
     return out
 
 

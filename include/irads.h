@@ -53,6 +53,18 @@ int irads_msda_fwd(int dtype, const void *value, const int64_t *shapes, const in
 int irads_msda_bwd(int dtype, const void *value, const int64_t *shapes, const int64_t *level_start,
                    const void *loc, const void *aw, const void *grad_out, int bs, int S, int M, int D,
                    int L, int Q, int P, void *grad_value, void *grad_loc, void *grad_aw, void *stream);
+/* Atomic-free fp32 backward (same contract as irads_msda_bwd for float32, same reference
+ * interface ms_deform_attn_cuda.cu:84-154): samples are bucketed by their top-left corner cell
+ * (int atomics on bs*M*S counters) and every grad_value row is GATHERED from the samples that
+ * touch it and written once -- grad_value need NOT be zero-filled.  Served for D % 4 == 0 with
+ * D/4 a power of two <= 64 and 16-B aligned value / grad_out / grad_value / workspace;
+ * irads_msda_bwd_workspace_bytes returns the caller-allocated workspace size, or 0 when the
+ * shape is not served (use irads_msda_bwd then). */
+long irads_msda_bwd_workspace_bytes(int dtype, int bs, int S, int M, int D, int L, int Q, int P);
+int irads_msda_bwd_gather(const float *value, const int64_t *shapes, const int64_t *level_start,
+                          const float *loc, const float *aw, const float *grad_out, int bs, int S, int M,
+                          int D, int L, int Q, int P, float *grad_value, float *grad_loc, float *grad_aw,
+                          void *workspace, long workspace_bytes, void *stream);
 /* Debug export: the integer corners (x0, y0) per sample, (bs, Q, M, L, P, 2) int32. */
 int irads_msda_corner_index(int dtype, const void *loc, const int64_t *shapes, int bs, int Q, int M,
                             int L, int P, int32_t *corners, void *stream);

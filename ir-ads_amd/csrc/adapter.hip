@@ -62,25 +62,32 @@ __global__ __launch_bounds__(256) void adapter_down_kernel(
     const bool hi = row0 >= Mh;
     const u16 *w = hi ? w1 : w0;
     const int nch = C / 32;
-    bf16x8_t af[CH], wf[CH][NT];
-#pragma unroll
-    for (int c = 0; c < CH; ++c) {
-        const int kc = wave + 4 * c;
-        const bool ok = kc < nch;
-        af[c] = ld8<true>(a + (row0 + li) * C + kc * 32 + 8 * lg, ok ? 8 : 0);
-#pragma unroll
-        for (int n = 0; n < NT; ++n) {
-            const int col = n * 16 + li;
-            wf[c][n] = ld8<true>(w + (long)(col < R ? col : 0) * C + kc * 32 + 8 * lg, ok && col < R ? 8 : 0);
-        }
-    }
+    // operands of GC chunks are loaded before their MFMAs: all CH at once when the fragments fit
+    // the register file (CH (NT + 1) 4 <= 160 VGPRs), else in rounds (wide C with wide R would
+    // otherwise spill the fragment arrays to scratch)
+    constexpr int GC = CH * (NT + 1) * 4 <= 160 ? CH : (40 / (NT + 1) >= 4 ? 4 : (40 / (NT + 1) >= 2 ? 2 : 1));
     f32x4 acc[NT];
 #pragma unroll
     for (int n = 0; n < NT; ++n) acc[n] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int c = 0; c < CH; ++c)
+    for (int c0 = 0; c0 < CH; c0 += GC) {
+        bf16x8_t af[GC], wf[GC][NT];
 #pragma unroll
-        for (int n = 0; n < NT; ++n) acc[n] = mfma16(af[c], wf[c][n], acc[n]);
+        for (int c = 0; c < GC; ++c) {
+            const int kc = wave + 4 * (c0 + c);
+            const bool ok = kc < nch;
+            af[c] = ld8<true>(a + (row0 + li) * C + kc * 32 + 8 * lg, ok ? 8 : 0);
+#pragma unroll
+            for (int n = 0; n < NT; ++n) {
+                const int col = n * 16 + li;
+                wf[c][n] = ld8<true>(w + (long)(col < R ? col : 0) * C + kc * 32 + 8 * lg, ok && col < R ? 8 : 0);
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < GC; ++c)
+#pragma unroll
+            for (int n = 0; n < NT; ++n) acc[n] = mfma16(af[c], wf[c][n], acc[n]);
+    }
 #pragma unroll
     for (int n = 0; n < NT; ++n) red[wave][n][lane] = acc[n];
     __syncthreads();

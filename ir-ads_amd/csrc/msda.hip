@@ -273,6 +273,336 @@ __global__ void __launch_bounds__(256) msda_bwd_kernel(const T *__restrict__ val
     }
 }
 
+// ------------------------------------------------------------------ atomic-free fp32 backward
+// The reference's col2im adds every sample's 4 corner contributions into grad_value with float
+// atomics (ms_deform_im2col_cuda.cuh:301-921); at the DINO encoder shape that is 2.9 GB of atomic
+// adds per launch, held at the chip-wide float-atomic rate.  Here grad_value is GATHERED instead:
+//   1. count / scan / fill: samples are bucketed by (b, m, top-left corner cell) -- the corner
+//      clamped into the level, so a sample whose x0 or y0 is -1 sits in the cell of its one valid
+//      corner column / row; samples with no valid corner are dropped -- with int atomics on
+//      bs·M·S counters (one per sample, not per channel);
+//   2. gather: one group of V = D/4 lanes per (b, s, m) value cell walks the buckets of its own
+//      cell and of its left, upper and upper-left neighbours, recomputes each sample's corners
+//      with the forward's arithmetic (bit-identical corners), keeps the corner that is this cell
+//      and adds w_corner · (grad_out · attn) -- the reference's per-contribution rounding -- into
+//      registers; the row is written once (no zero-fill, no float atomics);
+//   3. grad_loc / grad_aw: the forward's 16-B gather per (b, q, m) group, channel partial sums
+//      reduced over the group's lanes by shuffles, stored once per sample.
+// The bucket order within a cell follows the fill's int atomics, so the summation order of a
+// grad_value row varies run to run, as the reference's float atomics do.
+__device__ __forceinline__ int level_of(int s, const int *sS, int L) {
+    int l = 0;
+    for (int k = 1; k < L; ++k) l = s >= sS[k] ? k : l;
+    return l;
+}
+
+// bucket of one sample, or -1 (no corner inside the level)
+__device__ __forceinline__ long sample_bucket(const float *loc, long sid, int l, const int *sH, const int *sW,
+                                              const int *sS, int b, int m, int M, int S) {
+    const int H = sH[l], W = sW[l];
+    const Samp<float> sp = locate(loc[2 * sid], loc[2 * sid + 1], H, W);
+    if (sp.x0 < -1 || sp.x0 >= W || sp.y0 < -1 || sp.y0 >= H) return -1;
+    const int x = max(sp.x0, 0), y = max(sp.y0, 0);
+    return ((long)b * M + m) * S + sS[l] + y * W + x;
+}
+
+__device__ __forceinline__ void load_levels(const int64_t *shapes, const int64_t *lsi, int L, int *sH, int *sW,
+                                            int *sS) {
+    if (threadIdx.x < L) {
+        sH[threadIdx.x] = (int)shapes[2 * threadIdx.x];
+        sW[threadIdx.x] = (int)shapes[2 * threadIdx.x + 1];
+        sS[threadIdx.x] = (int)lsi[threadIdx.x];
+    }
+    __syncthreads();
+}
+
+__global__ void __launch_bounds__(256) msda_bucket_count(const float *__restrict__ loc, const int64_t *__restrict__ shapes,
+                                                         const int64_t *__restrict__ lsi, int bs, int S, int M, int L,
+                                                         int Q, int P, int *__restrict__ cnt) {
+    __shared__ int sH[kMaxLevels], sW[kMaxLevels], sS[kMaxLevels];
+    load_levels(shapes, lsi, L, sH, sW, sS);
+    const long sid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    const int LP = L * P;
+    if (sid >= (long)bs * Q * M * LP) return;
+    const int l = (int)(sid % LP) / P;
+    const int m = (int)((sid / LP) % M);
+    const int b = (int)(sid / ((long)LP * M * Q));
+    const long bk = sample_bucket(loc, sid, l, sH, sW, sS, b, m, M, S);
+    if (bk >= 0) atomicAdd(cnt + bk, 1);
+}
+
+// exclusive scan of cnt (n entries) in blocks of 1024: per-block scan + block totals
+__global__ void __launch_bounds__(256) msda_scan_blocks(const int *__restrict__ cnt, long n, int *__restrict__ off,
+                                                        int *__restrict__ block_sum) {
+    __shared__ int wsum[4];
+    const long base = (long)blockIdx.x * 1024 + 4 * threadIdx.x;
+    int v[4], t = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        v[j] = base + j < n ? cnt[base + j] : 0;
+        t += v[j];
+    }
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    int inc = t;  // inclusive wave scan of the per-thread totals
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += y;
+    }
+    if (lane == 63) wsum[wave] = inc;
+    __syncthreads();
+    int wofs = 0;
+    for (int w = 0; w < wave; ++w) wofs += wsum[w];
+    int run = wofs + inc - t;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        if (base + j < n) off[base + j] = run;
+        run += v[j];
+    }
+    if (threadIdx.x == 255) block_sum[blockIdx.x] = wofs + inc;
+}
+
+// one block: exclusive scan of the block totals in place (nb <= 256 * 64)
+__global__ void __launch_bounds__(256) msda_scan_totals(int *__restrict__ block_sum, int nb, int *__restrict__ total) {
+    __shared__ int wsum[4];
+    __shared__ int carry;
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (int c0 = 0; c0 < nb; c0 += 256) {
+        const int i = c0 + threadIdx.x;
+        const int t = i < nb ? block_sum[i] : 0;
+        int inc = t;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(inc, o, 64);
+            if (lane >= o) inc += y;
+        }
+        if (lane == 63) wsum[wave] = inc;
+        __syncthreads();
+        int wofs = carry;
+        for (int w = 0; w < wave; ++w) wofs += wsum[w];
+        if (i < nb) block_sum[i] = wofs + inc - t;
+        __syncthreads();
+        if (threadIdx.x == 255) carry = wofs + inc;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *total = carry;
+}
+
+// add the block offsets; the counters become the fill cursors (zeroed)
+__global__ void __launch_bounds__(256) msda_scan_add(int *__restrict__ off, long n, const int *__restrict__ block_sum,
+                                                     const int *__restrict__ total, int *__restrict__ cnt) {
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        off[i] += block_sum[i / 1024];
+        cnt[i] = 0;
+    }
+    if (i == 0) off[n] = *total;
+}
+
+__global__ void __launch_bounds__(256) msda_bucket_fill(const float *__restrict__ loc, const int64_t *__restrict__ shapes,
+                                                        const int64_t *__restrict__ lsi, int bs, int S, int M, int L,
+                                                        int Q, int P, const int *__restrict__ off,
+                                                        int *__restrict__ cursor, int *__restrict__ ids) {
+    __shared__ int sH[kMaxLevels], sW[kMaxLevels], sS[kMaxLevels];
+    load_levels(shapes, lsi, L, sH, sW, sS);
+    const long sid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    const int LP = L * P;
+    if (sid >= (long)bs * Q * M * LP) return;
+    const int l = (int)(sid % LP) / P;
+    const int m = (int)((sid / LP) % M);
+    const int b = (int)(sid / ((long)LP * M * Q));
+    const long bk = sample_bucket(loc, sid, l, sH, sW, sS, b, m, M, S);
+    if (bk >= 0) ids[off[bk] + atomicAdd(cursor + bk, 1)] = (int)sid;
+}
+
+// grad_value rows: V lanes (4 channels each) per (b, s, m) cell
+template <int V>
+__global__ void __launch_bounds__(256) msda_gather_gvalue(const int64_t *__restrict__ shapes,
+                                                          const int64_t *__restrict__ lsi, const float *__restrict__ loc,
+                                                          const float *__restrict__ aw, const float *__restrict__ gout,
+                                                          int bs, int S, int M, int D, int L, int Q, int P,
+                                                          const int *__restrict__ off, const int *__restrict__ ids,
+                                                          float *__restrict__ gvalue) {
+    __shared__ int sH[kMaxLevels], sW[kMaxLevels], sS[kMaxLevels];
+    load_levels(shapes, lsi, L, sH, sW, sS);
+    const long gid = ((long)blockIdx.x * blockDim.x + threadIdx.x) / V;  // = (b * S + s) * M + m
+    const int lane = threadIdx.x % V;
+    if (gid >= (long)bs * S * M) return;  // whole group exits together
+    const int m = (int)(gid % M);
+    const int s = (int)((gid / M) % S);
+    const int b = (int)(gid / ((long)M * S));
+    const int l = level_of(s, sS, L);
+    const int H = sH[l], W = sW[l];
+    const int c = s - sS[l], y = c / W, x = c - y * W;
+    const int LP = L * P;
+    const long bkb = ((long)b * M + m) * S;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb) {  // buckets of cells (y, x), (y, x-1), (y-1, x), (y-1, x-1)
+        const int by = y - (nb >> 1), bx = x - (nb & 1);
+        if (by < 0 || bx < 0) continue;  // uniform over the group
+        const long bk = bkb + sS[l] + by * W + bx;
+        const int e0 = off[bk], e1 = off[bk + 1];
+        for (int e = e0; e < e1; e += V) {
+            // lane j takes entry e + j: its sample's corner weight for this cell and its attention weight
+            float wc = 0.f, a = 0.f;
+            int q = 0;
+            if (e + lane < e1) {
+                const long sid = ids[e + lane];
+                const Samp<float> sp = locate(loc[2 * sid], loc[2 * sid + 1], H, W);
+                const int dy = y - sp.y0, dx = x - sp.x0;
+                if ((unsigned)dy <= 1u && (unsigned)dx <= 1u)
+                    wc = dy == 0 ? (dx == 0 ? sp.nw : sp.ne) : (dx == 0 ? sp.sw : sp.se);
+                a = aw[sid];
+                q = (int)((sid / ((long)LP * M)) % Q);
+            }
+            // chunks of up to 8 entries: every grad_out row load of the chunk is issued before the first
+            // accumulation (lanes past the bucket end and non-corner entries carry w = 0 and load nothing)
+            constexpr int KC = V < 8 ? V : 8;
+#pragma unroll
+            for (int k0 = 0; k0 < V; k0 += KC) {
+                float w[KC], ak[KC];
+                float4 go[KC];
+#pragma unroll
+                for (int k = 0; k < KC; ++k) {
+                    w[k] = __shfl(wc, k0 + k, V);
+                    ak[k] = __shfl(a, k0 + k, V);
+                    const int qk = __shfl(q, k0 + k, V);
+                    go[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+                    if (w[k] != 0.f) go[k] = *(const float4 *)(gout + (((long)b * Q + qk) * M + m) * D + 4 * lane);
+                }
+#pragma unroll
+                for (int k = 0; k < KC; ++k) {
+                    if (w[k] == 0.f) continue;  // not a corner of this cell: no contribution (as the reference)
+                    // the reference's contribution corner_w * (grad_out * attn), rounded as its atomicAdd operand
+                    acc.x += w[k] * (go[k].x * ak[k]);
+                    acc.y += w[k] * (go[k].y * ak[k]);
+                    acc.z += w[k] * (go[k].z * ak[k]);
+                    acc.w += w[k] * (go[k].w * ak[k]);
+                }
+                if (e + k0 + KC >= e1) break;  // uniform
+            }
+        }
+    }
+    *(float4 *)(gvalue + gid * D + 4 * lane) = acc;
+}
+
+// grad_loc / grad_aw: the forward's 16-B gathers, V lanes per (b, q, m)
+template <int V>
+__global__ void __launch_bounds__(256) msda_bwd_locaw_vec(const float *__restrict__ value,
+                                                          const int64_t *__restrict__ shapes,
+                                                          const int64_t *__restrict__ lsi, const float *__restrict__ loc,
+                                                          const float *__restrict__ aw, const float *__restrict__ gout,
+                                                          int bs, int S, int M, int D, int L, int Q, int P,
+                                                          float *__restrict__ gloc, float *__restrict__ gaw) {
+    __shared__ int sH[kMaxLevels], sW[kMaxLevels], sS[kMaxLevels];
+    load_levels(shapes, lsi, L, sH, sW, sS);
+    const long blk = xcd_block(blockIdx.x, gridDim.x);
+    const long gid = (blk * blockDim.x + threadIdx.x) / V;
+    const int lane = threadIdx.x % V;
+    if (gid >= (long)bs * Q * M) return;
+    const int m = (int)(gid % M);
+    const int b = (int)(gid / ((long)M * Q));
+    const int LP = L * P;
+    const long cs = (long)M * D;
+    const float *vb = value + (long)b * S * cs + (long)m * D + 4 * lane;
+    const float4 go = *(const float4 *)(gout + gid * D + 4 * lane);
+    for (int s0 = 0; s0 < LP; s0 += V) {
+        const int sl = s0 + lane;
+        float lx = 0.f, ly = 0.f, w = 0.f;
+        if (sl < LP) {
+            const long li = gid * LP + sl;
+            lx = loc[2 * li];
+            ly = loc[2 * li + 1];
+            w = aw[li];
+        }
+        float my_gaw = 0.f, my_gx = 0.f, my_gy = 0.f;
+#pragma unroll
+        for (int k = 0; k < V; ++k) {
+            const float xk = __shfl(lx, k, V), yk = __shfl(ly, k, V), a = __shfl(w, k, V);
+            if (s0 + k < LP) {  // uniform over the group
+            const int l = (s0 + k) / P;
+            const int H = sH[l], W = sW[l];
+            const Samp<float> sp = locate(xk, yk, H, W);
+            const float *v = vb + (long)sS[l] * cs;
+            const long rs = (long)W * cs;
+            const bool xl = sp.x0 >= 0 && sp.x0 < W, xh = sp.x0 + 1 >= 0 && sp.x0 + 1 < W;
+            const bool yl = sp.y0 >= 0 && sp.y0 < H, yh = sp.y0 + 1 >= 0 && sp.y0 + 1 < H;
+            const float *r0 = v + sp.y0 * rs, *r1 = r0 + rs;
+            float4 v_nw = make_float4(0.f, 0.f, 0.f, 0.f), v_ne = v_nw, v_sw = v_nw, v_se = v_nw;
+            if (yl && xl) v_nw = *(const float4 *)(r0 + sp.x0 * cs);
+            if (yl && xh) v_ne = *(const float4 *)(r0 + (sp.x0 + 1) * cs);
+            if (yh && xl) v_sw = *(const float4 *)(r1 + sp.x0 * cs);
+            if (yh && xh) v_se = *(const float4 *)(r1 + (sp.x0 + 1) * cs);
+            float p_aw = 0.f, p_ix = 0.f, p_iy = 0.f;
+#define IRADS_MSDA_BCH(c)                                                            \
+    {                                                                                \
+        float val = v_nw.c * sp.nw;                                                  \
+        val = fmaf(v_ne.c, sp.ne, val);                                              \
+        val = fmaf(v_sw.c, sp.sw, val);                                              \
+        val = fmaf(v_se.c, sp.se, val);                                              \
+        p_aw += go.c * val;                                                          \
+        const float ga = go.c * a;                                                   \
+        p_ix += ga * ((v_ne.c - v_nw.c) * (1.f - sp.fy) + (v_se.c - v_sw.c) * sp.fy); \
+        p_iy += ga * ((v_sw.c - v_nw.c) * (1.f - sp.fx) + (v_se.c - v_ne.c) * sp.fx); \
+    }
+            IRADS_MSDA_BCH(x) IRADS_MSDA_BCH(y) IRADS_MSDA_BCH(z) IRADS_MSDA_BCH(w)
+#undef IRADS_MSDA_BCH
+            p_aw = group_sum<float, V>(p_aw);
+            p_ix = group_sum<float, V>(p_ix);
+            p_iy = group_sum<float, V>(p_iy);
+            if (lane == k) {
+                my_gaw = p_aw;
+                my_gx = p_ix * (float)W;
+                my_gy = p_iy * (float)H;
+            }
+            }
+        }
+        if (sl < LP) {
+            const long li = gid * LP + sl;
+            gaw[li] = my_gaw;
+            gloc[2 * li] = my_gx;
+            gloc[2 * li + 1] = my_gy;
+        }
+    }
+}
+
+struct GatherWs {
+    int *cnt, *off, *bsum, *total, *ids;
+    long nb, n, nblk;
+};
+
+// workspace carve-up (256-B aligned pieces); bytes == 0 when the gather path does not apply
+long gather_ws_layout(int bs, int S, int M, int D, int L, int Q, int P, char *base, GatherWs *ws) {
+    const int V = D / 4;
+    if (D % 4 != 0 || V > 64 || (V & (V - 1)) != 0) return 0;
+    const long nb = (long)bs * M * S, n = (long)bs * Q * M * L * P;
+    if (n >= (1L << 31) || nb + 1 >= (1L << 31)) return 0;
+    const long nblk = (nb + 1023) / 1024;
+    if (nblk > 256L * 64) return 0;
+    auto al = [](long b) { return (b + 255) / 256 * 256; };
+    const long o_cnt = 0, o_off = o_cnt + al(4 * nb), o_bsum = o_off + al(4 * (nb + 1)),
+               o_tot = o_bsum + al(4 * nblk), o_ids = o_tot + 256, end = o_ids + al(4 * n);
+    if (ws) {
+        ws->cnt = (int *)(base + o_cnt);
+        ws->off = (int *)(base + o_off);
+        ws->bsum = (int *)(base + o_bsum);
+        ws->total = (int *)(base + o_tot);
+        ws->ids = (int *)(base + o_ids);
+        ws->nb = nb;
+        ws->n = n;
+        ws->nblk = nblk;
+    }
+    return end;
+}
+
+__global__ void msda_zero_ints(int *__restrict__ p, long n) {
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = 0;
+}
+
 template <typename T>
 __global__ void msda_corner_kernel(const T *__restrict__ loc, const int64_t *__restrict__ shapes, long n, int L, int P,
                                    int32_t *__restrict__ corners) {
@@ -384,6 +714,51 @@ extern "C" int irads_msda_bwd(int dtype, const void *value, const int64_t *shape
                                    grad_loc, grad_aw, st)
                : launch_bwd<double>(value, shapes, level_start, loc, aw, grad_out, bs, S, M, D, L, Q, P, grad_value,
                                     grad_loc, grad_aw, st);
+}
+
+extern "C" long irads_msda_bwd_workspace_bytes(int dtype, int bs, int S, int M, int D, int L, int Q, int P) {
+    if (dtype != IRADS_F32 || bs <= 0 || S <= 0 || M <= 0 || Q <= 0 || L <= 0 || L > kMaxLevels || P <= 0) return 0;
+    return gather_ws_layout(bs, S, M, D, L, Q, P, nullptr, nullptr);
+}
+
+extern "C" int irads_msda_bwd_gather(const float *value, const int64_t *shapes, const int64_t *level_start,
+                                     const float *loc, const float *aw, const float *grad_out, int bs, int S, int M,
+                                     int D, int L, int Q, int P, float *grad_value, float *grad_loc, float *grad_aw,
+                                     void *workspace, long workspace_bytes, void *stream) {
+    if (int e = check_args(IRADS_F32, bs, S, M, D, L, Q, P)) return e;
+    if ((long)bs * Q * M == 0 && (long)bs * S * M == 0) return IRADS_OK;
+    GatherWs ws;
+    const long need = gather_ws_layout(bs, S, M, D, L, Q, P, (char *)workspace, &ws);
+    IRADS_REQUIRE(need > 0, "irads_msda_bwd_gather: shape not served (D %% 4 / power-of-two D/4 <= 64 / sizes)");
+    IRADS_REQUIRE(workspace && workspace_bytes >= need, "irads_msda_bwd_gather: workspace %ld B < %ld B",
+                  workspace_bytes, need);
+    IRADS_REQUIRE(((((uintptr_t)value | (uintptr_t)grad_out | (uintptr_t)grad_value | (uintptr_t)workspace) & 15) == 0),
+                  "irads_msda_bwd_gather: value / grad_out / grad_value / workspace must be 16-B aligned");
+    hipStream_t st = (hipStream_t)stream;
+    const int V = D / 4;
+    auto g1 = [](long n) { return dim3((unsigned)((n + 255) / 256)); };
+    msda_zero_ints<<<g1(ws.nb), 256, 0, st>>>(ws.cnt, ws.nb);
+    if (ws.n > 0) msda_bucket_count<<<g1(ws.n), 256, 0, st>>>(loc, shapes, level_start, bs, S, M, L, Q, P, ws.cnt);
+    msda_scan_blocks<<<(unsigned)ws.nblk, 256, 0, st>>>(ws.cnt, ws.nb, ws.off, ws.bsum);
+    msda_scan_totals<<<1, 256, 0, st>>>(ws.bsum, (int)ws.nblk, ws.total);
+    msda_scan_add<<<g1(ws.nb), 256, 0, st>>>(ws.off, ws.nb, ws.bsum, ws.total, ws.cnt);
+    if (ws.n > 0)
+        msda_bucket_fill<<<g1(ws.n), 256, 0, st>>>(loc, shapes, level_start, bs, S, M, L, Q, P, ws.off, ws.cnt, ws.ids);
+    const dim3 gg = g1((long)bs * S * M * V), gq = g1((long)bs * Q * M * V);
+#define IRADS_MSDA_G(VV)                                                                                           \
+    case VV:                                                                                                       \
+        msda_gather_gvalue<VV><<<gg, 256, 0, st>>>(shapes, level_start, loc, aw, grad_out, bs, S, M, D, L, Q, P,  \
+                                                   ws.off, ws.ids, grad_value);                                    \
+        if ((long)bs * Q * M > 0)                                                                                  \
+            msda_bwd_locaw_vec<VV><<<gq, 256, 0, st>>>(value, shapes, level_start, loc, aw, grad_out, bs, S, M, D, \
+                                                       L, Q, P, grad_loc, grad_aw);                                \
+        break;
+    switch (V) {
+        IRADS_MSDA_G(1) IRADS_MSDA_G(2) IRADS_MSDA_G(4) IRADS_MSDA_G(8) IRADS_MSDA_G(16) IRADS_MSDA_G(32)
+        IRADS_MSDA_G(64)
+    }
+#undef IRADS_MSDA_G
+    return check_launch("irads_msda_bwd_gather");
 }
 
 extern "C" int irads_msda_corner_index(int dtype, const void *loc, const int64_t *shapes, int bs, int Q, int M, int L,

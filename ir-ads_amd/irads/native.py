@@ -22,6 +22,7 @@ SIGNATURES = {
     "irads_msda_fwd": [_i, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp, _vp],
     "irads_msda_bwd": [_i, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp],
     "irads_msda_corner_index": [_i, _vp, _vp, _i, _i, _i, _i, _i, _vp, _vp],
+    "irads_msda_bwd_gather": [_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _l, _vp],
     "irads_winattn_bias_quads": [_vp, _i, _f, _vp, _vp],
     "irads_winattn_fwd": [_i, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _f, _vp, _vp, _vp],
     "irads_winattn_bwd": [_i, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _f, _vp, _vp, _vp, _vp, _vp, _vp,
@@ -74,7 +75,8 @@ QUERIES = {"irads_wgrad_workspace": (ctypes.c_long, [_i, _i, _i]),
            "irads_mpg_partials": (ctypes.c_long, [_l, _i]),
            "irads_ln_bf16_partials": (ctypes.c_long, [_l, _i]),
            "irads_bnact_partials": (ctypes.c_long, [_l, _i]),
-           "irads_winattn_bias_quads_size": (ctypes.c_long, [_i])}
+           "irads_winattn_bias_quads_size": (ctypes.c_long, [_i]),
+           "irads_msda_bwd_workspace_bytes": (ctypes.c_long, [_i, _i, _i, _i, _i, _i, _i, _i])}
 CE_WORKSPACE = 2048
 
 _lib = None

@@ -211,12 +211,31 @@ class MSDAFn(torch.autograd.Function):
         bs, S, M, D = value.shape
         _, Q, _, L, P, _ = loc.shape
         grad_output = grad_output.contiguous()
-        gv = torch.zeros_like(value)
         gl = torch.empty_like(loc)
         ga = torch.empty_like(aw)
-        N.call("irads_msda_bwd", code, N.ptr(value), N.ptr(shapes), N.ptr(lsi), N.ptr(loc), N.ptr(aw),
-               N.ptr(grad_output), bs, S, M, D, L, Q, P, N.ptr(gv), N.ptr(gl), N.ptr(ga), N.stream())
+        ws_bytes = msda_gather_workspace_bytes(value, grad_output, loc)
+        if ws_bytes:
+            # fp32: grad_value gathered per value cell (written once, no zero-fill, no float atomics)
+            gv = torch.empty_like(value)
+            ws = torch.empty((ws_bytes,), device=value.device, dtype=torch.uint8)
+            N.call("irads_msda_bwd_gather", N.ptr(value), N.ptr(shapes), N.ptr(lsi), N.ptr(loc), N.ptr(aw),
+                   N.ptr(grad_output), bs, S, M, D, L, Q, P, N.ptr(gv), N.ptr(gl), N.ptr(ga), N.ptr(ws), ws_bytes,
+                   N.stream())
+        else:  # fp64 / other channel counts: the scatter form (atomics into a zero-filled grad_value)
+            gv = torch.zeros_like(value)
+            N.call("irads_msda_bwd", code, N.ptr(value), N.ptr(shapes), N.ptr(lsi), N.ptr(loc), N.ptr(aw),
+                   N.ptr(grad_output), bs, S, M, D, L, Q, P, N.ptr(gv), N.ptr(gl), N.ptr(ga), N.stream())
         return gv, None, None, gl, ga, None
+
+
+def msda_gather_workspace_bytes(value, grad_output, loc):
+    """Workspace of irads_msda_bwd_gather for this call, or 0 when the atomic-scatter kernel serves
+    it (fp64, D not 4·2^k, or a 16-B misaligned value / grad_output)."""
+    if value.dtype != torch.float32 or (value.data_ptr() | grad_output.data_ptr()) % 16:
+        return 0
+    bs, S, M, D = value.shape
+    _, Q, _, L, P, _ = loc.shape
+    return int(N.load().irads_msda_bwd_workspace_bytes(N.F32, bs, S, M, D, L, Q, P))
 
 
 def msda_corner_index(sampling_locations, spatial_shapes):

@@ -209,3 +209,63 @@ def test_reference_driver_import_surface():
     assert "CMNeXt" in models.__all__  # `from semseg.models import *` + eval(MODEL.NAME)
     datasets = importlib.import_module("semseg.datasets")
     assert {"NYU", "MFNet"} <= set(datasets.__all__)  # `from semseg.datasets import *` + eval(DATASET.NAME)
+
+
+def test_msda_gather_workspace_query(lib):
+    """irads_msda_bwd_workspace_bytes is a pure size query (no GPU work): counters (bs*M*S), their
+    exclusive scan and one int per sample; 0 where the gather backward does not apply."""
+    q = lib.irads_msda_bwd_workspace_bytes
+    q.restype = ctypes.c_long
+    bs, S, M, D, L, Q, P = 2, 22223, 8, 32, 4, 22223, 4
+    n = q(0, bs, S, M, D, L, Q, P)
+    assert n >= 4 * (2 * bs * M * S + bs * Q * M * L * P)
+    assert n < 4 * (2 * bs * M * S + bs * Q * M * L * P) + 8192 + 4 * (bs * M * S // 1024 + 1)
+    assert q(2, bs, S, M, D, L, Q, P) == 0  # fp64: the scatter kernel
+    assert q(0, bs, S, M, 30, L, Q, P) == 0  # D not 4 * 2^k
+    assert q(0, bs, S, M, 24, L, Q, P) == 0
+
+
+# kernels allowed to use private (scratch) memory, none of them launched by the Swin-B / Swin-L
+# training steps: the window-attention backward's optional rel-table / pad-bias gradient variant
+# (EX = true; the Adapter step's tables and qkv bias are frozen), the DAttn kernels for head
+# channels 16 / 24 (Swin-B and Swin-L DSCF blocks have 8 / 12), the fp64 LightSB kernels (the
+# reference-precision mode).  Every kernel the training steps launch must not.
+SCRATCH_ALLOWED = ("winattn_bwd_bf16ILi0ELb1E", "winattn_bwd_bf16ILi1ELb1E", "winattn_bwd_bf16ILi2ELb1E",
+                   "dattn_attn_bwd_k_kernelILi16E", "dattn_attn_bwd_k_kernelILi24E", "dattn_attn_bwd_q_kernelILi24E",
+                   "dattn_sample_bwd_lds_kernelILi16E", "sb_drift_kernelIdE", "sb_em_kernelIdE",
+                   "sb_logits_kernelIdE", "sb_potential_kernelIdE")
+
+
+def test_hot_kernels_use_no_scratch(tmp_path):
+    """Regression guard for the batched weight-gradient fault: hipcc's
+    kernel-resource-usage remarks must report ScratchSize 0 for every kernel of libirads.so
+    outside the whitelist above (a private array behind a maybe-null pointer once put the
+    wgrad column sums in scratch)."""
+    import concurrent.futures as cf
+    srcs = sorted(f for f in os.listdir(os.path.join(ROOT, "ir-ads_amd", "csrc")) if f.endswith(".hip"))
+
+    def remarks(src):
+        exact = ["-ffp-contract=off"] if src in ("msda.hip", "dattn.hip", "dattn_offset.hip", "lnorm.hip") else []
+        r = subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC",
+                            "--cuda-device-only", "-c", os.path.join(ROOT, "ir-ads_amd", "csrc", src), "-o",
+                            str(tmp_path / (src + ".o")), "-Rpass-analysis=kernel-resource-usage"] + exact,
+                           capture_output=True, text=True)
+        assert r.returncode == 0, r.stderr[-2000:]
+        return r.stderr
+    with cf.ThreadPoolExecutor(4) as ex:
+        outs = list(ex.map(remarks, srcs))
+    bad, seen = [], 0
+    for src, txt in zip(srcs, outs):
+        name = None
+        for line in txt.splitlines():
+            m = re.search(r"Function Name: (\S+)", line)
+            if m:
+                name = m.group(1)
+                continue
+            m = re.search(r"ScratchSize \[bytes/lane\]: (\d+)", line)
+            if m and name:
+                seen += 1
+                if int(m.group(1)) and not any(a in name for a in SCRATCH_ALLOWED):
+                    bad.append((src, name, int(m.group(1))))
+    assert seen > 50, seen
+    assert not bad, bad

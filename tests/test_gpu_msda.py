@@ -189,3 +189,57 @@ def test_fp32_vector_path_bitexact_vs_scalar_path(D):
     assert torch.equal(vec, sca), (vec - sca).abs().max().item()
     ref = ops.MSDAFn.apply(value.double(), shapes, lsi, loc.double(), aw.double(), 2)
     torch.testing.assert_close(vec.double(), ref, atol=1e-5, rtol=1e-5)
+
+
+@pytest.mark.parametrize("D", [4, 16, 32, 64, 256])
+def test_fp32_gather_backward_vs_scatter_and_fp64(D):
+    """The atomic-free fp32 backward (irads_msda_bwd_gather: samples bucketed by corner cell,
+    grad_value gathered per cell and written once) against the atomic-scatter kernel on the same
+    fp32 inputs and against the fp64 kernel (itself pinned to the reference above).  Locations
+    cover every boundary case: corners at -1 and at W-1 / H-1 (one valid corner column / row),
+    samples entirely outside (no contribution), a 1x1 level, value cells nothing samples
+    (their gradient rows must come out zero, not stale: grad_value is allocated uninitialised)."""
+    from irads import native as N
+    ops = _ops()
+    g = torch.Generator().manual_seed(100 + D)
+    lv = [(13, 17), (7, 9), (1, 1), (4, 5)]
+    shapes = torch.as_tensor(lv, dtype=torch.long, device=DEV)
+    lsi = torch.cat((shapes.new_zeros((1,)), shapes.prod(1).cumsum(0)[:-1]))
+    S, bs, M, Q, L, P = int(shapes.prod(1).sum()), 2, 3, 41, 4, 5
+    value = torch.randn(bs, S, M, D, generator=g).to(DEV)
+    loc = torch.rand(bs, Q, M, L, P, 2, generator=g) * 1.3 - 0.15  # ~10 % of corners outside
+    loc[:, :3] = torch.rand(bs, 3, M, L, P, 2, generator=g) * 0.02  # x0 / y0 = -1 (left / top edge)
+    loc[:, 3:6] = 1.0 - torch.rand(bs, 3, M, L, P, 2, generator=g) * 0.02  # right / bottom edge
+    loc[:, 6] = 2.5  # entirely outside: no contribution anywhere
+    loc = loc.contiguous().to(DEV)
+    aw = torch.rand(bs, Q, M, L, P, generator=g).to(DEV)
+    gout = torch.randn(bs, Q, M * D, generator=g).to(DEV)
+    ws_bytes = ops.msda_gather_workspace_bytes(value, gout, loc)
+    assert ws_bytes > 0
+    ws = torch.empty(ws_bytes, device=DEV, dtype=torch.uint8)
+    gv = torch.full_like(value, float("nan"))  # every row must be written
+    gl, ga = torch.empty_like(loc), torch.empty_like(aw)
+    N.call("irads_msda_bwd_gather", N.ptr(value), N.ptr(shapes), N.ptr(lsi), N.ptr(loc), N.ptr(aw), N.ptr(gout),
+           bs, S, M, D, L, Q, P, N.ptr(gv), N.ptr(gl), N.ptr(ga), N.ptr(ws), ws_bytes, N.stream())
+    gv2, gl2, ga2 = torch.zeros_like(value), torch.empty_like(loc), torch.empty_like(aw)
+    N.call("irads_msda_bwd", N.F32, N.ptr(value), N.ptr(shapes), N.ptr(lsi), N.ptr(loc), N.ptr(aw), N.ptr(gout),
+           bs, S, M, D, L, Q, P, N.ptr(gv2), N.ptr(gl2), N.ptr(ga2), N.stream())
+    torch.cuda.synchronize()
+    assert torch.isfinite(gv).all()
+    # grad_loc / grad_aw are D-channel fp32 dot products: absolute error grows with D
+    ka = max(1.0, D / 32)
+    torch.testing.assert_close(gv, gv2, atol=2e-5, rtol=1e-5)
+    torch.testing.assert_close(gl, gl2, atol=2e-4 * ka, rtol=1e-5)
+    torch.testing.assert_close(ga, ga2, atol=2e-5 * ka, rtol=1e-5)
+    v64, l64, a64 = (t.double().requires_grad_() for t in (value, loc, aw))
+    o64 = ops.MSDAFn.apply(v64, shapes, lsi, l64, a64, 2)
+    r = torch.autograd.grad((o64 * gout.double()).sum(), (v64, l64, a64))
+    torch.testing.assert_close(gv.double(), r[0], atol=2e-5, rtol=1e-5)
+    torch.testing.assert_close(gl.double(), r[1], atol=2e-4 * ka, rtol=1e-5)
+    torch.testing.assert_close(ga.double(), r[2], atol=2e-5 * ka, rtol=1e-5)
+    # the 1x1 level's cell and the cells no sample reaches: exact zeros where fp64 says zero
+    assert (gv[r[0] == 0] == 0).all()
+    # shapes the gather path does not serve fall back to the scatter kernel (workspace 0)
+    assert ops.msda_gather_workspace_bytes(value.double(), gout.double(), loc.double()) == 0
+    v30 = torch.randn(bs, S, M, 30, device=DEV)
+    assert ops.msda_gather_workspace_bytes(v30, torch.randn(bs, Q, M * 30, device=DEV), loc) == 0
