@@ -232,6 +232,62 @@ def msda_rooflines(device, reps=20):
     return out
 
 
+def dino_stack_line(device, msda, reps=5):
+    """vCLR DINO deformable transformer at C5 per-GPU shapes: bs = 2,
+    800x1333 levels (S = 22 223), 6 encoder + 6 decoder layers, 2000 two-stage proposals plus
+    200 denoising queries under the CDN attention mask; fp32 (the reference trains it without
+    AMP); forward + backward of all outputs, timed with HIP events.  Random-init weights."""
+    from detrex.layers import PositionEmbeddingSine
+    from projects.vCLR_deformable_mask.modeling import (DINOTransformer, DINOTransformerDecoder,
+                                                        DINOTransformerEncoder, attach_detection_heads)
+    torch.manual_seed(0)
+    bs, nprop, ndn = 2, 2000, 200
+    tr = attach_detection_heads(DINOTransformer(DINOTransformerEncoder(), DINOTransformerDecoder(),
+                                                two_stage_num_proposals=nprop)).to(device).train()
+    pe = PositionEmbeddingSine(num_pos_feats=128, temperature=10000, normalize=True, offset=-0.5)
+    feats = [torch.randn(bs, 256, h, w, device=device, requires_grad=True) for h, w in DINO_SHAPES]
+    masks = [torch.zeros(bs, h, w, dtype=torch.bool, device=device) for h, w in DINO_SHAPES]
+    for m in masks:  # second image padded on the right / bottom (~10 %)
+        m[1, -(-9 * m.shape[1] // 10):, :] = True
+        m[1, :, -(-9 * m.shape[2] // 10):] = True
+    pos = [pe(m) for m in masks]
+    n = ndn + nprop
+    attn = torch.zeros(n, n, dtype=torch.bool, device=device)
+    attn[ndn:, :ndn] = True
+    for g in range(ndn // 10):  # 20 denoising groups of 10 queries see only themselves
+        attn[g * 10:(g + 1) * 10, :ndn] = True
+        attn[g * 10:(g + 1) * 10, g * 10:(g + 1) * 10] = False
+    dn = (torch.randn(bs, ndn, 256, device=device), torch.randn(bs, ndn, 4, device=device))
+
+    def step(backward=True):
+        outs = tr(feats, masks, pos, dn, attn)
+        if backward:
+            sum(o.float().sum() for o in outs if o.requires_grad).backward()
+
+    res = {}
+    for tag, bwd in (("fwd", False), ("fwd_bwd", True)):
+        for _ in range(2):
+            step(bwd)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        a.record()
+        for _ in range(reps):
+            step(bwd)
+        b.record()
+        torch.cuda.synchronize()
+        res[f"ms_{tag}"] = round(a.elapsed_time(b) / reps, 3)
+    # MSDA kernel time inside one step, from the isolated launches at the same shapes
+    msda_ms = 6 * (msda["msda_fwd_encoder"]["avg_launch_ms"] + msda["msda_bwd_encoder"]["avg_launch_ms"]
+                   + msda["msda_fwd_decoder"]["avg_launch_ms"] + msda["msda_bwd_decoder"]["avg_launch_ms"])
+    res.update({"workload": "C5 vCLR DINO transformer (6 enc + 6 dec layers, d=256, 8 heads, 4 levels x 4 points) "
+                            "fwd+bwd, fp32, random init",
+                "shape": f"bs={bs} S=22223 queries={nprop}+{ndn} dn",
+                "images_per_s": round(bs / (res["ms_fwd_bwd"] * 1e-3), 2),
+                "msda_kernel_ms_per_step": round(msda_ms, 3),
+                "msda_share": round(msda_ms / res["ms_fwd_bwd"], 4)})
+    return res
+
+
 def traffic_from_profile():
     path = os.path.join(ROOT, "profiles", "r02_pmc_winattn_fwd.json")
     if not os.path.exists(path):
@@ -397,6 +453,11 @@ def main():
             result["kernels"] = msda_rooflines(device)
         except Exception as e:  # report, never fake
             result["kernels"] = {"error": repr(e)[:200]}
+        if "error" not in result["kernels"]:
+            try:
+                result["kernels"]["dino_transformer_c5"] = dino_stack_line(device, result["kernels"])
+            except Exception as e:  # report, never fake
+                result["kernels"]["dino_transformer_c5"] = {"error": repr(e)[:200]}
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == "c2":
         try:
             result["cpu_baseline"] = cpu_baseline(args)

@@ -1,4 +1,10 @@
+from .attention import MultiheadAttention
+from .mlp import FFN, MLP
 from .multi_scale_deform_attn import (MultiScaleDeformableAttention, MultiScaleDeformableAttnFunction,
                                       multi_scale_deformable_attn_pytorch)
+from .position_embedding import PositionEmbeddingSine, get_sine_pos_embed
+from .transformer import BaseTransformerLayer, TransformerLayerSequence
 
-__all__ = ['MultiScaleDeformableAttention', 'MultiScaleDeformableAttnFunction', 'multi_scale_deformable_attn_pytorch']
+__all__ = ['MultiScaleDeformableAttention', 'MultiScaleDeformableAttnFunction', 'multi_scale_deformable_attn_pytorch',
+           'MultiheadAttention', 'FFN', 'MLP', 'PositionEmbeddingSine', 'get_sine_pos_embed', 'BaseTransformerLayer',
+           'TransformerLayerSequence']

@@ -454,6 +454,60 @@ def gen_cmnext_train(ref, tags=None):
         save(f"train_{tag}.npz", **res)
 
 
+# --------------------------------------------------------------------------- vCLR DINO transformer
+from dino_case import DINO_BS, DINO_DN, DINO_LAYERS, DINO_LEVELS, DINO_PROPOSALS, dino_inputs  # noqa: E402
+
+
+def build_ref_dino(L):
+    """DINOTransformer with the detector's per-layer heads attached as dino.py:185-230 does."""
+    d = L.dino
+    enc = d.DINOTransformerEncoder(num_layers=DINO_LAYERS)
+    dec = d.DINOTransformerDecoder(num_layers=DINO_LAYERS)
+    tr = d.DINOTransformer(enc, dec, num_feature_levels=4, two_stage_num_proposals=DINO_PROPOSALS)
+    tr.decoder.class_embed = nn.ModuleList(nn.Linear(256, 1) for _ in range(DINO_LAYERS + 1))
+    tr.decoder.bbox_embed = nn.ModuleList(L.detrex_layers.MLP(256, 256, 4, 3) for _ in range(DINO_LAYERS + 1))
+    return tr
+
+
+DINO_FULL_GRADS = ("level_embeds", "encoder.layers.0.attentions.0.sampling_offsets.weight",
+                   "decoder.layers.0.attentions.1.attention_weights.weight", "decoder.layers.5.norms.2.weight",
+                   "decoder.bbox_embed.2.layers.2.bias", "tgt_embed.weight")
+
+
+def gen_dino(ref):
+    L = __import__("ref_import").load_dino()
+    torch.manual_seed(0)
+    tr = build_ref_dino(L)
+    fill_module(tr, seed=9)
+    tr = tr.double().eval()  # eval: dropout off (attn 0.1, ffn 0.1); everything else is train-mode math
+    feats, masks, dn_label, dn_box, attn = dino_inputs()
+    pe = L.detrex_layers.PositionEmbeddingSine(num_pos_feats=128, temperature=10000, normalize=True, offset=-0.5)
+    pos = [pe(m).double() for m in masks]
+    for f in feats:
+        f.requires_grad_()
+    dn_label.requires_grad_()
+    outs = tr(feats, masks, pos, (dn_label, dn_box), attn)
+    names = ("inter_states", "init_reference", "inter_references", "target_unact", "topk_coords", "memory")
+    gouts = [t(seeded(tuple(o.shape), 60 + i), torch.float64) for i, o in enumerate(outs)]
+    loss = sum((o * g).sum() for o, g in zip(outs, gouts) if o.requires_grad)
+    params = [(n, p) for n, p in tr.named_parameters()]
+    grads = torch.autograd.grad(loss, feats + [dn_label] + [p for _, p in params], allow_unused=True)
+    res = {"pos_%d" % i: p for i, p in enumerate(pos)}
+    res.update({n: o for n, o in zip(names, outs)})
+    res.update({f"gfeat_{i}": g for i, g in enumerate(grads[:4])})
+    res["gdn_label"] = grads[4]
+    res["loss"] = loss.detach()
+    for (n, p), g in zip(params, grads[5:]):
+        g = torch.zeros_like(p) if g is None else g
+        res["gcs." + n] = checksum(g.detach().numpy())
+        if n in DINO_FULL_GRADS:
+            res["g." + n] = g
+    res["topk_index"] = torch.topk(tr.decoder.class_embed[DINO_LAYERS](
+        tr.gen_encoder_output_proposals(outs[5], torch.cat([m.flatten(1) for m in masks], 1),
+                                        torch.as_tensor(DINO_LEVELS))[0]).max(-1)[0], DINO_PROPOSALS, dim=1)[1]
+    save("dino_transformer.npz", **res)
+
+
 # --------------------------------------------------------------------------- LightSB
 def gen_sb(ref):
     sbm = ref.sb.LightSB(dim=512, n_potentials=10, epsilon=0.1, is_diagonal=True)
@@ -544,7 +598,7 @@ if __name__ == "__main__":
     which = sys.argv[1:] or ["msda", "swin", "block", "dattn", "fusion", "cmnext", "sb", "metrics", "train"]
     ref = load_reference()
     torch.manual_seed(0)
-    fns = {"msda": gen_msda, "swin": gen_swin_wmsa, "block": gen_swin_block, "dattn": gen_dattn,
+    fns = {"dino": gen_dino, "msda": gen_msda, "swin": gen_swin_wmsa, "block": gen_swin_block, "dattn": gen_dattn,
            "fusion": gen_fusion_small, "cmnext": gen_cmnext, "sb": gen_sb, "metrics": gen_metrics_loss,
            "train": gen_cmnext_train}
     for w in which:

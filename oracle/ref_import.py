@@ -186,6 +186,34 @@ def load_reference():
     return types.SimpleNamespace(**_LOADED)
 
 
+def load_dino():
+    """The vCLR DINO transformer (projects/vCLR_deformable_mask/modeling/dino_transformer.py) on
+    the reference's own detrex layers.  Stand-ins: fairscale's ``checkpoint_wrapper`` (identity;
+    the reference discards its result anyway, :74-77) and an empty ``torchvision`` (only
+    detrex/utils/misc.py's unused box helpers need it).  MSDA takes its CPU PyTorch path."""
+    ref = load_reference()
+    if "dino" in _LOADED:
+        return ref
+    _mod("fairscale")
+    _mod("fairscale.nn")
+    _mod("fairscale.nn.checkpoint", checkpoint_wrapper=lambda m, *a, **k: m)
+    if importlib.util.find_spec("torchvision") is None:
+        _mod("torchvision")
+    lay = sys.modules["detrex.layers"]
+    for name, rel in (("transformer", "transformer.py"), ("attention", "attention.py"), ("mlp", "mlp.py"),
+                      ("position_embedding", "position_embedding.py")):
+        m = _load(f"detrex.layers.{name}", f"detrex/layers/{rel}")
+        for k in dir(m):
+            if not k.startswith("_"):
+                setattr(lay, k, getattr(m, k))
+    lay.MultiScaleDeformableAttention = _LOADED["msda"].MultiScaleDeformableAttention
+    misc = _load("detrex.utils.misc", "detrex/utils/misc.py")
+    _mod("detrex.utils", inverse_sigmoid=misc.inverse_sigmoid)
+    dino = _load("vclr_dino_transformer", "projects/vCLR_deformable_mask/modeling/dino_transformer.py")
+    _LOADED.update(dino=dino, detrex_layers=lay)
+    return types.SimpleNamespace(**_LOADED)
+
+
 if __name__ == "__main__":
     r = load_reference()
     print(sorted(vars(r)))

@@ -91,6 +91,23 @@ def test_product_parameter_order_matches_oracle():
     assert a == b
 
 
+def test_dino_transformer_parameter_schema():
+    """vCLR DINO transformer: same parameter names, order and shapes as the reference modules
+    (every reference parameter has a gradient checksum in the fixture, in registration order)."""
+    from dino_case import DINO_LAYERS, DINO_PROPOSALS
+    from projects.vCLR_deformable_mask.modeling import (DINOTransformer, DINOTransformerDecoder,
+                                                        DINOTransformerEncoder, attach_detection_heads)
+    fx = Fixture("dino_transformer.npz")
+    tr = attach_detection_heads(DINOTransformer(DINOTransformerEncoder(num_layers=DINO_LAYERS),
+                                                DINOTransformerDecoder(num_layers=DINO_LAYERS),
+                                                two_stage_num_proposals=DINO_PROPOSALS))
+    ref = [k[4:] for k in fx.keys() if k.startswith("gcs.")]
+    got = [n for n, _ in tr.named_parameters()]
+    assert got == ref
+    for n, p in tr.named_parameters():
+        assert fx["gcs." + n][3] == p.numel(), n
+
+
 def test_product_refuses_cpu_tensors():
     from semseg.models.backbones.swin import DAttentionMM, ShiftWindowMSA
     from detrex.layers import MultiScaleDeformableAttention
