@@ -587,3 +587,39 @@ def test_stage_tail_matches_separate_norms(C, H, W):
     (da,) = torch.autograd.grad(ya, xa, (gm, g1, g2))
     (db,) = torch.autograd.grad((ymb, y1b, y2b), xb, (gm, g1, g2))
     torch.testing.assert_close(da, db, rtol=2e-7, atol=1e-7)  # one fp32 rounding of the same two terms
+
+
+@pytest.mark.parametrize("count", [1, 2, 3, 4])
+@pytest.mark.parametrize("sums", ["none", "a", "b", "both"])
+@pytest.mark.parametrize("K,m,n", [(8192, 32, 512), (1000, 16, 128), (64, 128, 256)])
+def test_wgrad_batched_stays_in_its_workspace(count, sums, K, m, n):
+    """Regression for the round-1 illegal-address fault ("Scratch memory"): every
+    batched launch, with and without column-sum pointers, writes only inside the workspace
+    irads_wgrad_batched_workspace() sizes (a NaN-filled guard region behind it stays intact) and
+    gives the fp32 A^T B and column sums of each problem."""
+    from irads import native as N
+    from irads.ops import _WgradProblem
+    torch.manual_seed(count * 7 + K)
+    arr = (_WgradProblem * count)()
+    keep = []
+    for q in range(count):
+        A = (torch.randn(K, m, device=DEV) * 0.3).bfloat16()
+        B = (torch.randn(K, n, device=DEV) * 0.3).bfloat16()
+        D = torch.full((m, n), float("nan"), device=DEV)
+        sa = torch.full((m,), float("nan"), device=DEV) if sums in ("a", "both") else None
+        sb = torch.full((n,), float("nan"), device=DEV) if sums in ("b", "both") else None
+        arr[q] = _WgradProblem(A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), D.data_ptr(),
+                               None if sa is None else sa.data_ptr(), None if sb is None else sb.data_ptr(), 0)
+        keep.append((A, B, D, sa, sb))
+    need = N.load().irads_wgrad_batched_workspace(count, K, m, n)
+    guard = 1 << 16
+    ws = torch.full((need + guard,), float("nan"), device=DEV)
+    N.call("irads_wgrad_batched", count, arr, K, m, n, 1.0, 0, N.ptr(ws), N.stream())
+    torch.cuda.synchronize()
+    assert torch.isnan(ws[need:]).all(), "irads_wgrad_batched wrote past its workspace"
+    for A, B, D, sa, sb in keep:
+        torch.testing.assert_close(D, A.float().t() @ B.float(), rtol=1e-5, atol=1e-3)
+        if sa is not None:
+            torch.testing.assert_close(sa, A.float().sum(0), rtol=1e-5, atol=1e-3)
+        if sb is not None:
+            torch.testing.assert_close(sb, B.float().sum(0), rtol=1e-5, atol=1e-3)
