@@ -134,6 +134,18 @@ int irads_dattn_attn_bwd(const float *q, const float *k, const float *v, const f
                          const float *out, const float *lse, const float *grad_out, float *delta,
                          float *grad_q, float *grad_k, float *grad_v, float *grad_rpe,
                          float *grad_pos_x, float *grad_pos_y, void *stream);
+/* Same as irads_dattn_attn_bwd with a caller-provided workspace (>= the query below, 4-B
+ * aligned): the per-key pass writes per-query-chunk partial sums of grad_k / grad_v / grad_pos
+ * there and a second launch adds them in chunk order, so those three are written (not added)
+ * without float atomics and are bit-reproducible run to run.  grad_q / grad_rpe as above. */
+long irads_dattn_attn_bwd_workspace_bytes(int B, int nH, int G, int hc, int H, int W, int n);
+int irads_dattn_attn_bwd_ws(const float *q, const float *k, const float *v, const float *pos_x,
+                            const float *pos_y, const float *rpe, const float *qgrid_y, const float *qgrid_x,
+                            int B, int nH, int G, int hc, int H, int W, int n, int Ht, int Wt, float scale,
+                            const float *out, const float *lse, const float *grad_out, float *delta,
+                            float *grad_q, float *grad_k, float *grad_v, float *grad_rpe,
+                            float *grad_pos_x, float *grad_pos_y, void *workspace, long workspace_bytes,
+                            void *stream);
 /* Debug export: integer corners (x0, y0) of align_corners=True sampling at `grid`
  * ((N, 2) in (x, y) order, the grid_sample convention) on an H x W map. */
 /* Offset networks conv_offset_x / conv_offset_y of DAttentionMM (swin.py:777-786, :880-905) for

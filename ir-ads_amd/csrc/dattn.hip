@@ -13,15 +13,18 @@
 //    (swin.py:950-1016): out = softmax(scale·qᵀk + rpe_bias) v over 2n keys per query,
 //    where rpe_bias = grid_sample(rpe_table[h] (119x159), 0.5·(q_grid − pos)).  The
 //    reference materialises attn (B·h, HW, 2n) and two bias tensors of that size
-//    (16.8 M entries per image at stage 0); here one thread owns one query, streams the
-//    2n keys from LDS (broadcast reads) with an online softmax, and reads the whole
-//    per-head table from LDS (75.7 KB fp32).  head_dim is 8 (Swin-B) / 12 (Swin-L):
-//    too small for MFMA, so this is an fp32-VALU-bound kernel.
-//    Backward: pass Q (thread per query) recomputes the row and writes dq and
-//    delta = dO·O; pass K (thread per key) loops over a query chunk staged in LDS,
-//    accumulates dk, dv and d(pos) in registers and the table gradient in LDS
-//    (lanes = different keys hit scattered table cells: low atomic contention), then
-//    flushes per-workgroup partial sums with one atomic per element.
+//    (16.8 M entries per image at stage 0); here one thread owns one query, reads the 2n
+//    keys with wave-uniform loads under an online softmax, and reads the bias taps from the
+//    band of table rows its workgroup's queries can reach, staged in LDS.  head_dim is 8
+//    (Swin-B) / 12 (Swin-L): too small for MFMA, so this is an fp32-VALU-bound kernel
+//    (SURVEY §8(d)).
+//    Backward: pass Q (thread per query) recomputes the row, writes dq and delta = dO·O and
+//    accumulates the table gradient in LDS in fixed point; pass K (thread per key) loops
+//    over a contiguous query chunk staged in LDS and keeps dk, dv and d(pos) in registers;
+//    with a workspace each chunk writes those partial sums and a second launch adds them in
+//    chunk order (no float atomics, reproducible).
+#include <algorithm>
+
 #include "common.h"
 
 namespace irads {
@@ -283,12 +286,41 @@ __device__ __forceinline__ BiasPk rpe_bias_pk(const float *tab, int Ht, int Wt, 
 
 __device__ __forceinline__ int pad_cells(int Ht, int Wt) { return ((Ht + 1) * (Wt + 1) + 3) & ~3; }
 
+// Table rows [r0, r0 + nr) into LDS with a zero pad column Wt and zero rows past Ht.  Eight
+// independent loads per thread are in flight before their LDS stores (a plain element loop
+// serialises one global-load latency per element: ~20 per thread for a whole table), and the
+// (row, column) position advances without divisions.
+__device__ __forceinline__ void load_table_rows(float *tab, const float *__restrict__ src, int Ht, int Wt, int r0,
+                                                int nr) {
+    const int TP = Wt + 1, TT = nr * TP, step = blockDim.x;
+    const int dr = step / TP, dc = step - dr * TP;
+    int r = threadIdx.x / TP, c = threadIdx.x - r * TP;
+    for (int base = threadIdx.x; base < TT; base += 8 * step) {
+        float v[8];
+        int rr = r, cc = c;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int gr = r0 + rr;
+            v[u] = (base + u * step < TT && gr < Ht && cc < Wt) ? src[gr * Wt + cc] : 0.f;
+            rr += dr;
+            cc += dc;
+            if (cc >= TP) {
+                cc -= TP;
+                ++rr;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (base + u * step < TT) tab[base + u * step] = v[u];
+        r = rr;
+        c = cc;
+    }
+}
+
 __device__ __forceinline__ void load_table_padded(float *tab, const float *__restrict__ src, int Ht, int Wt) {
     const int TP = Wt + 1, TT = pad_cells(Ht, Wt);
-    for (int i = threadIdx.x; i < TT; i += blockDim.x) {
-        const int r = i / TP, c = i - r * TP;
-        tab[i] = (r < Ht && c < Wt) ? src[r * Wt + c] : 0.f;
-    }
+    load_table_rows(tab, src, Ht, Wt, 0, Ht + 1);
+    for (int i = (Ht + 1) * TP + threadIdx.x; i < TT; i += blockDim.x) tab[i] = 0.f;  // alignment tail
 }
 
 __device__ __forceinline__ float block_sum_f(float v, float *red) {
@@ -331,108 +363,6 @@ __device__ __forceinline__ f2 key_pos(const KeyRef &r, int n, int j) {
 // key-splits (QW * KSP = 16 waves); each wave runs an online softmax over its 2n/KSP keys,
 // four keys per step, and the KSP partial states of a query are merged through LDS.
 __device__ __forceinline__ int uniform_int(int v) { return __builtin_amdgcn_readfirstlane(v); }
-
-// ---------------------------------------------------------------- forward
-// LDS: table[pad_cells] | part[16 waves][HC + 2][64]
-template <int HC>
-__global__ void __launch_bounds__(1024) dattn_attn_fwd_kernel(AttnArgs a, int KSP, const float *__restrict__ kg,
-                                                              const float *__restrict__ vg,
-                                                              const float *__restrict__ pxg,
-                                                              const float *__restrict__ pyg, float *__restrict__ out,
-                                                              float *__restrict__ lse) {
-    static_assert(HC % 2 == 0, "packed fp32 needs an even head size");
-    extern __shared__ __attribute__((aligned(16))) float sm[];
-    const int n2 = 2 * a.n, HW = a.H * a.W;
-    float *tab = sm, *part = sm + pad_cells(a.Ht, a.Wt);
-    const int bh = blockIdx.y, b = bh / a.nH, h = bh % a.nH;
-    const int gi = h / (a.nH / a.G);
-    load_table_padded(tab, a.rpe + (long)h * a.Ht * a.Wt, a.Ht, a.Wt);
-    __syncthreads();
-    const KeyRef kr = key_ref(a, kg, vg, pxg, pyg, bh, b, gi, HC);
-    const int wave = uniform_int(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const int QW = 16 / KSP, qw = wave % QW, sp = wave / QW;
-    const int kb = uniform_int(sp * n2 / KSP), ke = uniform_int((sp + 1) * n2 / KSP);
-    const f2 sc = {((float)a.Wt - 1.0f) / 2.0f, ((float)a.Ht - 1.0f) / 2.0f};
-    float *mypart = part + (long)wave * (HC + 2) * 64 + lane;
-    for (int q0 = blockIdx.x * QW * 64; q0 < HW; q0 += gridDim.x * QW * 64) {
-        const int qi = q0 + qw * 64 + lane;
-        const bool valid = qi < HW;
-        const int qc = valid ? qi : HW - 1;
-        const f2 qg = {a.qgx[qc % a.W], a.qgy[qc / a.W]};
-        f2 qv[HC / 2], acc[HC / 2];
-#pragma unroll
-        for (int c = 0; c < HC / 2; ++c) {
-            qv[c] = (f2){a.q[((long)bh * HC + 2 * c) * HW + qc], a.q[((long)bh * HC + 2 * c + 1) * HW + qc]};
-            acc[c] = (f2){0.f, 0.f};
-        }
-        float m = -1e30f, l = 0.f;
-        for (int j0 = kb; j0 < ke; j0 += 4) {
-            float s2[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int j = min(j0 + u, ke - 1);
-                const f2 *kk = reinterpret_cast<const f2 *>(kr.k + (long)j * HC);
-                f2 d = {0.f, 0.f};
-#pragma unroll
-                for (int c = 0; c < HC / 2; ++c) d = pk_fma(qv[c], kk[c], d);
-                const BiasPk bi = rpe_bias_pk(tab, a.Ht, a.Wt, qg, key_pos(kr, a.n, j), sc);
-                s2[u] = (j0 + u < ke) ? ((d.x + d.y) * a.scale + bi.v) * kLog2e : -1e30f;  // swin.py:951-1010
-            }
-            const float mx = fmaxf(fmaxf(m, fmaxf(s2[0], s2[1])), fmaxf(s2[2], s2[3]));
-            const float corr = fast_exp2(m - mx);
-            l *= corr;
-#pragma unroll
-            for (int c = 0; c < HC / 2; ++c) acc[c] *= (f2){corr, corr};
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int j = min(j0 + u, ke - 1);
-                const float p = (j0 + u < ke) ? fast_exp2(s2[u] - mx) : 0.f;
-                l += p;
-                const f2 *vv = reinterpret_cast<const f2 *>(kr.v + (long)j * HC);
-#pragma unroll
-                for (int c = 0; c < HC / 2; ++c) acc[c] = pk_fma((f2){p, p}, vv[c], acc[c]);
-            }
-            m = mx;
-        }
-        if (KSP > 1) {  // merge the key splits of this query wave through LDS
-            mypart[0] = m;
-            mypart[64] = l;
-#pragma unroll
-            for (int c = 0; c < HC / 2; ++c) {
-                mypart[(2 + 2 * c) * 64] = acc[c].x;
-                mypart[(3 + 2 * c) * 64] = acc[c].y;
-            }
-            __syncthreads();
-            if (sp == 0) {
-                float M = m;
-                for (int o = 1; o < KSP; ++o) M = fmaxf(M, part[((long)(o * QW + qw) * (HC + 2)) * 64 + lane]);
-                const float f0 = fast_exp2(m - M);
-                l *= f0;
-#pragma unroll
-                for (int c = 0; c < HC / 2; ++c) acc[c] *= (f2){f0, f0};
-                for (int o = 1; o < KSP; ++o) {
-                    const float *pp = part + ((long)(o * QW + qw) * (HC + 2)) * 64 + lane;
-                    const float f = fast_exp2(pp[0] - M);
-                    l = fmaf(pp[64], f, l);
-#pragma unroll
-                    for (int c = 0; c < HC / 2; ++c)
-                        acc[c] = pk_fma((f2){f, f}, (f2){pp[(2 + 2 * c) * 64], pp[(3 + 2 * c) * 64]}, acc[c]);
-                }
-                m = M;
-            }
-            __syncthreads();
-        }
-        if (sp == 0 && valid) {
-            const float inv = 1.f / l;
-#pragma unroll
-            for (int c = 0; c < HC / 2; ++c) {
-                out[((long)bh * HC + 2 * c) * HW + qi] = acc[c].x * inv;
-                out[((long)bh * HC + 2 * c + 1) * HW + qi] = acc[c].y * inv;
-            }
-            lse[(long)bh * HW + qi] = m * kLn2 + logf(l);
-        }
-    }
-}
 
 // ---------------------------------------------------------------- backward, pass Q
 // dq (key splits add into the zero-filled gq with float atomics, one per query channel and
@@ -575,103 +505,340 @@ __global__ void __launch_bounds__(1024) dattn_attn_bwd_q_kernel(AttnArgs a, int 
     }
 }
 
-// ---------------------------------------------------------------- backward, pass K
-// Thread per key, looping over a range of queries staged through LDS (broadcast reads): dk,
-// dv and d(pos) of its key stay in registers and are added into the zero-filled outputs
-// once per workgroup.  The bias is recomputed from the padded table in LDS.
-// LDS: tab[pad] | qst[QCH][2*HC + 4]
+// staged query records per pass-K step
 constexpr int QCH = 64;
 
+// ---------------------------------------------------------------- backward, pass K (banded)
+// One thread per key over a contiguous query range, organised for occupancy:
+//  * the workgroup's queries are one contiguous range, so its bias samples only reach the
+//    table rows  floor((0.5·(qgy − py) + 1)·(Ht−1)/2)  for qgy in the range and py in [−1, 1]:
+//    about half the table plus the range's own extent (61 of 119 rows for one stage-0 query
+//    row).  Only that band goes to LDS (~40 KB instead of 77 KB: 3-4 workgroups per CU);
+//  * the query records (q, dO, lse, delta, grid) of 64 queries at a time are staged in LDS and
+//    read as broadcasts (scalar loads would share lgkmcnt with the table reads and serialise);
+//  * dk accumulates Σ ds·q and dpos Σ ds·∂bias/∂disp unscaled (scale, −½·(size−1)/2 applied
+//    once at the end); the dot products and accumulations use packed fp32.
+// Positions must lie in [−1, 1] and qgy must be the module's query grid (monotone in [−1, 1]):
+// the band is derived from that (include/irads.h); rows are clamped into the band regardless.
+__device__ __forceinline__ void band_rows(const float *__restrict__ qgy, int W, int Ht, float scy, int qa, int qb,
+                                          int nr_max, int &t_lo, int &nr) {
+    const float ya = qgy[qa / W], yb = qgy[(qb - 1) / W];
+    const float ylo = fminf(ya, yb), yhi = fmaxf(ya, yb);
+    const float lo = (0.5f * (ylo - 1.f) + 1.f) * scy, hi = (0.5f * (yhi + 1.f) + 1.f) * scy;
+    t_lo = max(0, (int)floorf(lo) - 1);
+    const int t_hi = min(Ht, (int)floorf(hi) + 2);  // y0 + 1 at most; row Ht is the zero pad row
+    nr = min(nr_max, t_hi - t_lo + 1);
+}
+
+__device__ __forceinline__ void load_table_band(float *tab, const float *__restrict__ src, int Ht, int Wt, int t_lo,
+                                                int nr) {
+    load_table_rows(tab, src, Ht, Wt, t_lo, nr);
+}
+
 template <int HC>
-__global__ void __launch_bounds__(1024) dattn_attn_bwd_k_kernel(AttnArgs a, const float *__restrict__ kg,
-                                                                const float *__restrict__ vg,
-                                                                const float *__restrict__ pxg,
-                                                                const float *__restrict__ pyg,
-                                                                const float *__restrict__ lse,
-                                                                const float *__restrict__ delta,
-                                                                const float *__restrict__ gout, int q_per_block,
-                                                                float *__restrict__ gk, float *__restrict__ gv,
-                                                                float *__restrict__ gpx, float *__restrict__ gpy) {
+__global__ void __launch_bounds__(1024) dattn_attn_bwd_k_band_kernel(AttnArgs a, const float *__restrict__ kg,
+                                                                     const float *__restrict__ vg,
+                                                                     const float *__restrict__ pxg,
+                                                                     const float *__restrict__ pyg,
+                                                                     const float *__restrict__ lse,
+                                                                     const float *__restrict__ delta,
+                                                                     const float *__restrict__ gout, int q_per_block,
+                                                                     int nr_max, float *__restrict__ gk,
+                                                                     float *__restrict__ gv, float *__restrict__ gpx,
+                                                                     float *__restrict__ gpy, float *__restrict__ part) {
+    static_assert(HC % 2 == 0, "packed fp32 needs an even head size");
     extern __shared__ __attribute__((aligned(16))) float sm[];
-    const int n2 = 2 * a.n, HW = a.H * a.W, PC = pad_cells(a.Ht, a.Wt);
-    constexpr int QS = 2 * HC + 4;
-    float *tab = sm, *qst = sm + PC;
+    constexpr int QS = 2 * HC + 4;  // staged query record: q, dO, lse, delta, qgy, qgx
+    const int n2 = 2 * a.n, HW = a.H * a.W, TP = a.Wt + 1;
     const int bh = blockIdx.y, b = bh / a.nH, h = bh % a.nH;
     const int gi = h / (a.nH / a.G);
-    load_table_padded(tab, a.rpe + (long)h * a.Ht * a.Wt, a.Ht, a.Wt);
+    const int q_begin = uniform_int(blockIdx.x * q_per_block);
+    const int q_end = uniform_int(min(HW, q_begin + q_per_block));
+    const f2 sc = {((float)a.Wt - 1.0f) / 2.0f, ((float)a.Ht - 1.0f) / 2.0f};
+    int t_lo, nr;
+    band_rows(a.qgy, a.W, a.Ht, sc.y, q_begin, q_end, nr_max, t_lo, nr);
+    t_lo = uniform_int(t_lo);
+    nr = uniform_int(nr);
+    float *tab = sm, *qst = sm + ((nr_max * TP + 3) & ~3);
+    load_table_band(tab, a.rpe + (long)h * a.Ht * a.Wt, a.Ht, a.Wt, t_lo, nr);
     const KeyRef kr = key_ref(a, kg, vg, pxg, pyg, bh, b, gi, HC);
     const int j = threadIdx.x;
     const bool active = j < n2;
     const int jc = active ? j : n2 - 1;
-    float kk[HC], vv[HC], dk[HC], dv[HC];
+    f2 kk[HC / 2], vv[HC / 2], dk[HC / 2], dv[HC / 2];
+    const f2 *kp = reinterpret_cast<const f2 *>(kr.k + (long)jc * HC);
+    const f2 *vp = reinterpret_cast<const f2 *>(kr.v + (long)jc * HC);
 #pragma unroll
-    for (int c = 0; c < HC; ++c) {
-        kk[c] = kr.k[(long)jc * HC + c];
-        vv[c] = kr.v[(long)jc * HC + c];
-        dk[c] = dv[c] = 0.f;
+    for (int c = 0; c < HC / 2; ++c) {
+        kk[c] = kp[c];
+        vv[c] = vp[c];
+        dk[c] = dv[c] = (f2){0.f, 0.f};
     }
     const f2 pk = key_pos(kr, a.n, jc);
-    float dpy = 0.f, dpx = 0.f;
-    const int q_begin = blockIdx.x * q_per_block;
-    const int q_end = min(HW, q_begin + q_per_block);
-    const f2 sc = {((float)a.Wt - 1.0f) / 2.0f, ((float)a.Ht - 1.0f) / 2.0f};
+    const f2 half = {0.5f, 0.5f};
+    const int ylo = t_lo, yhi = t_lo + nr - 2;
+    f2 dpos = {0.f, 0.f};  // Σ ds · (∂bias/∂ix, ∂bias/∂iy)
     for (int q0 = q_begin; q0 < q_end; q0 += QCH) {
         const int nq = min(QCH, q_end - q0);
         __syncthreads();
-        for (int i = threadIdx.x; i < nq * QS; i += blockDim.x) {
-            const int qq = i / QS, f = i % QS, qi = q0 + qq;
-            float val;
-            if (f < HC)
-                val = a.q[((long)bh * HC + f) * HW + qi];
-            else if (f < 2 * HC)
-                val = gout[((long)bh * HC + (f - HC)) * HW + qi];
-            else if (f == 2 * HC)
-                val = lse[(long)bh * HW + qi];
-            else if (f == 2 * HC + 1)
-                val = delta[(long)bh * HW + qi];
-            else if (f == 2 * HC + 2)
-                val = a.qgy[qi / a.W];
-            else
-                val = a.qgx[qi % a.W];
-            qst[qq * QS + f] = val;
+        for (int i0 = threadIdx.x; i0 < nq * QS; i0 += 4 * blockDim.x) {
+            float val[4];  // four independent loads in flight before the LDS stores
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int i = min(i0 + u * (int)blockDim.x, nq * QS - 1);
+                const int qq = i / QS, f = i - qq * QS, qi = q0 + qq;
+                const float *src;
+                if (f < HC)
+                    src = a.q + ((long)bh * HC + f) * HW + qi;
+                else if (f < 2 * HC)
+                    src = gout + ((long)bh * HC + (f - HC)) * HW + qi;
+                else if (f == 2 * HC)
+                    src = lse + (long)bh * HW + qi;
+                else if (f == 2 * HC + 1)
+                    src = delta + (long)bh * HW + qi;
+                else if (f == 2 * HC + 2)
+                    src = a.qgy + qi / a.W;
+                else
+                    src = a.qgx + qi % a.W;
+                val[u] = *src;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (i0 + u * (int)blockDim.x < nq * QS) qst[i0 + u * blockDim.x] = val[u];
         }
         __syncthreads();
         for (int qq = 0; qq < nq; ++qq) {
             const float *qs = qst + qq * QS;
-            float d = 0.f, dp = 0.f;
+            const f2 *qv = reinterpret_cast<const f2 *>(qs), *dov = reinterpret_cast<const f2 *>(qs + HC);
+            f2 d = {0.f, 0.f}, dp = {0.f, 0.f};
 #pragma unroll
-            for (int c = 0; c < HC; ++c) {
-                d = fmaf(qs[c], kk[c], d);
-                dp = fmaf(qs[HC + c], vv[c], dp);
+            for (int c = 0; c < HC / 2; ++c) {
+                d = pk_fma(qv[c], kk[c], d);
+                dp = pk_fma(dov[c], vv[c], dp);
             }
-            const BiasPk bi = rpe_bias_pk(tab, a.Ht, a.Wt, (f2){qs[2 * HC + 3], qs[2 * HC + 2]}, pk, sc);
-            const float s = d * a.scale + bi.v;
+            // bias: same rounding as rpe_bias_pk (the reference's grid_sample index arithmetic)
+            const f2 qg = {qs[2 * HC + 3], qs[2 * HC + 2]};
+            const f2 dd = (qg - pk) * half;
+            const f2 ii = (dd + (f2){1.f, 1.f}) * sc;
+            const f2 fl = {floorf(ii.x), floorf(ii.y)};
+            const f2 fr = ii - fl;
+            const int x0 = min(max((int)fl.x, 0), a.Wt - 1), y0 = min(max((int)fl.y, ylo), yhi);
+            const int o = (y0 - t_lo) * TP + x0;
+            const f2 t0 = {tab[o], tab[o + 1]}, t1 = {tab[o + TP], tab[o + TP + 1]};
+            const f2 om = (f2){1.f, 1.f} - fr;
+            const f2 wx = {om.x, fr.x};
+            const f2 bv = pk_fma(t1, wx * (f2){fr.y, fr.y}, t0 * (wx * (f2){om.y, om.y}));
+            const float s = fmaf(d.x + d.y, a.scale, bv.x + bv.y);
             const float p = __expf(s - qs[2 * HC]);
-            const float ds = p * (dp - qs[2 * HC + 1]);
-            const float dss = ds * a.scale;
+            const float ds = p * ((dp.x + dp.y) - qs[2 * HC + 1]);
 #pragma unroll
-            for (int c = 0; c < HC; ++c) {
-                dk[c] = fmaf(dss, qs[c], dk[c]);
-                dv[c] = fmaf(p, qs[HC + c], dv[c]);
+            for (int c = 0; c < HC / 2; ++c) {
+                dk[c] = pk_fma((f2){ds, ds}, qv[c], dk[c]);
+                dv[c] = pk_fma((f2){p, p}, dov[c], dv[c]);
             }
-            // d bias / d disp (disp = 0.5 (q_grid - pos)), the dsample expression
-            const float om_x = 1.0f - bi.fr.x, om_y = 1.0f - bi.fr.y;
-            const float dix = ds * ((bi.t0.y - bi.t0.x) * om_y + (bi.t1.y - bi.t1.x) * bi.fr.y);
-            const float diy = ds * ((bi.t1.x - bi.t0.x) * om_x + (bi.t1.y - bi.t0.y) * bi.fr.x);
-            dpx -= 0.5f * dix * sc.x;
-            dpy -= 0.5f * diy * sc.y;
+            // ∂bias/∂ix = (t0.y − t0.x)(1 − fy) + (t1.y − t1.x) fy, ∂bias/∂iy = (t1 − t0)·(1 − fx, fx)
+            const f2 ex = (f2){t0.y, t1.y} - (f2){t0.x, t1.x};
+            const f2 ey = t1 - t0;
+            const f2 gx2 = ex * (f2){om.y, fr.y}, gy2 = ey * (f2){om.x, fr.x};
+            dpos = pk_fma((f2){ds, ds}, (f2){gx2.x + gx2.y, gy2.x + gy2.y}, dpos);
         }
+    }
+    // disp = ½(q_grid − pos): d/dpos = −½ · (size − 1)/2 · ∂/∂i
+    const float gpy_ = -0.5f * sc.y * dpos.y, gpx_ = -0.5f * sc.x * dpos.x;
+    if (part) {  // this chunk's partial sums, field-major (coalesced over keys); summed by dattn_kpart_reduce
+        if (active) {
+            float *pp = part + ((long)blockIdx.x * gridDim.y + bh) * (2 * HC + 2) * n2 + j;
+#pragma unroll
+            for (int c = 0; c < HC / 2; ++c) {
+                pp[(long)(2 * c) * n2] = dk[c].x * a.scale;
+                pp[(long)(2 * c + 1) * n2] = dk[c].y * a.scale;
+                pp[(long)(HC + 2 * c) * n2] = dv[c].x;
+                pp[(long)(HC + 2 * c + 1) * n2] = dv[c].y;
+            }
+            pp[(long)(2 * HC) * n2] = gpy_;
+            pp[(long)(2 * HC + 1) * n2] = gpx_;
+        }
+        return;
     }
     if (active) {
+        float *gkp = gk + (long)bh * n2 * HC + (long)j * HC, *gvp = gv + (long)bh * n2 * HC + (long)j * HC;
 #pragma unroll
-        for (int c = 0; c < HC; ++c) {
-            atomicAdd(&gk[(long)bh * n2 * HC + (long)j * HC + c], dk[c]);
-            atomicAdd(&gv[(long)bh * n2 * HC + (long)j * HC + c], dv[c]);
+        for (int c = 0; c < HC / 2; ++c) {
+            atomicAdd(gkp + 2 * c, dk[c].x * a.scale);
+            atomicAdd(gkp + 2 * c + 1, dk[c].y * a.scale);
+            atomicAdd(gvp + 2 * c, dv[c].x);
+            atomicAdd(gvp + 2 * c + 1, dv[c].y);
         }
         float *gp = (j < a.n ? gpx : gpy) + ((long)(b * a.G + gi) * a.n + (j % a.n)) * 2;
-        atomicAdd(gp, dpy);
-        atomicAdd(gp + 1, dpx);
+        atomicAdd(gp, gpy_);
+        atomicAdd(gp + 1, gpx_);
     }
+}
+
+// Sum of the pass-K partials over the query chunks in chunk order (deterministic, no atomics):
+// thread per (b, group, field, key), coalesced over keys; fields < 2·hc are grad_k / grad_v of
+// each head of the group, the last two grad_pos of the key summed over the group's heads.
+template <int HC>
+__global__ void __launch_bounds__(256) dattn_kpart_reduce(const float *__restrict__ part, int chunks, int B, int nH,
+                                                          int G, int n, float *__restrict__ gk, float *__restrict__ gv,
+                                                          float *__restrict__ gpx, float *__restrict__ gpy) {
+    constexpr int F = 2 * HC + 2;
+    const int n2 = 2 * n, hpg = nH / G;
+    const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (long)B * G * F * n2) return;
+    const int j = (int)(t % n2), f = (int)((t / n2) % F), bg = (int)(t / ((long)n2 * F)), b = bg / G, gi = bg % G;
+    const long cstride = (long)B * nH * F * n2;
+    float pos = 0.f;
+    for (int hh = 0; hh < hpg; ++hh) {
+        const int bh = b * nH + gi * hpg + hh;
+        const float *pp = part + ((long)bh * F + f) * n2 + j;
+        float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;  // four loads in flight, combined in a fixed order
+        int c = 0;
+        for (; c + 3 < chunks; c += 4) {
+            a0 += pp[(long)c * cstride];
+            a1 += pp[(long)(c + 1) * cstride];
+            a2 += pp[(long)(c + 2) * cstride];
+            a3 += pp[(long)(c + 3) * cstride];
+        }
+        for (; c < chunks; ++c) a0 += pp[(long)c * cstride];
+        const float acc = (a0 + a1) + (a2 + a3);
+        if (f < HC)
+            gk[((long)bh * n2 + j) * HC + f] = acc;
+        else if (f < 2 * HC)
+            gv[((long)bh * n2 + j) * HC + f - HC] = acc;
+        else
+            pos += acc;
+    }
+    if (f >= 2 * HC) ((j < n ? gpx : gpy) + ((long)bg * n + (j % n)) * 2)[f - 2 * HC] = pos;
+}
+
+// ---------------------------------------------------------------- forward (banded)
+// Lanes = 64 consecutive queries, waves split the keys with an online softmax in base 2, merged
+// through LDS; 8-wave workgroups over ONE contiguous query range
+// (QW query-waves x KSP key-splits), so only the table band those queries reach is staged
+// (band_rows) and the key-split partials alias it after the last key: ~40 KB per workgroup,
+// three workgroups (24 waves) per CU instead of one 16-wave workgroup beside a 77 KB table.
+// LDS: band[nr_max][Wt+1]  ∪  part[8 waves][HC + 2][64]
+template <int HC>
+__global__ void __launch_bounds__(512) dattn_attn_fwd_band_kernel(AttnArgs a, int KSP, int nr_max,
+                                                                  const float *__restrict__ kg,
+                                                                  const float *__restrict__ vg,
+                                                                  const float *__restrict__ pxg,
+                                                                  const float *__restrict__ pyg,
+                                                                  float *__restrict__ out, float *__restrict__ lse) {
+    static_assert(HC % 2 == 0, "packed fp32 needs an even head size");
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    const int n2 = 2 * a.n, HW = a.H * a.W, TP = a.Wt + 1;
+    const int bh = blockIdx.y, b = bh / a.nH, h = bh % a.nH;
+    const int gi = h / (a.nH / a.G);
+    const int wave = uniform_int(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int QW = 8 / KSP, qw = wave % QW, sp = wave / QW;
+    const int q_begin = uniform_int(blockIdx.x * QW * 64), q_end = uniform_int(min(HW, q_begin + QW * 64));
+    const f2 sc = {((float)a.Wt - 1.0f) / 2.0f, ((float)a.Ht - 1.0f) / 2.0f};
+    int t_lo, nr;
+    band_rows(a.qgy, a.W, a.Ht, sc.y, q_begin, q_end, nr_max, t_lo, nr);
+    t_lo = uniform_int(t_lo);
+    nr = uniform_int(nr);
+    load_table_band(sm, a.rpe + (long)h * a.Ht * a.Wt, a.Ht, a.Wt, t_lo, nr);
+    const KeyRef kr = key_ref(a, kg, vg, pxg, pyg, bh, b, gi, HC);
+    const int kb = uniform_int(sp * n2 / KSP), ke = uniform_int((sp + 1) * n2 / KSP);
+    const int ylo = t_lo, yhi = t_lo + nr - 2;
+    const f2 half = {0.5f, 0.5f};
+    const int qi = q_begin + qw * 64 + lane;
+    const bool valid = qi < q_end;
+    const int qc = valid ? qi : q_end - 1;
+    const f2 qg = {a.qgx[qc % a.W], a.qgy[qc / a.W]};
+    f2 qv[HC / 2], acc[HC / 2];
+#pragma unroll
+    for (int c = 0; c < HC / 2; ++c) {
+        qv[c] = (f2){a.q[((long)bh * HC + 2 * c) * HW + qc], a.q[((long)bh * HC + 2 * c + 1) * HW + qc]};
+        acc[c] = (f2){0.f, 0.f};
+    }
+    __syncthreads();
+    float m = -1e30f, l = 0.f;
+    for (int j0 = kb; j0 < ke; j0 += 4) {
+        float s2[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int j = min(j0 + u, ke - 1);
+            const f2 *kk = reinterpret_cast<const f2 *>(kr.k + (long)j * HC);
+            f2 d = {0.f, 0.f};
+#pragma unroll
+            for (int c = 0; c < HC / 2; ++c) d = pk_fma(qv[c], kk[c], d);
+            // bias: rpe_bias_pk's arithmetic on the band (rows clamped into it)
+            const f2 dd = (qg - key_pos(kr, a.n, j)) * half;
+            const f2 ii = (dd + (f2){1.f, 1.f}) * sc;
+            const f2 fl = {floorf(ii.x), floorf(ii.y)};
+            const f2 fr = ii - fl;
+            const int x0 = min(max((int)fl.x, 0), a.Wt - 1), y0 = min(max((int)fl.y, ylo), yhi);
+            const int o = (y0 - t_lo) * TP + x0;
+            const f2 om = (f2){1.f, 1.f} - fr;
+            const f2 wx = {om.x, fr.x};
+            const f2 t0 = {sm[o], sm[o + 1]}, t1 = {sm[o + TP], sm[o + TP + 1]};
+            const f2 bv = pk_fma(t1, wx * (f2){fr.y, fr.y}, t0 * (wx * (f2){om.y, om.y}));
+            s2[u] = (j0 + u < ke) ? ((d.x + d.y) * a.scale + (bv.x + bv.y)) * kLog2e : -1e30f;  // swin.py:951-1010
+        }
+        const float mx = fmaxf(fmaxf(m, fmaxf(s2[0], s2[1])), fmaxf(s2[2], s2[3]));
+        const float corr = fast_exp2(m - mx);
+        l *= corr;
+#pragma unroll
+        for (int c = 0; c < HC / 2; ++c) acc[c] *= (f2){corr, corr};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int j = min(j0 + u, ke - 1);
+            const float p = (j0 + u < ke) ? fast_exp2(s2[u] - mx) : 0.f;
+            l += p;
+            const f2 *vv = reinterpret_cast<const f2 *>(kr.v + (long)j * HC);
+#pragma unroll
+            for (int c = 0; c < HC / 2; ++c) acc[c] = pk_fma((f2){p, p}, vv[c], acc[c]);
+        }
+        m = mx;
+    }
+    if (KSP > 1) {  // merge the key splits through LDS (aliasing the band: wait for every reader)
+        __syncthreads();
+        float *part = sm, *mypart = part + (long)wave * (HC + 2) * 64 + lane;
+        mypart[0] = m;
+        mypart[64] = l;
+#pragma unroll
+        for (int c = 0; c < HC / 2; ++c) {
+            mypart[(2 + 2 * c) * 64] = acc[c].x;
+            mypart[(3 + 2 * c) * 64] = acc[c].y;
+        }
+        __syncthreads();
+        if (sp == 0) {
+            float M = m;
+            for (int o = 1; o < KSP; ++o) M = fmaxf(M, part[((long)(o * QW + qw) * (HC + 2)) * 64 + lane]);
+            const float f0 = fast_exp2(m - M);
+            l *= f0;
+#pragma unroll
+            for (int c = 0; c < HC / 2; ++c) acc[c] *= (f2){f0, f0};
+            for (int o = 1; o < KSP; ++o) {
+                const float *pp = part + ((long)(o * QW + qw) * (HC + 2)) * 64 + lane;
+                const float f = fast_exp2(pp[0] - M);
+                l = fmaf(pp[64], f, l);
+#pragma unroll
+                for (int c = 0; c < HC / 2; ++c)
+                    acc[c] = pk_fma((f2){f, f}, (f2){pp[(2 + 2 * c) * 64], pp[(3 + 2 * c) * 64]}, acc[c]);
+            }
+            m = M;
+        }
+    }
+    if (sp == 0 && valid) {
+        const float inv = 1.f / l;
+#pragma unroll
+        for (int c = 0; c < HC / 2; ++c) {
+            out[((long)bh * HC + 2 * c) * HW + qi] = acc[c].x * inv;
+            out[((long)bh * HC + 2 * c + 1) * HW + qi] = acc[c].y * inv;
+        }
+        lse[(long)bh * HW + qi] = m * kLn2 + logf(l);
+    }
+}
+
+// table rows a contiguous range of `nq` queries can reach (see band_rows), for LDS sizing
+int band_rows_max(int H, int W, int Ht, int nq) {
+    const int rows_span = std::min(H, (nq + W - 1) / W + 1);
+    const float dq = H > 1 ? 2.f * (float)(rows_span - 1) / (float)(H - 1) : 0.f;
+    return std::min(Ht + 1, (int)(0.5f * (float)(Ht - 1) * (1.f + 0.5f * dq)) + 6);
 }
 
 __global__ void sample_index_kernel(const float *__restrict__ grid, int N, int H, int W, int32_t *__restrict__ out) {
@@ -693,7 +860,6 @@ int check_attn(const AttnArgs &a) {
 
 size_t pad_cells_h(int Ht, int Wt) { return (size_t)(((Ht + 1) * (Wt + 1) + 3) & ~3); }
 
-size_t fwd_smem(const AttnArgs &a) { return (pad_cells_h(a.Ht, a.Wt) + (size_t)16 * (a.hc + 2) * 64) * sizeof(float); }
 
 // key splits per query wave and query-wave workgroups per (b, head): ~8192 waves per launch
 void split_plan(int HW, int BH, int &ksp, int &blocks) {
@@ -777,18 +943,82 @@ extern "C" int irads_dattn_attn_fwd(const float *q, const float *k, const float 
     if (int e = check_attn(a)) return e;
     IRADS_REQUIRE(hc <= 16, "dattn_attn: head channels %d > 16", hc);
     if (B == 0) return IRADS_OK;
-    const size_t sh = fwd_smem(a);
+    // 8-wave workgroups over contiguous query ranges; key splits until ~8192 waves per launch
+    const int HW = H * W;
+    const long qwaves = (long)B * nH * ((HW + 63) / 64);
+    int ksp = 1;
+    while (ksp < 8 && qwaves * ksp < 8192) ksp <<= 1;
+    const int qw = 8 / ksp, blocks = (HW + qw * 64 - 1) / (qw * 64);
+    const int nr_max = band_rows_max(H, W, Ht, qw * 64);
+    const size_t sh = std::max((size_t)nr_max * (Wt + 1), (size_t)8 * (hc + 2) * 64) * sizeof(float);
     IRADS_REQUIRE(sh <= 160 * 1024, "dattn_attn: LDS request %zu exceeds 160 KiB", sh);
-    int ksp, blocks;
-    split_plan(H * W, B * nH, ksp, blocks);
     dim3 grid(blocks, B * nH);
     hipStream_t st = (hipStream_t)stream;
     IRADS_HC_DISPATCH(hc, {
-        (void)hipFuncSetAttribute((const void *)dattn_attn_fwd_kernel<HC>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)sh);
-        dattn_attn_fwd_kernel<HC><<<grid, 1024, sh, st>>>(a, ksp, k, v, pos_x, pos_y, out, lse);
+        (void)hipFuncSetAttribute((const void *)dattn_attn_fwd_band_kernel<HC>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
+        dattn_attn_fwd_band_kernel<HC><<<grid, 512, sh, st>>>(a, ksp, nr_max, k, v, pos_x, pos_y, out, lse);
     })
     return check_launch("irads_dattn_attn_fwd");
+}
+
+// pass K's query chunking: ~768 workgroups (3 per CU with the banded table); with a workspace
+// each chunk writes its partial sums (no float atomics), summed in chunk order afterwards
+static void pass_k_plan(int B, int nH, int H, int W, int &chunks, int &qpb) {
+    const int HW = H * W;
+    chunks = std::max(1, 768 / (B * nH));
+    qpb = (HW + chunks - 1) / chunks;
+    chunks = (HW + qpb - 1) / qpb;
+}
+
+extern "C" long irads_dattn_attn_bwd_workspace_bytes(int B, int nH, int G, int hc, int H, int W, int n) {
+    if (B <= 0 || nH <= 0 || G <= 0 || H <= 0 || W <= 0 || n <= 0 || hc <= 0) return 0;
+    int chunks, qpb;
+    pass_k_plan(B, nH, H, W, chunks, qpb);
+    return (long)chunks * B * nH * (2 * hc + 2) * (2L * n) * (long)sizeof(float);
+}
+
+static int attn_bwd(const float *q, const float *k, const float *v, const float *pos_x, const float *pos_y,
+                    const float *rpe, const float *qgrid_y, const float *qgrid_x, int B, int nH, int G, int hc, int H,
+                    int W, int n, int Ht, int Wt, float scale, const float *out, const float *lse,
+                    const float *grad_out, float *delta, float *grad_q, float *grad_k, float *grad_v, float *grad_rpe,
+                    float *grad_pos_x, float *grad_pos_y, float *part, void *stream) {
+    AttnArgs a{q, k, v, pos_x, pos_y, rpe, qgrid_y, qgrid_x, B, nH, G, hc, H, W, n, Ht, Wt, scale};
+    if (int e = check_attn(a)) return e;
+    IRADS_REQUIRE(hc <= 16, "dattn_attn: head channels %d > 16", hc);
+    if (B == 0) return IRADS_OK;
+    hipStream_t st = (hipStream_t)stream;
+    const int HW = H * W;
+    const size_t sh_q = 2 * pad_cells_h(Ht, Wt) * sizeof(float);
+    IRADS_REQUIRE(sh_q <= 160 * 1024, "dattn_attn_bwd: LDS request exceeds 160 KiB");
+    int ksp, blocks;
+    split_plan(HW, B * nH, ksp, blocks);
+    dim3 gq_grid(blocks, B * nH);
+    // pass K: one thread per key over a contiguous query range (band_rows bounds its table rows)
+    const int kthreads = ((2 * n + 63) / 64) * 64;
+    int chunks, qpb;
+    pass_k_plan(B, nH, H, W, chunks, qpb);
+    dim3 gk_grid(chunks, B * nH);
+    const int nr_max = band_rows_max(H, W, Ht, qpb);
+    const size_t sh_kb = ((((size_t)nr_max * (Wt + 1) + 3) & ~(size_t)3) + (size_t)QCH * (2 * hc + 4)) * sizeof(float);
+    IRADS_REQUIRE(sh_kb <= 160 * 1024, "dattn_attn_bwd: pass-K LDS request %zu exceeds 160 KiB", sh_kb);
+    IRADS_HC_DISPATCH(hc, {
+        (void)hipFuncSetAttribute((const void *)dattn_attn_bwd_q_kernel<HC>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)sh_q);
+        (void)hipFuncSetAttribute((const void *)dattn_attn_bwd_k_band_kernel<HC>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh_kb);
+        dattn_attn_bwd_q_kernel<HC><<<gq_grid, 1024, sh_q, st>>>(a, ksp, k, v, pos_x, pos_y, out, lse, grad_out, delta,
+                                                                 grad_q, grad_rpe);
+        dattn_attn_bwd_k_band_kernel<HC><<<gk_grid, kthreads, sh_kb, st>>>(a, k, v, pos_x, pos_y, lse, delta, grad_out,
+                                                                           qpb, nr_max, grad_k, grad_v, grad_pos_x,
+                                                                           grad_pos_y, part);
+        if (part) {
+            const long t = (long)B * G * (2 * HC + 2) * 2 * n;
+            dattn_kpart_reduce<HC><<<(unsigned)((t + 255) / 256), 256, 0, st>>>(part, chunks, B, nH, G, n, grad_k,
+                                                                                 grad_v, grad_pos_x, grad_pos_y);
+        }
+    })
+    return check_launch("irads_dattn_attn_bwd");
 }
 
 extern "C" int irads_dattn_attn_bwd(const float *q, const float *k, const float *v, const float *pos_x,
@@ -797,35 +1027,23 @@ extern "C" int irads_dattn_attn_bwd(const float *q, const float *k, const float 
                                     const float *out, const float *lse, const float *grad_out, float *delta,
                                     float *grad_q, float *grad_k, float *grad_v, float *grad_rpe, float *grad_pos_x,
                                     float *grad_pos_y, void *stream) {
-    AttnArgs a{q, k, v, pos_x, pos_y, rpe, qgrid_y, qgrid_x, B, nH, G, hc, H, W, n, Ht, Wt, scale};
-    if (int e = check_attn(a)) return e;
-    IRADS_REQUIRE(hc <= 16, "dattn_attn: head channels %d > 16", hc);
-    if (B == 0) return IRADS_OK;
-    hipStream_t st = (hipStream_t)stream;
-    const int HW = H * W;
-    const size_t sh_q = 2 * pad_cells_h(Ht, Wt) * sizeof(float);
-    const size_t sh_k = (pad_cells_h(Ht, Wt) + (size_t)QCH * (2 * hc + 4)) * sizeof(float);
-    IRADS_REQUIRE(sh_q <= 160 * 1024 && sh_k <= 160 * 1024, "dattn_attn_bwd: LDS request exceeds 160 KiB");
-    int ksp, blocks;
-    split_plan(HW, B * nH, ksp, blocks);
-    dim3 gq_grid(blocks, B * nH);
-    // pass K: one thread per key; query ranges sized for ~1024 workgroups (2 per CU fit in LDS)
-    const int kthreads = ((2 * n + 63) / 64) * 64;
-    int chunks = (1024 + B * nH - 1) / (B * nH);
-    int qpb = (HW + chunks - 1) / chunks;
-    qpb = ((qpb + QCH - 1) / QCH) * QCH;
-    dim3 gk_grid((HW + qpb - 1) / qpb, B * nH);
-    IRADS_HC_DISPATCH(hc, {
-        (void)hipFuncSetAttribute((const void *)dattn_attn_bwd_q_kernel<HC>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)sh_q);
-        (void)hipFuncSetAttribute((const void *)dattn_attn_bwd_k_kernel<HC>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)sh_k);
-        dattn_attn_bwd_q_kernel<HC><<<gq_grid, 1024, sh_q, st>>>(a, ksp, k, v, pos_x, pos_y, out, lse, grad_out, delta,
-                                                                 grad_q, grad_rpe);
-        dattn_attn_bwd_k_kernel<HC><<<gk_grid, kthreads, sh_k, st>>>(a, k, v, pos_x, pos_y, lse, delta, grad_out, qpb, grad_k, grad_v,
-                                                                     grad_pos_x, grad_pos_y);
-    })
-    return check_launch("irads_dattn_attn_bwd");
+    return attn_bwd(q, k, v, pos_x, pos_y, rpe, qgrid_y, qgrid_x, B, nH, G, hc, H, W, n, Ht, Wt, scale, out, lse,
+                    grad_out, delta, grad_q, grad_k, grad_v, grad_rpe, grad_pos_x, grad_pos_y, nullptr, stream);
+}
+
+extern "C" int irads_dattn_attn_bwd_ws(const float *q, const float *k, const float *v, const float *pos_x,
+                                       const float *pos_y, const float *rpe, const float *qgrid_y,
+                                       const float *qgrid_x, int B, int nH, int G, int hc, int H, int W, int n, int Ht,
+                                       int Wt, float scale, const float *out, const float *lse, const float *grad_out,
+                                       float *delta, float *grad_q, float *grad_k, float *grad_v, float *grad_rpe,
+                                       float *grad_pos_x, float *grad_pos_y, void *workspace, long workspace_bytes,
+                                       void *stream) {
+    const long need = irads_dattn_attn_bwd_workspace_bytes(B, nH, G, hc, H, W, n);
+    IRADS_REQUIRE(workspace && workspace_bytes >= need, "irads_dattn_attn_bwd_ws: workspace %ld B < %ld B",
+                  workspace_bytes, need);
+    return attn_bwd(q, k, v, pos_x, pos_y, rpe, qgrid_y, qgrid_x, B, nH, G, hc, H, W, n, Ht, Wt, scale, out, lse,
+                    grad_out, delta, grad_q, grad_k, grad_v, grad_rpe, grad_pos_x, grad_pos_y, (float *)workspace,
+                    stream);
 }
 
 extern "C" int irads_dattn_sample_index(const float *grid, int N, int H, int W, int32_t *corners, void *stream) {

@@ -403,8 +403,9 @@ __global__ void __launch_bounds__(256) msda_scan_add(int *__restrict__ off, long
 
 __global__ void __launch_bounds__(256) msda_bucket_fill(const float *__restrict__ loc, const int64_t *__restrict__ shapes,
                                                         const int64_t *__restrict__ lsi, int bs, int S, int M, int L,
-                                                        int Q, int P, const int *__restrict__ off,
-                                                        int *__restrict__ cursor, int *__restrict__ ids) {
+                                                        int Q, int P, const float *__restrict__ aw,
+                                                        const int *__restrict__ off, int *__restrict__ cursor,
+                                                        float4 *__restrict__ rec) {
     __shared__ int sH[kMaxLevels], sW[kMaxLevels], sS[kMaxLevels];
     load_levels(shapes, lsi, L, sH, sW, sS);
     const long sid = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -414,7 +415,11 @@ __global__ void __launch_bounds__(256) msda_bucket_fill(const float *__restrict_
     const int m = (int)((sid / LP) % M);
     const int b = (int)(sid / ((long)LP * M * Q));
     const long bk = sample_bucket(loc, sid, l, sH, sW, sS, b, m, M, S);
-    if (bk >= 0) ids[off[bk] + atomicAdd(cursor + bk, 1)] = (int)sid;
+    if (bk >= 0) {
+        // the gather's whole view of the sample in one 16-B record: query, attention weight, location
+        const int q = (int)((sid / ((long)LP * M)) % Q);
+        rec[off[bk] + atomicAdd(cursor + bk, 1)] = make_float4(__int_as_float(q), aw[sid], loc[2 * sid], loc[2 * sid + 1]);
+    }
 }
 
 // grad_value rows: V lanes (4 channels each) per (b, s, m) cell
@@ -423,11 +428,14 @@ __global__ void __launch_bounds__(256) msda_gather_gvalue(const int64_t *__restr
                                                           const int64_t *__restrict__ lsi, const float *__restrict__ loc,
                                                           const float *__restrict__ aw, const float *__restrict__ gout,
                                                           int bs, int S, int M, int D, int L, int Q, int P,
-                                                          const int *__restrict__ off, const int *__restrict__ ids,
+                                                          const int *__restrict__ off, const float4 *__restrict__ rec,
                                                           float *__restrict__ gvalue) {
     __shared__ int sH[kMaxLevels], sW[kMaxLevels], sS[kMaxLevels];
     load_levels(shapes, lsi, L, sH, sW, sS);
-    const long gid = ((long)blockIdx.x * blockDim.x + threadIdx.x) / V;  // = (b * S + s) * M + m
+    // neighbouring cells share samples (a sample feeds 4 cells) and their grad_out rows: keep
+    // consecutive cells on one XCD so those rows are L2 hits
+    const long blk = xcd_block(blockIdx.x, gridDim.x);
+    const long gid = (blk * blockDim.x + threadIdx.x) / V;  // = (b * S + s) * M + m
     const int lane = threadIdx.x % V;
     if (gid >= (long)bs * S * M) return;  // whole group exits together
     const int m = (int)(gid % M);
@@ -436,7 +444,6 @@ __global__ void __launch_bounds__(256) msda_gather_gvalue(const int64_t *__restr
     const int l = level_of(s, sS, L);
     const int H = sH[l], W = sW[l];
     const int c = s - sS[l], y = c / W, x = c - y * W;
-    const int LP = L * P;
     const long bkb = ((long)b * M + m) * S;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
@@ -450,13 +457,13 @@ __global__ void __launch_bounds__(256) msda_gather_gvalue(const int64_t *__restr
             float wc = 0.f, a = 0.f;
             int q = 0;
             if (e + lane < e1) {
-                const long sid = ids[e + lane];
-                const Samp<float> sp = locate(loc[2 * sid], loc[2 * sid + 1], H, W);
+                const float4 r = rec[e + lane];  // (query, attention weight, x, y), bucket-contiguous
+                const Samp<float> sp = locate(r.z, r.w, H, W);
                 const int dy = y - sp.y0, dx = x - sp.x0;
                 if ((unsigned)dy <= 1u && (unsigned)dx <= 1u)
                     wc = dy == 0 ? (dx == 0 ? sp.nw : sp.ne) : (dx == 0 ? sp.sw : sp.se);
-                a = aw[sid];
-                q = (int)((sid / ((long)LP * M)) % Q);
+                a = r.y;
+                q = __float_as_int(r.x);
             }
             // chunks of up to 8 entries: every grad_out row load of the chunk is issued before the first
             // accumulation (lanes past the bucket end and non-corner entries carry w = 0 and load nothing)
@@ -570,7 +577,8 @@ __global__ void __launch_bounds__(256) msda_bwd_locaw_vec(const float *__restric
 }
 
 struct GatherWs {
-    int *cnt, *off, *bsum, *total, *ids;
+    int *cnt, *off, *bsum, *total;
+    float4 *rec;
     long nb, n, nblk;
 };
 
@@ -584,13 +592,13 @@ long gather_ws_layout(int bs, int S, int M, int D, int L, int Q, int P, char *ba
     if (nblk > 256L * 64) return 0;
     auto al = [](long b) { return (b + 255) / 256 * 256; };
     const long o_cnt = 0, o_off = o_cnt + al(4 * nb), o_bsum = o_off + al(4 * (nb + 1)),
-               o_tot = o_bsum + al(4 * nblk), o_ids = o_tot + 256, end = o_ids + al(4 * n);
+               o_tot = o_bsum + al(4 * nblk), o_rec = o_tot + 256, end = o_rec + al(16 * n);
     if (ws) {
         ws->cnt = (int *)(base + o_cnt);
         ws->off = (int *)(base + o_off);
         ws->bsum = (int *)(base + o_bsum);
         ws->total = (int *)(base + o_tot);
-        ws->ids = (int *)(base + o_ids);
+        ws->rec = (float4 *)(base + o_rec);
         ws->nb = nb;
         ws->n = n;
         ws->nblk = nblk;
@@ -743,12 +751,13 @@ extern "C" int irads_msda_bwd_gather(const float *value, const int64_t *shapes, 
     msda_scan_totals<<<1, 256, 0, st>>>(ws.bsum, (int)ws.nblk, ws.total);
     msda_scan_add<<<g1(ws.nb), 256, 0, st>>>(ws.off, ws.nb, ws.bsum, ws.total, ws.cnt);
     if (ws.n > 0)
-        msda_bucket_fill<<<g1(ws.n), 256, 0, st>>>(loc, shapes, level_start, bs, S, M, L, Q, P, ws.off, ws.cnt, ws.ids);
+        msda_bucket_fill<<<g1(ws.n), 256, 0, st>>>(loc, shapes, level_start, bs, S, M, L, Q, P, aw, ws.off, ws.cnt,
+                                                   ws.rec);
     const dim3 gg = g1((long)bs * S * M * V), gq = g1((long)bs * Q * M * V);
 #define IRADS_MSDA_G(VV)                                                                                           \
     case VV:                                                                                                       \
         msda_gather_gvalue<VV><<<gg, 256, 0, st>>>(shapes, level_start, loc, aw, grad_out, bs, S, M, D, L, Q, P,  \
-                                                   ws.off, ws.ids, grad_value);                                    \
+                                                   ws.off, ws.rec, grad_value);                                    \
         if ((long)bs * Q * M > 0)                                                                                  \
             msda_bwd_locaw_vec<VV><<<gq, 256, 0, st>>>(value, shapes, level_start, loc, aw, grad_out, bs, S, M, D, \
                                                        L, Q, P, grad_loc, grad_aw);                                \

@@ -32,6 +32,7 @@ SIGNATURES = {
                                _vp, _vp],
     "irads_dattn_attn_fwd": [_vp] * 8 + [_i] * 9 + [_f, _vp, _vp, _vp],
     "irads_dattn_attn_bwd": [_vp] * 8 + [_i] * 9 + [_f] + [_vp] * 10 + [_vp],
+    "irads_dattn_attn_bwd_ws": [_vp] * 8 + [_i] * 9 + [_f] + [_vp] * 10 + [_vp, _l, _vp],
     "irads_dattn_sample_index": [_vp, _i, _i, _i, _vp, _vp],
     "irads_sb_drift": [_i, _vp, _vp, _vp, _vp, _vp, _d, _i, _i, _i, _vp, _vp],
     "irads_sb_em": [_i, _vp, _vp, _i, _vp, _vp, _vp, _d, _i, _i, _i, _vp, _vp],
@@ -76,7 +77,8 @@ QUERIES = {"irads_wgrad_workspace": (ctypes.c_long, [_i, _i, _i]),
            "irads_ln_bf16_partials": (ctypes.c_long, [_l, _i]),
            "irads_bnact_partials": (ctypes.c_long, [_l, _i]),
            "irads_winattn_bias_quads_size": (ctypes.c_long, [_i]),
-           "irads_msda_bwd_workspace_bytes": (ctypes.c_long, [_i, _i, _i, _i, _i, _i, _i, _i])}
+           "irads_msda_bwd_workspace_bytes": (ctypes.c_long, [_i, _i, _i, _i, _i, _i, _i, _i]),
+           "irads_dattn_attn_bwd_workspace_bytes": (ctypes.c_long, [_i] * 7)}
 CE_WORKSPACE = 2048
 
 _lib = None

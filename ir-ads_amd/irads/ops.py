@@ -419,13 +419,19 @@ class DAttnAttentionFn(torch.autograd.Function):
         B, nH, G, hc, H, W, n, Ht, Wt, scale = ctx.cfg
         gout = gout.contiguous().float()
         delta = torch.empty_like(lse)
-        # all six are atomically accumulated: zeroed by one fill (gq: key splits add into it;
-        # gk, gv key-major like k and v here)
-        gq, gk, gv, grpe, gpx, gpy = zeros_like_many(q, k, v, rpe, px, py)
+        # gq (key splits add into it) and grpe (per-workgroup flushes) are accumulated atomically:
+        # zeroed by one fill; gk, gv (key-major like k and v here), gpx, gpy are written from the
+        # pass-K partials in the workspace (deterministic)
+        gq, grpe = zeros_like_many(q, rpe)
+        gk, gv = torch.empty_like(k), torch.empty_like(v)
+        gpx, gpy = torch.empty_like(px), torch.empty_like(py)
+        ws_bytes = N.load().irads_dattn_attn_bwd_workspace_bytes(B, nH, G, hc, H, W, n)
+        ws = torch.empty((max(ws_bytes, 4) // 4,), device=q.device, dtype=torch.float32)
         ev = TIMER.start("dattn_bwd")
-        N.call("irads_dattn_attn_bwd", N.ptr(q), N.ptr(k), N.ptr(v), N.ptr(px), N.ptr(py), N.ptr(rpe), N.ptr(qgy),
+        N.call("irads_dattn_attn_bwd_ws", N.ptr(q), N.ptr(k), N.ptr(v), N.ptr(px), N.ptr(py), N.ptr(rpe), N.ptr(qgy),
                N.ptr(qgx), B, nH, G, hc, H, W, n, Ht, Wt, scale, N.ptr(out), N.ptr(lse), N.ptr(gout), N.ptr(delta),
-               N.ptr(gq), N.ptr(gk), N.ptr(gv), N.ptr(grpe), N.ptr(gpx), N.ptr(gpy), N.stream())
+               N.ptr(gq), N.ptr(gk), N.ptr(gv), N.ptr(grpe), N.ptr(gpx), N.ptr(gpy), N.ptr(ws), ws_bytes,
+               N.stream())
         TIMER.stop("dattn_bwd", ev, 8 * (2 * q.numel() + 2 * k.numel() + 2 * px.numel() + rpe.numel()),
                    88 * B * nH * H * W * 2 * n)  # backward = 2x the forward's 44 FLOP / pair
         return (gq, gk.transpose(1, 2), gv.transpose(1, 2), gpx, gpy, grpe, None, None, None, None, None, None, None,

@@ -230,13 +230,13 @@ def test_reference_driver_import_surface():
 
 def test_msda_gather_workspace_query(lib):
     """irads_msda_bwd_workspace_bytes is a pure size query (no GPU work): counters (bs*M*S), their
-    exclusive scan and one int per sample; 0 where the gather backward does not apply."""
+    exclusive scan and one 16-B record per sample; 0 where the gather backward does not apply."""
     q = lib.irads_msda_bwd_workspace_bytes
     q.restype = ctypes.c_long
     bs, S, M, D, L, Q, P = 2, 22223, 8, 32, 4, 22223, 4
     n = q(0, bs, S, M, D, L, Q, P)
-    assert n >= 4 * (2 * bs * M * S + bs * Q * M * L * P)
-    assert n < 4 * (2 * bs * M * S + bs * Q * M * L * P) + 8192 + 4 * (bs * M * S // 1024 + 1)
+    assert n >= 4 * (2 * bs * M * S) + 16 * bs * Q * M * L * P
+    assert n < 4 * (2 * bs * M * S) + 16 * bs * Q * M * L * P + 8192 + 4 * (bs * M * S // 1024 + 1)
     assert q(2, bs, S, M, D, L, Q, P) == 0  # fp64: the scatter kernel
     assert q(0, bs, S, M, 30, L, Q, P) == 0  # D not 4 * 2^k
     assert q(0, bs, S, M, 24, L, Q, P) == 0
@@ -249,6 +249,7 @@ def test_msda_gather_workspace_query(lib):
 # reference-precision mode).  Every kernel the training steps launch must not.
 SCRATCH_ALLOWED = ("winattn_bwd_bf16ILi0ELb1E", "winattn_bwd_bf16ILi1ELb1E", "winattn_bwd_bf16ILi2ELb1E",
                    "dattn_attn_bwd_k_kernelILi16E", "dattn_attn_bwd_k_kernelILi24E", "dattn_attn_bwd_q_kernelILi24E",
+                   "dattn_attn_bwd_k_band_kernelILi24E", "dattn_kpart_reduceILi24E", "dattn_kpart_reduceILi16E",
                    "dattn_sample_bwd_lds_kernelILi16E", "sb_drift_kernelIdE", "sb_em_kernelIdE",
                    "sb_logits_kernelIdE", "sb_potential_kernelIdE")
 
