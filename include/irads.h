@@ -134,11 +134,12 @@ int irads_dattn_attn_bwd(const float *q, const float *k, const float *v, const f
                          const float *out, const float *lse, const float *grad_out, float *delta,
                          float *grad_q, float *grad_k, float *grad_v, float *grad_rpe,
                          float *grad_pos_x, float *grad_pos_y, void *stream);
-/* Same as irads_dattn_attn_bwd with a caller-provided workspace (>= the query below, 4-B
- * aligned): the per-key pass writes per-query-chunk partial sums of grad_k / grad_v / grad_pos
- * there and a second launch adds them in chunk order, so those three are written (not added)
- * without float atomics and are bit-reproducible run to run.  grad_q / grad_rpe as above. */
-long irads_dattn_attn_bwd_workspace_bytes(int B, int nH, int G, int hc, int H, int W, int n);
+/* Same as irads_dattn_attn_bwd with a caller-provided workspace (>= the query below, 256-B
+ * aligned): both passes write their partial sums there (pass K per query chunk: grad_k, grad_v,
+ * grad_pos; pass Q per key split: grad_q, per workgroup: grad_rpe) and small launches add them
+ * in a fixed order.  All six outputs are then written, not added (no zero-fill needed), without
+ * float atomics, and are bit-reproducible run to run. */
+long irads_dattn_attn_bwd_workspace_bytes(int B, int nH, int G, int hc, int H, int W, int n, int Ht, int Wt);
 int irads_dattn_attn_bwd_ws(const float *q, const float *k, const float *v, const float *pos_x,
                             const float *pos_y, const float *rpe, const float *qgrid_y, const float *qgrid_x,
                             int B, int nH, int G, int hc, int H, int W, int n, int Ht, int Wt, float scale,

@@ -386,7 +386,8 @@ __global__ void __launch_bounds__(1024) dattn_attn_bwd_q_kernel(AttnArgs a, int 
                                                                 const float *__restrict__ lse,
                                                                 const float *__restrict__ gout,
                                                                 float *__restrict__ delta, float *__restrict__ gq,
-                                                                float *__restrict__ grpe) {
+                                                                float *__restrict__ grpe, float *__restrict__ dq_part,
+                                                                float *__restrict__ rpe_part) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
     __shared__ float red[16], vmx[16][HC];
     const int n2 = 2 * a.n, HW = a.H * a.W, PC = pad_cells(a.Ht, a.Wt);
@@ -481,7 +482,14 @@ __global__ void __launch_bounds__(1024) dattn_attn_bwd_q_kernel(AttnArgs a, int 
             atomicAdd(&tgi[bi.o + TP + 1], __float2int_rn(bi.wb.y * dsq));
         }
         if (valid) {
-            if (KSP > 1) {
+            if (KSP > 1 && dq_part) {  // this key split's dq, summed in split order by dattn_qpart_reduce
+                float *dp = dq_part + ((long)sp * gridDim.y + bh) * HC * HW + qi;
+#pragma unroll
+                for (int c = 0; c < HC / 2; ++c) {
+                    dp[(long)(2 * c) * HW] = dq[c].x;
+                    dp[(long)(2 * c + 1) * HW] = dq[c].y;
+                }
+            } else if (KSP > 1) {
 #pragma unroll
                 for (int c = 0; c < HC / 2; ++c) {
                     atomicAdd(&gq[((long)bh * HC + 2 * c) * HW + qi], dq[c].x);
@@ -498,11 +506,51 @@ __global__ void __launch_bounds__(1024) dattn_attn_bwd_q_kernel(AttnArgs a, int 
         }
     }
     __syncthreads();
+    if (rpe_part) {  // this workgroup's table gradient, every cell, summed by dattn_rpe_reduce in order
+        float *rp = rpe_part + ((long)blockIdx.y * gridDim.x + blockIdx.x) * a.Ht * a.Wt;
+        for (int i = threadIdx.x; i < a.Ht * a.Wt; i += blockDim.x) {
+            const int r = i / a.Wt, c = i - r * a.Wt;
+            rp[i] = (float)tgi[r * TP + c] * inv_fx;
+        }
+        return;
+    }
     for (int i = threadIdx.x; i < a.Ht * a.Wt; i += blockDim.x) {
         const int r = i / a.Wt, c = i - r * a.Wt;
         const int v = tgi[r * TP + c];
         if (v != 0) atomicAdd(&grpe[(long)h * a.Ht * a.Wt + i], (float)v * inv_fx);
     }
+}
+
+// Pass Q's partial sums, added in a fixed order (deterministic, no float atomics):
+// dq over the key splits, the table gradient over the (image, query-block) workgroups of a head.
+__global__ void __launch_bounds__(256) dattn_qpart_reduce(const float *__restrict__ part, int ksp, long per_split,
+                                                          float *__restrict__ gq) {
+    const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= per_split) return;
+    float acc = 0.f;
+    for (int sp = 0; sp < ksp; ++sp) acc += part[sp * per_split + t];
+    gq[t] = acc;
+}
+
+__global__ void __launch_bounds__(256) dattn_rpe_reduce(const float *__restrict__ part, int B, int nH, int nblk,
+                                                        int cells, float *__restrict__ grpe) {
+    const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (long)nH * cells) return;
+    const int h = (int)(t / cells), c = (int)(t - (long)h * cells);
+    // partial index i = b * nblk + blk; eight loads in flight, combined in a fixed order
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const int np = B * nblk;
+    for (int i0 = 0; i0 < np; i0 += 8) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int i = i0 + u;
+            if (i < np) {
+                const int b = i / nblk, k = i - b * nblk;
+                acc[u] += part[((long)(b * nH + h) * nblk + k) * cells + c];
+            }
+        }
+    }
+    grpe[t] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
 }
 
 // staged query records per pass-K step
@@ -971,18 +1019,35 @@ static void pass_k_plan(int B, int nH, int H, int W, int &chunks, int &qpb) {
     chunks = (HW + qpb - 1) / qpb;
 }
 
-extern "C" long irads_dattn_attn_bwd_workspace_bytes(int B, int nH, int G, int hc, int H, int W, int n) {
-    if (B <= 0 || nH <= 0 || G <= 0 || H <= 0 || W <= 0 || n <= 0 || hc <= 0) return 0;
-    int chunks, qpb;
+// workspace carve-up of the deterministic backward: pass-K partials | pass-Q dq partials (key
+// splits > 1) | pass-Q table-gradient partials; 256-B aligned pieces
+struct BwdWs {
+    long kpart, dqpart, rpepart, bytes;
+};
+static BwdWs bwd_ws_layout(int B, int nH, int hc, int H, int W, int n, int Ht, int Wt) {
+    int chunks, qpb, ksp, blocks;
     pass_k_plan(B, nH, H, W, chunks, qpb);
-    return (long)chunks * B * nH * (2 * hc + 2) * (2L * n) * (long)sizeof(float);
+    split_plan(H * W, B * nH, ksp, blocks);
+    auto al = [](long b) { return (b + 255) / 256 * 256; };
+    BwdWs w;
+    w.kpart = 0;
+    w.dqpart = al((long)chunks * B * nH * (2 * hc + 2) * (2L * n) * 4);
+    w.rpepart = w.dqpart + (ksp > 1 ? al((long)ksp * B * nH * hc * H * W * 4) : 0);
+    w.bytes = w.rpepart + al((long)B * nH * blocks * Ht * Wt * 4);
+    return w;
+}
+
+extern "C" long irads_dattn_attn_bwd_workspace_bytes(int B, int nH, int G, int hc, int H, int W, int n, int Ht,
+                                                     int Wt) {
+    if (B <= 0 || nH <= 0 || G <= 0 || H <= 0 || W <= 0 || n <= 0 || hc <= 0 || Ht <= 0 || Wt <= 0) return 0;
+    return bwd_ws_layout(B, nH, hc, H, W, n, Ht, Wt).bytes;
 }
 
 static int attn_bwd(const float *q, const float *k, const float *v, const float *pos_x, const float *pos_y,
                     const float *rpe, const float *qgrid_y, const float *qgrid_x, int B, int nH, int G, int hc, int H,
                     int W, int n, int Ht, int Wt, float scale, const float *out, const float *lse,
                     const float *grad_out, float *delta, float *grad_q, float *grad_k, float *grad_v, float *grad_rpe,
-                    float *grad_pos_x, float *grad_pos_y, float *part, void *stream) {
+                    float *grad_pos_x, float *grad_pos_y, char *ws, void *stream) {
     AttnArgs a{q, k, v, pos_x, pos_y, rpe, qgrid_y, qgrid_x, B, nH, G, hc, H, W, n, Ht, Wt, scale};
     if (int e = check_attn(a)) return e;
     IRADS_REQUIRE(hc <= 16, "dattn_attn: head channels %d > 16", hc);
@@ -1002,13 +1067,25 @@ static int attn_bwd(const float *q, const float *k, const float *v, const float 
     const int nr_max = band_rows_max(H, W, Ht, qpb);
     const size_t sh_kb = ((((size_t)nr_max * (Wt + 1) + 3) & ~(size_t)3) + (size_t)QCH * (2 * hc + 4)) * sizeof(float);
     IRADS_REQUIRE(sh_kb <= 160 * 1024, "dattn_attn_bwd: pass-K LDS request %zu exceeds 160 KiB", sh_kb);
+    const BwdWs wl = bwd_ws_layout(B, nH, hc, H, W, n, Ht, Wt);
+    float *part = ws ? (float *)(ws + wl.kpart) : nullptr;
+    float *dq_part = (ws && ksp > 1) ? (float *)(ws + wl.dqpart) : nullptr;
+    float *rpe_part = ws ? (float *)(ws + wl.rpepart) : nullptr;
     IRADS_HC_DISPATCH(hc, {
         (void)hipFuncSetAttribute((const void *)dattn_attn_bwd_q_kernel<HC>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)sh_q);
         (void)hipFuncSetAttribute((const void *)dattn_attn_bwd_k_band_kernel<HC>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh_kb);
         dattn_attn_bwd_q_kernel<HC><<<gq_grid, 1024, sh_q, st>>>(a, ksp, k, v, pos_x, pos_y, out, lse, grad_out, delta,
-                                                                 grad_q, grad_rpe);
+                                                                 grad_q, grad_rpe, dq_part, rpe_part);
+        if (dq_part) {
+            const long per = (long)B * nH * HC * HW;
+            dattn_qpart_reduce<<<(unsigned)((per + 255) / 256), 256, 0, st>>>(dq_part, ksp, per, grad_q);
+        }
+        if (rpe_part) {
+            const long t = (long)nH * Ht * Wt;
+            dattn_rpe_reduce<<<(unsigned)((t + 255) / 256), 256, 0, st>>>(rpe_part, B, nH, blocks, Ht * Wt, grad_rpe);
+        }
         dattn_attn_bwd_k_band_kernel<HC><<<gk_grid, kthreads, sh_kb, st>>>(a, k, v, pos_x, pos_y, lse, delta, grad_out,
                                                                            qpb, nr_max, grad_k, grad_v, grad_pos_x,
                                                                            grad_pos_y, part);
@@ -1038,11 +1115,11 @@ extern "C" int irads_dattn_attn_bwd_ws(const float *q, const float *k, const flo
                                        float *delta, float *grad_q, float *grad_k, float *grad_v, float *grad_rpe,
                                        float *grad_pos_x, float *grad_pos_y, void *workspace, long workspace_bytes,
                                        void *stream) {
-    const long need = irads_dattn_attn_bwd_workspace_bytes(B, nH, G, hc, H, W, n);
+    const long need = irads_dattn_attn_bwd_workspace_bytes(B, nH, G, hc, H, W, n, Ht, Wt);
     IRADS_REQUIRE(workspace && workspace_bytes >= need, "irads_dattn_attn_bwd_ws: workspace %ld B < %ld B",
                   workspace_bytes, need);
     return attn_bwd(q, k, v, pos_x, pos_y, rpe, qgrid_y, qgrid_x, B, nH, G, hc, H, W, n, Ht, Wt, scale, out, lse,
-                    grad_out, delta, grad_q, grad_k, grad_v, grad_rpe, grad_pos_x, grad_pos_y, (float *)workspace,
+                    grad_out, delta, grad_q, grad_k, grad_v, grad_rpe, grad_pos_x, grad_pos_y, (char *)workspace,
                     stream);
 }
 

@@ -419,13 +419,12 @@ class DAttnAttentionFn(torch.autograd.Function):
         B, nH, G, hc, H, W, n, Ht, Wt, scale = ctx.cfg
         gout = gout.contiguous().float()
         delta = torch.empty_like(lse)
-        # gq (key splits add into it) and grpe (per-workgroup flushes) are accumulated atomically:
-        # zeroed by one fill; gk, gv (key-major like k and v here), gpx, gpy are written from the
-        # pass-K partials in the workspace (deterministic)
-        gq, grpe = zeros_like_many(q, rpe)
+        # every gradient is written from partial sums in the workspace, added in a fixed order
+        # (no zero-fill, no float atomics: reproducible run to run); gk, gv key-major like k, v
+        gq, grpe = torch.empty_like(q), torch.empty_like(rpe)
         gk, gv = torch.empty_like(k), torch.empty_like(v)
         gpx, gpy = torch.empty_like(px), torch.empty_like(py)
-        ws_bytes = N.load().irads_dattn_attn_bwd_workspace_bytes(B, nH, G, hc, H, W, n)
+        ws_bytes = N.load().irads_dattn_attn_bwd_workspace_bytes(B, nH, G, hc, H, W, n, Ht, Wt)
         ws = torch.empty((max(ws_bytes, 4) // 4,), device=q.device, dtype=torch.float32)
         ev = TIMER.start("dattn_bwd")
         N.call("irads_dattn_attn_bwd_ws", N.ptr(q), N.ptr(k), N.ptr(v), N.ptr(px), N.ptr(py), N.ptr(rpe), N.ptr(qgy),

@@ -127,3 +127,48 @@ def test_dattn_amp_path_matches_module_path(tag):
             continue
         e_fast, e_mod = _rel(f, r), _rel(md, r)
         assert e_fast <= 1.5 * e_mod + 5e-3, (n, e_fast, e_mod)
+
+
+@pytest.mark.parametrize("tag", ["s0", "s3"])
+def test_dattn_attention_backward_is_reproducible(tag):
+    """The attention core's backward (irads_dattn_attn_bwd_ws) sums its partials in a fixed order:
+    two backward passes over the same inputs give bit-identical grad q, k, v, pos_x, pos_y and
+    rpe table (round-1 runs differed by ~0.8 % through float atomics); and
+    they match the atomic-accumulation entry (irads_dattn_attn_bwd) to fp32 summation-order noise."""
+    from irads import native as N
+    from irads.ops import DAttnAttentionFn
+    dims, stride, g, h, level, H, W, B = CFGS[tag]
+    hc = dims // h
+    Hk, Wk = H // stride, W // stride
+    torch.manual_seed(level + 3)
+    q = torch.randn(B * h, hc, H * W, device=DEV, requires_grad=True)
+    k = torch.randn(B * h, hc, 2 * Hk * Wk, device=DEV, requires_grad=True)
+    v = torch.randn(B * h, hc, 2 * Hk * Wk, device=DEV, requires_grad=True)
+    px = (torch.rand(B * g, Hk, Wk, 2, device=DEV) * 2 - 1).requires_grad_()
+    py = (torch.rand(B * g, Hk, Wk, 2, device=DEV) * 2 - 1).requires_grad_()
+    rpe = (torch.randn(h, 119, 159, device=DEV) * 0.1).requires_grad_()
+    qgy = torch.linspace(-1, 1, H, device=DEV)
+    qgx = torch.linspace(-1, 1, W, device=DEV)
+    go = torch.randn(B * h, hc, H * W, device=DEV)
+    ins = [q, k, v, px, py, rpe]
+
+    def grads():
+        o = DAttnAttentionFn.apply(q, k, v, px, py, rpe, qgy, qgx, B, h, g, H, W, hc ** -0.5)
+        return torch.autograd.grad(o, ins, go)
+
+    g1, g2 = grads(), grads()
+    for a, b_, name in zip(g1, g2, ("q", "k", "v", "pos_x", "pos_y", "rpe")):
+        assert torch.equal(a, b_), f"grad {name} differs between two identical backward passes"
+    # the atomic entry point on the same saved tensors
+    o = DAttnAttentionFn.apply(q, k, v, px, py, rpe, qgy, qgx, B, h, g, H, W, hc ** -0.5)
+    lse_src = o.grad_fn
+    qq, kk, vv, pxx, pyy, rp, qy, qx, out, lse = lse_src.saved_tensors
+    n = Hk * Wk
+    gq, gk, gv, gr, gpx, gpy = [torch.zeros_like(t) for t in (qq, kk, vv, rp, pxx, pyy)]
+    delta = torch.empty_like(lse)
+    N.call("irads_dattn_attn_bwd", N.ptr(qq), N.ptr(kk), N.ptr(vv), N.ptr(pxx), N.ptr(pyy), N.ptr(rp), N.ptr(qy),
+           N.ptr(qx), B, h, g, hc, H, W, n, 119, 159, hc ** -0.5, N.ptr(out), N.ptr(lse), N.ptr(go.contiguous()),
+           N.ptr(delta), N.ptr(gq), N.ptr(gk), N.ptr(gv), N.ptr(gr), N.ptr(gpx), N.ptr(gpy), N.stream())
+    for a, b_, name in ((gq, g1[0], "q"), (gk.transpose(1, 2), g1[1], "k"), (gv.transpose(1, 2), g1[2], "v"),
+                        (gpx, g1[3], "pos_x"), (gpy, g1[4], "pos_y"), (gr, g1[5], "rpe")):
+        assert _rel(a, b_) < 1e-5, (name, _rel(a, b_))

@@ -1,9 +1,10 @@
 """The training iteration captured into a HIP graph (irads/graph_step.py) against the eager
 iteration.  Eval mode removes the step's randomness (DropPath, Adapter dropout, apply_mask)
 and a zero learning rate keeps the weights fixed, so a replay must reproduce the eager
-loss (1e-5 relative) and every trainable parameter's gradient (8e-3 relative: float-atomic
-reordering in the DAttn sampling backward, and MIOpen's split-K bf16 convolution weight
-gradients, whose atomic order can move the bf16 rounding by one ulp, 2^-8).  Then a nonzero
+loss (1e-5 relative) and every trainable parameter's gradient (1.5e-2 relative: the remaining
+float-atomic reorderings - the DAttn feature-sampling backward's scatter and MIOpen's split-K
+bf16 convolution weight gradients, whose atomic order can move a bf16 rounding by one ulp, 2^-8;
+the DAttn attention core sums its partials in a fixed order since round 2).  Then a nonzero
 learning rate, filled into the device tensor between replays, must move the weights."""
 import pytest
 import torch
@@ -63,9 +64,9 @@ def test_graphed_step_matches_eager():
             ref = p0[n].grad
             den = torch.maximum(ref.norm(), 0.1 * rms * ref.numel() ** 0.5)
             err = ((p.grad - ref).norm() / den).item()
-            # both runs accumulate float atomics in a different order (DAttn table / offset
-            # gradients, split-K partials): observed 0.0075-0.0085 run to run on the DAttn and
-            # MPG stage-0 weights, a real graph-capture bug shows up at O(1)
+            # both runs accumulate float atomics in a different order (DAttn feature-sampling
+            # scatter, MIOpen split-K partials): round 1 observed 0.0075-0.0085 run to run on the
+            # DAttn and MPG stage-0 weights; a real graph-capture bug shows up at O(1)
             assert err < 1.5e-2, (n, err)
             n_checked += 1
     assert n_checked > 100
