@@ -532,25 +532,32 @@ __global__ void __launch_bounds__(256) dattn_qpart_reduce(const float *__restric
     gq[t] = acc;
 }
 
+// 64 cells per workgroup, its 4 waves sum interleaved quarters of the partials (4 loads in flight
+// each) and are combined through LDS in wave order: deterministic, 4x the parallelism of a
+// thread-per-cell loop (one (head, cell) row of partials is B * nblk long: 256 at stage 0)
 __global__ void __launch_bounds__(256) dattn_rpe_reduce(const float *__restrict__ part, int B, int nH, int nblk,
                                                         int cells, float *__restrict__ grpe) {
-    const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= (long)nH * cells) return;
-    const int h = (int)(t / cells), c = (int)(t - (long)h * cells);
-    // partial index i = b * nblk + blk; eight loads in flight, combined in a fixed order
-    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    __shared__ float red[4][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const long t = (long)blockIdx.x * 64 + lane;
+    const bool ok = t < (long)nH * cells;
+    const int h = ok ? (int)(t / cells) : 0, c = ok ? (int)(t - (long)h * cells) : 0;
     const int np = B * nblk;
-    for (int i0 = 0; i0 < np; i0 += 8) {
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int i = i0 + u;
-            if (i < np) {
-                const int b = i / nblk, k = i - b * nblk;
-                acc[u] += part[((long)(b * nH + h) * nblk + k) * cells + c];
-            }
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    if (ok) {
+        int i = w;
+        for (; i + 12 < np; i += 16) {
+            const int i1 = i + 4, i2 = i + 8, i3 = i + 12;
+            a0 += part[((long)((i / nblk) * nH + h) * nblk + i % nblk) * cells + c];
+            a1 += part[((long)((i1 / nblk) * nH + h) * nblk + i1 % nblk) * cells + c];
+            a2 += part[((long)((i2 / nblk) * nH + h) * nblk + i2 % nblk) * cells + c];
+            a3 += part[((long)((i3 / nblk) * nH + h) * nblk + i3 % nblk) * cells + c];
         }
+        for (; i < np; i += 4) a0 += part[((long)((i / nblk) * nH + h) * nblk + i % nblk) * cells + c];
     }
-    grpe[t] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+    red[w][lane] = (a0 + a1) + (a2 + a3);
+    __syncthreads();
+    if (w == 0 && ok) grpe[t] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
 }
 
 // staged query records per pass-K step
@@ -1084,7 +1091,7 @@ static int attn_bwd(const float *q, const float *k, const float *v, const float 
         }
         if (rpe_part) {
             const long t = (long)nH * Ht * Wt;
-            dattn_rpe_reduce<<<(unsigned)((t + 255) / 256), 256, 0, st>>>(rpe_part, B, nH, blocks, Ht * Wt, grad_rpe);
+            dattn_rpe_reduce<<<(unsigned)((t + 63) / 64), 256, 0, st>>>(rpe_part, B, nH, blocks, Ht * Wt, grad_rpe);
         }
         dattn_attn_bwd_k_band_kernel<HC><<<gk_grid, kthreads, sh_kb, st>>>(a, k, v, pos_x, pos_y, lse, delta, grad_out,
                                                                            qpb, nr_max, grad_k, grad_v, grad_pos_x,
