@@ -277,7 +277,7 @@ __global__ void __launch_bounds__(256) msda_bwd_kernel(const T *__restrict__ val
 // The reference's col2im adds every sample's 4 corner contributions into grad_value with float
 // atomics (ms_deform_im2col_cuda.cuh:301-921); at the DINO encoder shape that is 2.9 GB of atomic
 // adds per launch, held at the chip-wide float-atomic rate.  Here grad_value is GATHERED instead:
-//   1. count / scan / fill: samples are bucketed by (b, m, top-left corner cell) -- the corner
+//   1. count / scan / fill: samples are bucketed by (b, top-left corner cell, m) -- the corner
 //      clamped into the level, so a sample whose x0 or y0 is -1 sits in the cell of its one valid
 //      corner column / row; samples with no valid corner are dropped -- with int atomics on
 //      bs·M·S counters (one per sample, not per channel);
@@ -303,7 +303,7 @@ __device__ __forceinline__ long sample_bucket(const float *loc, long sid, int l,
     const Samp<float> sp = locate(loc[2 * sid], loc[2 * sid + 1], H, W);
     if (sp.x0 < -1 || sp.x0 >= W || sp.y0 < -1 || sp.y0 >= H) return -1;
     const int x = max(sp.x0, 0), y = max(sp.y0, 0);
-    return ((long)b * M + m) * S + sS[l] + y * W + x;
+    return ((long)b * S + sS[l] + y * W + x) * M + m;  // cell-major: a cell's M head counters share a line
 }
 
 __device__ __forceinline__ void load_levels(const int64_t *shapes, const int64_t *lsi, int L, int *sH, int *sW,
@@ -444,13 +444,13 @@ __global__ void __launch_bounds__(256) msda_gather_gvalue(const int64_t *__restr
     const int l = level_of(s, sS, L);
     const int H = sH[l], W = sW[l];
     const int c = s - sS[l], y = c / W, x = c - y * W;
-    const long bkb = ((long)b * M + m) * S;
+    const long bkb = (long)b * S;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
     for (int nb = 0; nb < 4; ++nb) {  // buckets of cells (y, x), (y, x-1), (y-1, x), (y-1, x-1)
         const int by = y - (nb >> 1), bx = x - (nb & 1);
         if (by < 0 || bx < 0) continue;  // uniform over the group
-        const long bk = bkb + sS[l] + by * W + bx;
+        const long bk = (bkb + sS[l] + by * W + bx) * M + m;
         const int e0 = off[bk], e1 = off[bk + 1];
         for (int e = e0; e < e1; e += V) {
             // lane j takes entry e + j: its sample's corner weight for this cell and its attention weight
