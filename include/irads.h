@@ -228,7 +228,7 @@ int irads_upsample_sum_fwd(int dtype, const void *base, const void *const *srcs,
  * not NULL it receives the MMST target of train_mm.py:137-141: target where
  * argmax_c(logits) == target, ignore_index elsewhere.  workspace: IRADS_CE_WORKSPACE doubles.
  * Targets outside [0, C) other than ignore_index are treated as ignored. */
-#define IRADS_CE_WORKSPACE 2048
+#define IRADS_CE_WORKSPACE 8192
 int irads_ce_fwd(int dtype, const void *logits, const int64_t *strides, int B, int C, int H, int W,
                  const int64_t *target, int ignore_index, const float *class_weight, float *lse,
                  int64_t *match_target, double *workspace, float *loss, void *stream);

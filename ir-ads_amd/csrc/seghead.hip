@@ -346,7 +346,8 @@ __global__ void __launch_bounds__(256) confusion_kernel(const T *__restrict__ x,
 }
 
 // ------------------------------------------------------------------ cross-entropy
-constexpr int CE_GRID = 1024;  // fixed grid: deterministic partial sums (IRADS_CE_WORKSPACE)
+constexpr int CE_GRID = 4096;  // fixed grid: deterministic partial sums (IRADS_CE_WORKSPACE); 16 per CU so one
+                               // workgroup's tile loads overlap the others' compute
 
 __device__ __forceinline__ double block_sum_d(double v, double *red) {
 #pragma unroll
@@ -417,8 +418,13 @@ __global__ void __launch_bounds__(1024) ce_finalize(const double *__restrict__ p
                                                     float *__restrict__ loss) {
     __shared__ double sa[1024], sb[1024];
     const int t = threadIdx.x;
-    sa[t] = t < nblk ? part[2 * t] : 0.0;
-    sb[t] = t < nblk ? part[2 * t + 1] : 0.0;
+    double a = 0.0, b = 0.0;
+    for (int i = t; i < nblk; i += 1024) {  // fixed order
+        a += part[2 * i];
+        b += part[2 * i + 1];
+    }
+    sa[t] = a;
+    sb[t] = b;
     __syncthreads();
     for (int o = 512; o > 0; o >>= 1) {
         if (t < o) {

@@ -79,7 +79,7 @@ QUERIES = {"irads_wgrad_workspace": (ctypes.c_long, [_i, _i, _i]),
            "irads_winattn_bias_quads_size": (ctypes.c_long, [_i]),
            "irads_msda_bwd_workspace_bytes": (ctypes.c_long, [_i, _i, _i, _i, _i, _i, _i, _i]),
            "irads_dattn_attn_bwd_workspace_bytes": (ctypes.c_long, [_i] * 9)}
-CE_WORKSPACE = 2048
+CE_WORKSPACE = 8192
 
 _lib = None
 
