@@ -33,6 +33,14 @@ Data parallel (world > 1; train_mm.py:94 / DDP semantics: gradients averaged ove
 import torch
 import torch.distributed as dist
 
+# "thread_local": only the capturing thread's capture-unsafe HIP calls are refused.  In the
+# default "global" mode a call from any thread of the process fails while a capture is open,
+# and a process with an RCCL communicator has threads of its own (RCCL's proxy thread, the
+# process group's watchdog) that poll events and streams at any time: a poll that lands inside
+# the capture window gets an error it treats as fatal.  Kernel launches from the autograd
+# thread onto the capturing stream are still recorded (capture is per stream).
+CAPTURE_MODE = "thread_local"
+
 
 class GraphedTrainStep:
     """restore: tensors (parameters, BN buffers) to snapshot before the warm-up iterations and
@@ -77,15 +85,15 @@ class GraphedTrainStep:
         self.graph = torch.cuda.CUDAGraph()
         self.opt_graph = None
         if self.comm == "split":
-            with torch.cuda.graph(self.graph):
+            with torch.cuda.graph(self.graph, capture_error_mode=CAPTURE_MODE):
                 self.loss = fwd_bwd()
                 pack_grads(self.params, self.flat)
             self.opt_graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.opt_graph, pool=self.graph.pool()):
+            with torch.cuda.graph(self.opt_graph, pool=self.graph.pool(), capture_error_mode=CAPTURE_MODE):
                 unpack_grads(self.params, self.flat, 1.0 / self.world)
                 optimizer.step()
         else:
-            with torch.cuda.graph(self.graph):
+            with torch.cuda.graph(self.graph, capture_error_mode=CAPTURE_MODE):
                 self.loss = self._run(fwd_bwd, capture=True)
                 optimizer.step()
         if snap is not None:

@@ -45,9 +45,11 @@ def main():
     rank, world, port, out = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4]
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = port
+    import datetime
     import torch
     import torch.distributed as dist
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # a peer that dies surfaces as a collective timeout well inside the test's own bound
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=90))
     from irads.graph_step import GraphedTrainStep
     dev = torch.device("cuda", 0)
     m = model(dev)

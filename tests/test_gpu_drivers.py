@@ -286,7 +286,13 @@ def test_dp_two_ranks_gradients(tmp_path):
     env = dict(os.environ)
     procs = [subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "_dp_worker.py"), str(r), "2", port, out],
                               env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT) for r in range(2)]
-    logs = [p.communicate(timeout=240)[0].decode()[-2000:] for p in procs]
+    try:
+        logs = [p.communicate(timeout=150)[0].decode()[-2000:] for p in procs]
+    finally:
+        for p in procs:  # our own children only
+            if p.poll() is None:
+                p.kill()
+                p.wait()
     assert all(p.returncode == 0 for p in procs), logs
     got = torch.load(out, weights_only=True)
     dev = torch.device("cuda", 0)
