@@ -203,8 +203,11 @@ __global__ __launch_bounds__(256) void wgrad_partial_kernel(WProbs probs, int K,
 
 // sum the per-split partials: out[e] = alpha * sum_s ws[s][e] (+ out[e]), for every problem's
 // weight block and column-sum vectors in one launch (segments by blockIdx).  A workgroup
-// owns 64 consecutive elements (coalesced across lanes); its 16 waves take the splits
-// s = w, w+16, ... and are combined in wave order through LDS: a fixed summation order.
+// owns 64 consecutive elements (coalesced across lanes); its NW waves take the splits
+// s = w, w+NW, ... and are combined in wave order through LDS: a fixed summation order.
+// NW follows nsplit (about 8 partials per lane): a few-split reduce of a large weight block
+// then runs one wave per 64 elements instead of 16 mostly idle ones (wave launches, not
+// bytes, set the time of those launches).
 struct Seg {
     const float *ws;
     float *out;
@@ -215,10 +218,10 @@ struct Segs {
     Seg s[3 * kMaxBatch];
     int nseg;
 };
-constexpr int kRedWaves = 16;  // waves per reduce workgroup: splits s = w, w + 16, ... per wave
-__global__ __launch_bounds__(64 * kRedWaves) void wgrad_reduce_kernel(Segs segs, int nsplit, float alpha,
-                                                                    int accumulate, int m, int n) {
-    __shared__ float part[kRedWaves][64];
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void wgrad_reduce_kernel(Segs segs, int nsplit, float alpha, int accumulate,
+                                                             int m, int n) {
+    __shared__ float part[NW][64];
     int blk = blockIdx.x;
     Seg sg = segs.s[0];  // segment walk with constant indices (no scratch copy of the argument)
 #pragma unroll
@@ -234,18 +237,23 @@ __global__ __launch_bounds__(64 * kRedWaves) void wgrad_reduce_kernel(Segs segs,
     float acc[4] = {0.f, 0.f, 0.f, 0.f};
     if (e < count) {
         int p = w;
-        for (; p + 3 * kRedWaves < nsplit; p += 4 * kRedWaves) {  // 4 independent loads in flight per lane
+        for (; p + 3 * NW < nsplit; p += 4 * NW) {  // 4 independent loads in flight per lane
 #pragma unroll
-            for (int u = 0; u < 4; ++u) acc[u] += sg.ws[(long)(p + u * kRedWaves) * count + e];
+            for (int u = 0; u < 4; ++u) acc[u] += sg.ws[(long)(p + u * NW) * count + e];
         }
-        for (; p < nsplit; p += kRedWaves) acc[0] += sg.ws[(long)p * count + e];
+        for (; p < nsplit; p += NW) acc[0] += sg.ws[(long)p * count + e];
     }
-    part[w][lane] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
-    __syncthreads();
-    if (w == 0 && e < count) {
-        float t = 0.f;
+    float t = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+    if (NW > 1) {
+        part[w][lane] = t;
+        __syncthreads();
+        if (w == 0) {
+            t = 0.f;
 #pragma unroll
-        for (int i = 0; i < kRedWaves; ++i) t += part[i][lane];  // fixed wave order: deterministic
+            for (int i = 0; i < NW; ++i) t += part[i][lane];  // fixed wave order: deterministic
+        }
+    }
+    if (w == 0 && e < count) {
         t *= alpha;
         long o = e;
         if (sg.transpose) {  // element (i, j) of the m x n result stored at (j, i)
@@ -351,8 +359,17 @@ extern "C" int irads_wgrad_batched(int count, const irads_wgrad_problem *problem
     }
     int blocks = 0;
     for (int i = 0; i < segs.nseg; ++i) blocks += segs.s[i].blocks;
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(64 * kRedWaves), 0, st, segs, (int)nsplit, alpha,
-                       accumulate, m, n);
+    const int ns = (int)nsplit;
+    if (nsplit >= 128)
+        hipLaunchKernelGGL(wgrad_reduce_kernel<16>, dim3(blocks), dim3(64 * 16), 0, st, segs, ns, alpha, accumulate, m, n);
+    else if (nsplit >= 64)
+        hipLaunchKernelGGL(wgrad_reduce_kernel<8>, dim3(blocks), dim3(64 * 8), 0, st, segs, ns, alpha, accumulate, m, n);
+    else if (nsplit >= 32)
+        hipLaunchKernelGGL(wgrad_reduce_kernel<4>, dim3(blocks), dim3(64 * 4), 0, st, segs, ns, alpha, accumulate, m, n);
+    else if (nsplit >= 16)
+        hipLaunchKernelGGL(wgrad_reduce_kernel<2>, dim3(blocks), dim3(64 * 2), 0, st, segs, ns, alpha, accumulate, m, n);
+    else
+        hipLaunchKernelGGL(wgrad_reduce_kernel<1>, dim3(blocks), dim3(64), 0, st, segs, ns, alpha, accumulate, m, n);
     return check_launch("irads_wgrad reduce");
 }
 
