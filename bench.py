@@ -51,6 +51,9 @@ def parse():
     p.add_argument("--eager", action="store_true", help="launch op by op (default: replay a captured HIP graph)")
     p.add_argument("--no-tuned-gemms", action="store_true", help="hipBLASLt default picks (ignore irads/tuned/)")
     p.add_argument("--no-kernels", action="store_true", help="skip the MSDeformAttn (C5) kernel roofline lines")
+    p.add_argument("--deterministic", action="store_true",
+                   help="MIOpen deterministic solvers: the whole step is then bit-reproducible "
+                        "(scripts/determinism_probe.py); the reference's setup_cudnn leaves it off")
     return p.parse_args()
 
 
@@ -306,6 +309,7 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     device = torch.device("cuda", local_rank)
     torch.backends.cudnn.benchmark = True
+    torch.backends.cudnn.deterministic = args.deterministic
     random.seed(3407 + rank)
     np.random.seed(3407 + rank)
     torch.manual_seed(3407 + rank)
@@ -403,7 +407,8 @@ def main():
                                       "with the backward, inside the graph", "split": "one flat all-reduce between "
                                       "backward and optimizer graphs"}[runner.comm] if graph else
                                      ("DDP buckets" if world > 1 else "none (1 rank)")),
-                   "gemm_selection": "TunableOp table irads/tuned" if tuned else "hipBLASLt heuristic"},
+                   "gemm_selection": "TunableOp table irads/tuned" if tuned else "hipBLASLt heuristic",
+                   "miopen": "deterministic solvers" if args.deterministic else "benchmark (fastest) solvers"},
         "loss": round(loss_val, 5),
     }
     if fwd:
