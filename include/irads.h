@@ -114,6 +114,16 @@ int irads_dattn_sample_bwd(const float *x, const float *y, const float *q, const
                            const float *pos_y, const float *gxs, const float *gys, const float *gqs,
                            int B, int C, int H, int W, int G, int n, float *grad_x, float *grad_y,
                            float *grad_q, float *grad_pos_x, float *grad_pos_y, void *stream);
+/* Same with a caller-provided workspace (>= the query below, 256-B aligned): the input gradients
+ * accumulate as int64 fixed point (per (tensor, map) power-of-two scale from the sum of |grad|
+ * over the map's samples; integer adds are exact and order-independent) and are then written as
+ * fp32, so grad_x/grad_y/grad_q need no zero-fill and are bit-reproducible run to run. */
+long irads_dattn_sample_bwd_workspace_bytes(int B, int C, int H, int W, int G);
+int irads_dattn_sample_bwd_ws(const float *x, const float *y, const float *q, const float *pos_x,
+                              const float *pos_y, const float *gxs, const float *gys, const float *gqs,
+                              int B, int C, int H, int W, int G, int n, float *grad_x, float *grad_y,
+                              float *grad_q, float *grad_pos_x, float *grad_pos_y, void *workspace,
+                              long workspace_bytes, void *stream);
 /* Fused attention with on-the-fly bilinear rpe bias (swin.py:950-1016):
  *   q (B*nH, hc, HW)  k, v KEY-MAJOR (B*nH, 2n, hc)  rpe (nH, Ht, Wt)  qgrid_y (H), qgrid_x (W)
  *   (the reference's _get_q_grid values)  out (B*nH, hc, HW)  lse (B*nH, HW).

@@ -7,7 +7,8 @@
 //    align_corners=True zero padding.  The six reference grid_sample calls become one
 //    launch; the sampled tensors are tiny (B, C, 2n).  Corner indices use the CPU
 //    grid_sample arithmetic ix = (gx + 1) * ((W-1)/2) (no FMA) — bit-exact with the
-//    reference (oracle/csrc/sampling_oracle.c).
+//    reference (oracle/csrc/sampling_oracle.c).  The backward's scatter into the feature-map
+//    gradients accumulates in int64 fixed point (irads_dattn_sample_bwd_ws): reproducible.
 //
 // 2. Fused attention with an on-the-fly bilinear relative-position bias
 //    (swin.py:950-1016): out = softmax(scale·qᵀk + rpe_bias) v over 2n keys per query,
@@ -86,6 +87,21 @@ __device__ __forceinline__ void scatter(float *plane, int H, int W, const Corner
     if (yh && xh) atomicAdd(plane + o + W + 1, c.se * g);
 }
 
+// Fixed-point variant for the reproducible backward: the contribution w * g scaled by the map's
+// power-of-two scale (dattn_sample_bound) is rounded to int64 and added with an integer atomic,
+// which is exact and order-independent; |Σ| <= Σ |w g| · scale <= 2^62 cannot overflow.
+typedef unsigned long long u64;
+__device__ __forceinline__ u64 fx64(float v, float sc) { return (u64)__float2ll_rn(v * sc); }
+__device__ __forceinline__ void scatter_fx(u64 *plane, int H, int W, const Corner &c, float g, float sc) {
+    const bool xl = c.x0 >= 0 && c.x0 < W, xh = c.x0 + 1 >= 0 && c.x0 + 1 < W;
+    const bool yl = c.y0 >= 0 && c.y0 < H, yh = c.y0 + 1 >= 0 && c.y0 + 1 < H;
+    const long o = (long)c.y0 * W + c.x0;
+    if (yl && xl) atomicAdd(plane + o, fx64(c.nw * g, sc));
+    if (yl && xh) atomicAdd(plane + o + 1, fx64(c.ne * g, sc));
+    if (yh && xl) atomicAdd(plane + o + W, fx64(c.sw * g, sc));
+    if (yh && xh) atomicAdd(plane + o + W + 1, fx64(c.se * g, sc));
+}
+
 // ---------------------------------------------------------------- feature sampling
 __global__ void dattn_sample_fwd_kernel(const float *__restrict__ x, const float *__restrict__ y,
                                         const float *__restrict__ q, const float *__restrict__ px,
@@ -113,13 +129,16 @@ __device__ __forceinline__ void dsample(const Taps &t, const Corner &c, float g,
 
 // thread per (b, group, key, channel-in-group); the GP lanes of one (b, group, key) hold
 // its channels, so d(pos) is a shuffle reduction over GP lanes (no atomics on pos)
-template <int GP>
+// FX: the input gradients go to the int64 fixed-point accumulators acc[3][B][C][H][W] with the
+// per-(tensor, map) scales scl[3][B*G] (reproducible); otherwise float atomics into gx / gy / gq
+template <int GP, bool FX>
 __global__ void dattn_sample_bwd_kernel(const float *__restrict__ x, const float *__restrict__ y,
                                         const float *__restrict__ q, const float *__restrict__ px,
                                         const float *__restrict__ py, const float *__restrict__ gxs,
                                         const float *__restrict__ gys, const float *__restrict__ gqs, int B, int C,
                                         int H, int W, int G, int n, float *__restrict__ gx, float *__restrict__ gy,
-                                        float *__restrict__ gq, float *__restrict__ gpx, float *__restrict__ gpy) {
+                                        float *__restrict__ gq, float *__restrict__ gpx, float *__restrict__ gpy,
+                                        u64 *__restrict__ acc, const float *__restrict__ scl) {
     const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
     const long total = (long)B * G * 2 * n * GP;
     if (i >= total) return;  // total is a multiple of GP: whole groups exit together
@@ -141,9 +160,17 @@ __global__ void dattn_sample_bwd_kernel(const float *__restrict__ x, const float
         dsample(taps(x + plane, H, W, cr), cr, g1, dix, diy);
         dsample(taps(y + plane, H, W, cr), cr, g2, dix, diy);
         dsample(taps(q + plane, H, W, cr), cr, g3, dix, diy);
-        scatter(gx + plane, H, W, cr, g1);
-        scatter(gy + plane, H, W, cr, g2);
-        scatter(gq + plane, H, W, cr, g3);
+        if (FX) {
+            const long tstride = (long)B * C * H * W;
+            const int map = b * G + gi, nm = B * G;
+            scatter_fx(acc + plane, H, W, cr, g1, scl[map]);
+            scatter_fx(acc + tstride + plane, H, W, cr, g2, scl[nm + map]);
+            scatter_fx(acc + 2 * tstride + plane, H, W, cr, g3, scl[2 * nm + map]);
+        } else {
+            scatter(gx + plane, H, W, cr, g1);
+            scatter(gy + plane, H, W, cr, g2);
+            scatter(gq + plane, H, W, cr, g3);
+        }
     }
 #pragma unroll
     for (int o = GP / 2; o > 0; o >>= 1) {
@@ -163,14 +190,17 @@ __global__ void dattn_sample_bwd_kernel(const float *__restrict__ x, const float
 // out once; `per_pass` of the three tensors (x, y, q) are accumulated per pass (the launcher
 // uses 3: all in LDS at once), the position gradient stays in registers across passes and is
 // reduced over the GP channel lanes at the end (same accumulation order as the kernel above).
-template <int GP, int SPT, int NT>
+// FX: the LDS accumulators are int64 fixed point at the scales scl[3][B*G] (ds_add_u64 is
+// also ~10x the rate of ds_add_f32 on gfx950), reproducible; otherwise float LDS atomics.
+template <int GP, int SPT, int NT, bool FX>
 __global__ __launch_bounds__(NT) void dattn_sample_bwd_lds_kernel(
     const float *__restrict__ x, const float *__restrict__ y, const float *__restrict__ q,
     const float *__restrict__ px, const float *__restrict__ py, const float *__restrict__ gxs,
     const float *__restrict__ gys, const float *__restrict__ gqs, int C, int H, int W, int G, int n, int per_pass,
     float *__restrict__ gx, float *__restrict__ gy, float *__restrict__ gq, float *__restrict__ gpx,
-    float *__restrict__ gpy) {
-    extern __shared__ float acc[];
+    float *__restrict__ gpy, const float *__restrict__ scl, int nmaps) {
+    extern __shared__ __attribute__((aligned(16))) float acc[];
+    u64 *acc64 = reinterpret_cast<u64 *>(acc);
     constexpr int SLOTS = NT / GP;
     const int map = blockIdx.x, b = map / G, gi = map % G, gc = C / G, HW = H * W;
     const int slot = threadIdx.x / GP, cc = threadIdx.x % GP;
@@ -183,7 +213,10 @@ __global__ __launch_bounds__(NT) void dattn_sample_bwd_lds_kernel(
     for (int it = 0; it < SPT; ++it) dix[it] = diy[it] = 0.f;
     const long cbase = (long)b * C + gi * gc;  // first channel of this map
     for (int t0 = 0; t0 < 3; t0 += per_pass) {
-        for (int i = threadIdx.x; i < per_pass * gc * HW; i += NT) acc[i] = 0.f;
+        for (int i = threadIdx.x; i < per_pass * gc * HW; i += NT) {
+            if (FX) acc64[i] = 0ull;
+            else acc[i] = 0.f;
+        }
         __syncthreads();
 #pragma unroll
         for (int it = 0; it < SPT; ++it) {
@@ -200,17 +233,30 @@ __global__ __launch_bounds__(NT) void dattn_sample_bwd_lds_kernel(
                 const long plane = (cbase + cc) * HW;
                 const float g = gouts[t][(cbase + cc) * ns + j2];
                 dsample(taps(planes[t] + plane, H, W, cr), cr, g, dix[it], diy[it]);
-                float *a = acc + (tt * gc + cc) * HW;
-                if (yl && xl) atomicAdd(a + o, cr.nw * g);
-                if (yl && xh) atomicAdd(a + o + 1, cr.ne * g);
-                if (yh && xl) atomicAdd(a + o + W, cr.sw * g);
-                if (yh && xh) atomicAdd(a + o + W + 1, cr.se * g);
+                if (FX) {
+                    u64 *a = acc64 + (tt * gc + cc) * HW;
+                    const float sc = scl[t * nmaps + map];
+                    if (yl && xl) atomicAdd(a + o, fx64(cr.nw * g, sc));
+                    if (yl && xh) atomicAdd(a + o + 1, fx64(cr.ne * g, sc));
+                    if (yh && xl) atomicAdd(a + o + W, fx64(cr.sw * g, sc));
+                    if (yh && xh) atomicAdd(a + o + W + 1, fx64(cr.se * g, sc));
+                } else {
+                    float *a = acc + (tt * gc + cc) * HW;
+                    if (yl && xl) atomicAdd(a + o, cr.nw * g);
+                    if (yl && xh) atomicAdd(a + o + 1, cr.ne * g);
+                    if (yh && xl) atomicAdd(a + o + W, cr.sw * g);
+                    if (yh && xh) atomicAdd(a + o + W + 1, cr.se * g);
+                }
             }
         }
         __syncthreads();
         for (int i = threadIdx.x; i < per_pass * gc * HW; i += NT) {
             const int tt = i / (gc * HW), r = i - tt * gc * HW;
-            gins[t0 + tt][cbase * HW + r] = acc[i];
+            if (FX)
+                gins[t0 + tt][cbase * HW + r] =
+                    (float)((double)(long long)acc64[i] * (1.0 / (double)scl[(t0 + tt) * nmaps + map]));
+            else
+                gins[t0 + tt][cbase * HW + r] = acc[i];
         }
         __syncthreads();
     }
@@ -231,6 +277,53 @@ __global__ __launch_bounds__(NT) void dattn_sample_bwd_lds_kernel(
             gp[1] = dx_ * (((float)W - 1.0f) / 2.0f);
         }
     }
+}
+
+// Per (tensor, map) fixed-point scale of the reproducible sampling backward: B = Σ |g| over the
+// map's gc channels x 2n samples bounds every cell's |Σ w g| (bilinear weights sum to <= 1), and
+// scale = 2^(62 - ceil(log2 B)) keeps it inside int64 (resolution B·2^-63).  The block sums in
+// a fixed order.  grid (B*G, 3), 1024 threads (a map is gc·2n <= 64·2n values: ~8 loads a lane).
+__global__ void __launch_bounds__(1024) dattn_sample_bound_kernel(const float *__restrict__ gxs,
+                                                                  const float *__restrict__ gys,
+                                                                  const float *__restrict__ gqs, int C, int G, int n,
+                                                                  float *__restrict__ scl) {
+    __shared__ float red[16];
+    const int map = blockIdx.x, t = blockIdx.y, gc = C / G;
+    const int b = map / G, gi = map % G;
+    const float *src = t == 0 ? gxs : (t == 1 ? gys : gqs);
+    const long base = ((long)b * C + (long)gi * gc) * 2 * n, cnt = (long)gc * 2 * n;
+    float a[4] = {0.f, 0.f, 0.f, 0.f};
+    long i = threadIdx.x;
+    for (; i + 3 * 1024 < cnt; i += 4 * 1024) {  // four loads in flight
+#pragma unroll
+        for (int u = 0; u < 4; ++u) a[u] += fabsf(src[base + i + u * 1024]);
+    }
+    for (; i < cnt; i += 1024) a[0] += fabsf(src[base + i]);
+    float v = wave_sum((a[0] + a[1]) + (a[2] + a[3]));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float tot = 0.f;
+        for (int w = 0; w < 16; ++w) tot += red[w];
+        const int e = (tot > 0.f && tot < 1e30f) ? min(100, 62 - (int)ceilf(log2f(tot))) : 0;
+        scl[(long)t * gridDim.x + map] = ldexpf(1.f, e);
+    }
+}
+
+// int64 fixed point -> fp32 gradients of x, y, q: acc[3][B][C][HW] at the scales scl[3][B*G]
+__global__ void __launch_bounds__(256) dattn_sample_fx_out(const u64 *__restrict__ acc, const float *__restrict__ scl,
+                                                           int B, int C, int HW, int G, float *__restrict__ gx,
+                                                           float *__restrict__ gy, float *__restrict__ gq) {
+    const long per = (long)B * C * HW;
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= 3 * per) return;
+    const int t = (int)(i / per);
+    const long r = i - t * per;
+    const long bc = r / HW;
+    const int b = (int)(bc / C), c = (int)(bc - (long)b * C);
+    const int map = b * G + c / (C / G);
+    float *out = t == 0 ? gx : (t == 1 ? gy : gq);
+    out[r] = (float)((double)(long long)acc[i] * (1.0 / (double)scl[(long)t * B * G + map]));
 }
 
 // ---------------------------------------------------------------- fused attention
@@ -951,10 +1044,14 @@ extern "C" int irads_dattn_sample_fwd(const float *x, const float *y, const floa
     return check_launch("irads_dattn_sample_fwd");
 }
 
-extern "C" int irads_dattn_sample_bwd(const float *x, const float *y, const float *q, const float *pos_x,
-                                      const float *pos_y, const float *gxs, const float *gys, const float *gqs, int B,
-                                      int C, int H, int W, int G, int n, float *grad_x, float *grad_y, float *grad_q,
-                                      float *grad_pos_x, float *grad_pos_y, void *stream) {
+static size_t sample_ws_scl_offset(int B, int C, int H, int W) {
+    return ((size_t)3 * B * C * H * W * sizeof(u64) + 255) & ~(size_t)255;
+}
+
+static int sample_bwd(const float *x, const float *y, const float *q, const float *pos_x, const float *pos_y,
+                      const float *gxs, const float *gys, const float *gqs, int B, int C, int H, int W, int G, int n,
+                      float *grad_x, float *grad_y, float *grad_q, float *grad_pos_x, float *grad_pos_y, char *ws,
+                      void *stream) {
     IRADS_REQUIRE(B >= 0 && C > 0 && G > 0 && C % G == 0 && n > 0 && H > 0 && W > 0, "dattn_sample: bad sizes");
     const int gc = C / G;
     IRADS_REQUIRE(gc <= 64, "dattn_sample: group channels %d > 64", gc);
@@ -964,25 +1061,77 @@ extern "C" int irads_dattn_sample_bwd(const float *x, const float *y, const floa
     if (total == 0) return IRADS_OK;
     const unsigned grid = (unsigned)((total + 255) / 256);
     hipStream_t st = (hipStream_t)stream;
+    const bool fx = ws != nullptr;
+    u64 *acc = fx ? reinterpret_cast<u64 *>(ws) : nullptr;
+    float *scl = fx ? reinterpret_cast<float *>(ws + sample_ws_scl_offset(B, C, H, W)) : nullptr;
+    if (fx) hipLaunchKernelGGL(dattn_sample_bound_kernel, dim3(B * G, 3), dim3(1024), 0, st, gxs, gys, gqs, C, G, n, scl);
     // small maps: a workgroup per (b, group) map with LDS accumulation (see the kernel)
     const long plane_bytes = (long)gc * H * W * 4;
     // (all three tensors' planes in LDS at once; a map too big for that runs faster on the
-    // global-atomic kernel than in three sequential LDS passes - measured at 32x32 x 16 ch)
+    // global-atomic kernel than in three sequential LDS passes - measured at 32x32 x 16 ch);
+    // the fixed-point accumulators take twice the bytes
     const int per_pass = 3 * plane_bytes <= 64 * 1024 ? 3 : 0;
     if (per_pass && GP == 16 && (2 * n + 63) / 64 <= 8) {
-        hipLaunchKernelGGL((dattn_sample_bwd_lds_kernel<16, 8, 1024>), dim3(B * G), dim3(1024),
-                           (size_t)per_pass * plane_bytes, st, x, y, q, pos_x, pos_y, gxs, gys, gqs, C, H, W, G, n,
-                           per_pass, grad_x, grad_y, grad_q, grad_pos_x, grad_pos_y);
+        const size_t sh = (size_t)per_pass * plane_bytes * (fx ? 2 : 1);
+        if (fx) {
+            (void)hipFuncSetAttribute((const void *)dattn_sample_bwd_lds_kernel<16, 8, 1024, true>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
+            hipLaunchKernelGGL((dattn_sample_bwd_lds_kernel<16, 8, 1024, true>), dim3(B * G), dim3(1024), sh, st, x, y,
+                               q, pos_x, pos_y, gxs, gys, gqs, C, H, W, G, n, per_pass, grad_x, grad_y, grad_q,
+                               grad_pos_x, grad_pos_y, scl, B * G);
+        } else {
+            hipLaunchKernelGGL((dattn_sample_bwd_lds_kernel<16, 8, 1024, false>), dim3(B * G), dim3(1024), sh, st, x,
+                               y, q, pos_x, pos_y, gxs, gys, gqs, C, H, W, G, n, per_pass, grad_x, grad_y, grad_q,
+                               grad_pos_x, grad_pos_y, nullptr, B * G);
+        }
         return check_launch("irads_dattn_sample_bwd (LDS)");
     }
-#define IRADS_SB(P)                                                                                             \
-    case P:                                                                                                     \
-        dattn_sample_bwd_kernel<P><<<grid, 256, 0, st>>>(x, y, q, pos_x, pos_y, gxs, gys, gqs, B, C, H, W, G, n, \
-                                                         grad_x, grad_y, grad_q, grad_pos_x, grad_pos_y);       \
+    if (fx) (void)hipMemsetAsync(acc, 0, (size_t)3 * B * C * H * W * sizeof(u64), st);
+#define IRADS_SB(P)                                                                                                 \
+    case P:                                                                                                         \
+        if (fx)                                                                                                     \
+            dattn_sample_bwd_kernel<P, true><<<grid, 256, 0, st>>>(x, y, q, pos_x, pos_y, gxs, gys, gqs, B, C, H, W, \
+                                                                   G, n, grad_x, grad_y, grad_q, grad_pos_x,        \
+                                                                   grad_pos_y, acc, scl);                           \
+        else                                                                                                        \
+            dattn_sample_bwd_kernel<P, false><<<grid, 256, 0, st>>>(x, y, q, pos_x, pos_y, gxs, gys, gqs, B, C, H,   \
+                                                                    W, G, n, grad_x, grad_y, grad_q, grad_pos_x,    \
+                                                                    grad_pos_y, nullptr, nullptr);                  \
         break;
     switch (GP) { IRADS_SB(1) IRADS_SB(2) IRADS_SB(4) IRADS_SB(8) IRADS_SB(16) IRADS_SB(32) IRADS_SB(64) }
 #undef IRADS_SB
+    if (fx) {
+        const long cnt = (long)3 * B * C * H * W;
+        hipLaunchKernelGGL(dattn_sample_fx_out, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, st, acc, scl, B, C,
+                           H * W, G, grad_x, grad_y, grad_q);
+    }
     return check_launch("irads_dattn_sample_bwd");
+}
+
+extern "C" int irads_dattn_sample_bwd(const float *x, const float *y, const float *q, const float *pos_x,
+                                      const float *pos_y, const float *gxs, const float *gys, const float *gqs, int B,
+                                      int C, int H, int W, int G, int n, float *grad_x, float *grad_y, float *grad_q,
+                                      float *grad_pos_x, float *grad_pos_y, void *stream) {
+    return sample_bwd(x, y, q, pos_x, pos_y, gxs, gys, gqs, B, C, H, W, G, n, grad_x, grad_y, grad_q, grad_pos_x,
+                      grad_pos_y, nullptr, stream);
+}
+
+extern "C" long irads_dattn_sample_bwd_workspace_bytes(int B, int C, int H, int W, int G) {
+    if (B <= 0 || C <= 0 || H <= 0 || W <= 0 || G <= 0) return 0;
+    return (long)(sample_ws_scl_offset(B, C, H, W) + (((size_t)3 * B * G * sizeof(float) + 255) & ~(size_t)255));
+}
+
+extern "C" int irads_dattn_sample_bwd_ws(const float *x, const float *y, const float *q, const float *pos_x,
+                                         const float *pos_y, const float *gxs, const float *gys, const float *gqs,
+                                         int B, int C, int H, int W, int G, int n, float *grad_x, float *grad_y,
+                                         float *grad_q, float *grad_pos_x, float *grad_pos_y, void *workspace,
+                                         long workspace_bytes, void *stream) {
+    IRADS_REQUIRE(workspace && ((uintptr_t)workspace % 256) == 0, "dattn_sample_bwd_ws: workspace must be 256-B aligned");
+    IRADS_REQUIRE(workspace_bytes >= irads_dattn_sample_bwd_workspace_bytes(B, C, H, W, G),
+                  "dattn_sample_bwd_ws: workspace of %ld bytes, need %ld", workspace_bytes,
+                  irads_dattn_sample_bwd_workspace_bytes(B, C, H, W, G));
+    return sample_bwd(x, y, q, pos_x, pos_y, gxs, gys, gqs, B, C, H, W, G, n, grad_x, grad_y, grad_q, grad_pos_x,
+                      grad_pos_y, (char *)workspace, stream);
 }
 
 static int attn_block(int HW) {

@@ -30,6 +30,7 @@ SIGNATURES = {
     "irads_dattn_sample_fwd": [_vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp],
     "irads_dattn_sample_bwd": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp,
                                _vp, _vp],
+    "irads_dattn_sample_bwd_ws": [_vp] * 8 + [_i] * 6 + [_vp] * 5 + [_vp, _l, _vp],
     "irads_dattn_attn_fwd": [_vp] * 8 + [_i] * 9 + [_f, _vp, _vp, _vp],
     "irads_dattn_attn_bwd": [_vp] * 8 + [_i] * 9 + [_f] + [_vp] * 10 + [_vp],
     "irads_dattn_attn_bwd_ws": [_vp] * 8 + [_i] * 9 + [_f] + [_vp] * 10 + [_vp, _l, _vp],
@@ -78,7 +79,8 @@ QUERIES = {"irads_wgrad_workspace": (ctypes.c_long, [_i, _i, _i]),
            "irads_bnact_partials": (ctypes.c_long, [_l, _i]),
            "irads_winattn_bias_quads_size": (ctypes.c_long, [_i]),
            "irads_msda_bwd_workspace_bytes": (ctypes.c_long, [_i, _i, _i, _i, _i, _i, _i, _i]),
-           "irads_dattn_attn_bwd_workspace_bytes": (ctypes.c_long, [_i] * 9)}
+           "irads_dattn_attn_bwd_workspace_bytes": (ctypes.c_long, [_i] * 9),
+           "irads_dattn_sample_bwd_workspace_bytes": (ctypes.c_long, [_i] * 5)}
 CE_WORKSPACE = 8192
 
 _lib = None

@@ -275,10 +275,15 @@ class DAttnSampleFn(torch.autograd.Function):
         def g(t):
             return torch.zeros((B, C, 2 * n), device=x.device) if t is None else t.contiguous().float()
         gxs, gys, gqs = g(gxs), g(gys), g(gqs)
-        gx, gy, gq = zeros_like_many(x, y, q)
+        # every element written by the kernels (fixed-point accumulation in the workspace:
+        # reproducible, no zero-fill of the gradients)
+        gx, gy, gq = (torch.empty_like(t) for t in (x, y, q))
         gpx, gpy = torch.empty_like(px), torch.empty_like(py)
-        N.call("irads_dattn_sample_bwd", N.ptr(x), N.ptr(y), N.ptr(q), N.ptr(px), N.ptr(py), N.ptr(gxs), N.ptr(gys),
-               N.ptr(gqs), B, C, H, W, G, n, N.ptr(gx), N.ptr(gy), N.ptr(gq), N.ptr(gpx), N.ptr(gpy), N.stream())
+        nb = N.load().irads_dattn_sample_bwd_workspace_bytes(B, C, H, W, G)
+        ws = torch.empty((nb,), device=x.device, dtype=torch.uint8)
+        N.call("irads_dattn_sample_bwd_ws", N.ptr(x), N.ptr(y), N.ptr(q), N.ptr(px), N.ptr(py), N.ptr(gxs),
+               N.ptr(gys), N.ptr(gqs), B, C, H, W, G, n, N.ptr(gx), N.ptr(gy), N.ptr(gq), N.ptr(gpx), N.ptr(gpy),
+               N.ptr(ws), nb, N.stream())
         return gx, gy, gq, gpx, gpy, None
 
 

@@ -1,10 +1,9 @@
 """Run-to-run reproducibility of the C2 training step.
 
 Every irads reduction on the path sums in a fixed order (the DAttn attention backward's partials,
-the cross-entropy partials, the split-K weight gradients, the MSDA gather backward); the one
-float-atomic scatter left is the DAttn grid-sample backward (dattn.hip `scatter`), whose adds
-rarely share an address.  MIOpen's default (benchmark) solvers for the DSCF fuse_q 3x3
-convolution are not reproducible; with `torch.backends.cudnn.deterministic` they are
+the cross-entropy partials, the split-K weight gradients, the MSDA gather backward) or in int64
+fixed point (the DAttn grid-sample backward's scatter, irads_dattn_sample_bwd_ws).  MIOpen's
+default (benchmark) solvers for the DSCF fuse_q 3x3 convolution are not reproducible; with `torch.backends.cudnn.deterministic` they are
 (bench.py --deterministic, +0.8 ms per step).  scripts/determinism_probe.py is the
 diagnostic this test condenses."""
 import pytest
@@ -16,9 +15,7 @@ pytestmark = pytest.mark.gpu
 def test_training_step_reproducible():
     """C2 model (Swin-B CMNeXt, eval mode so that no dropout / DropPath / apply_mask draws, batch 2,
     512x512, bf16 autocast), deterministic MIOpen solvers: two identical forward + backward passes
-    give bit-identical logits and bit-identical gradients for every tensor whose backward runs
-    before the first DAttn sampling backward (the three decode heads); the rest agree to relative
-    L2 1e-6 (the grid-sample scatter's float atomics)."""
+    give bit-identical logits and bit-identical gradients for every trainable tensor."""
     import bench
     prev = torch.backends.cudnn.deterministic
     torch.backends.cudnn.deterministic = True
@@ -43,11 +40,7 @@ def test_training_step_reproducible():
         (o0, g0), (o1, g1) = runs
         assert all(torch.equal(a, b) for a, b in zip(o0, o1)), "forward not bit-reproducible"
         assert set(g0) == set(g1) and len(g0) > 100
-        heads = [n for n in g0 if n.startswith("decode_head")]
-        assert heads and all(torch.equal(g0[n], g1[n]) for n in heads), \
-            [n for n in heads if not torch.equal(g0[n], g1[n])][:5]
-        num = sum(float((g0[n] - g1[n]).double().norm() ** 2) for n in g0)
-        den = sum(float(g0[n].double().norm() ** 2) for n in g0)
-        assert (num / den) ** 0.5 < 1e-6, (num / den) ** 0.5
+        diff = [n for n in g0 if not torch.equal(g0[n], g1[n])]
+        assert not diff, (len(diff), diff[:5])
     finally:
         torch.backends.cudnn.deterministic = prev
