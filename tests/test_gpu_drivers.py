@@ -168,7 +168,7 @@ def test_graph_step_overlapped_exchange_capture():
     """comm="overlap": the bucketed all-reduces are issued from post-accumulate-grad hooks on a side
     stream and captured into the graph with the backward and AdamW.  Here on a 1-rank RCCL group
     (the collective is the identity): gradients and the updated parameters equal the un-bucketed
-    graph step's (up to the DAttn backward's float-atomic ordering), so the hooks, the flat-buffer
+    graph step's (up to MIOpen's non-reproducible fuse_q convolution solvers), so the hooks, the flat-buffer
     pack / unpack and the capture of the RCCL calls are exercised; the 2-rank averaging is covered
     by test_dp_two_ranks_gradients."""
     import torch.distributed as dist
@@ -212,7 +212,7 @@ def test_graph_step_overlapped_exchange_capture():
                             [p.detach().clone() for p in m.parameters()], snap))
         (g0, p0, s0), (g1, p1, s1) = results
         assert all(torch.equal(a, b) for a, b in zip(s0, s1))
-        # the DAttn backward adds float atomics in a run-dependent order: equal up to that
+        # MIOpen's default fuse_q convolution solvers are not reproducible: equal up to that
         num = sum(float((a - b).float().norm() ** 2) for a, b in zip(g0, g1))
         den = sum(float(b.float().norm() ** 2) for b in g0)
         assert (num / den) ** 0.5 < 2e-2, (num / den) ** 0.5
@@ -275,7 +275,7 @@ def test_dp_two_ranks_gradients(tmp_path):
     all-reduced): 2 fresh processes, one per rank (gloo, on the one GPU of the box), each run the
     captured GraphedTrainStep on half of a 4-image batch; rank 0's averaged gradients equal a
     single-process 4-image step's (relative L2 2e-2 over all trainable tensors: bf16 GEMMs tile
-    batch 2 and batch 4 differently, and the DAttn backward's float atomics add in a run-dependent
+    batch 2 and batch 4 differently, and MIOpen's default convolution solvers reduce in a run-dependent
     order)."""
     import subprocess
     import sys
