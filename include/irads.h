@@ -124,6 +124,17 @@ int irads_dattn_sample_bwd_ws(const float *x, const float *y, const float *q, co
                               int B, int C, int H, int W, int G, int n, float *grad_x, float *grad_y,
                               float *grad_q, float *grad_pos_x, float *grad_pos_y, void *workspace,
                               long workspace_bytes, void *stream);
+/* DAttentionMM's output gate (swin.py:1016): y = deform_weight[c] * out + identity_weight[c] * xy.
+ * out_tok (B, HW, C) bf16 token-major (proj_out's output), xy (B, C, HW) bf16 NCHW (fuse_q's
+ * output), gates fp32 (C); y (B, HW, C) fp32 token-major.  C in 8..128, a multiple of 8; out_tok,
+ * y, grad_y and grad_out rows 16-B aligned.  Forward and the bf16 input gradients round as the
+ * reference's fp32 elementwise ops (bit-identical); partials (nblk, 2, C), nblk = ceil(B*HW/256),
+ * receive per-workgroup sums of grad_y*out and grad_y*xy (the gate gradients: sum over nblk). */
+int irads_dattn_gate_fwd(const void *out_tok, const void *xy, const float *deform_weight,
+                         const float *identity_weight, int B, int C, int HW, float *y, void *stream);
+int irads_dattn_gate_bwd(const float *grad_y, const void *out_tok, const void *xy, const float *deform_weight,
+                         const float *identity_weight, int B, int C, int HW, void *grad_out, void *grad_xy,
+                         float *partials, void *stream);
 /* Fused attention with on-the-fly bilinear rpe bias (swin.py:950-1016):
  *   q (B*nH, hc, HW)  k, v KEY-MAJOR (B*nH, 2n, hc)  rpe (nH, Ht, Wt)  qgrid_y (H), qgrid_x (W)
  *   (the reference's _get_q_grid values)  out (B*nH, hc, HW)  lse (B*nH, HW).

@@ -1286,3 +1286,125 @@ extern "C" int irads_dattn_sample_index(const float *grid, int N, int H, int W, 
     sample_index_kernel<<<(N + 255) / 256, 256, 0, (hipStream_t)stream>>>(grid, N, H, W, corners);
     return check_launch("irads_dattn_sample_index");
 }
+
+// ---------------------------------------------------------------- DAttentionMM output gate
+// y = deform_weight[c] * out + identity_weight[c] * xy (swin.py:1016), the last op of
+// DAttentionMM.forward, and its backward: one pass each instead of torch's broadcast muls, add,
+// casts and two reductions.  out is the token-major (B, HW, C) bf16 output of proj_out, xy the
+// NCHW (B, C, HW) bf16 fuse_q output; y is written token-major fp32 (a channels-last (B, C, H, W)
+// view, the layout U_fc1 reads).  A thread owns one pixel's C channels (16-B row loads; the
+// NCHW reads are coalesced across the wave's 64 pixels).  Products and sum are rounded as the
+// reference's fp32 ops (no FMA contraction): the forward and the bf16 input gradients are
+// bit-identical to the eager expression.  The gate gradients are per-workgroup partial sums
+// (nblk = ceil(B*HW / 256), then summed by the caller in a fixed order).
+namespace irads {
+namespace {
+__global__ void __launch_bounds__(256) dattn_gate_fwd_kernel(const unsigned short *__restrict__ out_tok,
+                                                             const unsigned short *__restrict__ xy,
+                                                             const float *__restrict__ dw,
+                                                             const float *__restrict__ iw, int B, int C, int HW,
+                                                             float *__restrict__ y) {
+    const long P = (long)blockIdx.x * 256 + threadIdx.x;
+    if (P >= (long)B * HW) return;
+    const long b = P / HW, p = P - b * HW;
+    const unsigned short *orow = out_tok + P * C;
+    const unsigned short *xcol = xy + b * C * HW + p;
+    float *yrow = y + P * C;
+    for (int c0 = 0; c0 < C; c0 += 8) {
+        const uint4 ov = *reinterpret_cast<const uint4 *>(orow + c0);
+        const unsigned short *o16 = reinterpret_cast<const unsigned short *>(&ov);
+        float r[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int c = c0 + u;
+            r[u] = __fadd_rn(__fmul_rn(dw[c], bf2f(o16[u])), __fmul_rn(iw[c], bf2f(xcol[(long)c * HW])));
+        }
+        *reinterpret_cast<float4 *>(yrow + c0) = make_float4(r[0], r[1], r[2], r[3]);
+        *reinterpret_cast<float4 *>(yrow + c0 + 4) = make_float4(r[4], r[5], r[6], r[7]);
+    }
+}
+
+__global__ void __launch_bounds__(256) dattn_gate_bwd_kernel(const float *__restrict__ g_tok,
+                                                             const unsigned short *__restrict__ out_tok,
+                                                             const unsigned short *__restrict__ xy,
+                                                             const float *__restrict__ dw,
+                                                             const float *__restrict__ iw, int B, int C, int HW,
+                                                             unsigned short *__restrict__ gout_tok,
+                                                             unsigned short *__restrict__ gxy,
+                                                             float *__restrict__ part) {
+    __shared__ float red[4][2][128];
+    const long P = (long)blockIdx.x * 256 + threadIdx.x;
+    const bool ok = P < (long)B * HW;
+    const long Pc = ok ? P : 0;
+    const long b = Pc / HW, p = Pc - b * HW;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (int c0 = 0; c0 < C; c0 += 8) {
+        float g[8], o[8], x[8];
+        if (ok) {
+            const float4 g0 = *reinterpret_cast<const float4 *>(g_tok + Pc * C + c0);
+            const float4 g1 = *reinterpret_cast<const float4 *>(g_tok + Pc * C + c0 + 4);
+            g[0] = g0.x, g[1] = g0.y, g[2] = g0.z, g[3] = g0.w, g[4] = g1.x, g[5] = g1.y, g[6] = g1.z, g[7] = g1.w;
+            const uint4 ov = *reinterpret_cast<const uint4 *>(out_tok + Pc * C + c0);
+            const unsigned short *o16 = reinterpret_cast<const unsigned short *>(&ov);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                o[u] = bf2f(o16[u]);
+                x[u] = bf2f(xy[(b * C + c0 + u) * HW + p]);
+            }
+            unsigned short go[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                go[u] = f2bf(__fmul_rn(g[u], dw[c0 + u]));
+                gxy[(b * C + c0 + u) * HW + p] = f2bf(__fmul_rn(g[u], iw[c0 + u]));
+            }
+            *reinterpret_cast<uint4 *>(gout_tok + Pc * C + c0) = *reinterpret_cast<const uint4 *>(go);
+        } else {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) g[u] = o[u] = x[u] = 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const float a = wave_sum(g[u] * o[u]), s = wave_sum(g[u] * x[u]);
+            if (lane == 0) {
+                red[w][0][c0 + u] = a;
+                red[w][1][c0 + u] = s;
+            }
+        }
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < 2 * C; t += 256) {
+        const int k = t / C, c = t - k * C;
+        part[((long)blockIdx.x * 2 + k) * C + c] = (red[0][k][c] + red[1][k][c]) + (red[2][k][c] + red[3][k][c]);
+    }
+}
+}  // namespace
+}  // namespace irads
+
+extern "C" int irads_dattn_gate_fwd(const void *out_tok, const void *xy, const float *deform_weight,
+                                    const float *identity_weight, int B, int C, int HW, float *y, void *stream) {
+    IRADS_REQUIRE(out_tok && xy && deform_weight && identity_weight && y, "dattn_gate: null pointer");
+    IRADS_REQUIRE(B >= 0 && HW >= 0 && C > 0 && C % 8 == 0 && C <= 128, "dattn_gate: C=%d must be 8..128, x8", C);
+    IRADS_REQUIRE(((uintptr_t)out_tok % 16) == 0 && ((uintptr_t)y % 16) == 0, "dattn_gate: 16-B aligned rows");
+    const long n = (long)B * HW;
+    if (n == 0) return IRADS_OK;
+    hipLaunchKernelGGL(dattn_gate_fwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       (const unsigned short *)out_tok, (const unsigned short *)xy, deform_weight, identity_weight, B,
+                       C, HW, y);
+    return check_launch("irads_dattn_gate_fwd");
+}
+
+extern "C" int irads_dattn_gate_bwd(const float *grad_y, const void *out_tok, const void *xy,
+                                    const float *deform_weight, const float *identity_weight, int B, int C, int HW,
+                                    void *grad_out, void *grad_xy, float *partials, void *stream) {
+    IRADS_REQUIRE(grad_y && out_tok && xy && deform_weight && identity_weight && grad_out && grad_xy && partials,
+                  "dattn_gate: null pointer");
+    IRADS_REQUIRE(B >= 0 && HW >= 0 && C > 0 && C % 8 == 0 && C <= 128, "dattn_gate: C=%d must be 8..128, x8", C);
+    IRADS_REQUIRE(((uintptr_t)grad_y % 16) == 0 && ((uintptr_t)out_tok % 16) == 0 && ((uintptr_t)grad_out % 16) == 0,
+                  "dattn_gate: 16-B aligned rows");
+    const long n = (long)B * HW;
+    if (n == 0) return IRADS_OK;
+    hipLaunchKernelGGL(dattn_gate_bwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       grad_y, (const unsigned short *)out_tok, (const unsigned short *)xy, deform_weight,
+                       identity_weight, B, C, HW, (unsigned short *)grad_out, (unsigned short *)grad_xy, partials);
+    return check_launch("irads_dattn_gate_bwd");
+}

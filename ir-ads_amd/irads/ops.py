@@ -287,6 +287,45 @@ class DAttnSampleFn(torch.autograd.Function):
         return gx, gy, gq, gpx, gpy, None
 
 
+def dattn_gate_ok(out_tok, xy):
+    """DAttnGateFn's preconditions: bf16 (B, HW, C) token-major out and (B, C, H, W) NCHW xy."""
+    return (out_tok.is_cuda and out_tok.dtype == torch.bfloat16 and xy.dtype == torch.bfloat16
+            and out_tok.dim() == 3 and xy.dim() == 4 and out_tok.is_contiguous() and xy.is_contiguous()
+            and out_tok.shape[0] == xy.shape[0] and out_tok.shape[2] == xy.shape[1]
+            and out_tok.shape[1] == xy.shape[2] * xy.shape[3] and xy.shape[1] % 8 == 0 and xy.shape[1] <= 128)
+
+
+class DAttnGateFn(torch.autograd.Function):
+    """deform_weight[c] * out + identity_weight[c] * xy (DAttentionMM's last op, swin.py:1016)
+    in one pass each way (irads_dattn_gate_fwd/bwd).  out_tok: (B, HW, C) bf16; xy: (B, C, H, W)
+    bf16.  Returns the fp32 (B, C, H, W) result as a channels-last view of token-major memory."""
+
+    @staticmethod
+    def forward(ctx, out_tok, xy, dw, iw):
+        B, C, H, W = xy.shape
+        dw32, iw32 = dw.detach().float().contiguous(), iw.detach().float().contiguous()
+        y = torch.empty((B, H * W, C), device=xy.device, dtype=torch.float32)
+        N.call("irads_dattn_gate_fwd", N.ptr(out_tok), N.ptr(xy), N.ptr(dw32), N.ptr(iw32), B, C, H * W, N.ptr(y),
+               N.stream())
+        ctx.save_for_backward(out_tok, xy, dw32, iw32)
+        ctx.dtypes = (dw.dtype, iw.dtype)
+        return y.view(B, H, W, C).permute(0, 3, 1, 2)
+
+    @staticmethod
+    def backward(ctx, gy):
+        out_tok, xy, dw32, iw32 = ctx.saved_tensors
+        B, C, H, W = xy.shape
+        g = gy.permute(0, 2, 3, 1).float().contiguous()  # token-major (a view when gy is channels-last)
+        gout = torch.empty_like(out_tok)
+        gxy = torch.empty_like(xy)
+        nblk = -(-B * H * W // 256)
+        part = torch.empty((nblk, 2, C), device=xy.device, dtype=torch.float32)
+        N.call("irads_dattn_gate_bwd", N.ptr(g), N.ptr(out_tok), N.ptr(xy), N.ptr(dw32), N.ptr(iw32), B, C, H * W,
+               N.ptr(gout), N.ptr(gxy), N.ptr(part), N.stream())
+        s = part.sum(0)  # fixed-order tree reduction over the workgroups
+        return gout, gxy, s[0].to(ctx.dtypes[0]), s[1].to(ctx.dtypes[1])
+
+
 def zeros_like_many(*ts):
     """Zero-filled gradients for several contiguous tensors of one dtype / device as views of
     ONE buffer (one fill launch instead of one per tensor); segments start on 256-B

@@ -450,6 +450,8 @@ class DAttentionMM(nn.Module):
         out = ops.DAttnAttentionFn.apply(q32.view(B * nH, hc, H * W), k, v, pos_x, pos_y, self.rpe_table.float(),
                                          gy, gx, B, nH, g, H, W, self.scale)
         out_tok = self._tok_linear(self.proj_out, out.view(B, C, H * W).transpose(1, 2))  # (B, HW, C) bf16
+        if ops.dattn_gate_ok(out_tok, xy):  # the output gate in one pass each way (same values)
+            return ops.DAttnGateFn.apply(out_tok, xy, self.deform_weight, self.identity_weight)
         out = out_tok.transpose(1, 2).view(B, C, H, W)  # proj_drop has p == 0 on this path: identity
         return self.deform_weight[None, :, None, None] * out + self.identity_weight[None, :, None, None] * xy
 

@@ -68,6 +68,7 @@ def main():
     ap.add_argument("--all-ops", action="store_true", help="every aten op, not just casts / copies / adds / fills")
     ap.add_argument("--min-numel", type=int, default=1 << 16)
     ap.add_argument("--by-count", action="store_true", help="sort sites by calls (launch-bound glue)")
+    ap.add_argument("--by-site", action="store_true", help="merge shapes: one row per (op, site, dtype)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.manual_seed(3407)
@@ -80,7 +81,15 @@ def main():
     with audit:
         bench.train_step(model, opt, sched, loss_fn, batch)
     torch.cuda.synchronize()
-    rows = sorted(audit.rows.items(), key=lambda kv: -kv[1][0 if a.by_count else 1])
+    items = audit.rows.items()
+    if a.by_site:
+        merged = {}
+        for (op, st, shape, dt), (n, b) in items:
+            r = merged.setdefault((op, st, ("*",), dt), [0, 0])
+            r[0] += n
+            r[1] += b
+        items = merged.items()
+    rows = sorted(items, key=lambda kv: -kv[1][0 if a.by_count else 1])
     print(f"{'MB out':>9} {'calls':>5}  op / site / shape / dtype")
     for (op, st, shape, dt), (n, b) in rows[:a.top]:
         print(f"{b / 1e6:9.1f} {n:5d}  {op:10s} {st[:90]:90s} {list(shape)} {dt.replace('torch.', '')}")

@@ -172,3 +172,28 @@ def test_dattn_attention_backward_is_reproducible(tag):
     for a, b_, name in ((gq, g1[0], "q"), (gk.transpose(1, 2), g1[1], "k"), (gv.transpose(1, 2), g1[2], "v"),
                         (gpx, g1[3], "pos_x"), (gpy, g1[4], "pos_y"), (gr, g1[5], "rpe")):
         assert _rel(a, b_) < 1e-5, (name, _rel(a, b_))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,C,H,W", [(2, 16, 128, 128), (8, 128, 16, 16), (3, 24, 15, 17)])
+def test_dattn_gate_matches_eager(B, C, H, W):
+    """DAttentionMM's output gate (swin.py:1016) on irads_dattn_gate_fwd/bwd against the eager
+    expression on the same bf16 operands: forward and the bf16 input gradients bit-identical (same
+    fp32 roundings), the gate gradients (sums over batch and pixels, another order) to 1e-5."""
+    from irads import ops
+    torch.manual_seed(B * C + H)
+    out_tok = torch.randn(B, H * W, C, device="cuda").to(torch.bfloat16).requires_grad_()
+    xy = torch.randn(B, C, H, W, device="cuda").to(torch.bfloat16).requires_grad_()
+    dw = (torch.rand(C, device="cuda") + 0.5).requires_grad_()
+    iw = (torch.rand(C, device="cuda") + 0.5).requires_grad_()
+    assert ops.dattn_gate_ok(out_tok, xy)
+    y = ops.DAttnGateFn.apply(out_tok, xy, dw, iw)
+    out = out_tok.transpose(1, 2).view(B, C, H, W)
+    ref = dw[None, :, None, None] * out + iw[None, :, None, None] * xy
+    assert y.shape == ref.shape and y.dtype == ref.dtype and torch.equal(y, ref)
+    gy = torch.randn_like(ref)
+    got = torch.autograd.grad(y, (out_tok, xy, dw, iw), gy)
+    want = torch.autograd.grad(ref, (out_tok, xy, dw, iw), gy)
+    assert torch.equal(got[0], want[0]) and torch.equal(got[1], want[1])
+    for a, b in zip(got[2:], want[2:]):
+        assert ((a - b).norm() / b.norm()).item() < 1e-5
