@@ -70,6 +70,12 @@ class GraphedTrainStep:
                 o += p.numel()
             if self.comm == "overlap":
                 self._make_buckets(bucket_mb)
+        if self.comm != "none":
+            # first collective from this (the main) thread, before the backward's hooks issue
+            # them from the autograd thread: the communicator's lazy set-up happens here
+            w = torch.zeros((1,), device=dev, dtype=torch.float32)
+            _all_reduce(w)
+            torch.cuda.synchronize(dev)
         side = torch.cuda.Stream(device=dev)
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):  # warm-up (kernel selection, allocator pools) off the capture

@@ -1,0 +1,69 @@
+"""Worker of test_gpu_zz_rccl.py (a fresh process, so that the RCCL communicator's threads never
+share a process with the rest of the GPU suite): the graph-captured training step with
+comm="overlap" (bucketed all-reduces from post-accumulate-grad hooks on a side stream, captured
+with the backward and AdamW) on a 1-rank RCCL group, against comm="none".  Exit status 0 and a
+final "OK" line when the gradients and updated parameters agree."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (os.path.join(ROOT, "ir-ads_amd"), os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")):
+    sys.path.insert(0, p)
+
+
+def main():
+    port = sys.argv[1]
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = port
+    import torch
+    import torch.distributed as dist
+    from fill import fill_module
+    from irads.graph_step import GraphedTrainStep
+    from semseg.losses import get_loss, mmst_loss
+    from semseg.optimizers import get_optimizer
+    from test_gpu_drivers import _tiny_model
+    dev = "cuda"
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    results = []
+    for comm in ("none", "overlap"):
+        torch.manual_seed(0)
+        m = _tiny_model().to(dev)
+        fill_module(m, seed=4)
+        m.eval()  # deterministic: no dropout / DropPath / apply_mask
+        opt = get_optimizer(m, "adamw", 1e-3, "Adapter", 0.01, lr_on_device=True)
+        loss_fn = get_loss("CrossEntropy", 255)
+        g = torch.Generator().manual_seed(1)
+        rgb = torch.randn(2, 3, 64, 96, generator=g).to(dev)
+        dep = torch.rand(2, 3, 64, 96, generator=g).to(dev)
+        lbl = torch.randint(0, 5, (2, 64, 96), generator=g).to(dev)
+
+        def fwd_bwd():
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                y, yr, yd = m([rgb, dep])
+                loss = mmst_loss(loss_fn, y, yr, yd, lbl)
+            loss.backward()
+            return loss
+        snap = [p.detach().clone() for p in m.parameters()]
+        step = GraphedTrainStep(m.parameters(), fwd_bwd, opt, world=1, warmup=1, comm=comm, bucket_mb=0.05,
+                                restore=[p for p in m.parameters() if p.requires_grad] + list(m.buffers()))
+        if comm == "overlap":
+            assert len(step._buckets) > 3
+        step.step()
+        torch.cuda.synchronize()
+        results.append(([p.grad.clone() for p in m.parameters() if p.requires_grad],
+                        [p.detach().clone() for p in m.parameters()], snap))
+        print(f"comm={comm} done", flush=True)
+    (g0, p0, s0), (g1, p1, s1) = results
+    assert all(torch.equal(a, b) for a, b in zip(s0, s1))
+    # MIOpen's default fuse_q convolution solvers are not reproducible: equal up to that
+    num = sum(float((a - b).float().norm() ** 2) for a, b in zip(g0, g1))
+    den = sum(float(b.float().norm() ** 2) for b in g0)
+    rel = (num / den) ** 0.5
+    assert rel < 2e-2, rel
+    assert all(torch.allclose(a, b, rtol=0, atol=2e-3) for a, b in zip(p0, p1))
+    dist.destroy_process_group()
+    print(f"OK rel {rel:.3e}", flush=True)
+
+
+if __name__ == "__main__":
+    main()

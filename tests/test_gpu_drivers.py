@@ -164,64 +164,6 @@ def test_graph_step_keeps_optimizer_state(tmp_path):
             assert torch.equal(st[k].cpu(), want[i][k].cpu()), (i, k)
 
 
-def test_graph_step_overlapped_exchange_capture():
-    """comm="overlap": the bucketed all-reduces are issued from post-accumulate-grad hooks on a side
-    stream and captured into the graph with the backward and AdamW.  Here on a 1-rank RCCL group
-    (the collective is the identity): gradients and the updated parameters equal the un-bucketed
-    graph step's (up to MIOpen's non-reproducible fuse_q convolution solvers), so the hooks, the flat-buffer
-    pack / unpack and the capture of the RCCL calls are exercised; the 2-rank averaging is covered
-    by test_dp_two_ranks_gradients."""
-    import torch.distributed as dist
-    from fill import fill_module
-    from irads.graph_step import GraphedTrainStep
-    from semseg.losses import get_loss, mmst_loss
-    from semseg.optimizers import get_optimizer
-    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    os.environ.setdefault("MASTER_PORT", "29517")
-    own = not dist.is_initialized()
-    if own:
-        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
-    try:
-        results = []
-        for comm in ("none", "overlap"):
-            torch.manual_seed(0)
-            m = _tiny_model().to(DEV)
-            fill_module(m, seed=4)
-            m.eval()  # deterministic: no dropout / DropPath / apply_mask
-            opt = get_optimizer(m, "adamw", 1e-3, "Adapter", 0.01, lr_on_device=True)
-            loss_fn = get_loss("CrossEntropy", 255)
-            g = torch.Generator().manual_seed(1)
-            rgb = torch.randn(2, 3, 64, 96, generator=g).to(DEV)
-            dep = torch.rand(2, 3, 64, 96, generator=g).to(DEV)
-            lbl = torch.randint(0, 5, (2, 64, 96), generator=g).to(DEV)
-
-            def fwd_bwd():
-                with torch.autocast("cuda", dtype=torch.bfloat16):
-                    y, yr, yd = m([rgb, dep])
-                    loss = mmst_loss(loss_fn, y, yr, yd, lbl)
-                loss.backward()
-                return loss
-            snap = [p.detach().clone() for p in m.parameters()]
-            step = GraphedTrainStep(m.parameters(), fwd_bwd, opt, world=1, warmup=1, comm=comm, bucket_mb=0.05,
-                                    restore=[p for p in m.parameters() if p.requires_grad] + list(m.buffers()))
-            if comm == "overlap":
-                assert len(step._buckets) > 3
-            step.step()
-            torch.cuda.synchronize()
-            results.append(([p.grad.clone() for p in m.parameters() if p.requires_grad],
-                            [p.detach().clone() for p in m.parameters()], snap))
-        (g0, p0, s0), (g1, p1, s1) = results
-        assert all(torch.equal(a, b) for a, b in zip(s0, s1))
-        # MIOpen's default fuse_q convolution solvers are not reproducible: equal up to that
-        num = sum(float((a - b).float().norm() ** 2) for a, b in zip(g0, g1))
-        den = sum(float(b.float().norm() ** 2) for b in g0)
-        assert (num / den) ** 0.5 < 2e-2, (num / den) ** 0.5
-        assert all(torch.allclose(a, b, rtol=0, atol=2e-3) for a, b in zip(p0, p1))
-    finally:
-        if own:
-            dist.destroy_process_group()
-
-
 @pytest.mark.gpu
 def test_sb_hook_step():
     """The build-defined SB hook (CMNeXt(..., sb=...)): in one bf16 training step the
