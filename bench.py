@@ -306,6 +306,8 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         torch.cuda.set_device(local_rank)
+        from irads.graph_step import rccl_capture_env
+        rccl_capture_env()  # the graph step captures its bucketed RCCL all-reduces
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     device = torch.device("cuda", local_rank)
     torch.backends.cudnn.benchmark = True

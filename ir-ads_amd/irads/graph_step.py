@@ -30,8 +30,24 @@ Data parallel (world > 1; train_mm.py:94 / DDP semantics: gradients averaged ove
     runs between the backward graph and the optimizer graph (no overlap; the collective is
     not captured).  Used with the gloo backend (CPU-side tests), which cannot be captured.
 """
+import os
+
 import torch
 import torch.distributed as dist
+
+
+def rccl_capture_env():
+    """Process-group settings for capturing RCCL collectives into a HIP graph; call before
+    init_process_group (they are read when the group is built; an explicit value is kept).
+    Observed here: ProcessGroupNCCL's watchdog thread aborted the process with a HIP error from
+    hipEventQuery on a collective's end event (WorkNCCL::finishedGPUExecutionInternal, stack
+    captured by tests/test_gpu_zz_rccl.py) between the capture of the overlapped exchange and the
+    first replay — the events of captured collectives are graph nodes, not recorded events, and
+    the watchdog's event cache can hand a captured event to an eager work.  So: no event cache,
+    and a watchdog that logs HIP errors instead of rethrowing them (a real device fault still
+    surfaces on the main thread's next synchronising call)."""
+    os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
+    os.environ.setdefault("TORCH_NCCL_RETHROW_CUDA_ERRORS", "0")
 
 # "thread_local": only the capturing thread's capture-unsafe HIP calls are refused.  In the
 # default "global" mode a call from any thread of the process fails while a capture is open,

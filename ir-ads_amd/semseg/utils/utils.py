@@ -30,6 +30,8 @@ def setup_ddp():
     if "RANK" in os.environ and "WORLD_SIZE" in os.environ and int(os.environ["WORLD_SIZE"]) > 1:
         gpu = int(os.environ.get("LOCAL_RANK", "0"))
         torch.cuda.set_device(gpu)
+        from irads.graph_step import rccl_capture_env
+        rccl_capture_env()  # the training step captures its RCCL all-reduces (TRAIN.GRAPH)
         dist.init_process_group("nccl", timeout=datetime.timedelta(seconds=7200),
                                 device_id=torch.device("cuda", gpu))
         dist.barrier()

@@ -22,7 +22,9 @@ def main():
     from semseg.losses import get_loss, mmst_loss
     from semseg.optimizers import get_optimizer
     from test_gpu_drivers import _tiny_model
+    from irads.graph_step import rccl_capture_env
     dev = "cuda"
+    rccl_capture_env()
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
     results = []
     for comm in ("none", "overlap"):
