@@ -305,8 +305,10 @@ __global__ void __launch_bounds__(1024) dattn_sample_bound_kernel(const float *_
     if (threadIdx.x == 0) {
         float tot = 0.f;
         for (int w = 0; w < 16; ++w) tot += red[w];
-        const int e = (tot > 0.f && tot < 1e30f) ? min(100, 62 - (int)ceilf(log2f(tot))) : 0;
-        scl[(long)t * gridDim.x + map] = ldexpf(1.f, e);
+        // a non-finite bound (inf / NaN upstream gradients, e.g. an fp16 GradScaler overflow) gives a
+        // NaN scale: the fixed-point sums then convert to NaN gradients, as float atomics would give
+        const int e = tot > 0.f ? max(-100, min(100, 62 - (int)ceilf(log2f(tot)))) : 0;
+        scl[(long)t * gridDim.x + map] = (tot <= 3.0e38f) ? ldexpf(1.f, e) : __builtin_nanf("");
     }
 }
 
@@ -530,8 +532,11 @@ __global__ void __launch_bounds__(1024) dattn_attn_bwd_q_kernel(AttnArgs a, int 
         }
     }
     const float btot = block_sum_f(bound, red);
-    const int e = (btot > 0.f && btot < 1e30f) ? min(100, 30 - (int)ceilf(log2f(btot))) : 0;
-    const float fxs = ldexpf(1.f, e), inv_fx = ldexpf(1.f, -e);
+    // non-finite bound (inf / NaN upstream gradient): NaN scales, so this workgroup's table
+    // partial, and hence the table gradient, comes out NaN instead of finite and wrong
+    const int e = btot > 0.f ? max(-100, min(100, 30 - (int)ceilf(log2f(btot)))) : 0;
+    const bool fin = btot <= 3.0e38f;
+    const float fxs = fin ? ldexpf(1.f, e) : __builtin_nanf(""), inv_fx = fin ? ldexpf(1.f, -e) : __builtin_nanf("");
     const f2 sc = {((float)a.Wt - 1.0f) / 2.0f, ((float)a.Ht - 1.0f) / 2.0f};
     const int TP = a.Wt + 1;
     for (int q0 = blockIdx.x * QW * 64; q0 < HW; q0 += gridDim.x * QW * 64) {
@@ -610,7 +615,7 @@ __global__ void __launch_bounds__(1024) dattn_attn_bwd_q_kernel(AttnArgs a, int 
     for (int i = threadIdx.x; i < a.Ht * a.Wt; i += blockDim.x) {
         const int r = i / a.Wt, c = i - r * a.Wt;
         const int v = tgi[r * TP + c];
-        if (v != 0) atomicAdd(&grpe[(long)h * a.Ht * a.Wt + i], (float)v * inv_fx);
+        if (v != 0 || !fin) atomicAdd(&grpe[(long)h * a.Ht * a.Wt + i], (float)v * inv_fx);
     }
 }
 

@@ -18,11 +18,12 @@ What makes the step capturable (all in this package):
     zeroed one: no per-parameter add kernels).
 
 Data parallel (world > 1; train_mm.py:94 / DDP semantics: gradients averaged over ranks):
-  * comm="overlap" (default with the RCCL backend): the trainable parameters are split into
-    buckets of ~bucket_mb in reverse registration order (the order their gradients become
-    final in backward, as DDP's buckets).  A post-accumulate-grad hook copies each gradient
-    into its slot of a flat fp32 buffer; when a bucket's last gradient lands, the bucket's
-    all-reduce (RCCL sum) is issued on a side stream that waits on an event recorded at that
+  * comm="overlap" (default with the RCCL backend, OverlappedGradExchange): the trainable
+    parameters are split into buckets of ~bucket_mb in reverse registration order (the order
+    their gradients become final in backward, as DDP's buckets).  A post-accumulate-grad hook
+    copies each gradient into its slot of a flat fp32 buffer; buckets are issued in index
+    order as they complete (bucket k after 0..k-1, the same collective sequence on every rank),
+    each all-reduce (RCCL sum) on a side stream that waits on an event recorded at that
     point of the backward, so the exchange of bucket k overlaps the backward of the layers
     below it.  The optimizer waits for the side stream, unpacks with the 1/world scale and
     steps.  Hooks, events, collectives and the optimizer are captured into the one graph.
@@ -39,15 +40,18 @@ import torch.distributed as dist
 def rccl_capture_env():
     """Process-group settings for capturing RCCL collectives into a HIP graph; call before
     init_process_group (they are read when the group is built; an explicit value is kept).
-    Observed here: ProcessGroupNCCL's watchdog thread aborted the process with a HIP error from
-    hipEventQuery on a collective's end event (WorkNCCL::finishedGPUExecutionInternal, stack
-    captured by tests/test_gpu_zz_rccl.py) between the capture of the overlapped exchange and the
-    first replay — the events of captured collectives are graph nodes, not recorded events, and
-    the watchdog's event cache can hand a captured event to an eager work.  So: no event cache,
-    and a watchdog that logs HIP errors instead of rethrowing them (a real device fault still
-    surfaces on the main thread's next synchronising call)."""
+    Observed here (round 2): ProcessGroupNCCL's watchdog thread aborted the process with a HIP
+    error from hipEventQuery on a collective's end event (WorkNCCL::finishedGPUExecutionInternal,
+    stack captured by tests/test_gpu_zz_rccl.py) between the capture of the overlapped exchange
+    and the first replay.  Works created while a capture is open are not handed to the watchdog
+    (ProcessGroupNCCL only enqueues works issued outside a capture), but their end events came
+    from the process group's event cache: released after the capture, such an event (now a node
+    of the graph, never recorded on a stream) was handed to the next EAGER work, whose completion
+    the watchdog then polled with hipEventQuery.  Without the cache every eager work records a
+    fresh event, so the watchdog never queries a captured one; the watchdog's error handling
+    stays the default (a HIP error on a watchdog query is rethrown and ends the process)."""
     os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
-    os.environ.setdefault("TORCH_NCCL_RETHROW_CUDA_ERRORS", "0")
+
 
 # "thread_local": only the capturing thread's capture-unsafe HIP calls are refused.  In the
 # default "global" mode a call from any thread of the process fails while a capture is open,
@@ -66,8 +70,10 @@ class GraphedTrainStep:
     warm-up updates."""
 
     def __init__(self, params, fwd_bwd, optimizer, world=1, warmup=3, before_capture=None, restore=None,
-                 comm=None, bucket_mb=8.0):
+                 comm=None, bucket_mb=8.0, graph=True):
         self.params = [p for p in params if p.requires_grad]
+        self.fwd_bwd = fwd_bwd
+        self.use_graph = graph
         self.world = world
         self.opt = optimizer
         dev = self.params[0].device
@@ -86,6 +92,8 @@ class GraphedTrainStep:
                 o += p.numel()
             if self.comm == "overlap":
                 self._make_buckets(bucket_mb)
+        if not graph:  # eager: the same exchange per step, nothing captured (gloo tests, debugging)
+            return
         if self.comm != "none":
             # first collective from this (the main) thread, before the backward's hooks issue
             # them from the autograd thread: the communicator's lazy set-up happens here
@@ -127,24 +135,8 @@ class GraphedTrainStep:
 
     # ------------------------------------------------------------------ overlapped exchange
     def _make_buckets(self, bucket_mb):
-        """Buckets of consecutive params in reverse registration order, ~bucket_mb each."""
-        limit = int(bucket_mb * (1 << 20) / 4)
-        order = list(range(len(self.params)))[::-1]
-        self._bucket_of = {}
-        self._buckets = []  # (lo, hi) element range of the flat buffer, param indices
-        cur, size = [], 0
-        for i in order:
-            cur.append(i)
-            size += self.params[i].numel()
-            if size >= limit:
-                self._buckets.append(cur)
-                cur, size = [], 0
-        if cur:
-            self._buckets.append(cur)
-        for b, idx in enumerate(self._buckets):
-            for i in idx:
-                self._bucket_of[i] = b
-        self._comm_stream = torch.cuda.Stream(device=self.params[0].device)
+        self._exchange = OverlappedGradExchange(self.params, self.flat, self._offsets, bucket_mb)
+        self._buckets = self._exchange.buckets
 
     def _run(self, fwd_bwd, capture):
         """fwd + bwd, with the bucketed all-reduces issued as buckets complete (overlap) or one
@@ -157,28 +149,89 @@ class GraphedTrainStep:
             _all_reduce(self.flat)
             unpack_grads(self.params, self.flat, 1.0 / self.world)
             return loss
-        main = torch.cuda.current_stream()
-        remaining = [len(b) for b in self._buckets]
-        handles = []
+        return self._exchange.run(fwd_bwd, self.world)
 
-        def make_hook(i):
-            def hook(p):
-                lo = self._offsets[i]
-                self.flat[lo:lo + p.numel()].copy_(p.grad.reshape(-1))
-                b = self._bucket_of[i]
-                remaining[b] -= 1
-                if remaining[b] == 0:
-                    idx = self._buckets[b]
-                    a = min(self._offsets[j] for j in idx)
-                    z = max(self._offsets[j] + self.params[j].numel() for j in idx)
-                    ev = torch.cuda.Event()
-                    ev.record()  # on the stream the backward (and this hook's copy) runs on
-                    self._comm_stream.wait_event(ev)
-                    with torch.cuda.stream(self._comm_stream):
-                        dist.all_reduce(self.flat[a:z])  # RCCL sum over xGMI, overlapping the backward
-            return hook
-        for i, p in enumerate(self.params):
-            handles.append(p.register_post_accumulate_grad_hook(make_hook(i)))
+    def step(self):
+        if not self.use_graph:
+            self.opt.zero_grad(set_to_none=True)
+            self.loss = self._run(self.fwd_bwd, capture=False)
+            self.opt.step()
+            return self.loss
+        self.graph.replay()
+        if self.opt_graph is not None:
+            _all_reduce(self.flat)  # RCCL / gloo sum; the optimizer graph scales by 1/world
+            self.opt_graph.replay()
+        return self.loss
+
+
+class OverlappedGradExchange:
+    """DDP-style bucketed gradient all-reduce overlapped with backward (train_mm.py:94).
+
+    Buckets hold consecutive parameters in reverse registration order (the order their
+    gradients become final in backward), ~bucket_mb each, as slices of one flat fp32 buffer.
+    A post-accumulate-grad hook copies each gradient into its slot; when a bucket is complete it
+    becomes READY, and buckets are ISSUED strictly in index order (bucket k only after buckets
+    0..k-1, as DDP's reducer does): every rank then issues the same sequence of collectives
+    whatever order its backward finishes the buckets in, which RCCL requires (collectives on a
+    communicator must be called in the same order on all ranks).  On a GPU the all-reduce runs
+    on a side stream that waits on an event recorded at that point of the backward, so the
+    exchange of bucket k overlaps the backward of the layers below it; on CPU tensors (gloo
+    tests) it is issued inline.  After the backward the caller's stream waits for the side
+    stream and the flat buffer is unpacked with the 1/world scale."""
+
+    def __init__(self, params, flat, offsets, bucket_mb):
+        self.params, self.flat, self.offsets = params, flat, offsets
+        limit = max(1, int(bucket_mb * (1 << 20) / 4))
+        self.buckets, cur, size = [], [], 0
+        for i in reversed(range(len(params))):
+            cur.append(i)
+            size += params[i].numel()
+            if size >= limit:
+                self.buckets.append(cur)
+                cur, size = [], 0
+        if cur:
+            self.buckets.append(cur)
+        self.bucket_of = {i: b for b, idx in enumerate(self.buckets) for i in idx}
+        self.ranges = [(min(offsets[j] for j in idx), max(offsets[j] + params[j].numel() for j in idx))
+                       for idx in self.buckets]
+        self.cuda = flat.is_cuda
+        self.comm_stream = torch.cuda.Stream(device=flat.device) if self.cuda else None
+        self.issue_log = []  # bucket indices in issue order, last run (tests)
+
+    def _issue(self, b):
+        a, z = self.ranges[b]
+        self.issue_log.append(b)
+        if not self.cuda:
+            dist.all_reduce(self.flat[a:z])
+            return
+        ev = torch.cuda.Event()
+        ev.record()  # on the stream the backward (and the hooks' copies) run on
+        self.comm_stream.wait_event(ev)
+        with torch.cuda.stream(self.comm_stream):
+            if dist.get_backend() == "gloo":
+                _all_reduce(self.flat[a:z])
+            else:
+                dist.all_reduce(self.flat[a:z])  # RCCL sum over xGMI, overlapping the backward
+
+    def run(self, fwd_bwd, world):
+        remaining = [len(b) for b in self.buckets]
+        ready = [False] * len(self.buckets)
+        nxt = [0]
+        self.issue_log = []
+
+        def land(i, p):
+            lo = self.offsets[i]
+            self.flat[lo:lo + p.numel()].copy_(p.grad.reshape(-1))
+            b = self.bucket_of[i]
+            remaining[b] -= 1
+            if remaining[b] == 0:
+                ready[b] = True
+                while nxt[0] < len(self.buckets) and ready[nxt[0]]:
+                    self._issue(nxt[0])
+                    nxt[0] += 1
+
+        handles = [p.register_post_accumulate_grad_hook(lambda p, i=i: land(i, p))
+                   for i, p in enumerate(self.params)]
         try:
             loss = fwd_bwd()
         finally:
@@ -188,17 +241,12 @@ class GraphedTrainStep:
         for i, p in enumerate(self.params):
             if p.grad is None:
                 p.grad = torch.zeros_like(p)
-                make_hook(i)(p)
-        main.wait_stream(self._comm_stream)
-        unpack_grads(self.params, self.flat, 1.0 / self.world)
+                land(i, p)
+        assert nxt[0] == len(self.buckets), "gradient buckets left unissued"
+        if self.cuda:
+            torch.cuda.current_stream().wait_stream(self.comm_stream)
+        unpack_grads(self.params, self.flat, 1.0 / world)
         return loss
-
-    def step(self):
-        self.graph.replay()
-        if self.opt_graph is not None:
-            _all_reduce(self.flat)  # RCCL / gloo sum; the optimizer graph scales by 1/world
-            self.opt_graph.replay()
-        return self.loss
 
 
 def _all_reduce(flat):

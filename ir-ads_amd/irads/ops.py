@@ -7,6 +7,8 @@ zero-filled here.  There is no CPU fallback: CPU tensors raise.
 """
 import ctypes
 
+import weakref
+
 import torch
 
 from . import amp_cache
@@ -67,25 +69,37 @@ def _winattn_geometry(H, W):
     return Hp, Wp, (Hp // WINDOW) * (Wp // WINDOW)
 
 
-_QUADS = {}  # (table data_ptr, version, nH) -> (table, quads): the table is held so its address stays its own
+_QUADS = {}  # id(owner table) -> (weakref to it, {(nH, scale, device): (version, data_ptr, quads)})
 
 
-def bias_quads(table_f, nH, scale):
-    """irads_winattn_bias_quads of a (529, nH) fp32 table (divided by scale), cached per table
-    version (the frozen trunk's tables are re-laid once; a trainable table after each update)."""
-    key = (table_f.data_ptr(), table_f._version, nH, float(scale), table_f.device)
-    hit = _QUADS.get(key)
-    if hit is not None:
-        return hit[1]
+def bias_quads(table_f, nH, scale, owner=None):
+    """irads_winattn_bias_quads of a (529, nH) fp32 table (divided by scale).
+
+    Cached on ``owner`` (the module's relative_position_bias_table) for exactly as long as that
+    tensor lives, per table version: a captured graph that reads the cached quads (a frozen
+    trunk's tables are re-laid once, eagerly, and every capture hits) then reads memory that
+    lives as long as the model the graph runs.  A trainable table that is being captured
+    recomputes its quads inside the graph, since a cached copy would go stale after the
+    optimizer's in-graph update.  Without an owner nothing is cached."""
+    use_cache = owner is not None and not (owner.requires_grad and torch.cuda.is_current_stream_capturing())
+    key = (nH, float(scale), table_f.device)
+    ent = _QUADS.get(id(owner)) if use_cache else None
+    if ent is not None and ent[0]() is owner:
+        hit = ent[1].get(key)
+        if hit is not None and hit[0] == owner._version and hit[1] == owner.data_ptr():
+            return hit[2]
     q = torch.empty((N.load().irads_winattn_bias_quads_size(nH),), device=table_f.device, dtype=torch.float32)
     N.call("irads_winattn_bias_quads", N.ptr(table_f), nH, float(scale), N.ptr(q), N.stream())
-    if len(_QUADS) >= 256:
-        _QUADS.clear()
-    _QUADS[key] = (table_f, q)
+    if use_cache:
+        if ent is None or ent[0]() is not owner:
+            k = id(owner)
+            ent = (weakref.ref(owner, lambda _r, k=k: _QUADS.pop(k, None)), {})
+            _QUADS[k] = ent
+        ent[1][key] = (owner._version, owner.data_ptr(), q)
     return q
 
 
-def winattn_fwd(qkv, bias_f, table_f, mask_f, H, W, num_heads, shift, scale):
+def winattn_fwd(qkv, bias_f, table_f, mask_f, H, W, num_heads, shift, scale, table_owner=None):
     """Raw forward launch: qkv (B, H*W, 3C) contiguous -> (out (B, H*W, C), lse)."""
     N.check(qkv, "qkv")
     B, L, C3 = qkv.shape
@@ -97,7 +111,7 @@ def winattn_fwd(qkv, bias_f, table_f, mask_f, H, W, num_heads, shift, scale):
     out = torch.empty((B, L, C), device=qkv.device, dtype=qkv.dtype)
     Hp, Wp, nW = _winattn_geometry(H, W)
     lse = torch.empty((B * nW * num_heads * WINDOW * WINDOW,), device=qkv.device, dtype=torch.float32)
-    quads = bias_quads(table_f, num_heads, scale) if code == N.BF16 else None
+    quads = bias_quads(table_f, num_heads, scale, table_owner) if code == N.BF16 else None
     ev = TIMER.start("winattn_fwd")
     N.call("irads_winattn_fwd", code, N.ptr(qkv), N.ptr(bias_f), N.ptr(table_f), N.ptr(quads), N.ptr(mask_f), n_mask,
            B, H, W,
@@ -111,7 +125,7 @@ def winattn_fwd(qkv, bias_f, table_f, mask_f, H, W, num_heads, shift, scale):
 
 
 def winattn_bwd(qkv, bias_f, table_f, mask_f, H, W, nH, shift, scale, out, lse, gout, need_bias=False,
-                need_table=False):
+                need_table=False, table_owner=None):
     """Raw backward launch -> (grad_qkv, grad_table or None, grad_bias_pad or None)."""
     B, L, C3 = qkv.shape
     C = C3 // 3
@@ -121,7 +135,7 @@ def winattn_bwd(qkv, bias_f, table_f, mask_f, H, W, nH, shift, scale, out, lse, 
     gqkv = torch.empty_like(qkv)
     gtable = torch.zeros_like(table_f) if need_table else None
     gbias = torch.zeros((3 * C,), device=qkv.device, dtype=torch.float32) if need_bias else None
-    quads = bias_quads(table_f, nH, scale) if code == N.BF16 else None
+    quads = bias_quads(table_f, nH, scale, table_owner) if code == N.BF16 else None
     ev = TIMER.start("winattn_bwd")
     N.call("irads_winattn_bwd", code, N.ptr(qkv), N.ptr(bias_f), N.ptr(table_f), N.ptr(quads), N.ptr(mask_f), n_mask,
            B, H, W, C, nH, shift, float(scale), N.ptr(out), N.ptr(lse), N.ptr(gout), N.ptr(gqkv), N.ptr(gtable),
@@ -144,7 +158,8 @@ class WindowAttentionFn(torch.autograd.Function):
         table_f = table.detach().float().contiguous()
         bias_f = None if qkv_bias is None else qkv_bias.detach().float().contiguous()
         mask_f = None if mask is None else mask.detach().float().contiguous()
-        out, lse = winattn_fwd(qkv, bias_f, table_f, mask_f, H, W, num_heads, shift, scale)
+        ctx.owner = table if table.is_leaf else None
+        out, lse = winattn_fwd(qkv, bias_f, table_f, mask_f, H, W, num_heads, shift, scale, ctx.owner)
         ctx.save_for_backward(qkv, bias_f, table_f, mask_f, out, lse)
         ctx.cfg = (H, W, num_heads, shift, float(scale))
         ctx.need = (qkv_bias is not None and ctx.needs_input_grad[1], ctx.needs_input_grad[2])
@@ -156,7 +171,7 @@ class WindowAttentionFn(torch.autograd.Function):
         qkv, bias_f, table_f, mask_f, out, lse = ctx.saved_tensors
         H, W, nH, shift, scale = ctx.cfg
         gqkv, gtable, gbias = winattn_bwd(qkv, bias_f, table_f, mask_f, H, W, nH, shift, scale, out, lse, gout,
-                                          need_bias=ctx.need[0], need_table=ctx.need[1])
+                                          need_bias=ctx.need[0], need_table=ctx.need[1], table_owner=ctx.owner)
         if gtable is not None:
             gtable = gtable.to(ctx.table_dtype)
         return gqkv, gbias, gtable, None, None, None, None, None, None

@@ -214,7 +214,7 @@ class SwinStageFn(torch.autograd.Function):
             bias_f = None if w_msa.qkv.bias is None else w_msa.qkv.bias.detach()
             table_f = w_msa.relative_position_bias_table.detach()
             a, lse = ops.winattn_fwd(qkv, bias_f, table_f, None, H, W, w_msa.num_heads, blk.attn.shift_size,
-                                     w_msa.scale)
+                                     w_msa.scale, table_owner=w_msa.relative_position_bias_table)
             o = F.linear(a.view(M, C), wp, bp)
             X1, h2, X1b, mean2, rstd2 = _resln_fwd(cur, M, C, L, add1=o, add1_scale=None if dp is None else dp[i, 0],
                                                   norm=blk.norm2, x_out=True, xb_out=True)
@@ -344,7 +344,8 @@ class SwinStageFn(torch.autograd.Function):
             da = torch.mm(do, wp).view(S, L, C)
             bias_f = None if w_msa.qkv.bias is None else w_msa.qkv.bias.detach()
             gqkv, _, _ = ops.winattn_bwd(qkv, bias_f, w_msa.relative_position_bias_table.detach(), None, H, W,
-                                         w_msa.num_heads, blk.attn.shift_size, w_msa.scale, a, lse, da)
+                                         w_msa.num_heads, blk.attn.shift_size, w_msa.scale, a, lse, da,
+                                         table_owner=w_msa.relative_position_bias_table)
             dh1 = torch.mm(gqkv.view(M, 3 * C), wq)
             if i > 0:
                 g, df, dd = _resln_bwd(M, C, L, dy=dh1, x=x, mean=mean1, rstd=rstd1, norm=blk.norm1, g_res=dX1,

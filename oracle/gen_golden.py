@@ -454,6 +454,76 @@ def gen_cmnext_train(ref, tags=None):
         save(f"train_{tag}.npz", **res)
 
 
+def _train_step_tf(model, rgb, dep, lbl, mask_lbl, dtype=torch.float32, amp=False):
+    """The reference step (train_mm.py:133-150) with the MMST target TEACHER-FORCED: the aux
+    heads' labels come from the stored fp32 argmax instead of this run's own argmax, so runs in
+    different precisions differ by rounding only, not by a handful of flipped pixel decisions."""
+    for p in model.parameters():
+        p.grad = None
+    with torch.autocast("cpu", dtype=torch.bfloat16, enabled=amp):
+        y, yr, yd = model([t(rgb, dtype), t(dep, dtype)])
+        lf = nn.CrossEntropyLoss(ignore_index=255)
+        lb = t(lbl)
+        loss = lf(y, lb) + 0.01 * lf(yr, mask_lbl) + 0.01 * lf(yd, mask_lbl)
+    loss.backward()
+    named = [(n, p) for n, p in model.named_parameters() if p.requires_grad]
+    return loss, (y.detach(), yr.detach(), yd.detach()), {n: p.grad.detach().clone() for n, p in named}
+
+
+def gen_cmnext_train_fp64(ref, tags=None):
+    """Precision envelopes of the reference's own training step, beside the fp32 fixture as
+    train_<tag>_fp64.npz (tests/test_gpu_train_parity.py):
+      * the step in fp64 (the truth): loss, logits subsample, per-tensor gradient norm and the
+        seeded projections, the FULL_GRAD_KEYS tensors;
+      * "ref32": exact per-tensor relative L2 of the reference's fp32 gradients from fp64;
+      * "ref16": exact per-tensor relative L2 of the reference under CPU bf16 autocast from fp64.
+    All three runs are teacher-forced on the fp32 fixture's argmax (_train_step_tf)."""
+    from train_fixture import (FULL_GRAD_KEYS, N_PROJ, TRAIN_FIXTURES, adapter_trainable, deterministic_train_mode,
+                               projection, train_inputs)
+    for tag, (bb, n_cls, B, H, W, fseed, iseed) in TRAIN_FIXTURES.items():
+        if tags and tag not in tags:
+            continue
+        f32 = np.load(os.path.join(OUT, f"train_{tag}.npz"), allow_pickle=False)
+        model = ref.cmnext.CMNeXt(bb, n_cls, ["img", "depth"])
+        fill_module(model, seed=fseed)
+        for n, p in model.named_parameters():
+            p.requires_grad_(adapter_trainable(n))
+        deterministic_train_mode(model)
+        rgb, dep, lbl = train_inputs(B, H, W, n_cls, iseed)
+        lb = t(lbl)
+        am = torch.from_numpy(f32["y_argmax"].astype(np.int64))
+        mask_lbl = torch.where(am == lb, lb, torch.full_like(lb, 255))
+        bn = model.decode_head.linear_fuse.bn
+        rm0 = bn.running_mean.detach().clone()
+        _, _, g32 = _train_step_tf(model, rgb, dep, lbl, mask_lbl)
+        with torch.no_grad():
+            bn.running_mean.copy_(rm0)
+        _, _, g16 = _train_step_tf(model, rgb, dep, lbl, mask_lbl, amp=True)
+        model = model.double()
+        loss, (y, yr, yd), g64 = _train_step_tf(model, rgb, dep, lbl, mask_lbl, dtype=torch.float64)
+        names = f32["grad_names"].tolist()
+        res = {"loss": np.array([loss.item()]), "grad_names": np.array(names)}
+        for name, a in (("y", y), ("y_rgb", yr), ("y_dte", yd)):
+            res[name + "_sub"] = a[:, :, ::8, ::8].float().numpy()  # fp32 storage: 6e-8 relative
+        norms, projs, r32, r16 = [], [], [], []
+        for n in names:
+            g = g64[n].numpy()
+            norms.append(float(np.sqrt((g * g).sum())))
+            projs.append([projection(n, g, j) for j in range(N_PROJ)])
+            r32.append(_rel_l2(g32[n], g64[n]))
+            r16.append(_rel_l2(g16[n], g64[n]))
+            if n in FULL_GRAD_KEYS:
+                res["g." + n] = g
+        res["grad_norms"] = np.array(norms)
+        res["grad_projs"] = np.array(projs)
+        res["ref32_rel"] = np.array(r32)
+        res["ref16_rel"] = np.array(r16)
+        print(tag, "fp64 loss", loss.item(), "ref32 worst", max(r32), names[int(np.argmax(r32))], "ref16 median",
+              float(np.median(r16)), "worst", max(r16), names[int(np.argmax(r16))], flush=True)
+        save(f"train_{tag}_fp64.npz", **res)
+        del model, y, yr, yd, loss, g64, g32, g16
+
+
 # --------------------------------------------------------------------------- vCLR DINO transformer
 from dino_case import DINO_BS, DINO_DN, DINO_LAYERS, DINO_LEVELS, DINO_PROPOSALS, dino_inputs  # noqa: E402
 
@@ -600,6 +670,10 @@ if __name__ == "__main__":
     torch.manual_seed(0)
     fns = {"dino": gen_dino, "msda": gen_msda, "swin": gen_swin_wmsa, "block": gen_swin_block, "dattn": gen_dattn,
            "fusion": gen_fusion_small, "cmnext": gen_cmnext, "sb": gen_sb, "metrics": gen_metrics_loss,
-           "train": gen_cmnext_train}
+           "train": gen_cmnext_train, "train64": gen_cmnext_train_fp64}
     for w in which:
-        fns[w](ref)
+        if ":" in w:  # e.g. train64:c2_swinb_512
+            w, tag = w.split(":")
+            fns[w](ref, tags=[tag])
+        else:
+            fns[w](ref)

@@ -1,6 +1,10 @@
 """Worker of test_gpu_drivers.py::test_dp_two_ranks_gradients (one process per rank, both on the
-one GPU of the box): the graph-captured training step of irads/graph_step.py with world = 2 over
-gloo (comm="split"), on this rank's half of a 4-image batch.  Writes rank 0's averaged gradients."""
+one GPU of the box): the training step of irads/graph_step.py with world = 2 over gloo, on this
+rank's half of a 4-image batch, in fp32 with deterministic MIOpen solvers.  mode "split": the
+graph-captured step (pack, one all-reduce between the backward and the optimizer graphs); mode
+"overlap": the bucketed exchange from post-accumulate-grad hooks (OverlappedGradExchange, the
+RCCL path's code with gloo collectives; eager, as gloo cannot be captured), >= 4 buckets.
+Writes rank 0's averaged gradients."""
 import os
 import sys
 
@@ -33,9 +37,8 @@ def fwd_bwd_fn(m, rgb, dep, lbl):
     import torch
 
     def fwd_bwd():
-        with torch.autocast("cuda", dtype=torch.bfloat16):
-            y = m([rgb, dep])[0]
-            loss = torch.nn.functional.cross_entropy(y.float(), lbl)
+        y = m([rgb, dep])[0]
+        loss = torch.nn.functional.cross_entropy(y.float(), lbl)
         loss.backward()
         return loss
     return fwd_bwd
@@ -43,6 +46,7 @@ def fwd_bwd_fn(m, rgb, dep, lbl):
 
 def main():
     rank, world, port, out = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4]
+    mode = sys.argv[5] if len(sys.argv) > 5 else "split"
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = port
     import datetime
@@ -51,15 +55,23 @@ def main():
     # a peer that dies surfaces as a collective timeout well inside the test's own bound
     dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=90))
     from irads.graph_step import GraphedTrainStep
+    torch.backends.cudnn.deterministic = True
     dev = torch.device("cuda", 0)
     m = model(dev)
     rgb, dep, lbl = batch(dev)
     half = slice(rank * 2, rank * 2 + 2)
     opt = torch.optim.SGD([p for p in m.parameters() if p.requires_grad], lr=0.0)
-    step = GraphedTrainStep(m.parameters(), fwd_bwd_fn(m, rgb[half], dep[half], lbl[half]), opt, world=world,
-                            warmup=1)
-    assert step.comm == "split"
+    if mode == "split":
+        step = GraphedTrainStep(m.parameters(), fwd_bwd_fn(m, rgb[half], dep[half], lbl[half]), opt, world=world,
+                                warmup=1)
+        assert step.comm == "split"
+    else:
+        step = GraphedTrainStep(m.parameters(), fwd_bwd_fn(m, rgb[half], dep[half], lbl[half]), opt, world=world,
+                                comm="overlap", bucket_mb=0.02, graph=False)
+        assert len(step._buckets) >= 4, len(step._buckets)
     step.step()
+    if mode == "overlap":
+        assert step._exchange.issue_log == list(range(len(step._buckets)))
     torch.cuda.synchronize()
     if rank == 0:
         torch.save({n: (p.grad if p.grad is not None else torch.zeros_like(p)).detach().cpu()

@@ -184,6 +184,82 @@ def test_graph_step_gradient_allreduce_gloo(tmp_path):
             torch.testing.assert_close(torch.from_numpy(res[r][i]), want)
 
 
+def _overlap_model(rank_order):
+    """Eight independent branches y_i = tanh(x W_i) b_i; ``rank_order`` decides the order the
+    branches enter the graph, hence the order autograd finishes their gradients (the engine runs
+    later-created nodes first), so two ranks complete the buckets in opposite orders."""
+    import torch
+    g = torch.Generator().manual_seed(5)
+    ws = [torch.nn.Parameter(torch.randn(6, 5 + i, generator=g, dtype=torch.float64)) for i in range(8)]
+    bs = [torch.nn.Parameter(torch.randn(5 + i, generator=g, dtype=torch.float64)) for i in range(8)]
+    params = [t for pair in zip(ws, bs) for t in pair]
+
+    def loss_of(x):
+        terms = [None] * 8
+        for i in (range(8) if rank_order == 0 else reversed(range(8))):
+            terms[i] = (torch.tanh(x @ ws[i]) * bs[i]).sum(1).pow(2).mean()
+        return sum(terms)
+    return params, loss_of
+
+
+def _overlap_worker(rank, world, init_file, q):
+    import torch
+    import torch.distributed as dist
+    from irads.graph_step import OverlappedGradExchange
+    dist.init_process_group("gloo", init_method=f"file://{init_file}", rank=rank, world_size=world)
+    params, loss_of = _overlap_model(rank)
+    x = torch.randn(8, 6, generator=torch.Generator().manual_seed(9), dtype=torch.float64)
+    mine = x[rank * 4:(rank + 1) * 4]
+    offs, o = [], 0
+    for p in params:
+        offs.append(o)
+        o += p.numel()
+    flat = torch.zeros(o, dtype=torch.float64)
+    ex = OverlappedGradExchange(params, flat, offs, bucket_mb=40 * 4 / (1 << 20))  # 40-element buckets: one branch each
+    assert len(ex.buckets) >= 4
+    order = []
+    for i, p in enumerate(params):  # the order gradients land on this rank
+        p.register_post_accumulate_grad_hook(lambda p, i=i: order.append(i))
+    loss = ex.run(lambda: loss_of(mine).backward(), world)
+    q.put((rank, [p.grad.numpy().copy() for p in params], ex.issue_log, order, len(ex.buckets)))
+    dist.destroy_process_group()
+    del loss
+
+
+def test_overlapped_exchange_two_ranks_gloo(tmp_path):
+    """The overlapped bucketed gradient exchange of the graph step (irads/graph_step.py
+    OverlappedGradExchange, comm="overlap"), world 2 over gloo: hooks, >= 4 buckets, real
+    averaging across ranks, and buckets completed in OPPOSITE orders on the two ranks still
+    issued in the same (index) order.  The averaged gradients equal a single-process step on
+    the full batch (fp64, equal halves of a mean loss: exact up to rounding)."""
+    import torch
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    init_file = str(tmp_path / "pg_init")
+    procs = [ctx.Process(target=_overlap_worker, args=(r, 2, init_file, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in procs:
+        r, grads, issued, order, nb = q.get(timeout=120)
+        res[r] = (grads, issued, order, nb)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    nb = res[0][3]
+    for r in range(2):
+        assert res[r][1] == list(range(nb)), res[r][1]
+    assert res[0][2] != res[1][2]  # the ranks did finish their gradients in different orders
+    params, loss_of = _overlap_model(0)
+    x = torch.randn(8, 6, generator=torch.Generator().manual_seed(9), dtype=torch.float64)
+    # mean over 8 rows = average of the two ranks' means over 4
+    loss_of(x).backward()
+    for p, g0, g1 in zip(params, res[0][0], res[1][0]):
+        torch.testing.assert_close(torch.from_numpy(g0), p.grad, rtol=1e-12, atol=1e-13)
+        torch.testing.assert_close(torch.from_numpy(g1), p.grad, rtol=1e-12, atol=1e-13)
+
+
 def test_split_streams_gradient_matches_slicing():
     """ops.split_streams: the batched-stream split whose backward concatenates the halves'
     gradients (one copy) — same gradient as plain slicing, including an unused half."""

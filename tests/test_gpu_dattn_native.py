@@ -197,3 +197,27 @@ def test_dattn_gate_matches_eager(B, C, H, W):
     assert torch.equal(got[0], want[0]) and torch.equal(got[1], want[1])
     for a, b in zip(got[2:], want[2:]):
         assert ((a - b).norm() / b.norm()).item() < 1e-5
+
+
+@pytest.mark.parametrize("amp", [False, True])
+def test_dattn_nonfinite_upstream_gradient_propagates(amp):
+    """An inf in the upstream gradient (an fp16 GradScaler overflow step) must reach the
+    gradients as inf / NaN, as the reference's float atomics carry it, so that the scaler's
+    finiteness check skips the step: the fixed-point accumulators of the grid-sample backward
+    and of the rpe-table gradient (dattn.hip) turn a non-finite bound into NaN scales instead of
+    converting inf to a finite integer."""
+    from semseg.models.backbones import swin
+    dims, stride, g, h, level, H, W, B = CFGS["s1"]
+    torch.manual_seed(5)
+    m = swin.DAttentionMM(dims, stride=stride, n_groups=g, n_heads=h, level=level).to(DEV).train()
+    fill_module(m, seed=13)
+    x = torch.randn(B, dims, H, W, device=DEV, requires_grad=True)
+    y = torch.rand(B, dims, H, W, device=DEV, requires_grad=True)
+    with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
+        o = m(x, y)
+    go = torch.randn_like(o)
+    go.view(-1)[go.numel() // 3] = float("inf")
+    o.backward(go)
+    for name, t in (("x", x.grad), ("y", y.grad), ("rpe_table", m.rpe_table.grad),
+                    ("conv_offset_x.0.weight", m.conv_offset_x[0].weight.grad)):
+        assert t is not None and not torch.isfinite(t).all(), f"grad {name} is finite despite an inf upstream"

@@ -623,3 +623,43 @@ def test_wgrad_batched_stays_in_its_workspace(count, sums, K, m, n):
             torch.testing.assert_close(sa, A.float().sum(0), rtol=1e-5, atol=1e-3)
         if sb is not None:
             torch.testing.assert_close(sb, B.float().sum(0), rtol=1e-5, atol=1e-3)
+
+
+def test_bias_quads_cache_lives_with_its_table():
+    """ops.bias_quads caches the re-laid bias table on its owner Parameter: a hit while the
+    table is unchanged, a recompute after an in-place update (new version), the entry dropped
+    when the table dies (so a graph that read cached quads holds valid memory exactly as long
+    as its model), and a trainable table being captured recomputes inside the graph."""
+    from irads import ops
+    table = torch.nn.Parameter(torch.randn(529, 4, device=DEV), requires_grad=False)
+    q1 = ops.bias_quads(table.detach(), 4, 32 ** -0.5, owner=table)
+    q2 = ops.bias_quads(table.detach(), 4, 32 ** -0.5, owner=table)
+    assert q1 is q2
+    ref = q1.clone()
+    with torch.no_grad():
+        table.mul_(2.0)
+    q3 = ops.bias_quads(table.detach(), 4, 32 ** -0.5, owner=table)
+    assert q3 is not q1 and not torch.equal(q3, ref)
+    assert ops.bias_quads(table.detach(), 4, 32 ** -0.5) is not q3  # no owner: no caching
+    k = id(table)
+    assert k in ops._QUADS
+    del table
+    import gc
+    gc.collect()
+    assert k not in ops._QUADS
+    tr = torch.nn.Parameter(torch.randn(529, 4, device=DEV))
+    eager = ops.bias_quads(tr.detach(), 4, 1.0, owner=tr)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            inside = ops.bias_quads(tr.detach(), 4, 1.0, owner=tr)
+    torch.cuda.synchronize()
+    assert inside is not eager
+    with torch.no_grad():
+        tr.add_(1.0)
+    g.replay()
+    torch.cuda.synchronize()
+    fresh = ops.bias_quads(tr.detach(), 4, 1.0)
+    assert torch.equal(inside, fresh)

@@ -1,50 +1,93 @@
 """The benchmarked training path against the reference, end to end (C2 / C1 / C4 geometries).
 
-The product runs exactly as bench.py runs it: CMNeXt in training mode under bf16 autocast,
-TRAIN_TYPE Adapter, the fused Swin stages, the bf16 DAttn path, the HIP segmentation-head
-kernels (BN batch statistics), the fused MMST loss, and the step captured into a HIP graph
-and replayed.  Only the random draws are switched off (oracle/train_fixture.py:
-apply_mask, DropPath, Adapter dropout, Dropout2d), identically in the reference fixture
-(oracle/gen_golden.py gen_cmnext_train: the reference modules on CPU in fp32).
+The product runs as bench.py runs it: CMNeXt in training mode, TRAIN_TYPE Adapter, the HIP
+segmentation-head kernels (BN batch statistics), the fused cross-entropy kernels.  Only the random
+draws are switched off (oracle/train_fixture.py: apply_mask, DropPath, Adapter dropout,
+Dropout2d), identically in the reference fixtures (oracle/gen_golden.py: the reference modules on
+CPU, swin.py:1423-1479, train_mm.py:133-148).
 
-Tolerances.  The product computes in bf16 (autocast) and the fixture is the reference in
-fp32, so every bound is set against the bf16 noise of the REFERENCE ITSELF: the fixture also
-holds the deviation of the reference run under bf16 autocast (CPU) from its own fp32 run,
-quantity by quantity ("ref16" below).  Checks:
-  * MMST loss: relative 1e-2;
-  * logits (stride-8 subsample of y, y_rgb, y_dte): relative L2 <= max(1e-2, 2 ref16);
-  * argmax agreement of y >= 99 % where the reference's top-2 margin exceeds 0.05, and
-    >= 97 % everywhere;
-  * trainable gradients: relative L2 <= max(3e-2, 2 ref16) for the 14 tensors stored in
-    full (measured on MI355X: the product's error is 0.8-1.1x the reference's own bf16 error,
-    which reaches 0.3-0.5 for the stage-0 DAttn parameters: those gradients are that
-    sensitive to bf16 rounding in the reference itself); for every trainable tensor, the norm
-    and two seeded random projections (|<g - g_ref, r>| ~ ||g - g_ref||) aggregated over the
-    model <= max(3e-2, 2 ref16), and per tensor <= max(0.15, 10 ref16) as a gross-error
-    detector (a single-sample noise estimate per tensor is heavy-tailed: measured ratios of
-    product to ref16 error have a median near 1 and reach 8 on tensors whose ref16 sample
-    is small; a wrong gradient is off by O(1)).  Conv biases ahead of a training-mode
-    BatchNorm have a mathematically zero gradient; their values are rounding noise on both
-    sides, covered by the ref16 term.
+Fixtures.  train_<tag>.npz: the reference's fp32 step (logits, loss, argmax, top-2 margin,
+gradient norms and seeded projections, 14 full gradients).  train_<tag>_fp64.npz: the same step in
+fp64 (the truth the gradients are compared with) and the reference's OWN precision envelopes,
+exact per tensor: ref32 = |g_ref fp32 - g_fp64| / |g_fp64|, ref16 = the same under CPU bf16
+autocast.
+
+Teacher forcing.  The MMST loss (train_mm.py:137-148) ignores, in the two aux heads' losses, the
+pixels the fused head gets wrong: a discrete decision per pixel.  Where the product's argmax
+differs from the reference's (a few pixels in fp32, ~1.7 % in bf16), the aux heads' gradients
+differ by whole pixels' contributions, which then dominate every gradient upstream of the aux
+heads (measured: C4's stage-2 DTE Adapters and DeformMPG 2's depth offset network at 5e-2 in fp32
+from two flipped pixels, while that block on its own inputs matches fp64 to 5e-4,
+scripts/diag_dmpg.py).  So gradients are compared on the step with the aux targets taken from the
+reference's argmax (same kernels, same loss), and the product's own MMST target is checked
+separately: it must equal the reference's wherever the reference's top-2 margin decides it.
+
+Mathematically zero gradients (ZERO_GRAD): the k bias of DAttn (swin.py:940-951: q.(k + b) shifts
+every key's logit of a query by the same q.b, which the softmax removes), the bias of the 3x3 conv
+ahead of fuse_q's training-mode BatchNorm (swin.py:713-723) and the SegFormer linear_c* biases
+(segformer.py:39-48: a per-channel constant through the bilinear upsample and linear_fuse's 1x1
+conv, removed by its training-mode BatchNorm).  Both sides hold rounding noise: judged against an
+absolute floor (1e-5 x the model's largest gradient norm) instead of relatively.
+
+fp32 (autocast off: the module path with the fp32 kernels), north_star's "fp32 logits within 1e-3":
+  * MMST loss relative 1e-4; logits (stride-8 subsample of y, y_rgb, y_dte) relative L2 <= 1e-3;
+  * argmax of y identical wherever the reference's top-2 margin exceeds 1e-2; the product's MMST
+    target equal to the reference's on those pixels;
+  * every non-zero trainable gradient vs fp64: norm and 2 seeded projections within
+    max(5e-3, 3 ref32) of the norm; the 14 full tensors relative L2 <= the same.
+
+bf16 (autocast, fused Swin stages, bf16 DAttn path; eager and HIP-graph replay):
+  * MMST loss relative 1e-2; logits relative L2 <= max(1e-2, 2 x the reference's bf16 logit error);
+    argmax >= 99 % where the top-2 margin exceeds 0.05, >= 97 % overall; the MMST target equal
+    to the reference's on >= 99 % of the pixels the margin decides;
+  * every non-zero trainable gradient, three ways:
+      - vs fp64 by norm/projections <= min(BF16_CAP = 0.3, max(0.05, K16 ref16)), for every tensor
+        whose reference bf16 noise leaves room under the cap (K16 ref16 <= BF16_CAP);
+      - vs the PRODUCT's own fp32 gradient (full tensors, same inputs, same teacher-forced loss):
+        relative L2 <= max(0.05, K16 ref16), for every tensor;
+      - direction and size: cosine with the fp32 gradient >= 0.5 and norm ratio in [0.5, 2]
+        (a zeroed or sign-flipped gradient fails these whatever its noise level).
+Every measured number is written to $IRADS_REPORT_DIR (default gpurun_out/parity/) as JSON;
+the committed copies are profiles/r03_parity_*.json.
 """
+import contextlib
+import json
+import os
+import re
+
 import numpy as np
 import pytest
 import torch
 
 from fill import fill_module
 from golden_util import Fixture
-from train_fixture import (FULL_GRAD_KEYS, N_PROJ, TRAIN_FIXTURES, adapter_trainable, deterministic_train_mode,
-                           projection, train_inputs)
+from train_fixture import (N_PROJ, TRAIN_FIXTURES, adapter_trainable, deterministic_train_mode, projection,
+                           train_inputs)
 
 DEV = torch.device("cuda", 0)
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPORT_DIR = os.environ.get("IRADS_REPORT_DIR", os.path.join(ROOT, "gpurun_out", "parity"))
 
 pytestmark = pytest.mark.gpu
+
+ZERO_GRAD = re.compile(r"(deform_atten\.proj_k\.bias|deform_atten\.fuse_q\.conv\.0\.bias|linear_c\d\.proj\.bias)$")
+FP32_TOL = 5e-3
+K32 = 3.0
+BF16_CAP = 0.3
+K16 = 4.0
+BF16_FLOOR = 0.05
 
 
 def _rel_l2(a, b):
     a = torch.as_tensor(a).double().cpu().flatten()
     b = torch.as_tensor(b).double().cpu().flatten()
     return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+
+def _write_report(name, report):
+    os.makedirs(REPORT_DIR, exist_ok=True)
+    with open(os.path.join(REPORT_DIR, name + ".json"), "w") as f:
+        json.dump(report, f, indent=1, sort_keys=True, default=float)
 
 
 def _build(fx):
@@ -61,102 +104,240 @@ def _build(fx):
     return model, [torch.from_numpy(a).to(DEV) for a in (rgb, dep, lbl)]
 
 
-def _fwd_bwd(model, loss_fn, batch):
+def _ref_mask(fx, lbl):
+    am = torch.from_numpy(fx["y_argmax"].astype(np.int64)).to(lbl.device)
+    return torch.where(am == lbl, lbl, torch.full_like(lbl, 255))
+
+
+def _fwd_bwd(model, loss_fn, batch, amp=True, aux_target=None):
+    """One training step.  aux_target None: the product's own MMST loss (semseg.losses.mmst_loss,
+    what bench.py runs).  Otherwise the same loss with the aux heads' target given (teacher
+    forcing); the product's own MMST target is returned beside it."""
+    from irads import ops
     from semseg.losses import mmst_loss
     rgb, dep, lbl = batch
-    with torch.autocast("cuda", dtype=torch.bfloat16):
+    ctx = torch.autocast("cuda", dtype=torch.bfloat16) if amp else contextlib.nullcontext()
+    own = None
+    with ctx:
         y, yr, yd = model([rgb, dep])
-        loss = mmst_loss(loss_fn, y, yr, yd, lbl)
+        if aux_target is None:
+            loss = mmst_loss(loss_fn, y, yr, yd, lbl)
+        else:
+            l1, own = ops.cross_entropy(y, lbl, 255, None, return_match=True)
+            loss = l1 + 0.01 * loss_fn(yr, aux_target) + 0.01 * loss_fn(yd, aux_target)
     loss.backward()
-    return loss, y, yr, yd
+    return loss, y, yr, yd, own
 
 
-def _check(fx, model, loss, y, yr, yd, what, report, fails):
+def _check_outputs(fx, loss, y, yr, yd, own_mask, lbl, what, report, fails, loss_tol, logit_tol, margin_min,
+                   argmax_all_min, mask_min):
     ref_loss = float(fx["loss"][0])
-    rl = abs(float(loss) - ref_loss) / abs(ref_loss)
+    rl = abs(float(loss.detach()) - ref_loss) / abs(ref_loss)
     report[f"{what}.loss_rel"] = rl
-    if not (rl <= 1e-2):
-        fails.append(f"{what}: MMST loss {float(loss)} vs reference {ref_loss}")
+    if not (rl <= loss_tol):
+        fails.append(f"{what}: MMST loss {float(loss)} vs reference {ref_loss} (rel {rl:.3e} > {loss_tol:.1e})")
     for name, t in (("y", y), ("y_rgb", yr), ("y_dte", yd)):
         sub = t.detach().float()[:, :, ::8, ::8].cpu()
         e = _rel_l2(sub, fx[name + "_sub"])
         report[f"{what}.{name}_rel_l2"] = e
-        tol = max(1e-2, 2 * float(fx[f"bf16_{name}_rel_l2"]))
+        tol = logit_tol(name)
         if not (e <= tol):
             fails.append(f"{what}: {name} relative L2 {e:.3e} > {tol:.3e}")
     am = y.detach().argmax(1).cpu().numpy()
     ref_am = fx["y_argmax"].astype(np.int64)
-    margin = fx["y_margin"].astype(np.float32)
+    decided = fx["y_margin"].astype(np.float32) > margin_min
     agree_all = float((am == ref_am).mean())
-    decided = margin > 0.05
     agree = float((am == ref_am)[decided].mean())
     report[f"{what}.argmax_agree"] = agree_all
     report[f"{what}.argmax_agree_decided"] = agree
     report[f"{what}.decided_frac"] = float(decided.mean())
-    if not (agree >= 0.99):
-        fails.append(f"{what}: argmax agreement {agree:.4f} on decided pixels")
-    if not (agree_all >= 0.97):
-        fails.append(f"{what}: argmax agreement {agree_all:.4f} overall")
-    names = fx["grad_names"].tolist()
-    norms, projs = fx["grad_norms"], fx["grad_projs"]
+    report[f"{what}.argmax_flipped_pixels"] = int((am != ref_am).sum())
+    if not (agree >= mask_min):
+        fails.append(f"{what}: argmax agreement {agree:.5f} on pixels with margin > {margin_min}")
+    if not (agree_all >= argmax_all_min):
+        fails.append(f"{what}: argmax agreement {agree_all:.5f} overall")
+    l = lbl.cpu().numpy()
+    want = np.where(ref_am == l, l, 255)
+    got = own_mask.cpu().numpy()
+    m_agree = float((got == want)[decided].mean())
+    report[f"{what}.mmst_target_agree_decided"] = m_agree
+    report[f"{what}.mmst_target_differs_pixels"] = int((got != want).sum())
+    if not (m_agree >= mask_min):
+        fails.append(f"{what}: MMST target agrees with the reference on {m_agree:.5f} of decided pixels")
+
+
+def _grad_table(fx, fx64, model):
+    """Per trainable tensor: name, gradient (fp64 numpy), the norm/projection error vs fp64
+    relative to the fp64 norm, the absolute error and the fp64 norm."""
+    names = fx64["grad_names"].tolist()
+    norms, projs = fx64["grad_norms"], fx64["grad_projs"]
     params = dict(model.named_parameters())
     assert sorted(names) == sorted(n for n, p in params.items() if p.requires_grad)
-    num = den = 0.0
-    worst = (0.0, "")
-    table = []
-    # conv biases ahead of a training-mode BatchNorm (DAttn fuse_q) have a mathematically zero
-    # gradient (rounding noise on both sides): judged against an absolute floor
-    floor = 1e-5 * float(norms.max())
-    ref16 = fx["bf16_grad_err"]
+    out = []
     for k, n in enumerate(names):
         g = params[n].grad
-        if g is None:
-            fails.append(f"{what}: no gradient for {n}")
+        g64 = None if g is None else g.detach().double().cpu().numpy()
+        if g64 is None:
+            out.append((n, None, float("inf"), float("inf"), float(norms[k])))
             continue
-        g64 = g.detach().double().cpu().numpy()
-        if "g." + n in fx:
-            e = _rel_l2(g64, fx["g." + n])
-            report[f"{what}.full.{n}"] = e
-            tol = max(3e-2, 2 * float(fx["bf16_full_rel." + n]))
-            if not (e <= tol):
-                fails.append(f"{what}: gradient {n} relative L2 {e:.3e} > {tol:.3e}")
         nr = float(norms[k])
         d = [projection(n, g64, j) - float(projs[k][j]) for j in range(N_PROJ)]
-        dn = float(np.sqrt((g64 * g64).sum())) - nr
-        per = max(abs(x) for x in d + [dn]) / (nr + floor)
-        tol = max(0.15, 10 * float(ref16[k]))
-        table.append((per / max(float(ref16[k]), 1e-3), round(per, 4), round(float(ref16[k]), 4), n))
-        if per / tol > worst[0]:
-            worst = (per / tol, n)
-        num += sum(x * x for x in d) / N_PROJ
-        den += nr * nr
-        if not (per <= tol):
-            fails.append(f"{what}: gradient {n}: projection / norm error {per:.3e} > {tol:.3e}")
-    agg = float(np.sqrt(num / den))
-    report[f"{what}.grad_agg_rel"] = agg
-    report[f"{what}.grad_worst_frac_of_tol"] = worst
-    report[f"{what}.grad_ratio_to_ref16_median"] = float(np.median([r[0] for r in table]))
-    if what == "eager":
-        for row in sorted(table, reverse=True)[:5]:
-            print("  ratio %.2f err %.4f ref16 %.4f %s" % row)
-    tol = max(3e-2, 2 * float(fx["bf16_grad_agg_rel"]))
-    if not (agg <= tol):
-        fails.append(f"{what}: aggregate gradient error {agg:.3e} > {tol:.3e}")
+        d.append(float(np.sqrt((g64 * g64).sum())) - nr)
+        absd = max(abs(x) for x in d)
+        out.append((n, g64, absd / max(nr, 1e-300), absd, nr))
+    return out
+
+
+def _zero_floor(fx64):
+    return 1e-5 * float(fx64["grad_norms"].max())
+
+
+def _fp32_step(tag):
+    """The product's fp32 training step, teacher-forced, vs the fp64 reference; returns its
+    gradients (for the bf16 test) and the failures."""
+    from semseg.losses import get_loss
+    fx, fx64 = Fixture(f"train_{tag}.npz"), Fixture(f"train_{tag}_fp64.npz")
+    model, batch = _build(fx)
+    loss_fn = get_loss("CrossEntropy", 255)
+    report, fails = {"tag": tag, "mode": "fp32"}, []
+    bn = model.decode_head.linear_fuse.bn
+    loss, y, yr, yd, own = _fwd_bwd(model, loss_fn, batch, amp=False, aux_target=_ref_mask(fx, batch[2]))
+    torch.cuda.synchronize()
+    _check_outputs(fx, loss, y, yr, yd, own, batch[2], "fp32", report, fails, loss_tol=1e-4,
+                   logit_tol=lambda n: 1e-3, margin_min=1e-2, argmax_all_min=0.995, mask_min=1.0)
+    for name, t in (("y", y), ("y_rgb", yr), ("y_dte", yd)):
+        report[f"fp32.{name}_rel_l2_vs_fp64"] = _rel_l2(t.detach()[:, :, ::8, ::8], fx64[name + "_sub"])
+    e = _rel_l2(bn.running_mean.detach().cpu(), fx["bn_rm.decode_head"])
+    report["fp32.bn_running_mean_rel_l2"] = e
+    if e > 1e-4:
+        fails.append(f"fp32: head BN running mean relative L2 {e:.3e}")
+    floor = _zero_floor(fx64)
+    ref32 = fx64["ref32_rel"]
+    per, grads = {}, {}
+    for k, (n, g64, rel, absd, nr) in enumerate(_grad_table(fx, fx64, model)):
+        grads[n] = g64
+        if g64 is None:
+            fails.append(f"fp32: no gradient for {n}")
+            continue
+        gn = float(np.sqrt((g64 * g64).sum()))
+        if ZERO_GRAD.search(n):
+            per[n] = {"zero_grad": True, "norm": gn, "ref64_norm": nr, "floor": floor}
+            if not (gn <= floor):
+                fails.append(f"fp32: mathematically-zero gradient {n} has norm {gn:.2e} > {floor:.2e}")
+            continue
+        tol = max(FP32_TOL, K32 * float(ref32[k]))
+        row = {"proj_rel_vs_fp64": rel, "ref32": float(ref32[k]), "tol": tol}
+        if not (rel <= tol):
+            fails.append(f"fp32: gradient {n}: projection / norm error vs fp64 {rel:.3e} > {tol:.3e}")
+        if "g." + n in fx64:
+            fe = _rel_l2(g64, fx64["g." + n])
+            row["full_rel_l2_vs_fp64"] = fe
+            if not (fe <= tol):
+                fails.append(f"fp32: gradient {n} relative L2 vs fp64 {fe:.3e} > {tol:.3e}")
+        per[n] = row
+    rels = [(v["proj_rel_vs_fp64"], n) for n, v in per.items() if "proj_rel_vs_fp64" in v]
+    report["fp32.grad_rel_max"] = max(rels)
+    report["fp32.grad_rel_median"] = float(np.median([r for r, _ in rels]))
+    report["fp32.grad_worst_frac_of_tol"] = max((v["proj_rel_vs_fp64"] / v["tol"], n) for n, v in per.items()
+                                                if "tol" in v)
+    report["fp32.n_tensors"] = len(per)
+    report["fp32.n_zero_grad"] = sum(1 for v in per.values() if v.get("zero_grad"))
+    report["fp32.per_tensor"] = per
+    report["fails"] = fails
+    _write_report(f"train_{tag}_fp32", report)
+    del model, loss, y, yr, yd
+    torch.cuda.empty_cache()
+    return grads, fails
+
+
+_FP32 = {}
+
+
+def _fp32(tag):
+    if tag not in _FP32:
+        _FP32[tag] = _fp32_step(tag)
+    return _FP32[tag]
+
+
+@pytest.mark.parametrize("tag", list(TRAIN_FIXTURES))
+def test_train_step_fp32_vs_reference(tag):
+    _, fails = _fp32(tag)
+    assert not fails, fails
+
+
+def _check_bf16_grads(fx, fx64, model, own32, what, report, fails):
+    ref16 = fx64["ref16_rel"]
+    floor = _zero_floor(fx64)
+    per = {}
+    for k, (n, g64, rel, absd, nr) in enumerate(_grad_table(fx, fx64, model)):
+        if g64 is None:
+            fails.append(f"{what}: no gradient for {n}")
+            continue
+        gn = float(np.sqrt((g64 * g64).sum()))
+        if ZERO_GRAD.search(n):
+            per[n] = {"zero_grad": True, "norm": gn, "floor": floor}
+            if not (gn <= 100 * floor):
+                fails.append(f"{what}: mathematically-zero gradient {n} has norm {gn:.2e} > {100 * floor:.2e}")
+            continue
+        r16 = float(ref16[k])
+        o = own32[n]
+        on = float(np.sqrt((o * o).sum()))
+        own = _rel_l2(g64, o)
+        cos = float((g64 * o).sum() / max(gn * on, 1e-300))
+        ratio = gn / max(on, 1e-300)
+        tol = max(BF16_FLOOR, K16 * r16)
+        row = {"proj_rel_vs_fp64": rel, "vs_own_fp32": own, "cos_own_fp32": cos, "norm_ratio_own_fp32": ratio,
+               "ref16": r16, "tol": tol}
+        if tol <= BF16_CAP:
+            if not (rel <= tol):
+                fails.append(f"{what}: gradient {n}: projection / norm error vs fp64 {rel:.3e} > {tol:.3e}")
+        else:
+            row["ref_noise_above_cap"] = True
+        if "g." + n in fx64:
+            fe = _rel_l2(g64, fx64["g." + n])
+            row["full_rel_l2_vs_fp64"] = fe
+            if tol <= BF16_CAP and not (fe <= tol):
+                fails.append(f"{what}: gradient {n} relative L2 vs fp64 {fe:.3e} > {tol:.3e}")
+        if not (own <= tol):
+            fails.append(f"{what}: gradient {n} vs the product's fp32 gradient: relative L2 {own:.3e} > {tol:.3e}")
+        if not (cos >= 0.5 and 0.5 <= ratio <= 2.0):
+            fails.append(f"{what}: gradient {n} vs the product's fp32 gradient: cosine {cos:.3f}, norm ratio {ratio:.3f}")
+        per[n] = row
+    rows = [v for v in per.values() if "vs_own_fp32" in v]
+    report[f"{what}.grad_vs_own_fp32_median"] = float(np.median([v["vs_own_fp32"] for v in rows]))
+    report[f"{what}.grad_vs_own_fp32_worst"] = max((v["vs_own_fp32"], n) for n, v in per.items()
+                                                   if "vs_own_fp32" in v)
+    report[f"{what}.grad_worst_frac_of_tol"] = max((max(v["vs_own_fp32"], 0 if v.get("ref_noise_above_cap")
+                                                        else v["proj_rel_vs_fp64"]) / v["tol"], n)
+                                                   for n, v in per.items() if "tol" in v)
+    report[f"{what}.grad_ratio_to_ref16_median"] = float(np.median([v["vs_own_fp32"] / max(v["ref16"], 1e-6)
+                                                                    for v in rows]))
+    report[f"{what}.n_checked_vs_fp64"] = sum(1 for v in rows if not v.get("ref_noise_above_cap"))
+    report[f"{what}.n_ref_noise_above_cap"] = sum(1 for v in rows if v.get("ref_noise_above_cap"))
+    report[f"{what}.min_cos_own_fp32"] = min((v["cos_own_fp32"], n) for n, v in per.items() if "cos_own_fp32" in v)
+    report[f"{what}.per_tensor"] = per
 
 
 @pytest.mark.parametrize("tag", list(TRAIN_FIXTURES))
 def test_train_step_vs_reference(tag):
     from semseg.losses import get_loss
     from irads import swin_fused  # noqa: F401  (the fused stage must be the path that runs)
-    fx = Fixture(f"train_{tag}.npz")
+    own32, _ = _fp32(tag)
+    fx, fx64 = Fixture(f"train_{tag}.npz"), Fixture(f"train_{tag}_fp64.npz")
     model, batch = _build(fx)
     loss_fn = get_loss("CrossEntropy", 255)
-    report, fails = {}, []
-    # eager step: also the BatchNorm running statistics of one training step
+    aux = _ref_mask(fx, batch[2])
+    report, fails = {"tag": tag, "mode": "bf16"}, []
+
+    def logit_tol(name):
+        return max(1e-2, 2 * float(fx[f"bf16_{name}_rel_l2"]))
+
+    out_kw = dict(loss_tol=1e-2, logit_tol=logit_tol, margin_min=0.05, argmax_all_min=0.97, mask_min=0.99)
     bn = model.decode_head.linear_fuse.bn
-    loss, y, yr, yd = _fwd_bwd(model, loss_fn, batch)
+    loss, y, yr, yd, own = _fwd_bwd(model, loss_fn, batch, aux_target=aux)
     torch.cuda.synchronize()
-    _check(fx, model, loss, y, yr, yd, "eager", report, fails)
+    _check_outputs(fx, loss, y, yr, yd, own, batch[2], "eager", report, fails, **out_kw)
+    _check_bf16_grads(fx, fx64, model, own32, "eager", report, fails)
     e = _rel_l2(bn.running_mean.detach().cpu(), fx["bn_rm.decode_head"])
     report["eager.bn_running_mean_rel_l2"] = e
     if e > 1e-2:
@@ -164,7 +345,7 @@ def test_train_step_vs_reference(tag):
     # graph replay, as bench.py / GraphedTrainStep run it.  The eager step's autograd graph is
     # released first: capturing while it is alive ended in a segfault inside capture_end
     # (hipGraphInstantiate) on ROCm 7.2 / torch 2.10; GraphedTrainStep never holds one.
-    del loss, y, yr, yd
+    del loss, y, yr, yd, own
     torch.cuda.synchronize()
     params = [p for p in model.parameters() if p.requires_grad]
     side = torch.cuda.Stream(DEV)
@@ -173,16 +354,28 @@ def test_train_step_vs_reference(tag):
         for _ in range(2):
             for p in params:
                 p.grad = None
-            _fwd_bwd(model, loss_fn, batch)
+            _fwd_bwd(model, loss_fn, batch, aux_target=aux)
     torch.cuda.current_stream(DEV).wait_stream(side)
     torch.cuda.synchronize()
     for p in params:
         p.grad = None
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g):
-        out = _fwd_bwd(model, loss_fn, batch)
+        out = _fwd_bwd(model, loss_fn, batch, aux_target=aux)
     g.replay()
     torch.cuda.synchronize()
-    _check(fx, model, *out, "graph", report, fails)
-    print(tag, {k: (round(v, 6) if isinstance(v, float) else v) for k, v in report.items()})
+    _check_outputs(fx, *out, batch[2], "graph", report, fails, **out_kw)
+    _check_bf16_grads(fx, fx64, model, own32, "graph", report, fails)
+    # the product's own MMST loss (no teacher forcing), as bench.py runs it: same value up to the
+    # pixels whose decision flipped
+    for p in params:
+        p.grad = None
+    l_own = _fwd_bwd(model, loss_fn, batch)[0]
+    report["eager_own_mmst.loss_rel"] = abs(float(l_own.detach()) - float(fx["loss"][0])) / abs(float(fx["loss"][0]))
+    if not (report["eager_own_mmst.loss_rel"] <= 1e-2):
+        fails.append(f"own MMST loss relative error {report['eager_own_mmst.loss_rel']:.3e}")
+    report["fails"] = fails
+    _write_report(f"train_{tag}_bf16", report)
+    print(tag, {k: (round(v, 6) if isinstance(v, float) else v) for k, v in report.items()
+                if not k.endswith("per_tensor")})
     assert not fails, fails
