@@ -19,7 +19,7 @@ import torch.nn as nn
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 from fill import fill_module, seeded  # noqa: E402
-from ref_import import load_reference  # noqa: E402
+from ref_import import load_reference, load_val_mm  # noqa: E402
 
 OUT = os.path.join(os.path.dirname(HERE), "tests", "golden")
 torch.set_num_threads(8)
@@ -524,6 +524,49 @@ def gen_cmnext_train_fp64(ref, tags=None):
         del model, y, yr, yd, loss, g64, g32, g16
 
 
+# --------------------------------------------------------------------------- MSF evaluation
+from msf_case import MSF_CASE, msf_inputs  # noqa: E402
+
+
+def gen_msf(ref):
+    """The reference's evaluate_msf (val_mm.py:87-120) on the tiny fp32 CMNeXt, two images one per
+    batch, with configs/nyu_rgbd.yaml's MSF scales and flip: the per-image summed probabilities
+    that reach Metrics.update (recorded by a Metrics subclass) and the returned IoUs."""
+    L = load_val_mm()
+    vm = L.val_mm
+    c = MSF_CASE
+    h = build_ref_tiny(ref, c["n_cls"])
+
+    class Tiny(type(h)):
+        def forward(self, x):
+            return ref.cmnext.CMNeXt.forward(self, x)
+    h.__class__ = Tiny
+    fill_module(h, seed=c["fill_seed"])
+    rgb, dep, lbl = msf_inputs()
+    seen = []
+
+    class RecMetrics(L.metrics.Metrics):
+        def update(self, pred, target):
+            seen.append(pred.detach().clone())
+            return super().update(pred, target)
+
+    class Loader(list):
+        dataset = types.SimpleNamespace(n_classes=c["n_cls"], ignore_label=255)
+    loader = Loader([([t(rgb[i:i + 1]), t(dep[i:i + 1])], t(lbl[i:i + 1])) for i in range(c["B"])])
+    orig = vm.Metrics
+    vm.Metrics = RecMetrics
+    try:
+        acc, macc, f1, mf1, ious, miou = vm.evaluate_msf(h, loader, "cpu", list(c["scales"]), c["flip"])
+    finally:
+        vm.Metrics = orig
+    probs = torch.cat(seen)
+    top2 = probs.topk(2, dim=1).values
+    print("msf miou", miou, "ious", ious)
+    save("msf_eval.npz", probs=probs.float(), margin=(top2[:, 0] - top2[:, 1]).float(),
+         argmax=probs.argmax(1).to(torch.uint8), ious=np.array(ious, dtype=np.float64), miou=np.array(miou),
+         state_keys=np.array(sorted(h.state_dict().keys())))
+
+
 # --------------------------------------------------------------------------- vCLR DINO transformer
 from dino_case import DINO_BS, DINO_DN, DINO_LAYERS, DINO_LEVELS, DINO_PROPOSALS, dino_inputs  # noqa: E402
 
@@ -670,7 +713,7 @@ if __name__ == "__main__":
     torch.manual_seed(0)
     fns = {"dino": gen_dino, "msda": gen_msda, "swin": gen_swin_wmsa, "block": gen_swin_block, "dattn": gen_dattn,
            "fusion": gen_fusion_small, "cmnext": gen_cmnext, "sb": gen_sb, "metrics": gen_metrics_loss,
-           "train": gen_cmnext_train, "train64": gen_cmnext_train_fp64}
+           "train": gen_cmnext_train, "train64": gen_cmnext_train_fp64, "msf": gen_msf}
     for w in which:
         if ":" in w:  # e.g. train64:c2_swinb_512
             w, tag = w.split(":")

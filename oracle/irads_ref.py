@@ -591,6 +591,45 @@ def metrics_tp_fp_fn(pred_logits, gt, n_classes, ignore=255):
     return tp, fp, fn
 
 
+def metrics_iou(tp, fp, fn):
+    """semseg/metrics.py:85-96 compute_iou: per-class Jaccard tp / max(tp + fp + fn, 1e-8) as
+    fractions (the reference's rounding loop rebinds a loop variable and changes nothing), and
+    round(mean * 100, 2)."""
+    jac = [float(a) / max(float(a + b + c), 1e-8) for a, b, c in zip(tp, fp, fn)]
+    return jac, round(sum(jac) / len(jac) * 100, 2)
+
+
+def evaluate_msf(model, batches, n_classes, scales, flip, ignore=255):
+    """val_mm.py:87-120: for each batch, the softmax probabilities of the model at every scale
+    (sizes int(scale * H) rounded UP to a multiple of 32, align_corners=True bilinear resizes of
+    every modality, and the logits resized back the same way), plus the horizontally flipped
+    input's (logits flipped back), summed; Metrics (semseg/metrics.py) on the sums.  Returns the
+    per-batch summed probabilities and (ious, miou)."""
+    import math
+    import torch.nn.functional as F
+    model.eval()
+    sums, tp, fp, fn = [], [0] * n_classes, [0] * n_classes, [0] * n_classes
+    with torch.no_grad():
+        for images, labels in batches:
+            B, H, W = labels.shape
+            acc = torch.zeros(B, n_classes, H, W)
+            for scale in scales:
+                nH, nW = int(scale * H), int(scale * W)
+                nH, nW = int(math.ceil(nH / 32)) * 32, int(math.ceil(nW / 32)) * 32
+                xs = [F.interpolate(img, size=(nH, nW), mode="bilinear", align_corners=True) for img in images]
+                for flipped in ([False, True] if flip else [False]):
+                    inp = [torch.flip(x, dims=(3,)) for x in xs] if flipped else xs
+                    logits = model(inp)[0]
+                    if flipped:
+                        logits = torch.flip(logits, dims=(3,))
+                    logits = F.interpolate(logits, size=(H, W), mode="bilinear", align_corners=True)
+                    acc += logits.softmax(dim=1)
+            sums.append(acc)
+            a, b, c = metrics_tp_fp_fn(acc, labels, n_classes, ignore)
+            tp, fp, fn = [x + y for x, y in zip(tp, a)], [x + y for x, y in zip(fp, b)], [x + y for x, y in zip(fn, c)]
+    return sums, metrics_iou(tp, fp, fn)
+
+
 # ====================================================================== training objective
 def mmst_loss(logits, logits_rgb, logits_dte, lbl, ignore_label=255, weight=None):
     """train_mm.py:137-148 with CrossEntropy (semseg/losses.py:6-19): the two modality

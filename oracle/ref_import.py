@@ -214,6 +214,22 @@ def load_dino():
     return types.SimpleNamespace(**_LOADED)
 
 
+def load_val_mm():
+    """The reference's evaluation driver val_mm.py (evaluate / evaluate_msf, val_mm.py:64-120).
+    Its module-level imports that the evaluation functions never use (datasets, augmentations,
+    the utils' DDP / logging helpers) are empty stand-ins; semseg.metrics is the reference's."""
+    ref = load_reference()
+    if "val_mm" in _LOADED:
+        return ref
+    _mod("semseg.datasets").__path__ = []
+    _mod("semseg.augmentations_mm", get_val_augmentation=None)
+    _mod("semseg.utils").__path__ = []
+    _mod("semseg.utils.utils", fix_seeds=None, setup_cudnn=None, cleanup_ddp=None, setup_ddp=None,
+         get_logger=None, cal_flops=None, print_iou=None)
+    _LOADED.update(val_mm=_load("reference_val_mm", "val_mm.py"))
+    return types.SimpleNamespace(**_LOADED)
+
+
 if __name__ == "__main__":
     r = load_reference()
     print(sorted(vars(r)))

@@ -39,11 +39,47 @@ def main():
             out.register_hook(lambda g: cap[i].__setitem__("gout", g.detach().clone()))
         return h
     hs = [model.backbone.DeformMPGBlocks[i].register_forward_hook(fwd_hook(i)) for i in blocks]
-    T._fwd_bwd(model, get_loss("CrossEntropy", 255), batch, amp=False)
+    amp = bool(os.environ.get("DIAG_AMP"))
+    T._fwd_bwd(model, get_loss("CrossEntropy", 255), batch, amp=amp)
     torch.cuda.synchronize()
     for h in hs:
         h.remove()
+    if amp:  # bf16: the block's fast path vs its module path vs fp32, on the captured inputs
+        from irads import ops
+        for i in blocks:
+            blk = model.backbone.DeformMPGBlocks[i]
+            args, gout = cap[i]["args"], cap[i]["gout"]
+            res = {}
+            for mode in ("fast", "module", "fp32"):
+                orig = ops.dattn_offset_ok
+                if mode != "fast":
+                    ops.dattn_offset_ok = lambda *a, **k: False
+                try:
+                    for p in blk.parameters():
+                        p.grad = None
+                    a = (args[0].float() if mode == "fp32" else args[0]).clone().requires_grad_()
+                    b = (args[1].float() if mode == "fp32" else args[1]).clone().requires_grad_()
+                    with torch.autocast("cuda", dtype=torch.bfloat16, enabled=mode != "fp32"):
+                        o = blk(a, b, *args[2:])
+                    o.backward(gout.to(o.dtype))
+                finally:
+                    ops.dattn_offset_ok = orig
+                res[mode] = {n: p.grad.detach().double().cpu() for n, p in blk.named_parameters() if p.grad is not None}
+            print(f"block {i} (bf16 fast / module vs fp32 on the captured inputs):", flush=True)
+            rows = sorted(((rel(res["fast"][n], res["fp32"][n]), rel(res["module"][n], res["fp32"][n]), n)
+                           for n in res["fp32"] if float(res["fp32"][n].norm()) > 0), reverse=True)
+            for r in rows[:12]:
+                print("   fast %.2e  module %.2e  %s" % r, flush=True)
+            for r in rows:
+                if "get_sample_weight" in r[2]:
+                    print("   fast %.2e  module %.2e  %s" % r, flush=True)
+        return
     report = {}
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    if os.environ.get("DIAG_SAVE"):
+        for i in blocks:
+            torch.save({"x_rgb": cap[i]["args"][0].cpu(), "x_dte": cap[i]["args"][1].cpu(), "gout": cap[i]["gout"].cpu()},
+                       os.path.join(ROOT, "gpurun_out", f"dmpg_io_{tag}_{i}.pt"))
     for i in blocks:
         blk = model.backbone.DeformMPGBlocks[i]
         bb = model.backbone

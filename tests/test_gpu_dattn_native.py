@@ -16,7 +16,9 @@ DEV = "cuda"
 
 # (dims, stride, groups, heads, level, H, W, B): the four Swin-B stages at 512², Swin-L stage 0
 CFGS = {"s0": (16, 8, 1, 2, 0, 128, 128, 2), "s1": (32, 4, 2, 4, 1, 64, 64, 2), "s2": (64, 2, 4, 8, 2, 32, 32, 2),
-        "s3": (128, 1, 8, 16, 3, 16, 16, 4), "swinl_s0": (24, 8, 1, 2, 0, 128, 128, 2)}
+        "s3": (128, 1, 8, 16, 3, 16, 16, 4), "swinl_s0": (24, 8, 1, 2, 0, 128, 128, 2),
+        # Swin-L at C4's 480x640 (head channels 12, group channels 24)
+        "swinl_s1": (48, 4, 2, 4, 1, 60, 80, 2), "swinl_s2": (96, 2, 4, 8, 2, 30, 40, 2)}
 
 
 def _rel(a, b):
@@ -82,7 +84,7 @@ def test_dattn_offset_kernel_matches_module_path(tag, channels_last):
         assert _rel(a, b) < 2e-2, (n, _rel(a, b))
 
 
-@pytest.mark.parametrize("tag", ["s0", "s1", "s2", "s3"])
+@pytest.mark.parametrize("tag", ["s0", "s1", "s2", "s3", "swinl_s1", "swinl_s2"])
 def test_dattn_amp_path_matches_module_path(tag):
     """DAttentionMM under bf16 autocast: the token-major fast path (1x1 convs as GEMMs, offset
     kernels, one fp32 cast of q) against the module path it replaces (MIOpen convolutions,
@@ -221,3 +223,51 @@ def test_dattn_nonfinite_upstream_gradient_propagates(amp):
     for name, t in (("x", x.grad), ("y", y.grad), ("rpe_table", m.rpe_table.grad),
                     ("conv_offset_x.0.weight", m.conv_offset_x[0].weight.grad)):
         assert t is not None and not torch.isfinite(t).all(), f"grad {name} is finite despite an inf upstream"
+
+
+def _attn_core_ref(q, k, v, px, py, rpe, qgy, qgx, B, nH, G, H, W, scale):
+    """The attention core of DAttentionMM (swin.py:940-1016) in plain torch: scale q^T k plus the
+    rpe bias grid_sample(rpe_table, 0.5 (q_grid - pos), bilinear, align_corners=True) for the x-
+    and y-modality keys, softmax over the 2n keys, times v."""
+    import torch.nn.functional as F
+    hpg = nH // G
+    qg = torch.stack(torch.meshgrid(qgy, qgx, indexing="ij"), -1).reshape(1, H * W, 1, 2)
+    bias = []
+    for pos in (px, py):
+        disp = (qg - pos.reshape(B * G, 1, -1, 2)) * 0.5                      # (B*G, HW, n, 2) (y, x)
+        tab = rpe.reshape(G, hpg, *rpe.shape[1:]).repeat(B, 1, 1, 1)           # (B*G, hpg, Ht, Wt)
+        bias.append(F.grid_sample(tab, disp[..., (1, 0)], mode="bilinear", align_corners=True))
+    bias = torch.cat(bias, -1).reshape(B * nH, H * W, -1)
+    attn = torch.einsum("bcm,bcn->bmn", q, k) * scale + bias
+    return torch.einsum("bmn,bcn->bcm", attn.softmax(-1), v)
+
+
+@pytest.mark.parametrize("Hk,Wk", [(16, 32), (24, 30)])
+def test_dattn_attention_core_many_keys_vs_fp64(Hk, Wk):
+    """The fused attention core (irads_dattn_attn_fwd / _bwd_ws) with 2n = 1024 and 1440 keys (the
+    backward's pass K then spans one or two key blocks) against the plain-torch core in fp64:
+    output and the q, k, v, position gradients to 2e-4; the rpe-table gradient to 1e-3 (pass Q
+    accumulates it per workgroup in int32 fixed point at 2^-31 of the workgroup's L1 bound:
+    measured 3-5e-4)."""
+    from irads.ops import DAttnAttentionFn
+    B, nH, G, hc, H, W = 2, 2, 1, 8, 32, 40
+    torch.manual_seed(11)
+    n = Hk * Wk
+    q = torch.randn(B * nH, hc, H * W, dtype=torch.float64)
+    k = torch.randn(B * nH, hc, 2 * n, dtype=torch.float64)
+    v = torch.randn(B * nH, hc, 2 * n, dtype=torch.float64)
+    px = (torch.rand(B * G, Hk, Wk, 2, dtype=torch.float64) * 2 - 1)
+    py = (torch.rand(B * G, Hk, Wk, 2, dtype=torch.float64) * 2 - 1)
+    rpe = torch.randn(nH, 119, 159, dtype=torch.float64) * 0.5
+    qgy, qgx = torch.linspace(-1, 1, H, dtype=torch.float64), torch.linspace(-1, 1, W, dtype=torch.float64)
+    go = torch.randn(B * nH, hc, H * W, dtype=torch.float64)
+    ins = [q, k, v, px, py, rpe]
+    ref_in = [t.clone().requires_grad_() for t in ins]
+    o_ref = _attn_core_ref(*ref_in, qgy, qgx, B, nH, G, H, W, hc ** -0.5)
+    g_ref = torch.autograd.grad(o_ref, ref_in, go)
+    dev_in = [t.float().to(DEV).requires_grad_() for t in ins]
+    o = DAttnAttentionFn.apply(*dev_in, qgy.float().to(DEV), qgx.float().to(DEV), B, nH, G, H, W, hc ** -0.5)
+    g = torch.autograd.grad(o, dev_in, go.float().to(DEV))
+    assert _rel(o.cpu(), o_ref.float()) < 1e-5
+    for name, a, b in zip(("q", "k", "v", "pos_x", "pos_y", "rpe"), g, g_ref):
+        assert _rel(a.cpu(), b.float()) < (1e-3 if name == "rpe" else 2e-4), (name, _rel(a.cpu(), b.float()))

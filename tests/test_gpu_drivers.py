@@ -257,3 +257,73 @@ def test_dp_two_ranks_gradients(tmp_path, mode):
     rel = (num / den) ** 0.5
     print(f"dp {mode}: relative L2 vs single process {rel:.3e}")
     assert rel < 1e-4, rel
+
+
+def test_evaluate_msf_matches_reference():
+    """val_mm.evaluate_msf (multi-scale + flip evaluation, the path the +-0.2 mIoU target is
+    measured on) against the reference's evaluate_msf (val_mm.py:87-120) on the tiny fp32 CMNeXt:
+    configs/nyu_rgbd.yaml's six scales with flip, two images one per batch (msf_eval.npz,
+    oracle/gen_golden.py gen_msf).  The summed probabilities that reach Metrics.update within
+    2e-5 of the reference (12 softmaxes of an fp32 model, CPU vs GPU summation order), the
+    argmax identical wherever the reference's top-2 margin exceeds 1e-3, and the IoUs equal."""
+    import val_mm
+    from fill import fill_module
+    from msf_case import MSF_CASE, msf_inputs
+    from semseg.metrics import Metrics
+    fx = Fixture("msf_eval.npz")
+    c = MSF_CASE
+    m = _tiny_model(c["n_cls"]).cuda()
+    assert sorted(m.state_dict().keys()) == fx["state_keys"].tolist()
+    fill_module(m, seed=c["fill_seed"])
+    rgb, dep, lbl = (torch.from_numpy(a) for a in msf_inputs())
+    seen = []
+
+    class RecMetrics(Metrics):
+        def update(self, pred, target):
+            seen.append(pred.detach().float().cpu())
+            return super().update(pred, target)
+
+    class Loader(list):
+        dataset = type("D", (), {"n_classes": c["n_cls"], "ignore_label": 255})
+    loader = Loader([([rgb[i:i + 1], dep[i:i + 1]], lbl[i:i + 1]) for i in range(c["B"])])
+    orig, amp = val_mm.Metrics, dict(val_mm._AMP)
+    val_mm.Metrics = RecMetrics
+    val_mm._AMP["dtype"] = None  # fp32, as the reference evaluates
+    try:
+        acc, macc, f1, mf1, ious, miou = val_mm.evaluate_msf(m, loader, torch.device("cuda"), list(c["scales"]),
+                                                             c["flip"])
+    finally:
+        val_mm.Metrics = orig
+        val_mm._AMP.update(amp)
+    probs = torch.cat(seen)
+    ref = torch.from_numpy(fx["probs"])
+    err = float((probs - ref).abs().max())
+    decided = torch.from_numpy(fx["margin"]) > 1e-3
+    agree = float((probs.argmax(1) == torch.from_numpy(fx["argmax"]).long())[decided].float().mean())
+    print(f"msf: max |dprob| {err:.2e}, argmax agreement on decided pixels {agree}, miou {miou} vs {float(fx['miou'])}")
+    assert err <= 2e-5, err
+    assert agree == 1.0
+    assert np.allclose(np.asarray(ious, dtype=np.float64), fx["ious"], rtol=0, atol=1e-9), (ious, fx["ious"])
+    assert float(miou) == float(fx["miou"])
+
+
+def test_val_driver_c1_msf_settings(tmp_path):
+    """C1 as configured: val_mm.main with configs/nyu_rgbd.yaml's evaluation settings unchanged
+    (480x640, batch 1, MSF on with scales 0.5-1.75 and flip, Swin-B, fp32), on two synthetic
+    RGB-D images (no dataset offline) and a freshly initialised, saved model."""
+    import val_mm
+    from fill import fill_module
+    from semseg.models import CMNeXt
+    with open(os.path.join(ROOT, "configs", "nyu_rgbd.yaml")) as f:
+        cfg = yaml.safe_load(f)
+    assert cfg["EVAL"]["IMAGE_SIZE"] == [480, 640] and cfg["EVAL"]["MSF"]["ENABLE"]
+    assert cfg["EVAL"]["MSF"]["SCALES"] == [0.5, 0.75, 1.0, 1.25, 1.5, 1.75] and cfg["EVAL"]["MSF"]["FLIP"]
+    cfg["SAVE_DIR"] = str(tmp_path)
+    cfg["DATASET"].update(NAME="Synthetic", LENGTH=2)
+    m = CMNeXt(cfg["MODEL"]["BACKBONE"], 40, cfg["DATASET"]["MODALS"])
+    fill_module(m, seed=5)
+    path = tmp_path / "model.pth"
+    torch.save(m.state_dict(), path)
+    cfg["EVAL"]["MODEL_PATH"] = str(path)
+    (miou,) = val_mm.main(cfg)
+    assert 0.0 <= miou <= 100.0

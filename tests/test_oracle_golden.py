@@ -342,3 +342,20 @@ def test_oracle_train_step_c2():
         nr = float(fx["grad_norms"][k])
         assert abs(np.sqrt((g64 * g64).sum()) - nr) <= 1e-3 * nr + floor, n
         assert abs(projection(n, g64, 0) - fx["grad_projs"][k][0]) <= 1e-3 * nr + floor, n
+
+
+def test_evaluate_msf_oracle():
+    """The oracle's evaluate_msf restatement (val_mm.py:87-120) against the reference's own
+    evaluate_msf on the tiny fp32 CMNeXt (msf_eval.npz, oracle/gen_golden.py gen_msf):
+    configs/nyu_rgbd.yaml's six scales with flip, two images."""
+    from msf_case import MSF_CASE, msf_inputs
+    fx = Fixture("msf_eval.npz")
+    c = MSF_CASE
+    m = R.CMNeXt(num_classes=c["n_cls"], _tiny=True)
+    assert sorted(m.state_dict().keys()) == fx["state_keys"].tolist()
+    fill_module(m, seed=c["fill_seed"])
+    rgb, dep, lbl = (torch.from_numpy(a) for a in msf_inputs())
+    batches = [([rgb[i:i + 1], dep[i:i + 1]], lbl[i:i + 1]) for i in range(c["B"])]
+    sums, (ious, miou) = R.evaluate_msf(m, batches, c["n_cls"], c["scales"], c["flip"])
+    close(torch.cat(sums), fx["probs"], 1e-5, 1e-5, "summed probabilities")
+    assert np.allclose(ious, fx["ious"], rtol=0, atol=1e-12) and float(miou) == float(fx["miou"])
