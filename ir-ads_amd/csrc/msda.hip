@@ -121,6 +121,44 @@ __device__ __forceinline__ long xcd_block(long bid, long nblk) {
     return x * q + min(x, r) + bid / 8;
 }
 
+// Group placement of the 16-B kernels (V lanes per (row, head) group, rows = (b, q) or (b, s)).
+// With M % 8 == 0 (DINO: M = 8) XCD x = blockIdx % 8 owns heads x, x + 8, ...: its blocks walk the
+// rows of one head at a time, b-major, so the XCD's L2 holds one (image, head) slice of value /
+// grad_out (S·D·4 B = 2.8 MB at the encoder shape) instead of all eight heads' 45 MB.  Otherwise
+// consecutive blocks of an XCD take consecutive (row, head) groups (xcd_block).
+struct GroupMap {
+    long row;
+    int m;
+    bool valid;
+};
+
+template <int V>
+__device__ __forceinline__ GroupMap map_group(long nrows, int M) {
+    constexpr int gpb = 256 / V;
+    const int gi = threadIdx.x / V;
+    GroupMap g;
+    if (M % 8 == 0) {
+        const long rb = (nrows + gpb - 1) / gpb;
+        const long x = blockIdx.x % 8, j = blockIdx.x / 8;
+        const long ml = j / rb;
+        g.m = (int)(x + 8 * ml);
+        g.row = (j - ml * rb) * gpb + gi;
+        g.valid = g.m < M && g.row < nrows;
+    } else {
+        const long gid = xcd_block(blockIdx.x, gridDim.x) * gpb + gi;
+        g.row = gid / M;
+        g.m = (int)(gid - g.row * M);
+        g.valid = gid < nrows * M;
+    }
+    return g;
+}
+
+dim3 group_grid(long nrows, int M, int V) {
+    const int gpb = 256 / V;
+    if (M % 8 == 0) return dim3((unsigned)(M * ((nrows + gpb - 1) / gpb)));
+    return dim3((unsigned)((nrows * M * V + 255) / 256));
+}
+
 template <int V>
 __global__ void __launch_bounds__(256) msda_fwd_vec_kernel(const float *__restrict__ value,
                                                            const int64_t *__restrict__ shapes,
@@ -135,12 +173,12 @@ __global__ void __launch_bounds__(256) msda_fwd_vec_kernel(const float *__restri
         sS[threadIdx.x] = (int)lsi[threadIdx.x];
     }
     __syncthreads();
-    const long blk = xcd_block(blockIdx.x, gridDim.x);
-    const long gid = (blk * blockDim.x + threadIdx.x) / V;
+    const GroupMap gm = map_group<V>((long)bs * Q, M);
     const int lane = threadIdx.x % V;
-    if (gid >= (long)bs * Q * M) return;  // whole group exits together
-    const int m = (int)(gid % M);
-    const int b = (int)(gid / ((long)M * Q));
+    if (!gm.valid) return;  // whole group exits together
+    const int m = gm.m;
+    const long gid = gm.row * M + m;
+    const int b = (int)(gm.row / Q);
     const int LP = L * P;
     const long cs = (long)M * D;
     const float *vb = value + (long)b * S * cs + (long)m * D + 4 * lane;
@@ -460,15 +498,15 @@ __global__ void __launch_bounds__(256) msda_gather_gvalue(const int64_t *__restr
                                                           float *__restrict__ gvalue) {
     __shared__ int sH[kMaxLevels], sW[kMaxLevels], sS[kMaxLevels];
     load_levels(shapes, lsi, L, sH, sW, sS);
-    // neighbouring cells share samples (a sample feeds 4 cells) and their grad_out rows: keep
-    // consecutive cells on one XCD so those rows are L2 hits
-    const long blk = xcd_block(blockIdx.x, gridDim.x);
-    const long gid = (blk * blockDim.x + threadIdx.x) / V;  // = (b * S + s) * M + m
+    // neighbouring cells share samples (a sample feeds 4 cells) and their grad_out rows: consecutive
+    // cells of one head on one XCD (map_group) so those rows are L2 hits
+    const GroupMap gm = map_group<V>((long)bs * S, M);
     const int lane = threadIdx.x % V;
-    if (gid >= (long)bs * S * M) return;  // whole group exits together
-    const int m = (int)(gid % M);
-    const int s = (int)((gid / M) % S);
-    const int b = (int)(gid / ((long)M * S));
+    if (!gm.valid) return;  // whole group exits together
+    const int m = gm.m;
+    const long gid = gm.row * M + m;  // = (b * S + s) * M + m
+    const int s = (int)(gm.row % S);
+    const int b = (int)(gm.row / S);
     const int l = level_of(s, sS, L);
     const int H = sH[l], W = sW[l];
     const int c = s - sS[l], y = c / W, x = c - y * W;
@@ -534,12 +572,12 @@ __global__ void __launch_bounds__(256) msda_bwd_locaw_vec(const float *__restric
                                                           float *__restrict__ gloc, float *__restrict__ gaw) {
     __shared__ int sH[kMaxLevels], sW[kMaxLevels], sS[kMaxLevels];
     load_levels(shapes, lsi, L, sH, sW, sS);
-    const long blk = xcd_block(blockIdx.x, gridDim.x);
-    const long gid = (blk * blockDim.x + threadIdx.x) / V;
+    const GroupMap gm = map_group<V>((long)bs * Q, M);
     const int lane = threadIdx.x % V;
-    if (gid >= (long)bs * Q * M) return;
-    const int m = (int)(gid % M);
-    const int b = (int)(gid / ((long)M * Q));
+    if (!gm.valid) return;
+    const int m = gm.m;
+    const long gid = gm.row * M + m;
+    const int b = (int)(gm.row / Q);
     const int LP = L * P;
     const long cs = (long)M * D;
     const float *vb = value + (long)b * S * cs + (long)m * D + 4 * lane;
@@ -664,8 +702,7 @@ int launch_fwd(const void *value, const int64_t *shapes, const int64_t *lsi, con
         const int V = D / 4;
         const bool aligned = (((uintptr_t)value | (uintptr_t)out) & 15) == 0;
         if (D % 4 == 0 && V <= 64 && (V & (V - 1)) == 0 && aligned) {
-            const long threads = (long)bs * Q * M * V;
-            dim3 grid((unsigned)((threads + 255) / 256));
+            const dim3 grid = group_grid((long)bs * Q, M, V);
 #define IRADS_MSDA_V(VV)                                                                                        \
     case VV:                                                                                                    \
         msda_fwd_vec_kernel<VV><<<grid, 256, 0, st>>>((const float *)value, shapes, lsi, (const float *)loc,   \
@@ -782,7 +819,7 @@ extern "C" int irads_msda_bwd_gather(const float *value, const int64_t *shapes, 
     if (ws.n > 0)
         msda_bucket_fill<<<gs(ws.n), 256, 0, st>>>(loc, shapes, level_start, bs, S, M, L, Q, P, aw, ws.off, ws.cnt,
                                                    ws.rec);
-    const dim3 gg = g1((long)bs * S * M * V), gq = g1((long)bs * Q * M * V);
+    const dim3 gg = group_grid((long)bs * S, M, V), gq = group_grid((long)bs * Q, M, V);
 #define IRADS_MSDA_G(VV)                                                                                           \
     case VV:                                                                                                       \
         msda_gather_gvalue<VV><<<gg, 256, 0, st>>>(shapes, level_start, loc, aw, grad_out, bs, S, M, D, L, Q, P,  \
