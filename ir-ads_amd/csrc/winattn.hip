@@ -8,13 +8,12 @@
 // of the reference never touch HBM.  Pad tokens carry q = k = v = qkv bias (the
 // reference pads after norm1 and before the Linear, swin.py:186-190 / :90).
 //
-// One workgroup = one (window, head): 144 tokens x head_dim 32.  Block ids are remapped
-// so the heads of one window run on one XCD (shared L2 lines of the 3C-wide token rows).
+// Block ids are remapped so the heads of one window run on one XCD (shared L2 lines of the
+// 3C-wide token rows).
 //
-// bf16 path (the training path): 3 waves; MFMA v_mfma_f32_16x16x32_bf16.
-//   forward: Sᵀ = K·Qᵀ per 16x16 tile (query on the lane), so each lane owns whole
-//   softmax rows (reduced over 4 registers x 9 tiles + 2 xor-shuffles) and the Pᵀ
-//   accumulator registers are directly the B operand of Oᵀ = Vᵀ·Pᵀ (k order permuted
+// bf16 path (the training path): MFMA v_mfma_f32_16x16x32_bf16.
+//   forward: Sᵀ = K·Qᵀ per 16x16 tile (query on the lane), so each lane owns whole softmax rows
+//   and the Pᵀ accumulator registers are directly the B operand of Oᵀ = Vᵀ·Pᵀ (k order permuted
 //   consistently in Vᵀ's LDS reads) — P never leaves registers.
 //   backward: key-on-lane (S = Q·Kᵀ); dVᵀ += dOᵀ·P and dKᵀ += Qᵀ·dS take P / dS straight
 //   from the accumulators; dS crosses LDS once for dQᵀ = Kᵀ·dSᵀ.  LSE from the forward.
@@ -233,13 +232,11 @@ __global__ void __launch_bounds__(256) winattn_bwd_f32(const float *__restrict__
 }
 
 // ====================================================================== bf16 MFMA path
-// Persistent-chunk design: one workgroup = 9 waves = one head x a contiguous chunk of
-// windows (grid ~ one workgroup per CU).  Per workgroup the 36 relative-position biases
-// each lane needs are gathered ONCE into registers (pre-scaled by log2 e: softmax runs in
-// base 2 with v_exp_f32), so the per-window work is MFMA + a handful of VALU ops per
-// score.  K/V (and Q/dO in backward) rows are staged into LDS row-major with plain 16-B
-// copies; the transposed MFMA operands (Vᵀ, dOᵀ, Qᵀ, Kᵀ) are read with ds_read_b64_tr_b16.
-// The next window's tiles are loaded into registers while the current one computes.
+// Forward: one 3-wave workgroup per (window, head), ~6 per CU; backward: persistent 9-wave
+// workgroups over a chunk of windows of one head.  K/V (and Q/dO in backward) rows are staged into
+// LDS row-major with plain 16-B copies; the transposed MFMA operands (Vᵀ, dOᵀ, Qᵀ, Kᵀ) are read
+// with ds_read_b64_tr_b16.  Scores are in base-2 units: q is rounded to bf16(q·scale·log2 e) when
+// staged and the bias table is seeded as T·log2 e, so the softmax is v_exp_f32 of the MFMA output.
 __device__ __forceinline__ f32x4 mfma16(const bf16x8_t &a, const bf16x8_t &b, const f32x4 &c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
@@ -265,6 +262,7 @@ constexpr float LOG2E = 1.4426950408889634f;
 // error <= 2^-11 |b|, far below the bf16 rounding the reference's AMP applies to the
 // q·kᵀ logits themselves; forward and backward use the same rounded values.
 typedef __attribute__((ext_vector_type(2))) _Float16 h2;
+typedef __attribute__((ext_vector_type(2))) float f2v;
 
 struct Chunk {
     int h, w_begin, w_end;
@@ -306,60 +304,38 @@ struct WinOrigin {
 };
 
 // ---------------------------------------------------------------------------------------------
-// Forward, one workgroup per (window, head): 3 waves, wave w owns query tiles 3w..3w+2.
+// Relative-position biases enter both directions as the MFMA accumulator seed: for one query and 4
+// consecutive keys of one window row (or one key and 4 consecutive queries) the 4 biases are 4
+// consecutive entries of a (reversed) 23x23 table, so each seed is ONE 16-B LDS read.
 //
-// The relative-position biases come from LDS as the MFMA accumulator seed itself: for a lane's
-// query and its 4 consecutive keys (one row of the window, since 4 | 12) the 4 biases are 4
-// consecutive entries of the reversed 23x23 table, so the head's table is staged as 16-byte
-// quads F[si] = (R[si], R[si+1], R[si+2], R[si+3]) and each seed is ONE ds_read_b128 at a
-// per-lane byte offset.  A workgroup is one (window, head); all of its global loads are issued
-// up front and retire behind one wait (no load waits on another), 5 workgroups share a CU (LDS
-// 31.5 KB, <= 128 VGPRs), so one workgroup's load latency is covered by the others' MFMA /
-// softmax work.
-//
-// Scale folding: the MFMA computes s' = q·k + b / scale on the raw bf16 q (the quads hold the
-// table divided by scale), and the softmax runs in base 2 on s'·(scale·log2 e): one fma per
-// score turns s' into the exponent, no per-element q·scale pass.  (The reference's AMP rounds
-// q·scale to bf16 before the product; here q·k is accumulated in fp32 from the unscaled bf16 q,
-// one bf16 rounding closer to the fp32 module.)
-constexpr int QF_STRIDE = 28;  // row stride of the (dr, dc) quad grids (23 x 28)
-constexpr int QF = 23 * QF_STRIDE;
-constexpr int QH = 2 * QF;     // quads per head: forward grid, then backward grid
-
-// quads (nH, QH, 4) fp32, pre-divided by scale.
-//   forward, a query's 4 consecutive keys of one window row: F[28 (dr + 11) + (dc + 11)][r] =
-//     T[(11 - dr) * 23 + (11 - dc - r)] with dr = row(k) - row(q), dc = col(k0) - col(q).  The row
-//     stride 28 (not 23) spreads the 16 lanes of each ds_read_b128 group over the LDS bank slots
-//     (1.4-way on average instead of 2.1-way for the 81 (query tile, key tile) pairs).
-//   backward (offset QF), a key's 4 consecutive queries of one window row: B[28 (dr + 11) + (dc + 11)][r]
-//     = T[(dr + 11) * 23 + (dc + r + 11)] with dr = row(q) - row(k), dc = col(q0) - col(k).
-// 0 outside the table.  One launch per (table version, scale).
-// After the nH quad grids: each head's table REVERSED and divided by scale, R[e] = T[528 - e] / scale
-// (RT floats per head, zero past 528).  A query's seed over 4 consecutive keys of one window row is
-// then 4 consecutive entries R[264 + A(k0) - A(q) + r] (A(t) = 23 row(t) + col(t)), and a key's seed
-// over 4 consecutive queries is the same 4 entries read backwards from R[264 + A(k) - A(q0)]:
-// one 2.1 KB LDS image serves both orientations (the backward kernel winattn_bwd_bf16_rc).
+// Bias buffer per head (irads_winattn_bias_quads; one launch per (table version, scale)), fp32 and
+// divided by scale (the kernels multiply by c2 = scale·log2 e while staging: T·log2 e):
+//   [0, 4 QB): backward quads, a key's 4 consecutive queries of one window row:
+//       B[28 (dr + 11) + (dc + 11)][r] = T[(dr + 11) * 23 + (dc + r + 11)], dr = row(q) - row(k),
+//       dc = col(q0) - col(k); the row stride 28 (not 23) spreads the 16 lanes of each ds_read_b128
+//       group over the LDS bank slots; 0 outside the table.
+//   [4 QB, 4 QB + RT): the table REVERSED, R[e] = T[528 - e] (zero past 528).  A query's seed over 4
+//       consecutive keys k0 .. k0 + 3 is R[264 + A(k0) - A(q) + r], A(t) = 23 row(t) + col(t); the
+//       forward stages 4 copies shifted by 0..3 entries so that every such run is one aligned b128.
+constexpr int QF_STRIDE = 28;  // row stride of the (dr, dc) quad grid (23 x 28)
+constexpr int QB = 23 * QF_STRIDE;
 constexpr int RT = 544;
+constexpr int QH = 4 * QB + RT;  // floats per head
+
 __global__ void winattn_bias_quads_kernel(const float *__restrict__ table, int nH, float inv_scale,
                                           float *__restrict__ quads) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= nH * QH * 4) {
-        const int j = i - nH * QH * 4;
-        if (j >= nH * RT) return;
-        const int h = j / RT, e = j % RT;
-        quads[i] = e < TBL ? table[(TBL - 1 - e) * nH + h] * inv_scale : 0.f;
-        return;
-    }
-    const int h = i / (QH * 4), e = (i / 4) % QH, r = i % 4;
-    const int eg = e < QF ? e : e - QF;
-    const int dr = eg / QF_STRIDE - 11, dc = eg % QF_STRIDE - 11;
+    if (i >= nH * QH) return;
+    const int h = i / QH, f = i % QH;
     int idx;
-    if (e < QF) {
-        const int tc = 11 - dc - r;
-        idx = (dc <= 11 && tc >= 0 && tc < 23) ? (11 - dr) * 23 + tc : -1;
-    } else {
+    if (f < 4 * QB) {
+        const int e = f / 4, r = f % 4;
+        const int dr = e / QF_STRIDE - 11, dc = e % QF_STRIDE - 11;
         const int tc = dc + r + 11;
         idx = (dc <= 11 && tc >= 0 && tc < 23) ? (dr + 11) * 23 + tc : -1;
+    } else {
+        const int e = f - 4 * QB;
+        idx = e < TBL ? TBL - 1 - e : -1;
     }
     quads[i] = (idx >= 0 && idx < TBL) ? table[idx * nH + h] * inv_scale : 0.f;
 }
@@ -410,346 +386,36 @@ __device__ __forceinline__ u16x8 pad_frag(const float *qbias, int c0) {
     return r;
 }
 
-// One (window, head) item of the forward once its Q / K / V tiles are in LDS (Qs, Ks, Vs swizzled
-// as kv_swz) and the head's quads in Bq: wave `wave` computes query tiles 3 wave .. 3 wave + 2 and
-// writes their O rows (token tok[j], -1 = pad: not written) and base-2 LSE.
-template <int MM>
-__device__ __forceinline__ void fwd_item(const Geo &g, int bw, int h, const unsigned short *Qs,
-                                         const unsigned short *Ks, const unsigned short *Vs, const f32x4 *Bq,
-                                         const int (&tok)[3], int wave, int lane, const float *__restrict__ mask,
-                                         float c2, unsigned short *__restrict__ out, float *__restrict__ lse) {
-    const int l16 = lane & 15, grp = lane >> 4;
-    const int swz_l = kv_swz(l16);
-    int kofs[9];  // (28 row(k0) + col(k0)) * 16 B
+// bf16 fragment x c2, rounded to bf16
+__device__ __forceinline__ u16x8 scale_frag(u16x8 v, float c) {
+    u16x8 r;
 #pragma unroll
-    for (int kt = 0; kt < 9; ++kt) {
-        const int k0 = kt * 16 + grp * 4;
-        kofs[kt] = (QF_STRIDE * (k0 / WS) + k0 % WS) * 16;
-    }
-    unsigned long long hbits = 0, wbits = 0;
-    bool lastH = false, lastW = false;
-    if (MM == 1) {
-        key_class_bits(g.shift, grp, hbits, wbits);
-        const int wi = bw % g.nW;
-        lastH = wi / g.nWw == g.nWh - 1;
-        lastW = wi % g.nWw == g.nWw - 1;
-    }
-    const float mneg100 = -100.0f / g.scale;
-    const bf16x8_t ones = as_bf(u16x8{0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80});
-    const int vsw = kv_swz(4 * grp), vch = ((l16 & 3) >> 1), vin = (l16 & 1) * 4;
-    const int vrow = 4 * grp + (l16 >> 2);
-    const unsigned short *vb0 = Vs + vrow * HD + ((vch ^ vsw) * 8) + vin;
-    const unsigned short *vb1 = Vs + vrow * HD + (((vch ^ 2) ^ vsw) * 8) + vin;
-    const int rfrag = l16 * HD + (grp ^ swz_l) * 8;  // row 16 n + l16, chunk grp
-    const char *bqb = (const char *)Bq;
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-        asm volatile("" ::: "memory");  // re-read the K fragments per tile (no 36-VGPR hoist)
-        const int qi = (3 * wave + j) * 16 + l16;
-        const bf16x8_t qf = as_bf(*(const u16x8 *)(Qs + (3 * wave + j) * 16 * HD + rfrag));
-        const char *bq_q = bqb + (QF_STRIDE * 11 + 11 - (QF_STRIDE * (qi / WS) + qi % WS)) * 16;
-        f32x4 s[9];
-#pragma unroll
-        for (int kt = 0; kt < 9; ++kt) {
-            const f32x4 b4 = *(const f32x4 *)(bq_q + kofs[kt]);
-            const bf16x8_t kf = as_bf(*(const u16x8 *)(Ks + kt * 16 * HD + rfrag));
-            s[kt] = mfma16(kf, qf, b4);
-            if (MM == 2) {
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-                    s[kt][r] = fmaf(mask[((long)(bw % g.n_mask) * NT + qi) * NT + kt * 16 + grp * 4 + r], 1.0f / g.scale,
-                                    s[kt][r]);
-            }
-        }
-        if (MM == 1 && (lastH || lastW)) {
-            unsigned long long mbits = 0;
-            if (lastH) mbits |= hi_row(g, qi) ? ~hbits : hbits;
-            if (lastW) mbits |= hi_col(g, qi) ? ~wbits : wbits;
-#pragma unroll
-            for (int kt = 0; kt < 9; ++kt)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) s[kt][r] += mask_term(mbits, kt * 4 + r, mneg100);
-        }
-        float mx = s[0][0];
-#pragma unroll
-        for (int kt = 0; kt < 9; ++kt)
-#pragma unroll
-            for (int r = (kt == 0); r < 4; ++r) mx = fmaxf(mx, s[kt][r]);
-        mx = max_xor16_32(mx);
-        const float mneg = -mx * c2;
-#pragma unroll
-        for (int kt = 0; kt < 9; ++kt)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) s[kt][r] = fast_exp2(fmaf(s[kt][r], c2, mneg));
-        f32x4 o0 = {0.f, 0.f, 0.f, 0.f}, o1 = o0, os = o0;
-#pragma unroll
-        for (int ks = 0; ks < 5; ++ks) {
-            bf16x8_t pb;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                pb[r] = (__bf16)s[2 * ks][r];
-                pb[4 + r] = (2 * ks + 1 < 9) ? (__bf16)s[2 * ks + 1][r] : (__bf16)0.f;
-            }
-            const int r0 = 32 * ks * HD, r1 = ks < 4 ? r0 + 16 * HD : r0;
-            const u16x8 a0 = cat4(tr_read(vb0 + r0), tr_read(vb0 + r1));
-            const u16x8 a1 = cat4(tr_read(vb1 + r0), tr_read(vb1 + r1));
-            o0 = mfma16(as_bf(a0), pb, o0);
-            o1 = mfma16(as_bf(a1), pb, o1);
-            os = mfma16(ones, pb, os);
-        }
-        const float inv = __builtin_amdgcn_rcpf(os[0]);
-        if (tok[j] >= 0) {
-            u16x4 w0, w1;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                w0[r] = f2bf(o0[r] * inv);
-                w1[r] = f2bf(o1[r] * inv);
-            }
-            unsigned short *op = out + (long)tok[j] * g.C + h * HD;
-            *(u16x4 *)(op + grp * 4) = w0;
-            *(u16x4 *)(op + 16 + grp * 4) = w1;
-        }
-        if (grp == 0) lse[((long)bw * g.nH + h) * NT + qi] = mx * c2 + __log2f(os[0]);
-    }
+    for (int e = 0; e < 8; ++e) r[e] = f2bf(bf2f(v[e]) * c);
+    return r;
 }
 
-// Persistent forward: one workgroup (3 waves) = one head x a contiguous chunk of windows, several
-// workgroups per CU.  The next window's q, k, v are loaded into registers while the current one
-// computes (the load is issued right after the current window's tiles reach LDS), so each
-// workgroup keeps ~27 KB of loads in flight through its whole chunk instead of one
-// load-then-compute burst per (window, head).  The head's quads are staged once per workgroup.
+// Forward, one workgroup per (window, head): 3 waves, wave w owns query tiles 3w..3w+2.  All global
+// loads of the workgroup are issued up front and retire behind one wait; 27 KB of LDS and <= 96
+// VGPRs let 6 workgroups share a CU, so one workgroup's load latency is covered by the others'
+// MFMA / softmax work.  The seeds come from 4 shifted copies of the reversed table (one aligned
+// ds_read_b128 per 4 keys).  Scores are formed directly in base-2 units: q is pre-multiplied by
+// c2 = scale·log2 e when it is loaded (one bf16 rounding of q·c2, where the reference's AMP rounds
+// q·scale, swin.py:95) and the table by log2 e, so s'' = q''·k + T·log2 e and P = 2^s'' needs no
+// scaling fma per score.  The row maximum is still formed; only a wave holding a row whose maximum
+// lies outside [-60, 60] (where 2^s'' could overflow, or lose precision to underflow) shifts its
+// scores, by one more MFMA per key tile that adds 32·bf16(-max/32) to every score of the row
+// (exact, so the LSE records the shift that was applied).
 template <int MM>
-__global__ void __launch_bounds__(192) winattn_fwd_bf16_pc(const unsigned short *__restrict__ qkv, const float *__restrict__ qbias,
-                    const float *__restrict__ quads, const float *__restrict__ mask, Geo g, int cw, float c2,
-                    unsigned short *__restrict__ out, float *__restrict__ lse) {
-    __shared__ __attribute__((aligned(16))) unsigned short Qs[NT * HD];
-    __shared__ __attribute__((aligned(16))) unsigned short Ks[NT * HD];
-    __shared__ __attribute__((aligned(16))) unsigned short Vs[NT * HD];
-    __shared__ __attribute__((aligned(16))) f32x4 Bq[QF];
-    const Chunk ck = decode_chunk(g, cw);
-    const int h = ck.h;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int l16 = lane & 15, grp = lane >> 4;
-    const char *base = (const char *)qkv;
-    const unsigned rowb = 6u * (unsigned)g.C, cb = 2u * (unsigned)g.C, hb = (unsigned)(h * HD + grp * 8) * 2u;
-    int tok[3];
-    u16x8 qreg[3], kreg[3], vreg[3];
-    auto prefetch = [&](int bw) {
-        const WinOrigin wo(g, bw);
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-            tok[j] = wo.tok(g, (3 * wave + j) * 16 + l16);
-            const unsigned off = (unsigned)max(tok[j], 0) * rowb + hb;
-            qreg[j] = *(const u16x8 *)(base + off);
-            kreg[j] = *(const u16x8 *)(base + off + cb);
-            vreg[j] = *(const u16x8 *)(base + off + 2 * cb);
-        }
-    };
-    if (ck.w_begin >= ck.w_end) return;
-    prefetch(ck.w_begin);
-    {
-        const f32x4 *qsrc = (const f32x4 *)quads + (long)h * QH;
-        f32x4 bq[3];
-        f32x4 bq4 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int j = 0; j < 3; ++j) bq[j] = qsrc[tid + 192 * j];
-        if (tid < QF - 576) bq4 = qsrc[576 + tid];
-#pragma unroll
-        for (int j = 0; j < 3; ++j) Bq[tid + 192 * j] = bq[j];
-        if (tid < QF - 576) Bq[576 + tid] = bq4;
-    }
-    const int c0 = h * HD + grp * 8;
-    const int swz_l = kv_swz(l16);
-    for (int bw = ck.w_begin; bw < ck.w_end; ++bw) {
-        if (wave_any(tok[0] < 0 || tok[1] < 0 || tok[2] < 0)) {
-            const u16x8 qp = pad_frag(qbias, c0), kp = pad_frag(qbias, g.C + c0), vp = pad_frag(qbias, 2 * g.C + c0);
-#pragma unroll
-            for (int j = 0; j < 3; ++j)
-                if (tok[j] < 0) {
-                    qreg[j] = qp;
-                    kreg[j] = kp;
-                    vreg[j] = vp;
-                }
-        }
-        __syncthreads();  // the previous window's tile reads are done
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-            const int o = ((3 * wave + j) * 16 + l16) * HD + (grp ^ swz_l) * 8;
-            *(u16x8 *)(Qs + o) = qreg[j];
-            *(u16x8 *)(Ks + o) = kreg[j];
-            *(u16x8 *)(Vs + o) = vreg[j];
-        }
-        const int tcur[3] = {tok[0], tok[1], tok[2]};
-        __syncthreads();
-        if (bw + 1 < ck.w_end) prefetch(bw + 1);
-        fwd_item<MM>(g, bw, h, Qs, Ks, Vs, Bq, tcur, wave, lane, mask, c2, out, lse);
-    }
-}
-
-template <int MM>
-__global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(4))) winattn_fwd_bf16_wg(const unsigned short *__restrict__ qkv,
+__global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(5))) winattn_fwd_bf16_rt(const unsigned short *__restrict__ qkv,
                                                             const float *__restrict__ qbias,
                                                             const float *__restrict__ quads,
                                                             const float *__restrict__ mask, Geo g, float c2,
                                                             unsigned short *__restrict__ out, float *__restrict__ lse) {
     __shared__ __attribute__((aligned(16))) unsigned short Ks[NT * HD];  // swizzled 64-B rows (kv_swz)
     __shared__ __attribute__((aligned(16))) unsigned short Vs[NT * HD];
-    __shared__ __attribute__((aligned(16))) f32x4 Bq[QF];  // forward quads of this head
-    const int lid = xcd_remap(blockIdx.x, gridDim.x);      // the heads of one window on one XCD
-    const int h = lid % g.nH, bw = lid / g.nH;
-    const WinOrigin wo(g, bw);
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int l16 = lane & 15, grp = lane >> 4;
-    // ---- every global load of the workgroup first.  Thread (wave, l16, grp) owns tokens
-    // t_j = (3 wave + j) 16 + l16 and 16-B chunk grp of their q, k and v: its q rows are exactly
-    // its MFMA B fragments, its k / v chunks are staged to LDS.  32-bit byte offsets (< 4 GiB).
-    const char *base = (const char *)qkv;
-    const unsigned rowb = 6u * (unsigned)g.C, cb = 2u * (unsigned)g.C, hb = (unsigned)(h * HD + grp * 8) * 2u;
-    int tok[3];
-    u16x8 qreg[3], kreg[3], vreg[3];
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-        tok[j] = wo.tok(g, (3 * wave + j) * 16 + l16);
-        const unsigned off = (unsigned)max(tok[j], 0) * rowb + hb;
-        qreg[j] = *(const u16x8 *)(base + off);
-        kreg[j] = *(const u16x8 *)(base + off + cb);
-        vreg[j] = *(const u16x8 *)(base + off + 2 * cb);
-    }
-    f32x4 bq[3];
-    f32x4 bq4 = {0.f, 0.f, 0.f, 0.f};
-    const f32x4 *qsrc = (const f32x4 *)quads + (long)h * QH;
-#pragma unroll
-    for (int j = 0; j < 3; ++j) bq[j] = qsrc[tid + 192 * j];  // QF = 644 >= 3 * 192
-    if (tid < QF - 576) bq4 = qsrc[576 + tid];
-    if (wave_any(tok[0] < 0 || tok[1] < 0 || tok[2] < 0)) {  // uniform: only waves holding pad tokens
-        const int c0 = h * HD + grp * 8;
-        const u16x8 qp = pad_frag(qbias, c0), kp = pad_frag(qbias, g.C + c0), vp = pad_frag(qbias, 2 * g.C + c0);
-#pragma unroll
-        for (int j = 0; j < 3; ++j)
-            if (tok[j] < 0) {
-                qreg[j] = qp;
-                kreg[j] = kp;
-                vreg[j] = vp;
-            }
-    }
-    const int swz_l = kv_swz(l16);  // rows t = 16 n + l16 all have the swizzle of l16
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-        const int t = (3 * wave + j) * 16 + l16;
-        *(u16x8 *)(Ks + t * HD + (grp ^ swz_l) * 8) = kreg[j];
-        *(u16x8 *)(Vs + t * HD + (grp ^ swz_l) * 8) = vreg[j];
-        Bq[tid + 192 * j] = bq[j];
-    }
-    if (tid < QF - 576) Bq[576 + tid] = bq4;
-    __syncthreads();
-    // ---- per-lane constants: byte offset of the key group of every key tile (keys kt*16 + 4 grp + r,
-    // one window row) in the quads, and the key class bits (MM == 1)
-    int kofs[9];  // (28 row(k0) + col(k0)) * 16 B
-#pragma unroll
-    for (int kt = 0; kt < 9; ++kt) {
-        const int k0 = kt * 16 + grp * 4;
-        kofs[kt] = (QF_STRIDE * (k0 / WS) + k0 % WS) * 16;
-    }
-    unsigned long long hbits = 0, wbits = 0;
-    if (MM == 1) key_class_bits(g.shift, grp, hbits, wbits);
-    bool lastH = false, lastW = false;
-    if (MM == 1) {
-        const int wi = bw % g.nW;
-        lastH = wi / g.nWw == g.nWh - 1;
-        lastW = wi % g.nWw == g.nWw - 1;
-    }
-    const float mneg100 = -100.0f / g.scale;  // the region mask in s' units
-    const bf16x8_t ones = as_bf(u16x8{0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80});
-    // Vᵀ transposed reads: rows 32 ks + 4 grp + (l16 >> 2) (+16), all with the swizzle of grp; elements
-    // 4 (l16 & 3) .. +3 of d-half 0 (chunk (l16 & 3) >> 1) and of d-half 1 (that chunk ^ 2)
-    const int vsw = kv_swz(4 * grp), vch = ((l16 & 3) >> 1), vin = (l16 & 1) * 4;
-    const int vrow = 4 * grp + (l16 >> 2);
-    const unsigned short *vb0 = Vs + vrow * HD + ((vch ^ vsw) * 8) + vin;
-    const unsigned short *vb1 = Vs + vrow * HD + (((vch ^ 2) ^ vsw) * 8) + vin;
-    const unsigned short *kb = Ks + l16 * HD + (grp ^ swz_l) * 8;
-    const char *bqb = (const char *)Bq;
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-        const int qi = (3 * wave + j) * 16 + l16;
-        const bf16x8_t qf = as_bf(qreg[j]);
-        const char *bq_q = bqb + (QF_STRIDE * 11 + 11 - (QF_STRIDE * (qi / WS) + qi % WS)) * 16;  // + key offset
-        f32x4 s[9];
-#pragma unroll
-        for (int kt = 0; kt < 9; ++kt) {
-            const f32x4 b4 = *(const f32x4 *)(bq_q + kofs[kt]);
-            const bf16x8_t kf = as_bf(*(const u16x8 *)(kb + kt * 16 * HD));
-            s[kt] = mfma16(kf, qf, b4);  // s'ᵀ (key rows, query on the lane), bias seeded
-            if (MM == 2) {
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-                    s[kt][r] = fmaf(mask[((long)(bw % g.n_mask) * NT + qi) * NT + kt * 16 + grp * 4 + r], 1.0f / g.scale,
-                                    s[kt][r]);
-            }
-        }
-        if (MM == 1 && (lastH || lastW)) {  // uniform branch: only edge windows of the shifted grid
-            unsigned long long mbits = 0;
-            if (lastH) mbits |= hi_row(g, qi) ? ~hbits : hbits;
-            if (lastW) mbits |= hi_col(g, qi) ? ~wbits : wbits;
-#pragma unroll
-            for (int kt = 0; kt < 9; ++kt)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) s[kt][r] += mask_term(mbits, kt * 4 + r, mneg100);
-        }
-        float mx = s[0][0];
-#pragma unroll
-        for (int kt = 0; kt < 9; ++kt)
-#pragma unroll
-            for (int r = (kt == 0); r < 4; ++r) mx = fmaxf(mx, s[kt][r]);
-        mx = max_xor16_32(mx);
-        const float mneg = -mx * c2;
-#pragma unroll
-        for (int kt = 0; kt < 9; ++kt)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) s[kt][r] = fast_exp2(fmaf(s[kt][r], c2, mneg));
-        f32x4 o0 = {0.f, 0.f, 0.f, 0.f}, o1 = o0, os = o0;
-#pragma unroll
-        for (int ks = 0; ks < 5; ++ks) {
-            bf16x8_t pb;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                pb[r] = (__bf16)s[2 * ks][r];
-                pb[4 + r] = (2 * ks + 1 < 9) ? (__bf16)s[2 * ks + 1][r] : (__bf16)0.f;
-            }
-            // keys 144..159 do not exist: their P is 0, so any finite rows serve (tile 8 again)
-            const int r0 = 32 * ks * HD, r1 = ks < 4 ? r0 + 16 * HD : r0;
-            const u16x8 a0 = cat4(tr_read(vb0 + r0), tr_read(vb0 + r1));
-            const u16x8 a1 = cat4(tr_read(vb1 + r0), tr_read(vb1 + r1));
-            o0 = mfma16(as_bf(a0), pb, o0);
-            o1 = mfma16(as_bf(a1), pb, o1);
-            os = mfma16(ones, pb, os);
-        }
-        const float inv = __builtin_amdgcn_rcpf(os[0]);
-        if (tok[j] >= 0) {
-            u16x4 w0, w1;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                w0[r] = f2bf(o0[r] * inv);
-                w1[r] = f2bf(o1[r] * inv);
-            }
-            unsigned short *op = out + (long)tok[j] * g.C + h * HD;
-            *(u16x4 *)(op + grp * 4) = w0;
-            *(u16x4 *)(op + 16 + grp * 4) = w1;
-        }
-        if (grp == 0) lse[((long)bw * g.nH + h) * NT + qi] = mx * c2 + __log2f(os[0]);  // base-2 LSE of s'·scale
-    }
-}
-
-// As winattn_fwd_bf16_wg with the bias seeds read from the head's reversed table (2.1 KB of LDS
-// instead of the 10 KB quad grid): 20.6 KB per workgroup, 6 workgroups per CU (VGPR-bound).
-template <int MM>
-__global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(4))) winattn_fwd_bf16_rt(const unsigned short *__restrict__ qkv,
-                                                            const float *__restrict__ qbias,
-                                                            const float *__restrict__ quads,
-                                                            const float *__restrict__ mask, Geo g, float c2,
-                                                            unsigned short *__restrict__ out, float *__restrict__ lse) {
-    __shared__ __attribute__((aligned(16))) unsigned short Ks[NT * HD];  // swizzled 64-B rows (kv_swz)
-    __shared__ __attribute__((aligned(16))) unsigned short Vs[NT * HD];
-    __shared__ __attribute__((aligned(16))) float Rs[RT];  // reversed, scaled table of this head
+    // reversed table of this head x log2 e in 4 copies, copy c at c·RT holding R[e + c], so that any 4
+    // consecutive entries are one 16-B aligned ds_read_b128 (8.5 KB instead of the 10 KB quad grid)
+    __shared__ __attribute__((aligned(16))) float Rs[4 * RT];
     const int lid = xcd_remap(blockIdx.x, gridDim.x);      // the heads of one window on one XCD
     const int h = lid % g.nH, bw = lid / g.nH;
     const WinOrigin wo(g, bw);
@@ -771,7 +437,7 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(4))) w
         vreg[j] = *(const u16x8 *)(base + off + 2 * cb);
     }
     f32x4 rt = {0.f, 0.f, 0.f, 0.f};
-    if (tid < RT / 4) rt = ((const f32x4 *)(quads + (long)g.nH * QH * 4 + (long)h * RT))[tid];
+    if (tid < RT / 4) rt = ((const f32x4 *)(quads + (long)h * QH + 4 * QB))[tid];
     if (wave_any(tok[0] < 0 || tok[1] < 0 || tok[2] < 0)) {  // uniform: only waves holding pad tokens
         const int c0 = h * HD + grp * 8;
         const u16x8 qp = pad_frag(qbias, c0), kp = pad_frag(qbias, g.C + c0), vp = pad_frag(qbias, 2 * g.C + c0);
@@ -790,10 +456,18 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(4))) w
         *(u16x8 *)(Ks + t * HD + (grp ^ swz_l) * 8) = kreg[j];
         *(u16x8 *)(Vs + t * HD + (grp ^ swz_l) * 8) = vreg[j];
     }
-    if (tid < RT / 4) ((f32x4 *)Rs)[tid] = rt;
+    if (tid < RT / 4) {
+        rt = rt * c2;  // T / scale -> T·log2 e
+        ((f32x4 *)Rs)[tid] = rt;
+#pragma unroll
+        for (int c = 1; c < 4; ++c)
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (4 * tid + k - c >= 0) Rs[c * RT + 4 * tid + k - c] = rt[k];  // copy c: R[e + c]
+    }
+#pragma unroll
+    for (int j = 0; j < 3; ++j) qreg[j] = scale_frag(qreg[j], c2);
     __syncthreads();
-    // ---- per-lane constants: byte offset of the key group of every key tile (keys kt*16 + 4 grp + r,
-    // one window row) in the quads, and the key class bits (MM == 1)
     int part3[3];  // A(16 j + 4 grp); key group of tile 3a + j: part3[j] + 92 a
 #pragma unroll
     for (int j = 0; j < 3; ++j) part3[j] = tok_a(16 * j + 4 * grp);
@@ -805,7 +479,7 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(4))) w
         lastH = wi / g.nWw == g.nWh - 1;
         lastW = wi % g.nWw == g.nWw - 1;
     }
-    const float mneg100 = -100.0f / g.scale;  // the region mask in s' units
+    const float mneg100 = -100.0f * LOG2E;  // the region mask in s'' units
     const bf16x8_t ones = as_bf(u16x8{0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80});
     // Vᵀ transposed reads: rows 32 ks + 4 grp + (l16 >> 2) (+16), all with the swizzle of grp; elements
     // 4 (l16 & 3) .. +3 of d-half 0 (chunk (l16 & 3) >> 1) and of d-half 1 (that chunk ^ 2)
@@ -818,19 +492,24 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(4))) w
     for (int j = 0; j < 3; ++j) {
         const int qi = (3 * wave + j) * 16 + l16;
         const bf16x8_t qf = as_bf(qreg[j]);
-        const float *rq = Rs + 264 - tok_a(qi);  // + A(k0): the seed over keys k0 .. k0 + 3
+        // seed of keys k0 .. k0 + 3: R[264 + A(k0) - A(qi) + r], from the copy where it starts 16-B aligned
+        const float *rq[3];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            const int e = 264 - tok_a(qi) + part3[a];
+            rq[a] = Rs + (e & 3) * (RT - 1) + e;
+        }
         f32x4 s[9];
 #pragma unroll
         for (int kt = 0; kt < 9; ++kt) {
-            const float *rb = rq + part3[kt % 3] + 92 * (kt / 3);
-            const f32x4 b4 = {rb[0], rb[1], rb[2], rb[3]};
+            const float *rb = rq[kt % 3] + 92 * (kt / 3);
+            const f32x4 b4 = *(const f32x4 *)rb;
             const bf16x8_t kf = as_bf(*(const u16x8 *)(kb + kt * 16 * HD));
-            s[kt] = mfma16(kf, qf, b4);  // s'ᵀ (key rows, query on the lane), bias seeded
+            s[kt] = mfma16(kf, qf, b4);  // s''ᵀ (key rows, query on the lane), bias seeded
             if (MM == 2) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
-                    s[kt][r] = fmaf(mask[((long)(bw % g.n_mask) * NT + qi) * NT + kt * 16 + grp * 4 + r], 1.0f / g.scale,
-                                    s[kt][r]);
+                    s[kt][r] = fmaf(mask[((long)(bw % g.n_mask) * NT + qi) * NT + kt * 16 + grp * 4 + r], LOG2E, s[kt][r]);
             }
         }
         if (MM == 1 && (lastH || lastW)) {  // uniform branch: only edge windows of the shifted grid
@@ -848,11 +527,18 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(4))) w
 #pragma unroll
             for (int r = (kt == 0); r < 4; ++r) mx = fmaxf(mx, s[kt][r]);
         mx = max_xor16_32(mx);
-        const float mneg = -mx * c2;
+        float shift = 0.f;
+        if (wave_any(!(mx >= -60.f && mx <= 60.f))) {  // rare: shift the row by -max (NaN rows too)
+            const unsigned short sh = f2bf(-mx * (1.0f / 32.0f));
+            shift = -32.0f * bf2f(sh);
+            const bf16x8_t shb = as_bf(u16x8{sh, sh, sh, sh, sh, sh, sh, sh});
+#pragma unroll
+            for (int kt = 0; kt < 9; ++kt) s[kt] = mfma16(ones, shb, s[kt]);
+        }
 #pragma unroll
         for (int kt = 0; kt < 9; ++kt)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) s[kt][r] = fast_exp2(fmaf(s[kt][r], c2, mneg));
+            for (int r = 0; r < 4; ++r) s[kt][r] = fast_exp2(s[kt][r]);
         f32x4 o0 = {0.f, 0.f, 0.f, 0.f}, o1 = o0, os = o0;
 #pragma unroll
         for (int ks = 0; ks < 5; ++ks) {
@@ -882,7 +568,7 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(4))) w
             *(u16x4 *)(op + grp * 4) = w0;
             *(u16x4 *)(op + 16 + grp * 4) = w1;
         }
-        if (grp == 0) lse[((long)bw * g.nH + h) * NT + qi] = mx * c2 + __log2f(os[0]);  // base-2 LSE of s'·scale
+        if (grp == 0) lse[((long)bw * g.nH + h) * NT + qi] = __log2f(os[0]) + shift;  // base-2 LSE of s''
     }
 }
 
@@ -908,7 +594,7 @@ __global__ void __launch_bounds__(576) winattn_bwd_bf16(
     const float *__restrict__ lse,
     const unsigned short *__restrict__ gout, unsigned short *__restrict__ gqkv, float *__restrict__ gtable,
     float *__restrict__ gbias) {
-    __shared__ __attribute__((aligned(16))) f32x4 Bf[QF];  // backward quads (stride-28 grid) of this head
+    __shared__ __attribute__((aligned(16))) f32x4 Bf[QB];  // backward quads (stride-28 grid) of this head
     __shared__ __attribute__((aligned(16))) unsigned short Qs[NT * HD];
     __shared__ __attribute__((aligned(16))) unsigned short dOs[NT * HD];
     __shared__ __attribute__((aligned(16))) unsigned short Ks[NT * HD];
@@ -920,16 +606,16 @@ __global__ void __launch_bounds__(576) winattn_bwd_bf16(
     __shared__ float tgS[EX ? TBL : 1];  // EX: this workgroup's rel-table gradient, flushed once
     const Chunk ck = decode_chunk(g, cw);
     const int h = ck.h;
-    const float mneg100 = -100.0f / g.scale;  // the region mask in s' units
+    const float mneg100 = -100.0f * LOG2E;  // the region mask in s'' units
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int l16 = lane & 15, grp = lane >> 4;
     {  // the head's backward quads (16-B loads, both issued before either store)
-        const f32x4 *src = (const f32x4 *)quads + (long)h * QH + QF;
+        const f32x4 *src = (const f32x4 *)(quads + (long)h * QH);
         const f32x4 b0 = src[tid];
         f32x4 b1 = {0.f, 0.f, 0.f, 0.f};
-        if (tid < QF - 576) b1 = src[576 + tid];
-        Bf[tid] = b0;
-        if (tid < QF - 576) Bf[576 + tid] = b1;
+        if (tid < QB - 576) b1 = src[576 + tid];
+        Bf[tid] = b0 * c2;  // T / scale -> T·log2 e: scores in base-2 units s'' (see winattn_fwd_bf16_rt)
+        if (tid < QB - 576) Bf[576 + tid] = b1 * c2;
     }
     for (int i = tid; i < (NR - NT) * DST; i += 576) dSt[NT * DST + i] = 0;
     if (EX)
@@ -1001,7 +687,7 @@ __global__ void __launch_bounds__(576) winattn_bwd_bf16(
             }
         }
         __syncthreads();
-        *(u16x8 *)(Qs + st_off) = qreg;  // raw q: the scale is folded into c2, as forward
+        *(u16x8 *)(Qs + st_off) = scale_frag(qreg, c2);  // q'' = bf16(q·c2), as the forward
         *(u16x8 *)(dOs + st_off) = dreg;
         *(u16x8 *)(Ks + st_off) = kreg;
         *(u16x8 *)(Vs + st_off) = vreg;
@@ -1061,8 +747,8 @@ __global__ void __launch_bounds__(576) winattn_bwd_bf16(
                     float v = sa[r];
                     if (MASKED) v += mask_term(mbits, qt * 4 + r, mneg100);
                     if (MM == 2)
-                        v = fmaf(mask[((long)(bw % g.n_mask) * NT + qt * 16 + grp * 4 + r) * NT + kkey], 1.0f / g.scale, v);
-                    const float p = fast_exp2(fmaf(v, c2, -l4[r]));
+                        v = fmaf(mask[((long)(bw % g.n_mask) * NT + qt * 16 + grp * 4 + r) * NT + kkey], LOG2E, v);
+                    const float p = fast_exp2(v - l4[r]);
                     const float ds = p * dpa[r];
                     pb[4 * half + r] = (__bf16)p;
                     sb[4 * half + r] = (__bf16)ds;
@@ -1097,8 +783,8 @@ __global__ void __launch_bounds__(576) winattn_bwd_bf16(
                 u16x4 k0, k1, v0, v1;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    k0[r] = f2bf(dk0[r] * g.scale);  // dK = scale · dSᵀ·q
-                    k1[r] = f2bf(dk1[r] * g.scale);
+                    k0[r] = f2bf(dk0[r] * (1.0f / LOG2E));  // dK = scale · dSᵀ·q = dSᵀ·q'' / log2 e
+                    k1[r] = f2bf(dk1[r] * (1.0f / LOG2E));
                     v0[r] = f2bf(dv0[r]);
                     v1[r] = f2bf(dv1[r]);
                 }
@@ -1110,8 +796,8 @@ __global__ void __launch_bounds__(576) winattn_bwd_bf16(
             } else if (EX && gbias) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    atomicAdd(&gbias[g.C + c0 + r], dk0[r] * g.scale);
-                    atomicAdd(&gbias[g.C + c0 + 16 + r], dk1[r] * g.scale);
+                    atomicAdd(&gbias[g.C + c0 + r], dk0[r] * (1.0f / LOG2E));
+                    atomicAdd(&gbias[g.C + c0 + 16 + r], dk1[r] * (1.0f / LOG2E));
                     atomicAdd(&gbias[2 * g.C + c0 + r], dv0[r]);
                     atomicAdd(&gbias[2 * g.C + c0 + 16 + r], dv1[r]);
                 }
@@ -1160,260 +846,6 @@ __global__ void __launch_bounds__(576) winattn_bwd_bf16(
     }
 }
 
-// Backward, one workgroup (4 waves) per (window, head), ~4 workgroups per CU.  dS never crosses LDS:
-// key-tile jobs (key on the lane) form S, dP, P, dS and accumulate dVᵀ += dOᵀ·P, dKᵀ += Qᵀ·dS as
-// the persistent kernel's phase 1 does; query-tile jobs (query on the lane, the forward's Sᵀ = K·Qᵀ
-// orientation) recompute Sᵀ and dPᵀ and accumulate dQᵀ += Kᵀ·dSᵀ with dSᵀ straight from the
-// accumulators (as the forward's Pᵀ feeds Oᵀ).  That costs two more 144x144x32 products and a second
-// exp per score, and buys an LDS image of 40 KB (Q, dO, K, V, the reversed bias table, LSE, δ)
-// instead of ~100 KB, so 4 workgroups share a CU and hide each other's load latency, with no
-// barrier between the two kinds of job.  The 18 jobs (9 key tiles ≈ 38 MFMA each, 9 query tiles
-// ≈ 28) are dealt to the 4 waves in fixed lists that are balanced to 93 %.
-// EX (trainable table / pad bias) keeps the persistent kernel.
-// job lists packed 5 bits a job (count in bits 25..27): kept in scalar registers, no private array
-__device__ __forceinline__ unsigned rc_jobs(int wave) {  // job 0..8: key tile, 9..17: query tile job - 9
-    constexpr unsigned w0 = 4u << 25 | 0u | 4u << 5 | 8u << 10 | 12u << 15;                // K0 K4 K8 Q3
-    constexpr unsigned w1 = 5u << 25 | 1u | 5u << 5 | 9u << 10 | 13u << 15 | 17u << 20;   // K1 K5 Q0 Q4 Q8
-    constexpr unsigned w2 = 4u << 25 | 2u | 6u << 5 | 10u << 10 | 14u << 15;               // K2 K6 Q1 Q5
-    constexpr unsigned w3 = 5u << 25 | 3u | 7u << 5 | 11u << 10 | 15u << 15 | 16u << 20;  // K3 K7 Q2 Q6 Q7
-    return wave == 0 ? w0 : wave == 1 ? w1 : wave == 2 ? w2 : w3;
-}
-
-
-template <int MM>
-__global__ void __launch_bounds__(256) winattn_bwd_bf16_rc(
-    const unsigned short *__restrict__ qkv, const float *__restrict__ qbias, const float *__restrict__ rtab,
-    const float *__restrict__ mask, Geo g, float c2, const unsigned short *__restrict__ out,
-    const float *__restrict__ lse, const unsigned short *__restrict__ gout, unsigned short *__restrict__ gqkv) {
-    __shared__ __attribute__((aligned(16))) unsigned short Qs[NT * HD];
-    __shared__ __attribute__((aligned(16))) unsigned short dOs[NT * HD];
-    __shared__ __attribute__((aligned(16))) unsigned short Ks[NT * HD];
-    __shared__ __attribute__((aligned(16))) unsigned short Vs[NT * HD];
-    __shared__ __attribute__((aligned(16))) float Rs[RT];
-    __shared__ __attribute__((aligned(16))) float lseS[NT], ndS[NT];  // ndS = -δ
-    const int lid = xcd_remap(blockIdx.x, gridDim.x);  // the heads of one window on one XCD
-    const int h = lid % g.nH, bw = lid / g.nH;
-    const WinOrigin wo(g, bw);
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int l16 = lane & 15, grp = lane >> 4;
-    // ---- staging: thread (token t = i / 4, 16-B chunk c = i % 4) for i = tid, tid + 256, tid + 512 (< 576);
-    // every load issued before the first use
-    const char *qkvb = (const char *)qkv;
-    const unsigned rowb = 6u * (unsigned)g.C, cb = 2u * (unsigned)g.C, orow = 2u * (unsigned)g.C;
-    u16x8 qr[3], kr[3], vr[3], dr[3], orr[3];
-    int tk[3];
-    const int nst = wave == 0 ? 3 : 2;  // 576 = 2 x 256 + 64: the third chunk is wave 0's
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-        if (j < nst) {
-            const int i = tid + 256 * j, t = i >> 2, c = i & 3;
-            tk[j] = wo.tok(g, t);
-            const unsigned hcb = (unsigned)(h * HD + c * 8) * 2u;
-            const unsigned off = (unsigned)max(tk[j], 0) * rowb + hcb;
-            qr[j] = *(const u16x8 *)(qkvb + off);
-            kr[j] = *(const u16x8 *)(qkvb + off + cb);
-            vr[j] = *(const u16x8 *)(qkvb + off + 2 * cb);
-            const unsigned so = (unsigned)max(tk[j], 0) * orow + hcb;
-            dr[j] = *(const u16x8 *)((const char *)gout + so);
-            orr[j] = *(const u16x8 *)((const char *)out + so);
-        }
-    }
-    f32x4 rt = {0.f, 0.f, 0.f, 0.f};
-    if (tid < RT / 4) rt = ((const f32x4 *)(rtab + (long)h * RT))[tid];
-    float lv = 0.f;
-    if (tid < NT) lv = lse[((long)bw * g.nH + h) * NT + tid];
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-        if (j < nst) {
-            const int i = tid + 256 * j, t = i >> 2, c = i & 3;
-            if (wave_any(tk[j] < 0)) {  // uniform: only waves staging pad tokens
-                if (tk[j] < 0) {
-                    const int c0 = h * HD + c * 8;
-                    const u16x8 zero = {0, 0, 0, 0, 0, 0, 0, 0};
-                    qr[j] = pad_frag(qbias, c0);
-                    kr[j] = pad_frag(qbias, g.C + c0);
-                    vr[j] = pad_frag(qbias, 2 * g.C + c0);
-                    dr[j] = zero;  // a cropped token's output carries no gradient
-                    orr[j] = zero;
-                }
-            }
-            const int o = t * HD + (c ^ kv_swz(t)) * 8;
-            *(u16x8 *)(Qs + o) = qr[j];  // raw q: the scale is folded into c2, as the forward
-            *(u16x8 *)(Ks + o) = kr[j];
-            *(u16x8 *)(Vs + o) = vr[j];
-            *(u16x8 *)(dOs + o) = dr[j];
-            float part = 0.f;  // δ_t = dO_t · O_t, 4 lanes per token
-#pragma unroll
-            for (int e = 0; e < 8; ++e) part = fmaf(bf2f(dr[j][e]), bf2f(orr[j][e]), part);
-            part += __shfl_xor(part, 1, 64);
-            part += __shfl_xor(part, 2, 64);
-            if (c == 0) ndS[t] = -part;
-        }
-    }
-    if (tid < RT / 4) ((f32x4 *)Rs)[tid] = rt;
-    if (tid < NT) lseS[tid] = lv;
-    __syncthreads();
-
-    // ---- lane constants shared by both job kinds
-    const int swz_l = kv_swz(l16);
-    const int rfrag = l16 * HD + (grp ^ swz_l) * 8;  // row fragment: row 16 n + l16, chunk grp
-    const int vsw = kv_swz(4 * grp), vch = ((l16 & 3) >> 1), vin = (l16 & 1) * 4;
-    const int trow = (4 * grp + (l16 >> 2)) * HD;
-    const int tc0 = ((vch ^ vsw) * 8) + vin, tc1 = (((vch ^ 2) ^ vsw) * 8) + vin;  // transposed reads, d-half 0 / 1
-    int part3[3];  // A(16 j + 4 grp): A of a 4-token group of tile 3a + j is part3[j] + 92 a
-#pragma unroll
-    for (int j = 0; j < 3; ++j) part3[j] = tok_a(16 * j + 4 * grp);
-    const float mneg100 = -100.0f / g.scale;
-    unsigned long long hb = 0, wb = 0;  // class bits of the 36 tokens 16 n + 4 grp + r (MM == 1)
-    bool lastH = false, lastW = false;
-    if (MM == 1) {
-        key_class_bits(g.shift, grp, hb, wb);
-        const int wi = bw % g.nW;
-        lastH = wi / g.nWw == g.nWh - 1;
-        lastW = wi % g.nWw == g.nWw - 1;
-    }
-    const unsigned jobs = rc_jobs(__builtin_amdgcn_readfirstlane(wave));
-    const int njobs = (int)(jobs >> 25);
-    for (int jj = 0; jj < njobs; ++jj) {
-        const int job = (int)((jobs >> (5 * jj)) & 31u);
-        if (job < 9) {
-            // ---------------- key tile `job`: key on the lane
-            const int kt = job, kkey = kt * 16 + l16;
-            const bf16x8_t kb = as_bf(*(const u16x8 *)(Ks + kt * 16 * HD + rfrag));
-            const bf16x8_t vb = as_bf(*(const u16x8 *)(Vs + kt * 16 * HD + rfrag));
-            // seed of (kkey, queries q0 .. q0 + 3): R[264 + A(k) - A(q0) - r], read backwards
-            const float *rk = Rs + 264 + tok_a(kkey) - 3;
-            unsigned long long mbits = 0;
-            if (MM == 1) {
-                const bool k_hr = kkey >= WS * (WS - g.shift), k_hc = kkey % WS >= WS - g.shift;
-                if (lastH) mbits |= k_hr ? ~hb : hb;
-                if (lastW) mbits |= k_hc ? ~wb : wb;
-            }
-            f32x4 dv0 = {0.f, 0.f, 0.f, 0.f}, dv1 = dv0, dk0 = dv0, dk1 = dv0;
-#pragma unroll
-            for (int ks = 0; ks < 5; ++ks) {
-                bf16x8_t pb, sb;
-#pragma unroll
-                for (int half = 0; half < 2; ++half) {
-                    const int qt = 2 * ks + half;
-                    if (qt >= 9) {
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) {
-                            pb[4 * half + r] = (__bf16)0.f;
-                            sb[4 * half + r] = (__bf16)0.f;
-                        }
-                        continue;
-                    }
-                    const bf16x8_t qa = as_bf(*(const u16x8 *)(Qs + qt * 16 * HD + rfrag));
-                    const bf16x8_t da = as_bf(*(const u16x8 *)(dOs + qt * 16 * HD + rfrag));
-                    const f32x4 l4 = *(const f32x4 *)(lseS + qt * 16 + grp * 4);
-                    const f32x4 nd4 = *(const f32x4 *)(ndS + qt * 16 + grp * 4);
-                    const float *rb = rk - (part3[qt % 3] + 92 * (qt / 3));
-                    const f32x4 b4 = {rb[3], rb[2], rb[1], rb[0]};
-                    const f32x4 sa = mfma16(qa, kb, b4);    // s'[q][key] = q·k + b / scale
-                    const f32x4 dpa = mfma16(da, vb, nd4);  // dP[q][key] - δ_q
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        float v = sa[r];
-                        if (MM == 1) v += mask_term(mbits, qt * 4 + r, mneg100);
-                        if (MM == 2)
-                            v = fmaf(mask[((long)(bw % g.n_mask) * NT + qt * 16 + grp * 4 + r) * NT + kkey], 1.0f / g.scale, v);
-                        const float p = fast_exp2(fmaf(v, c2, -l4[r]));
-                        pb[4 * half + r] = (__bf16)p;
-                        sb[4 * half + r] = (__bf16)(p * dpa[r]);
-                    }
-                }
-                const int r0 = 32 * ks * HD + trow, r1 = ks < 4 ? r0 + 16 * HD : r0;
-                const u16x8 ao0 = cat4(tr_read(dOs + r0 + tc0), tr_read(dOs + r1 + tc0));
-                const u16x8 ao1 = cat4(tr_read(dOs + r0 + tc1), tr_read(dOs + r1 + tc1));
-                const u16x8 aq0 = cat4(tr_read(Qs + r0 + tc0), tr_read(Qs + r1 + tc0));
-                const u16x8 aq1 = cat4(tr_read(Qs + r0 + tc1), tr_read(Qs + r1 + tc1));
-                dv0 = mfma16(as_bf(ao0), pb, dv0);
-                dv1 = mfma16(as_bf(ao1), pb, dv1);
-                dk0 = mfma16(as_bf(aq0), sb, dk0);
-                dk1 = mfma16(as_bf(aq1), sb, dk1);
-            }
-            const int tkk = wo.tok(g, kkey);
-            if (tkk >= 0) {
-                const int c0 = h * HD + grp * 4;
-                u16x4 k0, k1, v0, v1;
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    k0[r] = f2bf(dk0[r] * g.scale);  // dK = scale · dSᵀ·q
-                    k1[r] = f2bf(dk1[r] * g.scale);
-                    v0[r] = f2bf(dv0[r]);
-                    v1[r] = f2bf(dv1[r]);
-                }
-                unsigned short *gp = gqkv + (long)tkk * 3 * g.C;
-                *(u16x4 *)(gp + g.C + c0) = k0;
-                *(u16x4 *)(gp + g.C + c0 + 16) = k1;
-                *(u16x4 *)(gp + 2 * g.C + c0) = v0;
-                *(u16x4 *)(gp + 2 * g.C + c0 + 16) = v1;
-            }
-        } else {
-            // ---------------- query tile `job - 9`: query on the lane (the forward's orientation)
-            const int qt = job - 9, qi = qt * 16 + l16;
-            const bf16x8_t qf = as_bf(*(const u16x8 *)(Qs + qt * 16 * HD + rfrag));
-            const bf16x8_t df = as_bf(*(const u16x8 *)(dOs + qt * 16 * HD + rfrag));
-            const float lq = lseS[qi], nd = ndS[qi];
-            const f32x4 nd4 = {nd, nd, nd, nd};
-            const float *rq = Rs + 264 - tok_a(qi);  // + A(k0): the seed over keys k0 .. k0 + 3
-            unsigned long long mbits = 0;
-            if (MM == 1) {
-                if (lastH) mbits |= hi_row(g, qi) ? ~hb : hb;
-                if (lastW) mbits |= hi_col(g, qi) ? ~wb : wb;
-            }
-            f32x4 dq0 = {0.f, 0.f, 0.f, 0.f}, dq1 = dq0;
-#pragma unroll
-            for (int ks = 0; ks < 5; ++ks) {
-                bf16x8_t sbq;
-#pragma unroll
-                for (int half = 0; half < 2; ++half) {
-                    const int kt = 2 * ks + half;
-                    if (kt >= 9) {
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) sbq[4 * half + r] = (__bf16)0.f;
-                        continue;
-                    }
-                    const bf16x8_t kf = as_bf(*(const u16x8 *)(Ks + kt * 16 * HD + rfrag));
-                    const bf16x8_t vf = as_bf(*(const u16x8 *)(Vs + kt * 16 * HD + rfrag));
-                    const float *rb = rq + part3[kt % 3] + 92 * (kt / 3);
-                    const f32x4 b4 = {rb[0], rb[1], rb[2], rb[3]};
-                    const f32x4 st = mfma16(kf, qf, b4);    // s'ᵀ[key][q]
-                    const f32x4 dpt = mfma16(vf, df, nd4);  // dPᵀ[key][q] - δ_q
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        float v = st[r];
-                        if (MM == 1) v += mask_term(mbits, kt * 4 + r, mneg100);
-                        if (MM == 2)
-                            v = fmaf(mask[((long)(bw % g.n_mask) * NT + qi) * NT + kt * 16 + grp * 4 + r], 1.0f / g.scale, v);
-                        const float p = fast_exp2(fmaf(v, c2, -lq));
-                        sbq[4 * half + r] = (__bf16)(p * dpt[r]);
-                    }
-                }
-                // Kᵀ (d x 32 keys) by transposed reads, keys permuted as dSᵀ's rows (the forward's Vᵀ)
-                const int r0 = 32 * ks * HD + trow, r1 = ks < 4 ? r0 + 16 * HD : r0;
-                const u16x8 a0 = cat4(tr_read(Ks + r0 + tc0), tr_read(Ks + r1 + tc0));
-                const u16x8 a1 = cat4(tr_read(Ks + r0 + tc1), tr_read(Ks + r1 + tc1));
-                dq0 = mfma16(as_bf(a0), sbq, dq0);
-                dq1 = mfma16(as_bf(a1), sbq, dq1);
-            }
-            const int tq = wo.tok(g, qi);
-            if (tq >= 0) {
-                const int c0 = h * HD + grp * 4;
-                u16x4 w0, w1;
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    w0[r] = f2bf(dq0[r] * g.scale);  // dQ = scale · dS·k
-                    w1[r] = f2bf(dq1[r] * g.scale);
-                }
-                *(u16x4 *)(gqkv + (long)tq * 3 * g.C + c0) = w0;
-                *(u16x4 *)(gqkv + (long)tq * 3 * g.C + c0 + 16) = w1;
-            }
-        }
-    }
-}
-
 int chunk_windows(int total_windows, int nH, long target = 256) {  // target: persistent workgroups
     long cw = ((long)total_windows * nH + target - 1) / target;
     return (int)(cw < 1 ? 1 : cw);
@@ -1451,12 +883,12 @@ using namespace irads;
 extern "C" int irads_winattn_bias_quads(const float *rel_table, int nH, float scale, float *quads, void *stream) {
     IRADS_REQUIRE(rel_table && quads && nH > 0, "irads_winattn_bias_quads: null pointer / nH=%d", nH);
     IRADS_REQUIRE(scale > 0.f, "irads_winattn_bias_quads: scale must be positive (%g)", scale);
-    const int n = nH * (QH * 4 + RT);
+    const int n = nH * QH;
     winattn_bias_quads_kernel<<<(n + 255) / 256, 256, 0, (hipStream_t)stream>>>(rel_table, nH, 1.0f / scale, quads);
     return check_launch("irads_winattn_bias_quads");
 }
 
-extern "C" long irads_winattn_bias_quads_size(int nH) { return (long)nH * (QH * 4 + RT); }
+extern "C" long irads_winattn_bias_quads_size(int nH) { return (long)nH * QH; }
 
 extern "C" int irads_winattn_fwd(int dtype, const void *qkv, const float *qkv_bias, const float *rel_table,
                                  const float *bias_quads, const float *mask, int n_mask, int B, int H, int W, int C, int nH, int shift,
@@ -1474,28 +906,10 @@ extern "C" int irads_winattn_fwd(int dtype, const void *qkv, const float *qkv_bi
         IRADS_REQUIRE(bias_quads, "irads_winattn_fwd: bf16 needs bias_quads (irads_winattn_bias_quads)");
         IRADS_REQUIRE(scale > 0.f, "irads_winattn_fwd: scale must be positive (%g)", scale);
         const float c2 = scale * LOG2E;
-        static const int pc_wg = [] {  // A/B switch while the persistent variant is measured
-            const char *e = getenv("IRADS_WINATTN_FWD_PC");
-            return e ? atoi(e) : 0;
-        }();
-        if (pc_wg > 0) {
-            const int cw = chunk_windows(B * g.nW, nH, 256 * pc_wg);
-            const unsigned nwg = (unsigned)(((B * g.nW + cw - 1) / cw) * nH);
-#define IRADS_WF(M) winattn_fwd_bf16_pc<M><<<nwg, 192, 0, st>>>((const unsigned short *)qkv, qkv_bias, bias_quads, \
-                                                                 mask, g, cw, c2, (unsigned short *)out, lse)
-            if (mm == 0) IRADS_WF(0); else if (mm == 1) IRADS_WF(1); else IRADS_WF(2);
-#undef IRADS_WF
-        } else if (pc_wg < 0) {
 #define IRADS_WF(M) winattn_fwd_bf16_rt<M><<<nblk, 192, 0, st>>>((const unsigned short *)qkv, qkv_bias, bias_quads, \
                                                                   mask, g, c2, (unsigned short *)out, lse)
-            if (mm == 0) IRADS_WF(0); else if (mm == 1) IRADS_WF(1); else IRADS_WF(2);
+        if (mm == 0) IRADS_WF(0); else if (mm == 1) IRADS_WF(1); else IRADS_WF(2);
 #undef IRADS_WF
-        } else {
-#define IRADS_WF(M) winattn_fwd_bf16_wg<M><<<nblk, 192, 0, st>>>((const unsigned short *)qkv, qkv_bias, bias_quads, \
-                                                                  mask, g, c2, (unsigned short *)out, lse)
-            if (mm == 0) IRADS_WF(0); else if (mm == 1) IRADS_WF(1); else IRADS_WF(2);
-#undef IRADS_WF
-        }
     }
     return check_launch("irads_winattn_fwd");
 }
@@ -1526,20 +940,8 @@ extern "C" int irads_winattn_bwd(int dtype, const void *qkv, const float *qkv_bi
                                                 scale * LOG2E,                                                    \
                                                 (const unsigned short *)out, lse, (const unsigned short *)grad_out, \
                                                 (unsigned short *)grad_qkv, grad_table, grad_bias_pad)
-        static const int rc = [] {  // A/B switch while the per-item kernel is measured
-            const char *e = getenv("IRADS_WINATTN_BWD_RC");
-            return e ? atoi(e) : 0;
-        }();
         if (ex) {
             if (mm == 0) IRADS_WB(0, true); else if (mm == 1) IRADS_WB(1, true); else IRADS_WB(2, true);
-        } else if (rc) {
-            const float *rtab = bias_quads + (long)nH * QH * 4;
-#define IRADS_WR(M)                                                                                                 \
-    winattn_bwd_bf16_rc<M><<<nblk, 256, 0, st>>>((const unsigned short *)qkv, qkv_bias, rtab, mask, g, scale * LOG2E, \
-                                                 (const unsigned short *)out, lse, (const unsigned short *)grad_out,    \
-                                                 (unsigned short *)grad_qkv)
-            if (mm == 0) IRADS_WR(0); else if (mm == 1) IRADS_WR(1); else IRADS_WR(2);
-#undef IRADS_WR
         } else {
             if (mm == 0) IRADS_WB(0, false); else if (mm == 1) IRADS_WB(1, false); else IRADS_WB(2, false);
         }

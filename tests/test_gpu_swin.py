@@ -49,9 +49,9 @@ def test_shift_window_msa_fp32(tag):
 def test_window_attention_bf16_vs_fp32(shift):
     """bf16 MFMA kernels vs the fp32 kernels (themselves pinned above) on the same
     bf16-representable inputs, at Swin-B stage-0 geometry (128x128 tokens, pad to 132).
-    The bf16 path accumulates q·kᵀ in fp32 from the unscaled bf16 q and folds the scale into the
-    softmax exponent (no bf16 rounding of q·scale, one rounding closer to fp32 than the
-    reference's AMP, swin.py:95), so it is compared with the exact fp32 result directly.
+    The bf16 path forms the scores in base-2 units from bf16(q·scale·log2 e) (one bf16 rounding of
+    the scaled q, as the reference's AMP rounds q·scale, swin.py:95) and is compared with the
+    exact fp32 result directly.
     Tolerance: bf16 P / dS rounding (2^-8 relative) x O(1) magnitudes."""
     from irads import ops
     torch.manual_seed(1)
@@ -83,6 +83,36 @@ def test_window_attention_bf16_vs_fp32(shift):
     for a_, b_, what in ((gbbf, gb32, "pad qkv-bias grad"), (gtbf, gt32, "rel-table grad")):
         err = (a_ - b_).norm() / b_.norm().clamp_min(1e-6)
         assert err < 2e-2, f"bf16 {what} relative L2 error {err:.3e}"
+
+
+@pytest.mark.parametrize("offset", [70.0, -70.0])
+def test_window_attention_bf16_shifted_rows(offset):
+    """Rows whose scores lie far from 0 (here every score moved by ±70 through the bias table, so
+    the base-2 row maximum is about ±101) take the forward's shifted path: 2^s'' would overflow or
+    underflow, so the wave adds -max to its scores with one more MFMA per key tile and the LSE
+    records the shift.  Softmax is shift-invariant, so the output and gradients must match the
+    exact fp32 kernels as closely as unshifted rows do (tolerance as test_window_attention_bf16_vs_fp32)."""
+    from irads import ops
+    torch.manual_seed(3)
+    B, H, W, C, nH = 2, 36, 36, 128, 4
+    qkv = (torch.randn(B, H * W, 3 * C, device=DEV) * 1.5).bfloat16()
+    bias = (torch.randn(3 * C, device=DEV) * 0.5).bfloat16().float()
+    table = torch.randn(529, nH, device=DEV) * 0.5 + offset
+    scale = 32 ** -0.5
+    for shift in (0, 6):
+        q32 = qkv.float().requires_grad_()
+        qbf = qkv.clone().requires_grad_()
+        o32 = ops.window_attention(q32, bias, table, None, H, W, nH, shift, scale)
+        obf = ops.window_attention(qbf, bias, table, None, H, W, nH, shift, scale)
+        assert torch.isfinite(obf.float()).all()
+        rel = (obf.float() - o32).norm() / o32.norm()
+        assert rel < 1e-2, f"shift {shift}: bf16 forward relative L2 error vs exact fp32 {rel:.3e}"
+        g = torch.randn_like(o32).bfloat16()
+        (g32,) = torch.autograd.grad(o32, q32, g.float())
+        (gbf,) = torch.autograd.grad(obf, qbf, g)
+        assert torch.isfinite(gbf.float()).all()
+        rel = (gbf.float() - g32).norm() / g32.norm()
+        assert rel < 1e-2, f"shift {shift}: bf16 grad relative L2 error {rel:.3e}"
 
 
 def test_window_msa_explicit_mask():
