@@ -39,9 +39,10 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=50)   # >= 50 timed
     p.add_argument("--warmup", type=int, default=10)  # 10 warm-up iterations
-    p.add_argument("--workload", choices=("c2", "c4"), default="c2",
-                   help="c2: the headline C2 step (default); c4: BASELINE config C4 (MFNet RGB-T, Swin-L, "
-                        "480x640, B=4 per GPU, SB hook on) as a separate line")
+    p.add_argument("--workload", choices=("c2", "c3", "c4"), default="c2",
+                   help="c2: the headline C2 step (default); c3: BASELINE config C3 (DeepCrack RGB+HHA, Swin-B "
+                        "512x512, B=4 per GPU, 2 classes); c4: BASELINE config C4 (MFNet RGB-T, Swin-L, "
+                        "480x640, B=4 per GPU, SB hook on); c3 / c4 print a separate line")
     p.add_argument("--batch", type=int, default=None, help="images per GPU (C2: 8, C4: 4)")
     p.add_argument("--size", type=int, default=None, help="square side (C2: 512); C4 is 480x640")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -62,6 +63,11 @@ WORKLOADS = {
     "c2": dict(batch=8, hw=(512, 512), n_cls=N_CLASSES, backbone="SwinTransformer-B", modals=["img", "depth"],
                sb=None, desc="C2: NYU-Depth-v2 RGB-D CMNeXt(SwinTransformer-B) 512x512 train step "
                              "(fwd+bwd+AdamW, TRAIN_TYPE Adapter, MMST loss)"),
+    # C3: DeepCrack RGB+HHA, global batch 32 over 8 GPUs = 4 per GPU, 2 classes (crack / background,
+    # SURVEY §8(d)); weak scaling, so one GPU runs the per-GPU share
+    "c3": dict(batch=4, hw=(512, 512), n_cls=2, backbone="SwinTransformer-B", modals=["img", "hha"], sb=None,
+               desc="C3: DeepCrack RGB+HHA CMNeXt(SwinTransformer-B) 512x512 train step, 4 images per GPU "
+                    "(fwd+bwd+AdamW, TRAIN_TYPE Adapter, MMST loss)"),
     "c4": dict(batch=4, hw=(480, 640), n_cls=9, backbone="SwinTransformer-L", modals=["img", "thermal"],
                sb={"weight": 0.01, "n_potentials": 10, "epsilon": 0.1},
                desc="C4: MFNet RGB-T CMNeXt(SwinTransformer-L) 480x640 train step (fwd+bwd+AdamW, TRAIN_TYPE "
@@ -174,6 +180,7 @@ def msda_inputs(device, bs=2, Q=None, seed=0):
 
 
 TIMED_KERNELS = ("winattn_fwd", "winattn_bwd", "dattn_fwd", "dattn_bwd")
+TIMER_REPS = 4  # idempotent window-attention launches per event pair in the eager timing pass
 FP32_PEAK_TFLOPS = 157.3  # MI355X fp32 vector peak (MI355X_MICROARCH.md)
 GATHER_PEAK_GBS = 18800.0  # L2-resident random-row gather rate (upper end), MI355X_MICROARCH.md
 
@@ -292,11 +299,15 @@ def dino_stack_line(device, msda, reps=5):
 
 
 def traffic_from_profile():
-    path = os.path.join(ROOT, "profiles", "r02_pmc_winattn_fwd.json")
-    if not os.path.exists(path):
-        return None
-    with open(path) as f:
-        return json.load(f).get("hbm_bytes_per_launch")
+    """HBM bytes per forward launch from the newest committed PMC passes of the same 24 launches
+    (scripts/pmc_winattn_kind.sh: FETCH_SIZE x2 + WRITE_SIZE, separate rocprofv3 passes); PMC
+    counters cannot be read from inside this process."""
+    for tag in ("r03", "r02"):
+        path = os.path.join(ROOT, "profiles", f"{tag}_pmc_winattn_fwd.json")
+        if os.path.exists(path):
+            with open(path) as f:
+                return json.load(f).get("hbm_bytes_per_launch")
+    return None
 
 
 def main():
@@ -379,9 +390,11 @@ def main():
         ops.TIMER.records.clear()
         ops.TIMER.enabled = set(TIMED_KERNELS)
         ops.TIMER.lead_cycles = 200_000
+        ops.TIMER.reps = TIMER_REPS
         fwd_bwd(model, loss_fn, batch)  # gradients land in the graph's buffer, re-zeroed by the next replay
         ops.TIMER.enabled = set()
         ops.TIMER.lead_cycles = 0
+        ops.TIMER.reps = 1
     if world > 1:
         t = torch.tensor([elapsed], device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -423,11 +436,12 @@ def main():
             "kernel": "irads_winattn_fwd (bf16, Swin-B shifted-window attention, all 4 stages x 2 streams)",
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-            "launches": fwd["launches"], "avg_launch_ms": round(avg_ms, 5),
+            "launches": fwd["calls"], "timed_launches": fwd["launches"], "avg_launch_ms": round(avg_ms, 5),
             "algorithmic_bytes_per_launch": round(per_launch_bytes),
             "timing": ("HIP events captured in the graph, last timed replay" if timer_in_graph else
-                       "HIP events on the launch stream" + (" (eager step after the timed region, each launch "
-                                                            "queued behind a GPU spin)" if graph else "")),
+                       "HIP events on the launch stream" + (f" (eager step after the timed region; each call's "
+                                                            f"kernel issued {TIMER_REPS}x back to back inside one "
+                                                            f"event pair, queued behind a GPU spin)" if graph else "")),
             "bytes_definition": "SURVEY §8(d): read q,k,v + write o per padded token (8·Np·C bytes, bf16)",
             "achieved_real_tokens_gbs": round(achieved_real, 1),
             "mfma_tflops": round(fwd["flops"] / (fwd["total_ms"] * 1e-3) / 1e12, 2)}
@@ -436,8 +450,10 @@ def main():
             result["roofline_bwd"] = {"kernel": "irads_winattn_bwd (bf16)", "achieved": round(ab, 1),
                                       "unit": "GB/s", "frac": round(ab / HBM_PEAK_GBS, 4),
                                       "avg_launch_ms": round(bwd["total_ms"] / bwd["launches"], 5),
-                                      "share_of_step": round(bwd["total_ms"] / timer_steps / (1e3 * elapsed / args.steps), 4)}
-            result["roofline"]["share_of_step"] = round(fwd["total_ms"] / timer_steps / (1e3 * elapsed / args.steps), 4)
+                                      "share_of_step": round(bwd["total_ms"] * bwd["calls"] / bwd["launches"] / timer_steps
+                                                             / (1e3 * elapsed / args.steps), 4)}
+            result["roofline"]["share_of_step"] = round(fwd["total_ms"] * fwd["calls"] / fwd["launches"] / timer_steps
+                                                        / (1e3 * elapsed / args.steps), 4)
     for tag in ("fwd", "bwd"):
         d = ops.TIMER.summary(f"dattn_{tag}")
         if d:
@@ -451,10 +467,12 @@ def main():
                                     "pairs = B·heads·H·W·2n per stage",
                 "share_of_step": round(d["total_ms"] / timer_steps / (1e3 * elapsed / args.steps), 4)}
     if args.workload != "c2":  # a separate line for another BASELINE config, not the headline metric
-        result["metric"] = ("train images/sec @480x640 RGB-T Swin-L, SB hook on (BASELINE.json config C4), "
-                            "1 MI355X" if args.workload == "c4" else f"train images/sec ({args.workload})")
-        result["data"] = ("synthetic (RGB N(0,1), thermal U[0,1), labels U{0..%d} with 10%% ignore=255; random-init "
-                          "weights)" % (wl["n_cls"] - 1))
+        result["metric"] = {"c4": "train images/sec @480x640 RGB-T Swin-L, SB hook on (BASELINE.json config C4), "
+                                  "1 MI355X",
+                            "c3": "train images/sec @512² RGB+HHA Swin-B, 4 per GPU (BASELINE.json config C3)"}.get(
+                                args.workload, f"train images/sec ({args.workload})")
+        result["data"] = ("synthetic (RGB N(0,1), %s U[0,1), labels U{0..%d} with 10%% ignore=255; random-init "
+                          "weights)" % ({"c3": "HHA"}.get(args.workload, "thermal"), wl["n_cls"] - 1))
     if rank == 0 and not args.no_kernels and args.workload == "c2":
         try:
             result["kernels"] = msda_rooflines(device)

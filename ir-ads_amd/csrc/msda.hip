@@ -359,6 +359,30 @@ __device__ __forceinline__ void load_levels(const int64_t *shapes, const int64_t
 // memory-side int atomic per sample; PMC: ~88 % of wave cycles waiting at one sample per thread).
 constexpr int kSPT = 4;
 
+// The 4 lanes of a DPP quad often hold samples of one bucket (the P points of one (b, q, m, l) are
+// consecutive sample ids, and at the coarse levels they fall in one cell): the quad's first lane of
+// each bucket adds for all of them.  count = lanes of the quad with this key, rank = those before
+// this lane, first = the first such lane.  All 4 lanes of every quad must be active.
+template <int I>
+__device__ __forceinline__ int quad_bcast(int v) { return __builtin_amdgcn_mov_dpp(v, I * 0x55, 0xF, 0xF, false); }
+
+struct QuadAgg {
+    int count, rank, first;
+};
+__device__ __forceinline__ QuadAgg quad_agg(int key) {
+    const int me = threadIdx.x & 3;
+    const int k[4] = {quad_bcast<0>(key), quad_bcast<1>(key), quad_bcast<2>(key), quad_bcast<3>(key)};
+    QuadAgg a{0, 0, 4};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const bool eq = k[j] == key;
+        a.count += eq;
+        a.rank += eq && j < me;
+        if (eq && a.first == 4) a.first = j;
+    }
+    return a;
+}
+
 __global__ void __launch_bounds__(256) msda_bucket_count(const float *__restrict__ loc, const int64_t *__restrict__ shapes,
                                                          const int64_t *__restrict__ lsi, int bs, int S, int M, int L,
                                                          int Q, int P, int *__restrict__ cnt) {
@@ -380,8 +404,10 @@ __global__ void __launch_bounds__(256) msda_bucket_count(const float *__restrict
         }
     }
 #pragma unroll
-    for (int k = 0; k < kSPT; ++k)
-        if (bk[k] >= 0) atomicAdd(cnt + bk[k], 1);
+    for (int k = 0; k < kSPT; ++k) {
+        const QuadAgg a = quad_agg((int)bk[k]);  // buckets < 2^31 (gather_ws_layout)
+        if (bk[k] >= 0 && a.first == (int)(threadIdx.x & 3)) atomicAdd(cnt + bk[k], a.count);
+    }
 }
 
 // exclusive scan of cnt (n entries) in blocks of 1024: per-block scan + block totals
@@ -481,8 +507,19 @@ __global__ void __launch_bounds__(256) msda_bucket_fill(const float *__restrict_
         }
     }
     int slot[kSPT];
+    QuadAgg ag[kSPT];
 #pragma unroll
-    for (int k = 0; k < kSPT; ++k) slot[k] = bk[k] >= 0 ? atomicAdd(cursor + bk[k], 1) : 0;
+    for (int k = 0; k < kSPT; ++k) {
+        ag[k] = quad_agg((int)bk[k]);
+        slot[k] = (bk[k] >= 0 && ag[k].first == (int)(threadIdx.x & 3)) ? atomicAdd(cursor + bk[k], ag[k].count) : 0;
+    }
+#pragma unroll
+    for (int k = 0; k < kSPT; ++k) {  // the first lane's slot base, + this lane's rank among its bucket's lanes
+        const int b0 = quad_bcast<0>(slot[k]), b1 = quad_bcast<1>(slot[k]), b2 = quad_bcast<2>(slot[k]),
+                  b3 = quad_bcast<3>(slot[k]);
+        const int f = ag[k].first;
+        slot[k] = (f == 0 ? b0 : f == 1 ? b1 : f == 2 ? b2 : b3) + ag[k].rank;
+    }
 #pragma unroll
     for (int k = 0; k < kSPT; ++k)
         if (bk[k] >= 0) rec[off[bk[k]] + slot[k]] = r[k];

@@ -27,12 +27,19 @@ class LaunchTimer:
     lead_cycles > 0 enqueues a GPU spin of that many cycles before the start event, so the stream
     is still busy when the host enqueues the launch: the event pair then brackets the kernel alone
     (no host-side enqueue latency inside the interval), which is what rocprofv3's kernel trace
-    reports for the same launch."""
+    reports for the same launch.  reps > 1 has an idempotent launch (one that only overwrites its
+    outputs) issued that many times back to back inside one event pair, so the pair's own
+    dispatch latency (a few us) is spread over reps launches."""
 
     def __init__(self):
         self.enabled = set()
-        self.records = []  # (name, start_event, end_event, algorithmic_bytes, flops, real_token_bytes)
+        self.records = []  # (name, start_event, end_event, algorithmic_bytes, flops, real_token_bytes, launches)
         self.lead_cycles = 0
+        self.reps = 1
+
+    def launches(self, name):
+        """How many times the caller should issue an idempotent launch of `name`."""
+        return self.reps if name in self.enabled else 1
 
     def start(self, name):
         if name not in self.enabled:
@@ -43,12 +50,13 @@ class LaunchTimer:
         ev.record()
         return ev
 
-    def stop(self, name, ev, nbytes, flops, real_bytes=None):
+    def stop(self, name, ev, nbytes, flops, real_bytes=None, launches=1):
         if ev is None:
             return
         end = torch.cuda.Event(enable_timing=True)
         end.record()
-        self.records.append((name, ev, end, nbytes, flops, nbytes if real_bytes is None else real_bytes))
+        rb = nbytes if real_bytes is None else real_bytes
+        self.records.append((name, ev, end, nbytes * launches, flops * launches, rb * launches, launches))
 
     def summary(self, name):
         torch.cuda.synchronize()
@@ -56,8 +64,8 @@ class LaunchTimer:
         if not rec:
             return None
         ms = [r[1].elapsed_time(r[2]) for r in rec]
-        return {"launches": len(rec), "total_ms": sum(ms), "bytes": sum(r[3] for r in rec),
-                "flops": sum(r[4] for r in rec), "real_bytes": sum(r[5] for r in rec)}
+        return {"launches": sum(r[6] for r in rec), "calls": len(rec), "total_ms": sum(ms),
+                "bytes": sum(r[3] for r in rec), "flops": sum(r[4] for r in rec), "real_bytes": sum(r[5] for r in rec)}
 
 
 TIMER = LaunchTimer()
@@ -113,14 +121,15 @@ def winattn_fwd(qkv, bias_f, table_f, mask_f, H, W, num_heads, shift, scale, tab
     lse = torch.empty((B * nW * num_heads * WINDOW * WINDOW,), device=qkv.device, dtype=torch.float32)
     quads = bias_quads(table_f, num_heads, scale, table_owner) if code == N.BF16 else None
     ev = TIMER.start("winattn_fwd")
-    N.call("irads_winattn_fwd", code, N.ptr(qkv), N.ptr(bias_f), N.ptr(table_f), N.ptr(quads), N.ptr(mask_f), n_mask,
-           B, H, W,
-           C, num_heads, shift, float(scale), N.ptr(out), N.ptr(lse), N.stream())
+    reps = TIMER.launches("winattn_fwd")  # idempotent: out and lse are overwritten
+    for _ in range(reps):
+        N.call("irads_winattn_fwd", code, N.ptr(qkv), N.ptr(bias_f), N.ptr(table_f), N.ptr(quads), N.ptr(mask_f),
+               n_mask, B, H, W, C, num_heads, shift, float(scale), N.ptr(out), N.ptr(lse), N.stream())
     # algorithmic work: read q, k, v and write o for every PADDED token
     # (8·Np·C bytes in bf16); 4·N²·32 flops per (window, head).  Real-token bytes kept too.
     es = qkv.element_size()
     TIMER.stop("winattn_fwd", ev, B * Hp * Wp * 4 * C * es, 4 * (WINDOW * WINDOW) ** 2 * HEAD_DIM * B * nW * num_heads,
-               B * L * 4 * C * es)
+               B * L * 4 * C * es, reps)
     return out, lse
 
 
@@ -137,15 +146,18 @@ def winattn_bwd(qkv, bias_f, table_f, mask_f, H, W, nH, shift, scale, out, lse, 
     gbias = torch.zeros((3 * C,), device=qkv.device, dtype=torch.float32) if need_bias else None
     quads = bias_quads(table_f, nH, scale, table_owner) if code == N.BF16 else None
     ev = TIMER.start("winattn_bwd")
-    N.call("irads_winattn_bwd", code, N.ptr(qkv), N.ptr(bias_f), N.ptr(table_f), N.ptr(quads), N.ptr(mask_f), n_mask,
-           B, H, W, C, nH, shift, float(scale), N.ptr(out), N.ptr(lse), N.ptr(gout), N.ptr(gqkv), N.ptr(gtable),
-           N.ptr(gbias), N.stream())
+    # idempotent unless the table / pad-bias gradients are accumulated
+    reps = 1 if (need_bias or need_table) else TIMER.launches("winattn_bwd")
+    for _ in range(reps):
+        N.call("irads_winattn_bwd", code, N.ptr(qkv), N.ptr(bias_f), N.ptr(table_f), N.ptr(quads), N.ptr(mask_f),
+               n_mask, B, H, W, C, nH, shift, float(scale), N.ptr(out), N.ptr(lse), N.ptr(gout), N.ptr(gqkv),
+               N.ptr(gtable), N.ptr(gbias), N.stream())
     # algorithmic: read q, k, v, o, dO and write dq, dk, dv per padded token;
     # 8·N²·32 flops per (window, head)
     Hp, Wp, nW = _winattn_geometry(H, W)
     es = qkv.element_size()
     TIMER.stop("winattn_bwd", ev, B * Hp * Wp * 8 * C * es, 8 * (WINDOW * WINDOW) ** 2 * HEAD_DIM * B * nW * nH,
-               B * L * 8 * C * es)
+               B * L * 8 * C * es, reps)
     return gqkv, gtable, gbias
 
 

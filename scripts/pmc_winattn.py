@@ -19,6 +19,7 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KIND = os.environ.get("IRADS_PMC_KIND", "fwd")  # fwd | bwd: which window-attention kernel is counted
 STAGES = ((128, 128, 4, 2), (64, 256, 8, 2), (32, 512, 16, 18), (16, 1024, 32, 2))  # side, C, heads, depth
 
 
@@ -39,8 +40,20 @@ def run():
         for qkv, bias, table, side, nH, depth in ins:
             for blk in range(depth):
                 ops.winattn_fwd(qkv, bias, table, None, side, side, nH, 6 if blk % 2 else 0, 32 ** -0.5)
-    step()
-    step()
+
+    def step_bwd():  # the 24 backward launches, each on its own forward's output and LSE
+        for qkv, bias, table, side, nH, depth in ins:
+            for blk in range(depth):
+                shift = 6 if blk % 2 else 0
+                qq = qkv.clone().requires_grad_()
+                o = ops.window_attention(qq, bias, table, None, side, side, nH, shift, 32 ** -0.5)
+                o.backward(torch.ones_like(o))
+    if KIND == "bwd":
+        step_bwd()
+        step_bwd()
+    else:
+        step()
+        step()
     torch.cuda.synchronize()
 
 
@@ -48,7 +61,8 @@ def algorithmic_bytes():
     tot = 0
     for side, C, nH, depth in STAGES:
         Np = (-(-side // 12) * 12) ** 2
-        tot += depth * 16 * Np * 4 * C * 2  # read q, k, v + write o per padded token, bf16
+        # read q, k, v + write o per padded token (fwd); read q, k, v, o, dO + write dq, dk, dv (bwd)
+        tot += depth * 16 * Np * (4 if KIND == "fwd" else 8) * C * 2
     return tot / 24
 
 
@@ -58,7 +72,7 @@ def _values(d, counter):
     for f in files:
         with open(f) as fh:
             for r in csv.DictReader(fh):
-                if "winattn_fwd" in r.get("Kernel_Name", "") and r.get("Counter_Name") == counter:
+                if f"winattn_{KIND}" in r.get("Kernel_Name", "") and r.get("Counter_Name") == counter:
                     vals.append((int(r.get("Dispatch_Id", 0)), float(r["Counter_Value"])))
     vals.sort()
     return [v for _, v in vals][-24:]
@@ -72,7 +86,7 @@ def parse(dir_fetch, dir_write):
     kib = 1024.0
     read_b = 2.0 * sum(fetch) / 24 * kib  # gfx950: FETCH_SIZE = half the bytes of 16-B/lane reads
     write_b = sum(write) / 24 * kib
-    out = {"kernel": "irads_winattn_fwd (bf16)", "launches": 24,
+    out = {"kernel": f"irads_winattn_{KIND} (bf16)", "launches": 24,
            "fetch_size_kib_per_launch_raw": sum(fetch) / 24, "write_size_kib_per_launch": sum(write) / 24,
            "hbm_read_bytes_per_launch": round(read_b), "hbm_write_bytes_per_launch": round(write_b),
            "hbm_bytes_per_launch": round(read_b + write_b),
@@ -97,7 +111,7 @@ def parse_sq(dir_sq, *counters):
     names = counters or SQ_COUNTERS
     vals = {c: _values(dir_sq, c) for c in names}
     tot = {c: sum(v) for c, v in vals.items()}
-    out = {"kernel": "irads_winattn_fwd (bf16)", "launches": 24,
+    out = {"kernel": f"irads_winattn_{KIND} (bf16)", "launches": 24,
            "per_launch": {c: round(v / 24) for c, v in tot.items()},
            # dispatch order: stage 0 x2, stage 1 x2, stage 2 x18, stage 3 x2 (shift 0 / 6 alternating)
            "per_stage_sum": {c: [round(sum(v[a:b])) for a, b in ((0, 2), (2, 4), (4, 22), (22, 24))]

@@ -1,6 +1,6 @@
 """Worker of test_gpu_drivers.py::test_dp_two_ranks_gradients (one process per rank, both on the
 one GPU of the box): the training step of irads/graph_step.py with world = 2 over gloo, on this
-rank's half of a 4-image batch, in fp32 with deterministic MIOpen solvers.  mode "split": the
+rank's half of the batch (SHAPES), in fp32 with deterministic MIOpen solvers.  mode "split": the
 graph-captured step (pack, one all-reduce between the backward and the optimizer graphs); mode
 "overlap": the bucketed exchange from post-accumulate-grad hooks (OverlappedGradExchange, the
 RCCL path's code with gloo collectives; eager, as gloo cannot be captured), >= 4 buckets.
@@ -13,19 +13,30 @@ for p in (os.path.join(ROOT, "ir-ads_amd"), os.path.join(ROOT, "oracle"), os.pat
     sys.path.insert(0, p)
 
 
-def batch(dev):
+# kind "tiny": the tiny-Swin CMNeXt on 4 images of 64x96 (2 per rank); kind "c3": BASELINE config C3's
+# model and per-GPU share, CMNeXt('SwinTransformer-B', 2 classes, ['img', 'hha']) on 8 images of 512x512
+# (4 per rank, as C3's 32 over 8 GPUs)
+SHAPES = {"tiny": (4, 64, 96, 5), "c3": (8, 512, 512, 2)}
+
+
+def batch(dev, kind="tiny"):
     import torch
+    n, H, W, ncls = SHAPES[kind]
     g = torch.Generator().manual_seed(11)
-    rgb = torch.randn(4, 3, 64, 96, generator=g)
-    dep = torch.rand(4, 3, 64, 96, generator=g)
-    lbl = torch.randint(0, 5, (4, 64, 96), generator=g)  # no ignore pixels: per-rank means average exactly
+    rgb = torch.randn(n, 3, H, W, generator=g)
+    dep = torch.rand(n, 3, H, W, generator=g)
+    lbl = torch.randint(0, ncls, (n, H, W), generator=g)  # no ignore pixels: per-rank means average exactly
     return rgb.to(dev), dep.to(dev), lbl.to(dev)
 
 
-def model(dev):
+def model(dev, kind="tiny"):
     from fill import fill_module
-    from test_gpu_drivers import _tiny_model
-    m = _tiny_model().to(dev)
+    if kind == "c3":
+        from semseg.models import CMNeXt
+        m = CMNeXt("SwinTransformer-B", 2, ["img", "hha"]).to(dev)
+    else:
+        from test_gpu_drivers import _tiny_model
+        m = _tiny_model().to(dev)
     fill_module(m, seed=4)
     for n, p in m.named_parameters():
         p.requires_grad_(("Adapter" in n) or ("extra_patch_embed" in n) or ("head" in n) or ("MPG" in n))
@@ -47,6 +58,7 @@ def fwd_bwd_fn(m, rgb, dep, lbl):
 def main():
     rank, world, port, out = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4]
     mode = sys.argv[5] if len(sys.argv) > 5 else "split"
+    kind = sys.argv[6] if len(sys.argv) > 6 else "tiny"
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = port
     import datetime
@@ -57,9 +69,10 @@ def main():
     from irads.graph_step import GraphedTrainStep
     torch.backends.cudnn.deterministic = True
     dev = torch.device("cuda", 0)
-    m = model(dev)
-    rgb, dep, lbl = batch(dev)
-    half = slice(rank * 2, rank * 2 + 2)
+    m = model(dev, kind)
+    rgb, dep, lbl = batch(dev, kind)
+    per = rgb.shape[0] // world
+    half = slice(rank * per, rank * per + per)
     opt = torch.optim.SGD([p for p in m.parameters() if p.requires_grad], lr=0.0)
     if mode == "split":
         step = GraphedTrainStep(m.parameters(), fwd_bwd_fn(m, rgb[half], dep[half], lbl[half]), opt, world=world,
@@ -67,7 +80,7 @@ def main():
         assert step.comm == "split"
     else:
         step = GraphedTrainStep(m.parameters(), fwd_bwd_fn(m, rgb[half], dep[half], lbl[half]), opt, world=world,
-                                comm="overlap", bucket_mb=0.02, graph=False)
+                                comm="overlap", bucket_mb=0.02 if kind == "tiny" else 4.0, graph=False)
         assert len(step._buckets) >= 4, len(step._buckets)
     step.step()
     if mode == "overlap":

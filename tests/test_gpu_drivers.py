@@ -212,26 +212,28 @@ def test_sb_hook_step():
     assert amap.shape == (4, 32, 32) and torch.isfinite(amap).all()
 
 
-@pytest.mark.parametrize("mode", ["split", "overlap"])
-def test_dp_two_ranks_gradients(tmp_path, mode):
+@pytest.mark.parametrize("mode,kind", [("split", "tiny"), ("overlap", "tiny"), ("overlap", "c3")])
+def test_dp_two_ranks_gradients(tmp_path, mode, kind):
     """Data parallel at model level (north_star: per-image batch sharded over GPUs, gradients
     all-reduced): 2 fresh processes, one per rank (gloo, on the one GPU of the box), each run
     GraphedTrainStep on half of a 4-image batch, with the captured split exchange or the
     overlapped bucketed one (tests/_dp_worker.py); rank 0's averaged gradients equal a
     single-process 4-image step's.  fp32 with deterministic MIOpen solvers, so the only
     difference left is GEMM tiling of batch 2 against batch 4: relative L2 1e-4 over all
-    trainable tensors."""
+    trainable tensors.  kind "c3" is BASELINE config C3's model and per-GPU share (Swin-B, 512x512,
+    2 classes, 4 images per rank, 8 in the single-process reference)."""
     import subprocess
     import sys
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import _dp_worker as W
     out = str(tmp_path / "grads.pt")
-    port = str(29600 + os.getpid() % 300)
+    port = str(29600 + (os.getpid() + 101 * (mode == "overlap") + 211 * (kind == "c3")) % 300)
     env = dict(os.environ)
-    procs = [subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "_dp_worker.py"), str(r), "2", port, out, mode],
+    procs = [subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "_dp_worker.py"), str(r), "2", port, out, mode,
+                               kind],
                               env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT) for r in range(2)]
     try:
-        logs = [p.communicate(timeout=150)[0].decode()[-2000:] for p in procs]
+        logs = [p.communicate(timeout=200)[0].decode()[-2000:] for p in procs]
     finally:
         for p in procs:  # our own children only
             if p.poll() is None:
@@ -243,8 +245,8 @@ def test_dp_two_ranks_gradients(tmp_path, mode):
     det = torch.backends.cudnn.deterministic
     torch.backends.cudnn.deterministic = True
     try:
-        m = W.model(dev)
-        rgb, dep, lbl = W.batch(dev)
+        m = W.model(dev, kind)
+        rgb, dep, lbl = W.batch(dev, kind)
         W.fwd_bwd_fn(m, rgb, dep, lbl)()
     finally:
         torch.backends.cudnn.deterministic = det
@@ -255,7 +257,7 @@ def test_dp_two_ranks_gradients(tmp_path, mode):
     num = sum(float((got[n] - want[n]).double().norm() ** 2) for n in want)
     den = sum(float(want[n].double().norm() ** 2) for n in want)
     rel = (num / den) ** 0.5
-    print(f"dp {mode}: relative L2 vs single process {rel:.3e}")
+    print(f"dp {mode} {kind}: relative L2 vs single process {rel:.3e}")
     assert rel < 1e-4, rel
 
 
