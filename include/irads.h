@@ -81,10 +81,13 @@ int irads_msda_corner_index(int dtype, const void *loc, const int64_t *shapes, i
  *         NULL => the shift-region mask computed in-kernel when shift > 0
  *   out   (B, H, W, C) same dtype      lse (B*nW, nH, 144) fp32 workspace for backward
  * window = 12, head_dim = 32 (every Swin-B/L stage).  scale = qk_scale or 32^-0.5.
- *   bias_quads (nH, 2, 532, 4) fp32 from irads_winattn_bias_quads (required for BF16, ignored for
- *         F32): the table divided by scale and re-laid so that every 4-key (forward) / 4-query
- *         (backward) bias group of a window row is one 16-byte LDS read; recompute when rel_table
- *         or scale changes (a pure function of both; the frozen trunk's is built once). */
+ *   bias_quads (nH, 2, 460, 4) fp32 (irads_winattn_bias_quads_size floats) from
+ *         irads_winattn_bias_quads (required for BF16, ignored for F32): the table divided by
+ *         scale and re-laid so that every 4-key (forward) / 4-query (backward) bias group of a
+ *         window row is one 16-byte LDS read; recompute when rel_table or scale changes (a pure
+ *         function of both; the frozen trunk's is built once).
+ * BF16 scores are formed in base-2 units from bf16(q·scale·log2 e); lse holds the base-2
+ * log-sum-exp of those scores (the backward's input, from the same library version). */
 long irads_winattn_bias_quads_size(int nH);
 int irads_winattn_bias_quads(const float *rel_table, int nH, float scale, float *bias_quads, void *stream);
 int irads_winattn_fwd(int dtype, const void *qkv, const float *qkv_bias, const float *rel_table,

@@ -525,42 +525,49 @@ __global__ void __launch_bounds__(256) msda_bucket_fill(const float *__restrict_
         if (bk[k] >= 0) rec[off[bk[k]] + slot[k]] = r[k];
 }
 
-// grad_value rows: V lanes (4 channels each) per (b, s, m) cell
+// A coarse level's cell is a corner of hundreds of samples (DINO encoder: ~330 records over a level-2
+// cell's 4 buckets, ~1300 at level 3), so one group walking them serially is a chain of dependent
+// round trips that outlasts the whole rest of the launch.  Such levels are split: their cells are
+// written as zeros by msda_gather_gvalue and summed by msda_gather_split, `parts` groups per cell,
+// each walking every parts-th chunk of the records and adding its partial row with float atomics.
+__device__ __forceinline__ int split_parts(int Q, int P, int H, int W) {
+    const long rec4 = 4L * Q * P / ((long)H * W);  // mean records over a cell's 4 buckets
+    return rec4 > 128 ? (int)min(32L, (rec4 + 63) / 64) : 1;
+}
+
+// One group's walk over a cell's 4 buckets (cells (y, x), (y, x-1), (y-1, x), (y-1, x-1)): chunks
+// part, part + parts, ... of V records each, accumulated into acc (4 channels per lane).  Records
+// are loaded one chunk ahead, so a chunk's grad_out row loads wait only on their own records.
 template <int V>
-__global__ void __launch_bounds__(256) msda_gather_gvalue(const int64_t *__restrict__ shapes,
-                                                          const int64_t *__restrict__ lsi, const float *__restrict__ loc,
-                                                          const float *__restrict__ aw, const float *__restrict__ gout,
-                                                          int bs, int S, int M, int D, int L, int Q, int P,
-                                                          const int *__restrict__ off, const float4 *__restrict__ rec,
-                                                          float *__restrict__ gvalue) {
-    __shared__ int sH[kMaxLevels], sW[kMaxLevels], sS[kMaxLevels];
-    load_levels(shapes, lsi, L, sH, sW, sS);
-    // neighbouring cells share samples (a sample feeds 4 cells) and their grad_out rows: consecutive
-    // cells of one head on one XCD (map_group) so those rows are L2 hits
-    const GroupMap gm = map_group<V>((long)bs * S, M);
-    const int lane = threadIdx.x % V;
-    if (!gm.valid) return;  // whole group exits together
-    const int m = gm.m;
-    const long gid = gm.row * M + m;  // = (b * S + s) * M + m
-    const int s = (int)(gm.row % S);
-    const int b = (int)(gm.row / S);
-    const int l = level_of(s, sS, L);
-    const int H = sH[l], W = sW[l];
-    const int c = s - sS[l], y = c / W, x = c - y * W;
-    const long bkb = (long)b * S;
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+__device__ __forceinline__ void gather_walk(const int *__restrict__ off, const float4 *__restrict__ rec,
+                                            const float *__restrict__ gout, int b, int m, int M, int D, int Q,
+                                            long bkb, int s0l, int H, int W, int y, int x, int lane, int part,
+                                            int parts, float4 &acc) {
+    int eb[4], ee[4];  // the bounds of all four buckets in one round trip
 #pragma unroll
-    for (int nb = 0; nb < 4; ++nb) {  // buckets of cells (y, x), (y, x-1), (y-1, x), (y-1, x-1)
+    for (int nb = 0; nb < 4; ++nb) {
         const int by = y - (nb >> 1), bx = x - (nb & 1);
-        if (by < 0 || bx < 0) continue;  // uniform over the group
-        const long bk = (bkb + sS[l] + by * W + bx) * M + m;
-        const int e0 = off[bk], e1 = off[bk + 1];
-        for (int e = e0; e < e1; e += V) {
+        eb[nb] = ee[nb] = 0;
+        if (by >= 0 && bx >= 0) {  // uniform over the group
+            const long bk = (bkb + s0l + by * W + bx) * M + m;
+            eb[nb] = off[bk];
+            ee[nb] = off[bk + 1];
+        }
+    }
+    const int step = parts * V;
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb) {
+        const int e1 = ee[nb];
+        const int e0 = eb[nb] + part * V;
+        float4 rn = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (e0 + lane < e1) rn = rec[e0 + lane];
+        for (int e = e0; e < e1; e += step) {
             // lane j takes entry e + j: its sample's corner weight for this cell and its attention weight
+            const float4 r = rn;
+            if (e + step + lane < e1) rn = rec[e + step + lane];  // (query, attention weight, x, y)
             float wc = 0.f, a = 0.f;
             int q = 0;
             if (e + lane < e1) {
-                const float4 r = rec[e + lane];  // (query, attention weight, x, y), bucket-contiguous
                 const Samp<float> sp = locate(r.z, r.w, H, W);
                 const int dy = y - sp.y0, dx = x - sp.x0;
                 if ((unsigned)dy <= 1u && (unsigned)dx <= 1u)
@@ -568,8 +575,8 @@ __global__ void __launch_bounds__(256) msda_gather_gvalue(const int64_t *__restr
                 a = r.y;
                 q = __float_as_int(r.x);
             }
-            // chunks of up to 8 entries: every grad_out row load of the chunk is issued before the first
-            // accumulation (lanes past the bucket end and non-corner entries carry w = 0 and load nothing)
+            // every grad_out row load of the chunk is issued before the first accumulation (lanes past
+            // the bucket end and non-corner entries carry w = 0 and load nothing)
             constexpr int KC = V < 8 ? V : 8;
 #pragma unroll
             for (int k0 = 0; k0 < V; k0 += KC) {
@@ -596,7 +603,82 @@ __global__ void __launch_bounds__(256) msda_gather_gvalue(const int64_t *__restr
             }
         }
     }
+}
+
+// grad_value rows: V lanes (4 channels each) per (b, s, m) cell
+template <int V>
+__global__ void __launch_bounds__(256) msda_gather_gvalue(const int64_t *__restrict__ shapes,
+                                                          const int64_t *__restrict__ lsi, const float *__restrict__ loc,
+                                                          const float *__restrict__ aw, const float *__restrict__ gout,
+                                                          int bs, int S, int M, int D, int L, int Q, int P,
+                                                          const int *__restrict__ off, const float4 *__restrict__ rec,
+                                                          float *__restrict__ gvalue) {
+    __shared__ int sH[kMaxLevels], sW[kMaxLevels], sS[kMaxLevels];
+    load_levels(shapes, lsi, L, sH, sW, sS);
+    // neighbouring cells share samples (a sample feeds 4 cells) and their grad_out rows: consecutive
+    // cells of one head on one XCD (map_group) so those rows are L2 hits
+    const GroupMap gm = map_group<V>((long)bs * S, M);
+    const int lane = threadIdx.x % V;
+    if (!gm.valid) return;  // whole group exits together
+    const int m = gm.m;
+    const long gid = gm.row * M + m;  // = (b * S + s) * M + m
+    const int s = (int)(gm.row % S);
+    const int b = (int)(gm.row / S);
+    const int l = level_of(s, sS, L);
+    const int H = sH[l], W = sW[l];
+    const int c = s - sS[l], y = c / W, x = c - y * W;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (split_parts(Q, P, H, W) == 1)  // uniform over the group; split levels: zeros, msda_gather_split adds
+        gather_walk<V>(off, rec, gout, b, m, M, D, Q, (long)b * S, sS[l], H, W, y, x, lane, 0, 1, acc);
     *(float4 *)(gvalue + gid * D + 4 * lane) = acc;
+}
+
+// The cells of split levels: item = (level, b, m, cell, part) over the levels with split_parts > 1
+// in order, grid-strided over V-lane groups; one group per item adds its partial row into grad_value
+// (zeroed there by msda_gather_gvalue) with float atomics.  The summation order is the atomics',
+// as the bucket order within a cell already is the fill's.
+template <int V>
+__global__ void __launch_bounds__(256) msda_gather_split(const int64_t *__restrict__ shapes,
+                                                         const int64_t *__restrict__ lsi,
+                                                         const float *__restrict__ gout, int bs, int S, int M,
+                                                         int D, int L, int Q, int P, const int *__restrict__ off,
+                                                         const float4 *__restrict__ rec, float *__restrict__ gvalue) {
+    __shared__ int sH[kMaxLevels], sW[kMaxLevels], sS[kMaxLevels];
+    __shared__ long first[kMaxLevels + 1];  // item offset of each level (no items for unsplit levels)
+    load_levels(shapes, lsi, L, sH, sW, sS);
+    if (threadIdx.x == 0) {
+        first[0] = 0;
+        for (int l = 0; l < L; ++l) {
+            const int pl = split_parts(Q, P, sH[l], sW[l]);
+            first[l + 1] = first[l] + (pl > 1 ? (long)sH[l] * sW[l] * pl * M * bs : 0);
+        }
+    }
+    __syncthreads();
+    const int lane = threadIdx.x % V;
+    const long total = first[L];
+    const long groups = (long)gridDim.x * (256 / V);
+    // items of one cell and part are equal slices of work: a plain grid stride balances them (one
+    // shared work counter would serialise on its single address, ~90 increments per us)
+    for (long item = (long)blockIdx.x * (256 / V) + threadIdx.x / V; item < total; item += groups) {
+        int l = 0;
+        for (int k = 1; k < L; ++k) l = item >= first[k] ? k : l;
+        const int H = sH[l], W = sW[l], parts = split_parts(Q, P, H, W);
+        long r = item - first[l];
+        const int part = (int)(r % parts);
+        r /= parts;
+        const int c = (int)(r % ((long)H * W));
+        r /= (long)H * W;
+        const int m = (int)(r % M);
+        const int b = (int)(r / M);
+        const int y = c / W, x = c - y * W;
+        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+        gather_walk<V>(off, rec, gout, b, m, M, D, Q, (long)b * S, sS[l], H, W, y, x, lane, part, parts, acc);
+        float *dst = gvalue + (((long)b * S + sS[l] + c) * M + m) * D + 4 * lane;
+        atomicAdd(dst, acc.x);
+        atomicAdd(dst + 1, acc.y);
+        atomicAdd(dst + 2, acc.z);
+        atomicAdd(dst + 3, acc.w);
+    }
 }
 
 // grad_loc / grad_aw: the forward's 16-B gathers, V lanes per (b, q, m)
@@ -861,6 +943,8 @@ extern "C" int irads_msda_bwd_gather(const float *value, const int64_t *shapes, 
     case VV:                                                                                                       \
         msda_gather_gvalue<VV><<<gg, 256, 0, st>>>(shapes, level_start, loc, aw, grad_out, bs, S, M, D, L, Q, P,  \
                                                    ws.off, ws.rec, grad_value);                                    \
+        msda_gather_split<VV><<<2048, 256, 0, st>>>(shapes, level_start, grad_out, bs, S, M, D, L, Q, P, ws.off,   \
+                                                    ws.rec, grad_value);                                           \
         if ((long)bs * Q * M > 0)                                                                                  \
             msda_bwd_locaw_vec<VV><<<gq, 256, 0, st>>>(value, shapes, level_start, loc, aw, grad_out, bs, S, M, D, \
                                                        L, Q, P, grad_loc, grad_aw);                                \

@@ -281,7 +281,6 @@ __device__ __forceinline__ Chunk decode_chunk(const Geo &g, int cw) {
 // class bits of token t inside a boundary window: row / column in the second shift region
 __device__ __forceinline__ bool hi_row(const Geo &g, int t) { return t / WS >= WS - g.shift; }
 __device__ __forceinline__ bool hi_col(const Geo &g, int t) { return t % WS >= WS - g.shift; }
-__device__ __forceinline__ int tok_a(int t) { return 23 * (t / WS) + t % WS; }  // A(t) of the bias index
 
 // Window origin of one (image, window) work item, decoded once per workgroup (the runtime
 // divisions by nW / nWw are the expensive part); tok() is then divide-free per token.
@@ -308,34 +307,39 @@ struct WinOrigin {
 // consecutive keys of one window row (or one key and 4 consecutive queries) the 4 biases are 4
 // consecutive entries of a (reversed) 23x23 table, so each seed is ONE 16-B LDS read.
 //
-// Bias buffer per head (irads_winattn_bias_quads; one launch per (table version, scale)), fp32 and
-// divided by scale (the kernels multiply by c2 = scale·log2 e while staging: T·log2 e):
-//   [0, 4 QB): backward quads, a key's 4 consecutive queries of one window row:
-//       B[28 (dr + 11) + (dc + 11)][r] = T[(dr + 11) * 23 + (dc + r + 11)], dr = row(q) - row(k),
-//       dc = col(q0) - col(k); the row stride 28 (not 23) spreads the 16 lanes of each ds_read_b128
-//       group over the LDS bank slots; 0 outside the table.
-//   [4 QB, 4 QB + RT): the table REVERSED, R[e] = T[528 - e] (zero past 528).  A query's seed over 4
-//       consecutive keys k0 .. k0 + 3 is R[264 + A(k0) - A(q) + r], A(t) = 23 row(t) + col(t); the
-//       forward stages 4 copies shifted by 0..3 entries so that every such run is one aligned b128.
-constexpr int QF_STRIDE = 28;  // row stride of the (dr, dc) quad grid (23 x 28)
-constexpr int QB = 23 * QF_STRIDE;
-constexpr int RT = 544;
-constexpr int QH = 4 * QB + RT;  // floats per head
+// Bias buffer per head (irads_winattn_bias_quads; one launch per (table version, scale)): two grids
+// of 16-B quads, fp32 and divided by scale (the kernels multiply by c2 = scale·log2 e while staging,
+// giving T·log2 e).  A 4-token group always starts at column 0, 4 or 8 of a window row, so the
+// column offset dc lies in [-11, 8] and a grid is 23 rows of QF_STRIDE = 20 quads:
+//   [0, QB)   forward, a query's 4 consecutive keys k0 .. k0 + 3 of one window row:
+//             F[20 (dr + 11) + (dc + 11)][r] = T[(11 - dr) * 23 + (11 - dc - r)],
+//             dr = row(k0) - row(q), dc = col(k0) - col(q);
+//   [QB, 2QB) backward, a key's 4 consecutive queries q0 .. q0 + 3 of one window row:
+//             B[20 (dr + 11) + (dc + 11)][r] = T[(dr + 11) * 23 + (dc + r + 11)],
+//             dr = row(q0) - row(k), dc = col(q0) - col(k).
+// Row stride 20: the smallest grid on which the 16 lanes of each ds_read_b128 group spread over
+// the bank slots as well as any injective linear layout does (5.8 LDS cycles per read against 4
+// conflict-free, over all 81 (query tile, key tile) pairs; searched exhaustively with the lane
+// groups of MI355X_MICROARCH.md §LDS), in 7.4 KB per grid.
+constexpr int QF_STRIDE = 20;
+constexpr int QB = 23 * QF_STRIDE;  // quads per grid
+constexpr int QH = 8 * QB;          // floats per head (both grids)
 
 __global__ void winattn_bias_quads_kernel(const float *__restrict__ table, int nH, float inv_scale,
                                           float *__restrict__ quads) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nH * QH) return;
     const int h = i / QH, f = i % QH;
+    const bool fwd = f < 4 * QB;
+    const int e = (fwd ? f : f - 4 * QB) / 4, r = f % 4;
+    const int dr = e / QF_STRIDE - 11, dc = e % QF_STRIDE - 11;
     int idx;
-    if (f < 4 * QB) {
-        const int e = f / 4, r = f % 4;
-        const int dr = e / QF_STRIDE - 11, dc = e % QF_STRIDE - 11;
-        const int tc = dc + r + 11;
-        idx = (dc <= 11 && tc >= 0 && tc < 23) ? (dr + 11) * 23 + tc : -1;
+    if (fwd) {
+        const int tc = 11 - dc - r;
+        idx = (tc >= 0 && tc < 23) ? (11 - dr) * 23 + tc : -1;
     } else {
-        const int e = f - 4 * QB;
-        idx = e < TBL ? TBL - 1 - e : -1;
+        const int tc = dc + r + 11;
+        idx = (tc >= 0 && tc < 23) ? (dr + 11) * 23 + tc : -1;
     }
     quads[i] = (idx >= 0 && idx < TBL) ? table[idx * nH + h] * inv_scale : 0.f;
 }
@@ -395,27 +399,25 @@ __device__ __forceinline__ u16x8 scale_frag(u16x8 v, float c) {
 }
 
 // Forward, one workgroup per (window, head): 3 waves, wave w owns query tiles 3w..3w+2.  All global
-// loads of the workgroup are issued up front and retire behind one wait; 27 KB of LDS and <= 96
+// loads of the workgroup are issued up front and retire behind one wait; 25 KB of LDS and <= 96
 // VGPRs let 6 workgroups share a CU, so one workgroup's load latency is covered by the others'
-// MFMA / softmax work.  The seeds come from 4 shifted copies of the reversed table (one aligned
-// ds_read_b128 per 4 keys).  Scores are formed directly in base-2 units: q is pre-multiplied by
-// c2 = scale·log2 e when it is loaded (one bf16 rounding of q·c2, where the reference's AMP rounds
-// q·scale, swin.py:95) and the table by log2 e, so s'' = q''·k + T·log2 e and P = 2^s'' needs no
-// scaling fma per score.  The row maximum is still formed; only a wave holding a row whose maximum
-// lies outside [-60, 60] (where 2^s'' could overflow, or lose precision to underflow) shifts its
-// scores, by one more MFMA per key tile that adds 32·bf16(-max/32) to every score of the row
-// (exact, so the LSE records the shift that was applied).
+// MFMA / softmax work.  Each 4-key seed is one ds_read_b128 of the head's stride-20 quad grid.
+// Scores are formed directly in base-2 units: q is pre-multiplied by c2 = scale·log2 e when it is
+// loaded (one bf16 rounding of q·c2, where the reference's AMP rounds q·scale, swin.py:95) and the
+// table by log2 e, so s'' = q''·k + T·log2 e and P = 2^s'' needs no scaling fma per score.  The
+// row maximum is still formed; only a wave holding a row whose maximum lies outside [-60, 60]
+// (where 2^s'' could overflow, or lose precision to underflow) shifts its scores, by one more MFMA
+// per key tile that adds 32·bf16(-max/32) to every score of the row (exact, so the LSE records the
+// shift that was applied).
 template <int MM>
-__global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(5))) winattn_fwd_bf16_rt(const unsigned short *__restrict__ qkv,
+__global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(MM == 2 ? 4 : 5))) winattn_fwd_bf16_rt(const unsigned short *__restrict__ qkv,
                                                             const float *__restrict__ qbias,
                                                             const float *__restrict__ quads,
                                                             const float *__restrict__ mask, Geo g, float c2,
                                                             unsigned short *__restrict__ out, float *__restrict__ lse) {
     __shared__ __attribute__((aligned(16))) unsigned short Ks[NT * HD];  // swizzled 64-B rows (kv_swz)
     __shared__ __attribute__((aligned(16))) unsigned short Vs[NT * HD];
-    // reversed table of this head x log2 e in 4 copies, copy c at c·RT holding R[e + c], so that any 4
-    // consecutive entries are one 16-B aligned ds_read_b128 (8.5 KB instead of the 10 KB quad grid)
-    __shared__ __attribute__((aligned(16))) float Rs[4 * RT];
+    __shared__ __attribute__((aligned(16))) f32x4 Bq[QB];  // forward quads of this head x c2
     const int lid = xcd_remap(blockIdx.x, gridDim.x);      // the heads of one window on one XCD
     const int h = lid % g.nH, bw = lid / g.nH;
     const WinOrigin wo(g, bw);
@@ -436,8 +438,10 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(5))) w
         kreg[j] = *(const u16x8 *)(base + off + cb);
         vreg[j] = *(const u16x8 *)(base + off + 2 * cb);
     }
-    f32x4 rt = {0.f, 0.f, 0.f, 0.f};
-    if (tid < RT / 4) rt = ((const f32x4 *)(quads + (long)h * QH + 4 * QB))[tid];
+    f32x4 bq[3];  // QB = 460 <= 3 x 192 quads
+    const f32x4 *qsrc = (const f32x4 *)(quads + (long)h * QH);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) bq[j] = (tid + 192 * j < QB) ? qsrc[tid + 192 * j] : f32x4{0.f, 0.f, 0.f, 0.f};
     if (wave_any(tok[0] < 0 || tok[1] < 0 || tok[2] < 0)) {  // uniform: only waves holding pad tokens
         const int c0 = h * HD + grp * 8;
         const u16x8 qp = pad_frag(qbias, c0), kp = pad_frag(qbias, g.C + c0), vp = pad_frag(qbias, 2 * g.C + c0);
@@ -456,21 +460,15 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(5))) w
         *(u16x8 *)(Ks + t * HD + (grp ^ swz_l) * 8) = kreg[j];
         *(u16x8 *)(Vs + t * HD + (grp ^ swz_l) * 8) = vreg[j];
     }
-    if (tid < RT / 4) {
-        rt = rt * c2;  // T / scale -> T·log2 e
-        ((f32x4 *)Rs)[tid] = rt;
 #pragma unroll
-        for (int c = 1; c < 4; ++c)
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (4 * tid + k - c >= 0) Rs[c * RT + 4 * tid + k - c] = rt[k];  // copy c: R[e + c]
-    }
+    for (int j = 0; j < 3; ++j)
+        if (tid + 192 * j < QB) Bq[tid + 192 * j] = bq[j] * c2;  // T / scale -> T·log2 e
 #pragma unroll
     for (int j = 0; j < 3; ++j) qreg[j] = scale_frag(qreg[j], c2);
     __syncthreads();
-    int part3[3];  // A(16 j + 4 grp); key group of tile 3a + j: part3[j] + 92 a
+    int part3[3];  // quad offset 20 row + col of key group 16 j + 4 grp; tile 3a + j adds 80 a
 #pragma unroll
-    for (int j = 0; j < 3; ++j) part3[j] = tok_a(16 * j + 4 * grp);
+    for (int j = 0; j < 3; ++j) part3[j] = QF_STRIDE * ((16 * j + 4 * grp) / WS) + (16 * j + 4 * grp) % WS;
     unsigned long long hbits = 0, wbits = 0;
     if (MM == 1) key_class_bits(g.shift, grp, hbits, wbits);
     bool lastH = false, lastW = false;
@@ -492,18 +490,12 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(5))) w
     for (int j = 0; j < 3; ++j) {
         const int qi = (3 * wave + j) * 16 + l16;
         const bf16x8_t qf = as_bf(qreg[j]);
-        // seed of keys k0 .. k0 + 3: R[264 + A(k0) - A(qi) + r], from the copy where it starts 16-B aligned
-        const float *rq[3];
-#pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            const int e = 264 - tok_a(qi) + part3[a];
-            rq[a] = Rs + (e & 3) * (RT - 1) + e;
-        }
+        // seed of keys k0 .. k0 + 3: quad 20 (row(k0) - row(qi) + 11) + (col(k0) - col(qi) + 11)
+        const f32x4 *bqq = Bq + (QF_STRIDE * 11 + 11 - (QF_STRIDE * (qi / WS) + qi % WS));
         f32x4 s[9];
 #pragma unroll
         for (int kt = 0; kt < 9; ++kt) {
-            const float *rb = rq[kt % 3] + 92 * (kt / 3);
-            const f32x4 b4 = *(const f32x4 *)rb;
+            const f32x4 b4 = bqq[part3[kt % 3] + 4 * QF_STRIDE * (kt / 3)];
             const bf16x8_t kf = as_bf(*(const u16x8 *)(kb + kt * 16 * HD));
             s[kt] = mfma16(kf, qf, b4);  // s''ᵀ (key rows, query on the lane), bias seeded
             if (MM == 2) {
@@ -594,7 +586,7 @@ __global__ void __launch_bounds__(576) winattn_bwd_bf16(
     const float *__restrict__ lse,
     const unsigned short *__restrict__ gout, unsigned short *__restrict__ gqkv, float *__restrict__ gtable,
     float *__restrict__ gbias) {
-    __shared__ __attribute__((aligned(16))) f32x4 Bf[QB];  // backward quads (stride-28 grid) of this head
+    __shared__ __attribute__((aligned(16))) f32x4 Bf[QB];  // backward quads (stride-20 grid) of this head
     __shared__ __attribute__((aligned(16))) unsigned short Qs[NT * HD];
     __shared__ __attribute__((aligned(16))) unsigned short dOs[NT * HD];
     __shared__ __attribute__((aligned(16))) unsigned short Ks[NT * HD];
@@ -610,12 +602,8 @@ __global__ void __launch_bounds__(576) winattn_bwd_bf16(
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int l16 = lane & 15, grp = lane >> 4;
     {  // the head's backward quads (16-B loads, both issued before either store)
-        const f32x4 *src = (const f32x4 *)(quads + (long)h * QH);
-        const f32x4 b0 = src[tid];
-        f32x4 b1 = {0.f, 0.f, 0.f, 0.f};
-        if (tid < QB - 576) b1 = src[576 + tid];
-        Bf[tid] = b0 * c2;  // T / scale -> T·log2 e: scores in base-2 units s'' (see winattn_fwd_bf16_rt)
-        if (tid < QB - 576) Bf[576 + tid] = b1 * c2;
+        const f32x4 *src = (const f32x4 *)(quads + (long)h * QH) + QB;
+        if (tid < QB) Bf[tid] = src[tid] * c2;  // T / scale -> T·log2 e: scores in base-2 units s''
     }
     for (int i = tid; i < (NR - NT) * DST; i += 576) dSt[NT * DST + i] = 0;
     if (EX)

@@ -760,10 +760,13 @@ class CrossEntropyFn(torch.autograd.Function):
         ctx.cfg = (code, B, C, H, W, int(ignore_index))
         if match is not None:
             ctx.mark_non_differentiable(match)
+        ctx.set_materialize_grads(False)  # no zero-filled int64 "gradient" of the MMST target
         return (loss[0], match) if want_match else loss[0]
 
     @staticmethod
     def backward(ctx, gloss, *_):
+        if gloss is None:
+            return None, None, None, None, None
         logits, target, w, lse, loss = ctx.saved_tensors
         code, B, C, H, W, ignore = ctx.cfg
         _, ls = _layout(logits)

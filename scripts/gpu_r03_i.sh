@@ -8,3 +8,4 @@ IRADS_PMC_KIND=bwd bash scripts/pmc_winattn_kind.sh r03 || exit $?
 bash scripts/gpu_msda_iter.sh || exit $?
 timeout -k 10 400 python bench.py --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/bench_r03i.log 2>&1 || { tail -3 gpurun_out/bench_r03i.log; exit 1; }
 tail -1 gpurun_out/bench_r03i.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'], json.dumps(d['roofline'])[:600], json.dumps(d['roofline_bwd']), json.dumps(d['kernels']['msda_bwd_encoder'])[:300])"
+bash scripts/gpu_r03_j.sh

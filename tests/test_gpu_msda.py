@@ -191,21 +191,26 @@ def test_fp32_vector_path_bitexact_vs_scalar_path(D):
     torch.testing.assert_close(vec.double(), ref, atol=1e-5, rtol=1e-5)
 
 
-@pytest.mark.parametrize("D", [4, 16, 32, 64, 256])
-def test_fp32_gather_backward_vs_scatter_and_fp64(D):
+@pytest.mark.parametrize("D,case", [(4, "edges"), (16, "edges"), (32, "edges"), (64, "edges"), (256, "edges"),
+                                    (32, "split"), (8, "split")])
+def test_fp32_gather_backward_vs_scatter_and_fp64(D, case):
     """The atomic-free fp32 backward (irads_msda_bwd_gather: samples bucketed by corner cell,
     grad_value gathered per cell and written once) against the atomic-scatter kernel on the same
     fp32 inputs and against the fp64 kernel (itself pinned to the reference above).  Locations
     cover every boundary case: corners at -1 and at W-1 / H-1 (one valid corner column / row),
     samples entirely outside (no contribution), a 1x1 level, value cells nothing samples
-    (their gradient rows must come out zero, not stale: grad_value is allocated uninitialised)."""
+    (their gradient rows must come out zero, not stale: grad_value is allocated uninitialised).
+    Case "split": coarse levels with hundreds of records per cell, summed by msda_gather_split
+    (several groups per cell, partial rows added with float atomics); in "edges" only the 1x1
+    level is split."""
     from irads import native as N
     ops = _ops()
     g = torch.Generator().manual_seed(100 + D)
-    lv = [(13, 17), (7, 9), (1, 1), (4, 5)]
+    lv = [(13, 17), (7, 9), (1, 1), (4, 5)] if case == "edges" else [(13, 17), (6, 5), (2, 3), (1, 1)]
     shapes = torch.as_tensor(lv, dtype=torch.long, device=DEV)
     lsi = torch.cat((shapes.new_zeros((1,)), shapes.prod(1).cumsum(0)[:-1]))
-    S, bs, M, Q, L, P = int(shapes.prod(1).sum()), 2, 3, 41, 4, 5
+    S, bs, M, L = int(shapes.prod(1).sum()), 2, 3, 4
+    Q, P = (41, 5) if case == "edges" else (200, 8)
     value = torch.randn(bs, S, M, D, generator=g).to(DEV)
     loc = torch.rand(bs, Q, M, L, P, 2, generator=g) * 1.3 - 0.15  # ~10 % of corners outside
     loc[:, :3] = torch.rand(bs, 3, M, L, P, 2, generator=g) * 0.02  # x0 / y0 = -1 (left / top edge)
@@ -228,13 +233,15 @@ def test_fp32_gather_backward_vs_scatter_and_fp64(D):
     assert torch.isfinite(gv).all()
     # grad_loc / grad_aw are D-channel fp32 dot products: absolute error grows with D
     ka = max(1.0, D / 32)
-    torch.testing.assert_close(gv, gv2, atol=2e-5, rtol=1e-5)
+    # split case: up to 6400 samples per cell, summed in fp32 in two different orders
+    va, vr = (2e-5, 1e-5) if case == "edges" else (1e-4, 1e-4)
+    torch.testing.assert_close(gv, gv2, atol=va, rtol=vr)
     torch.testing.assert_close(gl, gl2, atol=2e-4 * ka, rtol=1e-5)
     torch.testing.assert_close(ga, ga2, atol=2e-5 * ka, rtol=1e-5)
     v64, l64, a64 = (t.double().requires_grad_() for t in (value, loc, aw))
     o64 = ops.MSDAFn.apply(v64, shapes, lsi, l64, a64, 2)
     r = torch.autograd.grad((o64 * gout.double()).sum(), (v64, l64, a64))
-    torch.testing.assert_close(gv.double(), r[0], atol=2e-5, rtol=1e-5)
+    torch.testing.assert_close(gv.double(), r[0], atol=va, rtol=vr)
     torch.testing.assert_close(gl.double(), r[1], atol=2e-4 * ka, rtol=1e-5)
     torch.testing.assert_close(ga.double(), r[2], atol=2e-5 * ka, rtol=1e-5)
     # the 1x1 level's cell and the cells no sample reaches: exact zeros where fp64 says zero
