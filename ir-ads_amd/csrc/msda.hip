@@ -334,14 +334,20 @@ __device__ __forceinline__ int level_of(int s, const int *sS, int L) {
     return l;
 }
 
-// bucket of one sample, or -1 (no corner inside the level)
-__device__ __forceinline__ long sample_bucket(const float *loc, long sid, int l, const int *sH, const int *sW,
-                                              const int *sS, int b, int m, int M, int S) {
+// bucket of one sample at location (lx, ly) of level l, or -1 (no corner inside the level)
+__device__ __forceinline__ long bucket_at(float lx, float ly, int l, const int *sH, const int *sW, const int *sS,
+                                          int b, int m, int M, int S) {
     const int H = sH[l], W = sW[l];
-    const Samp<float> sp = locate(loc[2 * sid], loc[2 * sid + 1], H, W);
+    const Samp<float> sp = locate(lx, ly, H, W);
     if (sp.x0 < -1 || sp.x0 >= W || sp.y0 < -1 || sp.y0 >= H) return -1;
     const int x = max(sp.x0, 0), y = max(sp.y0, 0);
-    return ((long)b * S + sS[l] + y * W + x) * M + m;  // cell-major: a cell's M head counters share a line
+    // head-major: the buckets of one row of cells are consecutive, so a cell's left and upper-left
+    // neighbours' buckets form one contiguous record range with its own (gather_walk)
+    return ((long)b * M + m) * S + sS[l] + y * W + x;
+}
+__device__ __forceinline__ long sample_bucket(const float *loc, long sid, int l, const int *sH, const int *sW,
+                                              const int *sS, int b, int m, int M, int S) {
+    return bucket_at(loc[2 * sid], loc[2 * sid + 1], l, sH, sW, sS, b, m, M, S);
 }
 
 __device__ __forceinline__ void load_levels(const int64_t *shapes, const int64_t *lsi, int L, int *sH, int *sW,
@@ -506,8 +512,10 @@ __global__ void __launch_bounds__(256) msda_bucket_fill(const float *__restrict_
             r[k] = make_float4(__int_as_float(q), aw[sid], loc[2 * sid], loc[2 * sid + 1]);
         }
     }
-    int slot[kSPT];
+    int slot[kSPT], base[kSPT];
     QuadAgg ag[kSPT];
+#pragma unroll
+    for (int k = 0; k < kSPT; ++k) base[k] = bk[k] >= 0 ? off[bk[k]] : 0;  // in flight beside the atomics
 #pragma unroll
     for (int k = 0; k < kSPT; ++k) {
         ag[k] = quad_agg((int)bk[k]);
@@ -522,7 +530,31 @@ __global__ void __launch_bounds__(256) msda_bucket_fill(const float *__restrict_
     }
 #pragma unroll
     for (int k = 0; k < kSPT; ++k)
-        if (bk[k] >= 0) rec[off[bk[k]] + slot[k]] = r[k];
+        if (bk[k] >= 0) rec[base[k] + slot[k]] = r[k];
+}
+
+// The fill when the grad_loc / grad_aw pass already ranked every sample in its bucket: a streaming
+// pass (location, rank, bucket offset -> one 16-B record), no atomics.  16 lanes per (b, q, m),
+// placed as map_group does, so with M % 8 == 0 XCD x writes only the record ranges of heads x, x + 8, ...
+__global__ void __launch_bounds__(256) msda_bucket_fill_ranked(const float *__restrict__ loc,
+                                                               const int64_t *__restrict__ shapes,
+                                                               const int64_t *__restrict__ lsi, int bs, int S, int M,
+                                                               int L, int Q, int P, const float *__restrict__ aw,
+                                                               const int *__restrict__ off,
+                                                               const int *__restrict__ rank, float4 *__restrict__ rec) {
+    __shared__ int sH[kMaxLevels], sW[kMaxLevels], sS[kMaxLevels];
+    load_levels(shapes, lsi, L, sH, sW, sS);
+    const GroupMap gm = map_group<16>((long)bs * Q, M);
+    if (!gm.valid) return;
+    const int m = gm.m, b = (int)(gm.row / Q), q = (int)(gm.row % Q);
+    const int LP = L * P;
+    const long sid0 = (gm.row * M + m) * LP;
+    for (int sl = threadIdx.x % 16; sl < LP; sl += 16) {
+        const long sid = sid0 + sl;
+        const float lx = loc[2 * sid], ly = loc[2 * sid + 1];
+        const long bk = bucket_at(lx, ly, sl / P, sH, sW, sS, b, m, M, S);
+        if (bk >= 0) rec[off[bk] + rank[sid]] = make_float4(__int_as_float(q), aw[sid], lx, ly);
+    }
 }
 
 // A coarse level's cell is a corner of hundreds of samples (DINO encoder: ~330 records over a level-2
@@ -535,28 +567,30 @@ __device__ __forceinline__ int split_parts(int Q, int P, int H, int W) {
     return rec4 > 128 ? (int)min(32L, (rec4 + 63) / 64) : 1;
 }
 
-// One group's walk over a cell's 4 buckets (cells (y, x), (y, x-1), (y-1, x), (y-1, x-1)): chunks
-// part, part + parts, ... of V records each, accumulated into acc (4 channels per lane).  Records
-// are loaded one chunk ahead, so a chunk's grad_out row loads wait only on their own records.
-template <int V>
+// One group's walk over a cell's 4 buckets (cells (y, x), (y, x-1), (y-1, x), (y-1, x-1)) as two
+// contiguous record ranges (buckets (y', x-1) and (y', x) are neighbours in the head-major order):
+// chunks part, part + parts, ... of V records each, accumulated into acc (4 channels per lane).
+// Records are loaded one chunk ahead, so a chunk's grad_out row loads wait only on their own records.
+// bkrow = bucket of cell 0 of this (b, m, level).
+template <int V, int KCM = 4>
 __device__ __forceinline__ void gather_walk(const int *__restrict__ off, const float4 *__restrict__ rec,
                                             const float *__restrict__ gout, int b, int m, int M, int D, int Q,
-                                            long bkb, int s0l, int H, int W, int y, int x, int lane, int part,
+                                            long bkrow, int H, int W, int y, int x, int lane, int part,
                                             int parts, float4 &acc) {
-    int eb[4], ee[4];  // the bounds of all four buckets in one round trip
+    int eb[2], ee[2];  // the bounds of both ranges in one round trip
 #pragma unroll
-    for (int nb = 0; nb < 4; ++nb) {
-        const int by = y - (nb >> 1), bx = x - (nb & 1);
+    for (int nb = 0; nb < 2; ++nb) {
+        const int by = y - nb;
         eb[nb] = ee[nb] = 0;
-        if (by >= 0 && bx >= 0) {  // uniform over the group
-            const long bk = (bkb + s0l + by * W + bx) * M + m;
-            eb[nb] = off[bk];
+        if (by >= 0) {  // uniform over the group
+            const long bk = bkrow + by * W + x;
+            eb[nb] = off[x > 0 ? bk - 1 : bk];
             ee[nb] = off[bk + 1];
         }
     }
     const int step = parts * V;
 #pragma unroll
-    for (int nb = 0; nb < 4; ++nb) {
+    for (int nb = 0; nb < 2; ++nb) {
         const int e1 = ee[nb];
         const int e0 = eb[nb] + part * V;
         float4 rn = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -577,9 +611,10 @@ __device__ __forceinline__ void gather_walk(const int *__restrict__ off, const f
             }
             // every grad_out row load of the chunk is issued before the first accumulation (lanes past
             // the bucket end and non-corner entries carry w = 0 and load nothing)
-            constexpr int KC = V < 8 ? V : 8;
+            constexpr int KC = V < KCM ? V : KCM;
 #pragma unroll
             for (int k0 = 0; k0 < V; k0 += KC) {
+                if (k0 > 0 && e + k0 >= e1) continue;  // uniform: past the range end
                 float w[KC], ak[KC];
                 float4 go[KC];
 #pragma unroll
@@ -599,7 +634,6 @@ __device__ __forceinline__ void gather_walk(const int *__restrict__ off, const f
                     acc.z += w[k] * (go[k].z * ak[k]);
                     acc.w += w[k] * (go[k].w * ak[k]);
                 }
-                if (e + k0 + KC >= e1) break;  // uniform
             }
         }
     }
@@ -629,66 +663,115 @@ __global__ void __launch_bounds__(256) msda_gather_gvalue(const int64_t *__restr
     const int c = s - sS[l], y = c / W, x = c - y * W;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     if (split_parts(Q, P, H, W) == 1)  // uniform over the group; split levels: zeros, msda_gather_split adds
-        gather_walk<V>(off, rec, gout, b, m, M, D, Q, (long)b * S, sS[l], H, W, y, x, lane, 0, 1, acc);
+        gather_walk<V>(off, rec, gout, b, m, M, D, Q, ((long)b * M + m) * S + sS[l], H, W, y, x, lane, 0, 1, acc);
     *(float4 *)(gvalue + gid * D + 4 * lane) = acc;
 }
 
-// The cells of split levels: item = (level, b, m, cell, part) over the levels with split_parts > 1
-// in order, grid-strided over V-lane groups; one group per item adds its partial row into grad_value
-// (zeroed there by msda_gather_gvalue) with float atomics.  The summation order is the atomics',
-// as the bucket order within a cell already is the fill's.
+// The cells of split levels: per head, item = (level, b, cell, part) over the levels with
+// split_parts > 1 in order.  With M % 8 == 0 the blocks of XCD x take the items of heads x, x + 8, ...
+// (as map_group: that XCD's L2 then serves one head's grad_out rows); otherwise one grid stride over
+// (head, item).  Each block takes 256 / V consecutive items per round, one V-lane group each, so the
+// parts of one cell mostly share a block: their partial rows are summed in LDS and the first group of
+// each cell run adds the sum into grad_value (zeroed there by msda_gather_gvalue) with float atomics,
+// one atomic row per (cell, block) instead of one per part.  The summation order is the atomics', as
+// the bucket order within a cell already is the fill's.
+template <int V>
+__device__ __forceinline__ void split_round(bool valid, int m, long it, const long *first, const int *sH,
+                                            const int *sW, const int *sS, int L, int S, int M, int D, int Q, int P,
+                                            const int *__restrict__ off, const float4 *__restrict__ rec,
+                                            const float *__restrict__ gout, float *__restrict__ gvalue,
+                                            long *cell_of, float4 (*part_row)[V]) {
+    constexpr int GPB = 256 / V;
+    const int lane = threadIdx.x % V, gi = threadIdx.x / V;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    long row = -1;
+    if (valid) {
+        int l = 0;
+        for (int k = 1; k < L; ++k) l = it >= first[k] ? k : l;
+        const int H = sH[l], W = sW[l], parts = split_parts(Q, P, H, W);
+        long r = it - first[l];
+        const int part = (int)(r % parts);
+        r /= parts;
+        const int c = (int)(r % ((long)H * W));
+        const int b = (int)(r / ((long)H * W));
+        const int y = c / W, x = c - y * W;
+        gather_walk<V>(off, rec, gout, b, m, M, D, Q, ((long)b * M + m) * S + sS[l], H, W, y, x, lane, part, parts,
+                       acc);
+        row = (((long)b * S + sS[l] + c) * M + m) * D;
+    }
+    part_row[gi][lane] = acc;
+    if (lane == 0) cell_of[gi] = row;
+    __syncthreads();
+    if (row >= 0 && (gi == 0 || cell_of[gi - 1] != row)) {  // first group of its cell's run
+        for (int g2 = gi + 1; g2 < GPB && cell_of[g2] == row; ++g2) {
+            const float4 o = part_row[g2][lane];
+            acc.x += o.x;
+            acc.y += o.y;
+            acc.z += o.z;
+            acc.w += o.w;
+        }
+        float *dst = gvalue + row + 4 * lane;
+        atomicAdd(dst, acc.x);
+        atomicAdd(dst + 1, acc.y);
+        atomicAdd(dst + 2, acc.z);
+        atomicAdd(dst + 3, acc.w);
+    }
+    __syncthreads();
+}
+
 template <int V>
 __global__ void __launch_bounds__(256) msda_gather_split(const int64_t *__restrict__ shapes,
                                                          const int64_t *__restrict__ lsi,
                                                          const float *__restrict__ gout, int bs, int S, int M,
                                                          int D, int L, int Q, int P, const int *__restrict__ off,
                                                          const float4 *__restrict__ rec, float *__restrict__ gvalue) {
+    constexpr int GPB = 256 / V;
     __shared__ int sH[kMaxLevels], sW[kMaxLevels], sS[kMaxLevels];
-    __shared__ long first[kMaxLevels + 1];  // item offset of each level (no items for unsplit levels)
+    __shared__ long first[kMaxLevels + 1];  // item offset of each level within a head (unsplit levels: none)
+    __shared__ long cell_of[GPB];           // grad_value row offset of each group's item (-1: none)
+    __shared__ float4 part_row[GPB][V];
     load_levels(shapes, lsi, L, sH, sW, sS);
     if (threadIdx.x == 0) {
         first[0] = 0;
         for (int l = 0; l < L; ++l) {
             const int pl = split_parts(Q, P, sH[l], sW[l]);
-            first[l + 1] = first[l] + (pl > 1 ? (long)sH[l] * sW[l] * pl * M * bs : 0);
+            first[l + 1] = first[l] + (pl > 1 ? (long)sH[l] * sW[l] * pl * bs : 0);
         }
     }
     __syncthreads();
-    const int lane = threadIdx.x % V;
-    const long total = first[L];
-    const long groups = (long)gridDim.x * (256 / V);
-    // items of one cell and part are equal slices of work: a plain grid stride balances them (one
-    // shared work counter would serialise on its single address, ~90 increments per us)
-    for (long item = (long)blockIdx.x * (256 / V) + threadIdx.x / V; item < total; item += groups) {
-        int l = 0;
-        for (int k = 1; k < L; ++k) l = item >= first[k] ? k : l;
-        const int H = sH[l], W = sW[l], parts = split_parts(Q, P, H, W);
-        long r = item - first[l];
-        const int part = (int)(r % parts);
-        r /= parts;
-        const int c = (int)(r % ((long)H * W));
-        r /= (long)H * W;
-        const int m = (int)(r % M);
-        const int b = (int)(r / M);
-        const int y = c / W, x = c - y * W;
-        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-        gather_walk<V>(off, rec, gout, b, m, M, D, Q, (long)b * S, sS[l], H, W, y, x, lane, part, parts, acc);
-        float *dst = gvalue + (((long)b * S + sS[l] + c) * M + m) * D + 4 * lane;
-        atomicAdd(dst, acc.x);
-        atomicAdd(dst + 1, acc.y);
-        atomicAdd(dst + 2, acc.z);
-        atomicAdd(dst + 3, acc.w);
+    const long per_head = first[L];
+    const int gi = threadIdx.x / V;
+    if (M % 8 == 0 && gridDim.x % 8 == 0) {  // loops uniform per block
+        const long jx = blockIdx.x / 8, gx = gridDim.x / 8;
+        for (int m = (int)(blockIdx.x % 8); m < M; m += 8)
+            for (long base = jx * GPB; base < per_head; base += gx * GPB)
+                split_round<V>(base + gi < per_head, m, base + gi, first, sH, sW, sS, L, S, M, D, Q, P, off, rec, gout,
+                               gvalue, cell_of, part_row);
+    } else {
+        const long total = per_head * M;
+        for (long base = (long)blockIdx.x * GPB; base < total; base += (long)gridDim.x * GPB) {
+            const long item = base + gi;
+            const bool ok = item < total;
+            split_round<V>(ok, ok ? (int)(item / per_head) : 0, ok ? item % per_head : 0, first, sH, sW, sS, L, S, M,
+                           D, Q, P, off, rec, gout, gvalue, cell_of, part_row);
+        }
     }
 }
 
-// grad_loc / grad_aw: the forward's 16-B gathers, V lanes per (b, q, m)
-template <int V>
+// grad_loc / grad_aw: the forward's 16-B gathers, V lanes per (b, q, m).  With COUNT (V % 4 == 0, so
+// a DPP quad never straddles two groups) the pass also makes the bucket counts of msda_bucket_count
+// from the locations it already holds, and keeps each sample's rank in its bucket (the counter's
+// value before its add, + its rank among the quad lanes of that bucket): the counter round trips
+// overlap the value gathers, and the fill pass after the scan needs no atomics at all.
+template <int V, bool COUNT>
 __global__ void __launch_bounds__(256) msda_bwd_locaw_vec(const float *__restrict__ value,
                                                           const int64_t *__restrict__ shapes,
                                                           const int64_t *__restrict__ lsi, const float *__restrict__ loc,
                                                           const float *__restrict__ aw, const float *__restrict__ gout,
                                                           int bs, int S, int M, int D, int L, int Q, int P,
-                                                          float *__restrict__ gloc, float *__restrict__ gaw) {
+                                                          float *__restrict__ gloc, float *__restrict__ gaw,
+                                                          int *__restrict__ cnt, int *__restrict__ rank) {
+    static_assert(!COUNT || V % 4 == 0, "bucket counting needs whole DPP quads per group");
     __shared__ int sH[kMaxLevels], sW[kMaxLevels], sS[kMaxLevels];
     load_levels(shapes, lsi, L, sH, sW, sS);
     const GroupMap gm = map_group<V>((long)bs * Q, M);
@@ -709,6 +792,14 @@ __global__ void __launch_bounds__(256) msda_bwd_locaw_vec(const float *__restric
             lx = loc[2 * li];
             ly = loc[2 * li + 1];
             w = aw[li];
+        }
+        long bk = -1;
+        QuadAgg qa{0, 0, 4};
+        int got = 0;
+        if constexpr (COUNT) {  // the counter add now, its value used after the gathers
+            bk = sl < LP ? bucket_at(lx, ly, sl / P, sH, sW, sS, b, m, M, S) : -1;
+            qa = quad_agg((int)bk);  // buckets < 2^31 (gather_ws_layout)
+            if (bk >= 0 && qa.first == (int)(threadIdx.x & 3)) got = atomicAdd(cnt + bk, qa.count);
         }
         float my_gaw = 0.f, my_gx = 0.f, my_gy = 0.f;
 #pragma unroll
@@ -758,11 +849,17 @@ __global__ void __launch_bounds__(256) msda_bwd_locaw_vec(const float *__restric
             gloc[2 * li] = my_gx;
             gloc[2 * li + 1] = my_gy;
         }
+        if constexpr (COUNT) {
+            const int b0 = quad_bcast<0>(got), b1 = quad_bcast<1>(got), b2 = quad_bcast<2>(got),
+                      b3 = quad_bcast<3>(got);
+            const int f = qa.first;
+            if (sl < LP) rank[gid * LP + sl] = (f == 0 ? b0 : f == 1 ? b1 : f == 2 ? b2 : b3) + qa.rank;
+        }
     }
 }
 
 struct GatherWs {
-    int *cnt, *off, *bsum, *total;
+    int *cnt, *off, *bsum, *total, *rank;
     float4 *rec;
     long nb, n, nblk;
 };
@@ -777,13 +874,15 @@ long gather_ws_layout(int bs, int S, int M, int D, int L, int Q, int P, char *ba
     if (nblk > 256L * 64) return 0;
     auto al = [](long b) { return (b + 255) / 256 * 256; };
     const long o_cnt = 0, o_off = o_cnt + al(4 * nb), o_bsum = o_off + al(4 * (nb + 1)),
-               o_tot = o_bsum + al(4 * nblk), o_rec = o_tot + 256, end = o_rec + al(16 * n);
+               o_tot = o_bsum + al(4 * nblk), o_rec = o_tot + 256, o_rank = o_rec + al(16 * n),
+               end = o_rank + al(4 * n);
     if (ws) {
         ws->cnt = (int *)(base + o_cnt);
         ws->off = (int *)(base + o_off);
         ws->bsum = (int *)(base + o_bsum);
         ws->total = (int *)(base + o_tot);
         ws->rec = (float4 *)(base + o_rec);
+        ws->rank = (int *)(base + o_rank);
         ws->nb = nb;
         ws->n = n;
         ws->nblk = nblk;
@@ -931,23 +1030,36 @@ extern "C" int irads_msda_bwd_gather(const float *value, const int64_t *shapes, 
     auto g1 = [](long n) { return dim3((unsigned)((n + 255) / 256)); };
     msda_zero_ints<<<g1(ws.nb), 256, 0, st>>>(ws.cnt, ws.nb);
     auto gs = [](long n) { return dim3((unsigned)((n + 256L * kSPT - 1) / (256L * kSPT))); };
-    if (ws.n > 0) msda_bucket_count<<<gs(ws.n), 256, 0, st>>>(loc, shapes, level_start, bs, S, M, L, Q, P, ws.cnt);
+    const dim3 gg = group_grid((long)bs * S, M, V), gq = group_grid((long)bs * Q, M, V);
+    // grad_loc / grad_aw first: for V % 4 == 0 that pass also counts the buckets
+#define IRADS_MSDA_LA(VV, CNT)                                                                                   \
+    case VV:                                                                                                     \
+        msda_bwd_locaw_vec<VV, CNT><<<gq, 256, 0, st>>>(value, shapes, level_start, loc, aw, grad_out, bs, S, M, \
+                                                        D, L, Q, P, grad_loc, grad_aw, ws.cnt, ws.rank);         \
+        break;
+    if (ws.n > 0) {
+        if (V % 4) msda_bucket_count<<<gs(ws.n), 256, 0, st>>>(loc, shapes, level_start, bs, S, M, L, Q, P, ws.cnt);
+        switch (V) {
+            IRADS_MSDA_LA(1, false) IRADS_MSDA_LA(2, false) IRADS_MSDA_LA(4, true) IRADS_MSDA_LA(8, true)
+            IRADS_MSDA_LA(16, true) IRADS_MSDA_LA(32, true) IRADS_MSDA_LA(64, true)
+        }
+    }
+#undef IRADS_MSDA_LA
     msda_scan_blocks<<<(unsigned)ws.nblk, 256, 0, st>>>(ws.cnt, ws.nb, ws.off, ws.bsum);
     msda_scan_totals<<<1, 256, 0, st>>>(ws.bsum, (int)ws.nblk, ws.total);
     msda_scan_add<<<g1(ws.nb), 256, 0, st>>>(ws.off, ws.nb, ws.bsum, ws.total, ws.cnt);
-    if (ws.n > 0)
+    if (ws.n > 0 && V % 4)
         msda_bucket_fill<<<gs(ws.n), 256, 0, st>>>(loc, shapes, level_start, bs, S, M, L, Q, P, aw, ws.off, ws.cnt,
                                                    ws.rec);
-    const dim3 gg = group_grid((long)bs * S, M, V), gq = group_grid((long)bs * Q, M, V);
+    else if (ws.n > 0)
+        msda_bucket_fill_ranked<<<group_grid((long)bs * Q, M, 16), 256, 0, st>>>(loc, shapes, level_start, bs, S, M,
+                                                                                 L, Q, P, aw, ws.off, ws.rank, ws.rec);
 #define IRADS_MSDA_G(VV)                                                                                           \
     case VV:                                                                                                       \
         msda_gather_gvalue<VV><<<gg, 256, 0, st>>>(shapes, level_start, loc, aw, grad_out, bs, S, M, D, L, Q, P,  \
                                                    ws.off, ws.rec, grad_value);                                    \
         msda_gather_split<VV><<<2048, 256, 0, st>>>(shapes, level_start, grad_out, bs, S, M, D, L, Q, P, ws.off,   \
                                                     ws.rec, grad_value);                                           \
-        if ((long)bs * Q * M > 0)                                                                                  \
-            msda_bwd_locaw_vec<VV><<<gq, 256, 0, st>>>(value, shapes, level_start, loc, aw, grad_out, bs, S, M, D, \
-                                                       L, Q, P, grad_loc, grad_aw);                                \
         break;
     switch (V) {
         IRADS_MSDA_G(1) IRADS_MSDA_G(2) IRADS_MSDA_G(4) IRADS_MSDA_G(8) IRADS_MSDA_G(16) IRADS_MSDA_G(32)

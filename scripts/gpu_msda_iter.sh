@@ -11,5 +11,18 @@ import csv, glob
 f = glob.glob("gpurun_out/pm/**/*kernel_stats.csv", recursive=True)[0]
 for r in sorted(csv.DictReader(open(f)), key=lambda r: -float(r["TotalDurationNs"]))[:6]:
     print(round(float(r["AverageNs"]) / 1e3, 1), r["Name"][:70])
+import collections
+t = glob.glob("gpurun_out/pm/**/*kernel_trace.csv", recursive=True)[0]
+agg = collections.defaultdict(list)
+for r in csv.DictReader(open(t)):
+    if "msda" in r["Kernel_Name"]:
+        agg[r["Kernel_Name"].replace("(anonymous namespace)::", "")[:48]].append(
+            (int(r["Start_Timestamp"]), (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3))
+# msda_bench runs the encoder shape first, then the decoder: first / second half of each kernel's calls
+for k, v in sorted(agg.items()):
+    v.sort()
+    h = len(v) // 2
+    enc, dec = [d for _, d in v[:h]], [d for _, d in v[h:]]
+    print("%-48s enc %.1f us  dec %.1f us  (n=%d)" % (k, sum(enc) / max(1, len(enc)), sum(dec) / max(1, len(dec)), len(v)))
 PY
 find gpurun_out/pm -name "*trace.csv" -delete

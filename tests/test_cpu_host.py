@@ -306,13 +306,15 @@ def test_reference_driver_import_surface():
 
 def test_msda_gather_workspace_query(lib):
     """irads_msda_bwd_workspace_bytes is a pure size query (no GPU work): counters (bs*M*S), their
-    exclusive scan and one 16-B record per sample; 0 where the gather backward does not apply."""
+    exclusive scan, one 16-B record and one int rank per sample; 0 where the gather backward does
+    not apply."""
     q = lib.irads_msda_bwd_workspace_bytes
     q.restype = ctypes.c_long
     bs, S, M, D, L, Q, P = 2, 22223, 8, 32, 4, 22223, 4
     n = q(0, bs, S, M, D, L, Q, P)
-    assert n >= 4 * (2 * bs * M * S) + 16 * bs * Q * M * L * P
-    assert n < 4 * (2 * bs * M * S) + 16 * bs * Q * M * L * P + 8192 + 4 * (bs * M * S // 1024 + 1)
+    need = 4 * (2 * bs * M * S) + (16 + 4) * bs * Q * M * L * P
+    assert n >= need
+    assert n < need + 8192 + 4 * (bs * M * S // 1024 + 1)
     assert q(2, bs, S, M, D, L, Q, P) == 0  # fp64: the scatter kernel
     assert q(0, bs, S, M, 30, L, Q, P) == 0  # D not 4 * 2^k
     assert q(0, bs, S, M, 24, L, Q, P) == 0
