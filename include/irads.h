@@ -420,6 +420,18 @@ long irads_bnact_partials(long M, int E);
 int irads_confusion_update(int dtype, const void *scores, const int64_t *strides, int B, int C, int H, int W,
                            const int64_t *target, int ignore_index, int64_t *hist, void *stream);
 
+/* The optimizer step of the training loop (reference semseg/optimizers.py:33-49: torch.optim.AdamW,
+ * betas (0.9, 0.999), eps 1e-8; replaces the multi-tensor launches of torch's fused AdamW): for
+ * each of the n fp32 tensors t (host arrays of device pointers, numel[t] elements each),
+ *   p -= lr*wd*p;  m = b1 m + (1-b1) g;  v = b2 v + (1-b2) g^2;
+ *   p -= (lr/bc1) m / (sqrt(v)/sqrt(bc2) + eps),   bc_i = 1 - b_i^step,
+ * with step[t] and lr[t] read on the device (fp32 scalars; the caller increments the steps
+ * first), so the launches are graph-capturable; 1 - beta_i is taken in double (as torch's
+ * 1 - 0.999 of the Python floats), then every element op in fp32.  40 tensors per launch. */
+int irads_adamw(int n, float *const *p, const float *const *g, float *const *m, float *const *v,
+                const float *const *step, const float *const *lr, const float *wd, const long *numel, double beta1,
+                double beta2, double eps, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

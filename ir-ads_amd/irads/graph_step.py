@@ -32,6 +32,7 @@ Data parallel (world > 1; train_mm.py:94 / DDP semantics: gradients averaged ove
     not captured).  Used with the gloo backend (CPU-side tests), which cannot be captured.
 """
 import os
+import time
 
 import torch
 import torch.distributed as dist
@@ -109,6 +110,14 @@ class GraphedTrainStep:
                 optimizer.step()
         torch.cuda.current_stream(dev).wait_stream(side)
         torch.cuda.synchronize(dev)
+        if self.comm != "none" and dist.is_initialized() and dist.get_backend() == "nccl":
+            # The warm-up's eager collectives stay on the process group's watchdog list until its
+            # next poll (one every 100 ms) sees them complete; their end events were recorded on
+            # the communicator stream that the capture below joins, and a poll of such an event
+            # while that stream is capturing fails (round-3 suite: WorkNCCL::isCompleted ->
+            # hipEventQuery error -> abort).  Everything is complete after the synchronize: give
+            # the watchdog three polls to retire it before the capture opens.
+            time.sleep(0.35)
         optimizer.zero_grad(set_to_none=True)
         if before_capture is not None:
             before_capture()

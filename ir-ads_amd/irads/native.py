@@ -71,6 +71,7 @@ SIGNATURES = {
     "irads_upsample_sum_fwd": [_i, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _vp, _vp],
     "irads_confusion_update": [_i, _vp, _vp, _i, _i, _i, _i, _vp, _i, _vp, _vp],
     "irads_wgrad": [_vp, _l, _vp, _l, _i, _i, _i, _f, _i, _i, _vp, _vp, _vp, _vp, _vp],
+    "irads_adamw": [_i] + [_vp] * 8 + [_d, _d, _d, _vp],
 }
 # entries that do not return an error code: name -> (restype, argtypes)
 QUERIES = {"irads_wgrad_workspace": (ctypes.c_long, [_i, _i, _i]),

@@ -2,7 +2,8 @@
 
 TRAIN_TYPE 'Adapter' trains only parameters whose name contains Adapter /
 extra_patch_embed / head / MPG (optimizers.py:7-30) and freezes the rest.  On GPU the
-AdamW update runs as PyTorch's fused multi-tensor kernel (one launch per step)."""
+AdamW update runs as irads_adamw (irads/optim.py: torch's AdamW object and state, capturable,
+the update in 40-tensor launches sized to the tensors)."""
 import torch
 from torch import nn
 from torch.optim import AdamW, SGD
@@ -44,5 +45,8 @@ def get_optimizer(model: nn.Module, optimizer: str, lr: float, train_type: str, 
                 dev = groups[0]["params"][0].device
                 lr = torch.tensor(float(lr), device=dev)
                 fused["capturable"] = True
+        if on_gpu:  # the update as irads_adamw launches (irads/optim.py): torch's AdamW object and state
+            from irads.optim import AdamW as NativeAdamW
+            return NativeAdamW(groups, lr, betas=(0.9, 0.999), eps=1e-8, weight_decay=weight_decay)
         return AdamW(groups, lr, betas=(0.9, 0.999), eps=1e-8, weight_decay=weight_decay, **fused)
     return SGD(groups, lr, momentum=0.9, weight_decay=weight_decay)

@@ -31,4 +31,5 @@ def test_graph_step_overlapped_exchange_capture():
         if p.poll() is None:  # our own child only
             p.kill()
             p.wait()
-    assert p.returncode == 0 and "OK rel" in out, (p.returncode, out[-3000:])
+    errs = [ln for ln in out.splitlines() if "error" in ln.lower() and "Traceback" not in ln][:8]
+    assert p.returncode == 0 and "OK rel" in out, (p.returncode, errs, out[-3000:])
