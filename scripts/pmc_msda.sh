@@ -8,15 +8,25 @@ for pass in "TCC_HIT_sum TCC_MISS_sum" "FETCH_SIZE" "SQ_WAVES SQ_WAVE_CYCLES SQ_
 done
 python3 - <<'PY'
 import csv, glob, collections
-agg = collections.defaultdict(lambda: collections.defaultdict(float)); cnt = collections.Counter()
+# per kernel: dispatches in order; msda_bench runs the encoder shape first, then the decoder
+disp = collections.defaultdict(lambda: collections.defaultdict(dict))
 for f in glob.glob("gpurun_out/pmc_msda_*/**/*counter_collection.csv", recursive=True):
+    tag = f.split("pmc_msda_")[1].split("/")[0]
     for r in csv.DictReader(open(f)):
-        k = r["Kernel_Name"].split("(")[0].split("::")[-1][:40]
-        agg[k][r["Counter_Name"]] += float(r["Counter_Value"]); cnt[(k, r["Counter_Name"])] += 1
-for k, d in agg.items():
+        k = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0][-44:]
+        d = disp[(k, tag)][int(r["Dispatch_Id"])]
+        d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+res = collections.defaultdict(lambda: collections.defaultdict(dict))
+for (k, tag), dd in disp.items():
     if "msda" not in k: continue
-    out = {c: v / cnt[(k, c)] for c, v in d.items()}
+    ids = sorted(dd); h = len(ids) // 2
+    for half, sel in (("enc", ids[:h]), ("dec", ids[h:])):
+        for c in dd[ids[0]]:
+            res[(k, half)][c] = sum(dd[i].get(c, 0.0) for i in sel) / max(1, len(sel))
+for (k, half), out in sorted(res.items()):
     hit = out.get("TCC_HIT_sum", 0); miss = out.get("TCC_MISS_sum", 0)
-    print(k, {c: f"{v:.3g}" for c, v in out.items()}, "L2 hit %.2f" % (hit / max(hit + miss, 1)))
+    raw_mb = out.get("FETCH_SIZE", 0) / 1024  # KB; gfx950 tallies a 128-B request at 64 B (MI355X_MICROARCH.md)
+    print("%-46s %s L2 hit %.2f  FETCH raw %.1f MB (x2 for 128-B requests: %.1f MB)"
+          % (k, half, hit / max(hit + miss, 1), raw_mb, 2 * raw_mb))
 PY
 find gpurun_out -path "*pmc_msda_*" -name "*trace.csv" -delete
