@@ -346,6 +346,10 @@ __global__ void __launch_bounds__(256) confusion_kernel(const T *__restrict__ x,
 }
 
 // ------------------------------------------------------------------ cross-entropy
+// exp(a) as 2^(a·log2 e) on v_exp_f32: the arguments are differences to the row maximum / LSE, so the
+// rounding of the product costs at most |a|·2^-24 relative in a term that is itself e^-|a| of the
+// largest (the full-precision expf's range reduction was most of the loss kernels' VALU time)
+constexpr float kLog2e = 1.4426950408889634f;
 constexpr int CE_GRID = 4096;  // fixed grid: deterministic partial sums (IRADS_CE_WORKSPACE); 16 per CU so one
                                // workgroup's tile loads overlap the others' compute
 
@@ -389,7 +393,7 @@ __global__ void __launch_bounds__(256) ce_fwd(const T *__restrict__ x, Dims d, c
         float s = 0.f;
 #pragma unroll
         for (int c = 0; c < CMAX; ++c)
-            if (c < d.C) s += expf(z[c] - m);
+            if (c < d.C) s += fast_exp2((z[c] - m) * kLog2e);
         const float l = m + logf(s);
         lse[p] = l;
         const long t = tgt[p];
@@ -454,7 +458,7 @@ __global__ void __launch_bounds__(256) ce_bwd(const T *__restrict__ x, Dims d, c
     float gv = 0.f;
     if (t != ignore && t >= 0 && t < d.C) {
         const float wt = cw ? cw[t] : 1.f;
-        gv = gs * wt * (expf(ldf(x, w.e) - lse[p]) - (w.c == t ? 1.f : 0.f));
+        gv = gs * wt * (fast_exp2((ldf(x, w.e) - lse[p]) * kLog2e) - (w.c == t ? 1.f : 0.f));
     }
     stf(gx, w.e, gv);
 }
@@ -499,7 +503,7 @@ __global__ void __launch_bounds__(256) ce_fwd_cl8(const T *__restrict__ x, Dims 
             float sum = 0.f;
 #pragma unroll
             for (int c = 0; c < CMAX; ++c)
-                if (c < d.C) sum += expf(z[c] - m);
+                if (c < d.C) sum += fast_exp2((z[c] - m) * kLog2e);
             const float l = m + logf(sum);
             lse[p] = l;
             const long t = tgt[p];
@@ -542,7 +546,7 @@ __global__ void __launch_bounds__(256) ce_bwd_cl8(const T *__restrict__ x, Dims 
         float v[8];
         V8<T>::ld(x + (long)r * 8, v);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) g[j] = gs * (expf(v[j] - l) - (c0 + j == t ? 1.f : 0.f));
+        for (int j = 0; j < 8; ++j) g[j] = gs * (fast_exp2((v[j] - l) * kLog2e) - (c0 + j == t ? 1.f : 0.f));
     }
     V8<T>::st(gx + (long)r * 8, g);
 }
