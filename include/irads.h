@@ -427,7 +427,8 @@ int irads_confusion_update(int dtype, const void *scores, const int64_t *strides
  *   p -= (lr/bc1) m / (sqrt(v)/sqrt(bc2) + eps),   bc_i = 1 - b_i^step,
  * with step[t] and lr[t] read on the device (fp32 scalars; the caller increments the steps
  * first), so the launches are graph-capturable; 1 - beta_i is taken in double (as torch's
- * 1 - 0.999 of the Python floats), then every element op in fp32.  40 tensors per launch. */
+ * 1 - 0.999 of the Python floats), then every element op in fp32.  Up to 72 tensors of one
+ * learning rate / weight decay per launch. */
 int irads_adamw(int n, float *const *p, const float *const *g, float *const *m, float *const *v,
                 const float *const *step, const float *const *lr, const float *wd, const long *numel, double beta1,
                 double beta2, double eps, void *stream);

@@ -1,6 +1,7 @@
 // AdamW update of a list of fp32 parameters (torch.optim.AdamW's fused / capturable step, the
 // reference's optimizer, semseg/optimizers.py:33-49) in a few launches instead of PyTorch's
-// multi-tensor chunks: the tensors go to the kernel as arguments in batches of kBatch, and each
+// multi-tensor chunks: the tensors go to the kernel as arguments in batches of kBatch (one learning
+// rate and weight decay per launch), and each
 // launch gives every tensor blocks in proportion to its size (4096 elements per block), so one big
 // tensor no longer leaves a launch nearly idle.  The step count and learning rate are read on the
 // device (per tensor), so the launches can be captured in a HIP graph and replayed.
@@ -13,25 +14,27 @@
 namespace irads {
 namespace {
 
-constexpr int kBatch = 40;       // tensors per launch (kernel arguments stay under 4 KiB)
+constexpr int kBatch = 72;       // tensors per launch (kernel arguments stay under 4 KiB)
 constexpr int kChunk = 4096;     // elements per block
 constexpr int kThreads = 256;
 
+// one launch: tensors sharing a learning rate and weight decay (a param group)
 struct AdamWBatch {
     float *p[kBatch];
     const float *g[kBatch];
     float *m[kBatch];
     float *v[kBatch];
     const float *step[kBatch];
-    const float *lr[kBatch];
-    float wd[kBatch];
-    long numel[kBatch];
+    int numel[kBatch];
     int first_block[kBatch + 1];  // block range of tensor t: [first_block[t], first_block[t + 1])
+    const float *lr;
+    float wd;
     int n;
     double beta1, beta2;       // the bias corrections are formed from these
     float b1, omb1, b2, omb2;  // beta_i and 1 - beta_i (taken in double), rounded once
     float eps;
 };
+static_assert(sizeof(AdamWBatch) <= 4096, "kernel arguments are limited to 4 KiB");
 
 __device__ __forceinline__ void adamw_elem(float &p, float g, float &m, float &v, float lr, float wd, float b1,
                                            float omb1, float b2, float omb2, float eps, float step_size,
@@ -60,7 +63,7 @@ __global__ void __launch_bounds__(kThreads) adamw_kernel(const AdamWBatch B) {
     const long n = B.numel[t];
     const long begin = (long)(blk - B.first_block[t]) * kChunk;
     const long end = min(n, begin + kChunk);
-    const float lr = *B.lr[t], step = *B.step[t], wd = B.wd[t];
+    const float lr = *B.lr, step = *B.step[t], wd = B.wd;
     const float b1 = B.b1, omb1 = B.omb1, b2 = B.b2, omb2 = B.omb2, eps = B.eps;
     // bias corrections in double, as ATen forms them from the double betas
     const float bc1 = (float)(1.0 - pow(B.beta1, (double)step));
@@ -115,9 +118,12 @@ extern "C" int irads_adamw(int n, float *const *p, const float *const *g, float 
     if (n == 0) return IRADS_OK;
     IRADS_REQUIRE(p && g && m && v && step && lr && wd && numel, "adamw: null array");
     hipStream_t st = (hipStream_t)stream;
-    for (int t0 = 0; t0 < n; t0 += kBatch) {
+    int t = 0;
+    while (t < n) {  // a launch per run of up to kBatch tensors with one learning rate and weight decay
         AdamWBatch B;
         B.n = 0;
+        B.lr = lr[t];
+        B.wd = wd[t];
         B.beta1 = beta1;
         B.beta2 = beta2;
         B.b1 = (float)beta1;
@@ -126,9 +132,9 @@ extern "C" int irads_adamw(int n, float *const *p, const float *const *g, float 
         B.omb2 = (float)(1.0 - beta2);
         B.eps = (float)eps;
         int blocks = 0;
-        for (int t = t0; t < n && t < t0 + kBatch; ++t) {
+        for (; t < n && B.n < kBatch && lr[t] == B.lr && wd[t] == B.wd; ++t) {
             IRADS_REQUIRE(p[t] && g[t] && m[t] && v[t] && step[t] && lr[t], "adamw: null pointer for tensor %d", t);
-            IRADS_REQUIRE(numel[t] >= 0 && numel[t] < (1L << 40), "adamw: bad size for tensor %d", t);
+            IRADS_REQUIRE(numel[t] >= 0 && numel[t] < (1L << 31), "adamw: bad size for tensor %d", t);
             const long nb = (numel[t] + kChunk - 1) / kChunk;
             IRADS_REQUIRE(blocks + nb < (1L << 30), "adamw: too many elements in one launch");
             const int i = B.n++;
@@ -137,9 +143,7 @@ extern "C" int irads_adamw(int n, float *const *p, const float *const *g, float 
             B.m[i] = m[t];
             B.v[i] = v[t];
             B.step[i] = step[t];
-            B.lr[i] = lr[t];
-            B.wd[i] = wd[t];
-            B.numel[i] = numel[t];
+            B.numel[i] = (int)numel[t];
             B.first_block[i] = blocks;
             blocks += (int)nb;
         }

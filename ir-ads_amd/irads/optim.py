@@ -6,7 +6,7 @@ whose blocks follow its fixed tensor-list chunks, so one large tensor leaves a l
 idle (0.41 ms per step for 7.5 M parameters, ~0.5 TB/s).  `AdamW` keeps torch's optimizer
 object (param groups, state layout exp_avg / exp_avg_sq / step, state_dict, capturable
 semantics with the step count and a tensor learning rate on the device) and replaces only
-the update: the steps are incremented with one foreach add, then irads_adamw updates 40
+the update: the steps are incremented with one foreach add, then irads_adamw updates up to 72
 tensors per launch with blocks in proportion to their sizes.
 """
 import ctypes
