@@ -569,7 +569,7 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(MM == 
 // dKᵀ += qᵀ·dS straight from the accumulators; dS to LDS), phase 2 dQᵀ = Kᵀ·dSᵀ.  The biases are the
 // forward's values, seeded into the s' accumulator as there: for a key and 4 consecutive queries of
 // one window row they are 4 consecutive table entries, one ds_read_b128 from the head's backward
-// quads (the stride-28 (dr, dc) grid) staged once per workgroup.  Q, dO, K and V tiles are 64-B rows
+// quads (the stride-20 (dr, dc) grid) staged once per workgroup.  Q, dO, K and V tiles are 64-B rows
 // swizzled as the forward's (kv_swz), dSᵀ rows are 160 bf16 with 8-B pieces XOR-placed by
 // ds_swz(row): conflict-free both for the dS stores (key on the lane) and for phase 2's transposed
 // reads.  The next window's q, k, v, dO, O and LSE are prefetched into registers while this one
