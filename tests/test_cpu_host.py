@@ -365,3 +365,20 @@ def test_hot_kernels_use_no_scratch(tmp_path):
                     bad.append((src, name, int(m.group(1))))
     assert seen > 50, seen
     assert not bad, bad
+
+
+def test_native_adamw_refuses_cpu_parameters():
+    """irads.optim.AdamW keeps torch's optimizer object but its update is the native launch only:
+    CPU parameters raise instead of silently taking torch's path; get_optimizer gives CPU models
+    torch's AdamW (the oracle's optimizer)."""
+    from irads.optim import AdamW
+    from semseg.optimizers import get_optimizer
+    p = torch.nn.Parameter(torch.zeros(4))
+    p.grad = torch.ones(4)
+    opt = AdamW([p], 1e-3)
+    assert set(opt.param_groups[0]) >= {"lr", "betas", "eps", "weight_decay"}
+    with pytest.raises(RuntimeError, match="GPU"):
+        opt.step()
+    m = torch.nn.Module()
+    m.Adapter = torch.nn.Linear(2, 2)
+    assert type(get_optimizer(m, "adamw", 1e-3, "Adapter")) is torch.optim.AdamW
