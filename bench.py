@@ -180,7 +180,10 @@ def msda_inputs(device, bs=2, Q=None, seed=0):
 
 
 TIMED_KERNELS = ("winattn_fwd", "winattn_bwd", "dattn_fwd", "dattn_bwd")
-TIMER_REPS = 4  # idempotent window-attention launches per event pair in the eager timing pass
+TIMER_REPS = 1  # launches per event pair in the eager timing pass: one, so no launch re-reads the
+#                previous one's q/k/v from the 256 MB Infinity Cache (round-3 verdict: 4 back-to-back
+#                repeats read 10 % faster than the same kernels in the traced step)
+MSDA_SETS = 4  # rotating input sets in msda_rooflines: > 2x the Infinity Cache between reuses
 FP32_PEAK_TFLOPS = 157.3  # MI355X fp32 vector peak (MI355X_MICROARCH.md)
 GATHER_PEAK_GBS = 18800.0  # L2-resident random-row gather rate (upper end), MI355X_MICROARCH.md
 
@@ -188,36 +191,42 @@ GATHER_PEAK_GBS = 18800.0  # L2-resident random-row gather rate (upper end), MI3
 def msda_rooflines(device, reps=20):
     """MSDeformAttn forward / backward at the DINO encoder (Q = S = 22 223) and decoder
     (Q = 2200) shapes, bs = 2 (C5 per GPU), timed with HIP events; algorithmic bytes of
-    SURVEY §8(d): fwd = 4(S·M·D + Q·M·L·P·3 + Q·M·D), bwd adds dOut, dValue, dLoc, dAw."""
+    SURVEY §8(d): fwd = 4(S·M·D + Q·M·L·P·3 + Q·M·D), bwd adds dOut, dValue, dLoc, dAw.
+    Launches cycle over MSDA_SETS independent input / output sets (the encoder's is ~250 MB),
+    so no launch finds its inputs left in the Infinity Cache by the previous one."""
     from irads import ops, native as N
     out = {}
     for name, Q in (("encoder", None), ("decoder", 2200)):
-        value, shapes, lsi, loc, aw = msda_inputs(device, Q=Q)
+        sets = []
+        for k in range(MSDA_SETS):
+            value, shapes, lsi, loc, aw = msda_inputs(device, Q=Q, seed=k)
+            o = ops.MSDAFn.apply(value, shapes, lsi, loc, aw, 64)
+            go = torch.randn_like(o)
+            sets.append((value, loc, aw, o, go, torch.empty_like(value), torch.empty_like(loc), torch.empty_like(aw)))
         bs, S, M, D = value.shape
         Qn, L, P = loc.shape[1], loc.shape[3], loc.shape[4]
         fwd_b = 4 * bs * (S * M * D + Qn * M * L * P * 3 + Qn * M * D)
         bwd_b = 4 * bs * (2 * S * M * D + 2 * Qn * M * L * P * 3 + Qn * M * D)
-        o = ops.MSDAFn.apply(value, shapes, lsi, loc, aw, 64)
-        go = torch.randn_like(o)
-        gv, gl, ga = torch.empty_like(value), torch.empty_like(loc), torch.empty_like(aw)
         ws_bytes = ops.msda_gather_workspace_bytes(value, go, loc)
         ws = torch.empty((ws_bytes,), device=device, dtype=torch.uint8)
 
-        def fwd():
-            ops.MSDAFn.apply(value, shapes, lsi, loc, aw, 64)
+        def fwd(k):
+            v_, l_, a_ = sets[k][:3]
+            ops.MSDAFn.apply(v_, shapes, lsi, l_, a_, 64)
 
-        def bwd():  # the product's fp32 backward (MSDAFn.backward): bucket + gather, no float atomics
-            N.call("irads_msda_bwd_gather", N.ptr(value), N.ptr(shapes), N.ptr(lsi), N.ptr(loc), N.ptr(aw),
-                   N.ptr(go), bs, S, M, D, L, Qn, P, N.ptr(gv), N.ptr(gl), N.ptr(ga), N.ptr(ws), ws_bytes,
+        def bwd(k):  # the product's fp32 backward (MSDAFn.backward): bucket + gather, no float atomics
+            v_, l_, a_, _, go_, gv, gl, ga = sets[k]
+            N.call("irads_msda_bwd_gather", N.ptr(v_), N.ptr(shapes), N.ptr(lsi), N.ptr(l_), N.ptr(a_),
+                   N.ptr(go_), bs, S, M, D, L, Qn, P, N.ptr(gv), N.ptr(gl), N.ptr(ga), N.ptr(ws), ws_bytes,
                    N.stream())
         for fn, tag, nbytes in ((fwd, "fwd", fwd_b), (bwd, "bwd", bwd_b)):
-            for _ in range(3):
-                fn()
+            for k in range(MSDA_SETS):
+                fn(k)
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             torch.cuda.synchronize()
             a.record()
-            for _ in range(reps):
-                fn()
+            for r in range(reps):
+                fn(r % MSDA_SETS)
             b.record()
             torch.cuda.synchronize()
             ms = a.elapsed_time(b) / reps
@@ -225,6 +234,8 @@ def msda_rooflines(device, reps=20):
             out[f"msda_{tag}_{name}"] = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
                                          "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
                                          "avg_launch_ms": round(ms, 4), "algorithmic_bytes_per_launch": nbytes,
+                                         "timing": f"{reps} launches between one HIP event pair, cycling over "
+                                                   f"{MSDA_SETS} input sets (no launch reuses cached inputs)",
                                          "shape": f"bs={bs} Q={Qn} S={S} M={M} D={D} L={L} P={P} fp32"}
             # The sampling itself moves 4 corners x D floats per sample through L2 / Infinity Cache:
             # forward = the value corners; backward = the value corners again (grad_loc / grad_aw)
@@ -301,13 +312,13 @@ def dino_stack_line(device, msda, reps=5):
 def traffic_from_profile():
     """HBM bytes per forward launch from the newest committed PMC passes of the same 24 launches
     (scripts/pmc_winattn_kind.sh: FETCH_SIZE x2 + WRITE_SIZE, separate rocprofv3 passes); PMC
-    counters cannot be read from inside this process."""
-    for tag in ("r03", "r02"):
-        path = os.path.join(ROOT, "profiles", f"{tag}_pmc_winattn_fwd.json")
-        if os.path.exists(path):
-            with open(path) as f:
-                return json.load(f).get("hbm_bytes_per_launch")
-    return None
+    counters cannot be read from inside this process.  Returns (bytes, source file)."""
+    for tag in ("r04", "r03", "r02"):
+        rel = os.path.join("profiles", f"{tag}_pmc_winattn_fwd.json")
+        if os.path.exists(os.path.join(ROOT, rel)):
+            with open(os.path.join(ROOT, rel)) as f:
+                return json.load(f).get("hbm_bytes_per_launch"), rel
+    return None, None
 
 
 def main():
@@ -431,17 +442,19 @@ def main():
         per_launch_bytes = fwd["bytes"] / fwd["launches"]
         achieved = fwd["bytes"] / (fwd["total_ms"] * 1e-3) / 1e9
         achieved_real = fwd["real_bytes"] / (fwd["total_ms"] * 1e-3) / 1e9
-        traffic = traffic_from_profile()
+        traffic, traffic_src = traffic_from_profile()
         result["roofline"] = {
             "kernel": "irads_winattn_fwd (bf16, Swin-B shifted-window attention, all 4 stages x 2 streams)",
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "traffic_source": (f"from committed PMC {traffic_src} (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE per launch, "
+                               f"not measured in this run)" if traffic_src else None),
             "launches": fwd["calls"], "timed_launches": fwd["launches"], "avg_launch_ms": round(avg_ms, 5),
             "algorithmic_bytes_per_launch": round(per_launch_bytes),
             "timing": ("HIP events captured in the graph, last timed replay" if timer_in_graph else
                        "HIP events on the launch stream" + (f" (eager step after the timed region; each call's "
-                                                            f"kernel issued {TIMER_REPS}x back to back inside one "
-                                                            f"event pair, queued behind a GPU spin)" if graph else "")),
+                                                            f"kernel issued {TIMER_REPS}x inside its own event "
+                                                            f"pair, queued behind a GPU spin)" if graph else "")),
             "bytes_definition": "SURVEY §8(d): read q,k,v + write o per padded token (8·Np·C bytes, bf16)",
             "achieved_real_tokens_gbs": round(achieved_real, 1),
             "mfma_tflops": round(fwd["flops"] / (fwd["total_ms"] * 1e-3) / 1e12, 2)}

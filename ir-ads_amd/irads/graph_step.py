@@ -32,7 +32,6 @@ Data parallel (world > 1; train_mm.py:94 / DDP semantics: gradients averaged ove
     not captured).  Used with the gloo backend (CPU-side tests), which cannot be captured.
 """
 import os
-import time
 
 import torch
 import torch.distributed as dist
@@ -52,6 +51,46 @@ def rccl_capture_env():
     fresh event, so the watchdog never queries a captured one; the watchdog's error handling
     stays the default (a HIP error on a watchdog query is rethrown and ends the process)."""
     os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
+
+
+_CAPTURE_GROUPS = {}  # (default group, device) -> process group used only inside captures
+
+
+def capture_group(device):
+    """The RCCL process group the captured collectives run on: a second communicator over the
+    same ranks (eagerly connected: a split of the default one when the default group is bound
+    to a device), on which no eager collective is ever issued.
+
+    Why a group of its own.  ProcessGroupNCCL records each collective's end event on the
+    group's internal stream, and its watchdog thread polls the end events of every EAGER work
+    (hipEventQuery) until it sees them complete, ~100 ms later.  A collective captured on the
+    same group joins that internal stream to the capture; a poll of an eager work's event whose
+    stream is being captured (or whose stream's work was captured into a graph still alive at
+    teardown) returns a HIP error, and the watchdog rethrows it, which aborts the process (round
+    3: tests/test_gpu_zz_rccl.py, WorkNCCL::isCompleted -> hipEventQuery).  With the captured
+    collectives on their own group, the captured stream never carries an eager work's event
+    and that group's watchdog has nothing to poll, whatever the timing; the eager collectives
+    (warm-up, the split exchange) stay on the default group.  gloo (CPU tests): the default
+    group (gloo collectives are never captured)."""
+    if not dist.is_initialized() or dist.get_backend() != "nccl":
+        return None
+    dev = torch.device(device)
+    key = (id(dist.group.WORLD), dev)
+    g = _CAPTURE_GROUPS.get(key)
+    if g is None:
+        g = dist.new_group(backend="nccl", device_id=dev, group_desc="irads_graph_capture")
+        if not g._get_backend(dev)._is_initialized():
+            # a lazily connected communicator would be set up by its first collective, which
+            # here is inside a capture
+            raise RuntimeError("irads capture group: the RCCL communicator was not connected eagerly; build the "
+                               "default process group with device_id=torch.device('cuda', local_rank)")
+        _CAPTURE_GROUPS[key] = g
+    return g
+
+
+def release_capture_groups():
+    """Forget the cached capture groups (destroy_process_group() destroys them with the rest)."""
+    _CAPTURE_GROUPS.clear()
 
 
 # "thread_local": only the capturing thread's capture-unsafe HIP calls are refused.  In the
@@ -93,6 +132,7 @@ class GraphedTrainStep:
                 o += p.numel()
             if self.comm == "overlap":
                 self._make_buckets(bucket_mb)
+        self._cap_group = None
         if not graph:  # eager: the same exchange per step, nothing captured (gloo tests, debugging)
             return
         if self.comm != "none":
@@ -101,6 +141,8 @@ class GraphedTrainStep:
             w = torch.zeros((1,), device=dev, dtype=torch.float32)
             _all_reduce(w)
             torch.cuda.synchronize(dev)
+            if self.comm == "overlap":
+                self._cap_group = capture_group(dev)
         side = torch.cuda.Stream(device=dev)
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):  # warm-up (kernel selection, allocator pools) off the capture
@@ -110,14 +152,6 @@ class GraphedTrainStep:
                 optimizer.step()
         torch.cuda.current_stream(dev).wait_stream(side)
         torch.cuda.synchronize(dev)
-        if self.comm != "none" and dist.is_initialized() and dist.get_backend() == "nccl":
-            # The warm-up's eager collectives stay on the process group's watchdog list until its
-            # next poll (one every 100 ms) sees them complete; their end events were recorded on
-            # the communicator stream that the capture below joins, and a poll of such an event
-            # while that stream is capturing fails (round-3 suite: WorkNCCL::isCompleted ->
-            # hipEventQuery error -> abort).  Everything is complete after the synchronize: give
-            # the watchdog three polls to retire it before the capture opens.
-            time.sleep(0.35)
         optimizer.zero_grad(set_to_none=True)
         if before_capture is not None:
             before_capture()
@@ -158,7 +192,8 @@ class GraphedTrainStep:
             _all_reduce(self.flat)
             unpack_grads(self.params, self.flat, 1.0 / self.world)
             return loss
-        return self._exchange.run(fwd_bwd, self.world)
+        # captured collectives on the capture-only group, eager ones on the default group
+        return self._exchange.run(fwd_bwd, self.world, group=self._cap_group if capture else None)
 
     def step(self):
         if not self.use_graph:
@@ -207,22 +242,22 @@ class OverlappedGradExchange:
         self.comm_stream = torch.cuda.Stream(device=flat.device) if self.cuda else None
         self.issue_log = []  # bucket indices in issue order, last run (tests)
 
-    def _issue(self, b):
+    def _issue(self, b, group=None):
         a, z = self.ranges[b]
         self.issue_log.append(b)
         if not self.cuda:
-            dist.all_reduce(self.flat[a:z])
+            dist.all_reduce(self.flat[a:z], group=group)
             return
         ev = torch.cuda.Event()
         ev.record()  # on the stream the backward (and the hooks' copies) run on
         self.comm_stream.wait_event(ev)
         with torch.cuda.stream(self.comm_stream):
             if dist.get_backend() == "gloo":
-                _all_reduce(self.flat[a:z])
+                _all_reduce(self.flat[a:z], group)
             else:
-                dist.all_reduce(self.flat[a:z])  # RCCL sum over xGMI, overlapping the backward
+                dist.all_reduce(self.flat[a:z], group=group)  # RCCL sum over xGMI, overlapping the backward
 
-    def run(self, fwd_bwd, world):
+    def run(self, fwd_bwd, world, group=None):
         remaining = [len(b) for b in self.buckets]
         ready = [False] * len(self.buckets)
         nxt = [0]
@@ -236,7 +271,7 @@ class OverlappedGradExchange:
             if remaining[b] == 0:
                 ready[b] = True
                 while nxt[0] < len(self.buckets) and ready[nxt[0]]:
-                    self._issue(nxt[0])
+                    self._issue(nxt[0], group)
                     nxt[0] += 1
 
         handles = [p.register_post_accumulate_grad_hook(lambda p, i=i: land(i, p))
@@ -258,14 +293,14 @@ class OverlappedGradExchange:
         return loss
 
 
-def _all_reduce(flat):
+def _all_reduce(flat, group=None):
     """Sum over ranks; gloo (tests) reduces a host copy."""
     if dist.get_backend() == "gloo" and flat.is_cuda:
         h = flat.cpu()
-        dist.all_reduce(h)
+        dist.all_reduce(h, group=group)
         flat.copy_(h)
     else:
-        dist.all_reduce(flat)
+        dist.all_reduce(flat, group=group)
 
 
 def _snapshot_optimizer(opt):

@@ -87,9 +87,10 @@ def bias_quads(table_f, nH, scale, owner=None):
     tensor lives, per table version: a captured graph that reads the cached quads (a frozen
     trunk's tables are re-laid once, eagerly, and every capture hits) then reads memory that
     lives as long as the model the graph runs.  A trainable table that is being captured
-    recomputes its quads inside the graph, since a cached copy would go stale after the
-    optimizer's in-graph update.  Without an owner nothing is cached."""
-    use_cache = owner is not None and not (owner.requires_grad and torch.cuda.is_current_stream_capturing())
+    recomputes its quads on every call (eager or captured): the optimizer's in-graph update
+    does not bump the table's version counter, so a cached copy could go stale after a replay.
+    Without an owner nothing is cached."""
+    use_cache = owner is not None and not owner.requires_grad
     key = (nH, float(scale), table_f.device)
     ent = _QUADS.get(id(owner)) if use_cache else None
     if ent is not None and ent[0]() is owner:
@@ -1004,6 +1005,7 @@ class LinearFn(torch.autograd.Function):
         ctx.save_for_backward(xb, wb)
         ctx.has_bias = bias is not None
         ctx.shape = shape
+        ctx.x_f32 = x.dtype == torch.float32
         return y.view(*shape[:-1], weight.shape[0])
 
     @staticmethod
@@ -1014,7 +1016,9 @@ class LinearFn(torch.autograd.Function):
             g = g.to(torch.bfloat16).contiguous()
         gx = gw = gb = None
         if ctx.needs_input_grad[0]:
-            gx = torch.mm(g, wb).view(ctx.shape)
+            # an fp32 input (DAttn's sampled features and attention output) gets its gradient
+            # straight from the GEMM's fp32 accumulator, not rounded to bf16 and cast back
+            gx = (torch.mm(g, wb, out_dtype=torch.float32) if ctx.x_f32 else torch.mm(g, wb)).view(ctx.shape)
         if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
             o = wb.shape[0]
             if o % 8:  # narrow output: zero-pad dY to 8 columns (16-B rows for the kernel)

@@ -32,6 +32,11 @@ class AdamW(torch.optim.AdamW):
                 raise RuntimeError("irads AdamW: a tensor learning rate must be one fp32 value on the parameters' "
                                    "device")
             return lr
+        if torch.cuda.is_current_stream_capturing():
+            # a replay never calls step(): a float lr would be baked into the graph and later
+            # scheduler changes to group['lr'] silently ignored
+            raise RuntimeError("irads AdamW: a captured step needs the learning rate as a device tensor "
+                               "(lr_on_device); group['lr'] is a float")
         ent = self._lr_dev.get(gi)
         if ent is None or ent[0].device != device:
             t = torch.tensor(float(lr), dtype=torch.float32, device=device)
@@ -39,9 +44,6 @@ class AdamW(torch.optim.AdamW):
             return t
         t, val = ent
         if val != float(lr):
-            if torch.cuda.is_current_stream_capturing():
-                raise RuntimeError("irads AdamW: a float learning rate changed during graph capture; keep the "
-                                   "learning rate as a device tensor (lr_on_device) for captured steps")
             t.fill_(float(lr))
             self._lr_dev[gi] = (t, float(lr))
         return t

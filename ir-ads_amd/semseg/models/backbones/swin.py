@@ -436,9 +436,14 @@ class DAttentionMM(nn.Module):
         pos_x, pos_y = ops.dattn_offsets(x, y, self.conv_offset_x, self.conv_offset_y, g, ref)
         n = Hk * Wk
         xs, ys, qs = ops.DAttnSampleFn.apply(x.float(), y.float(), q32.view(B, C, H, W), pos_x, pos_y, g)
-        # get_sample_weight + softmax over the two modalities, token-major: (B, 2n, 2)
+        # get_sample_weight + softmax over the two modalities, token-major: (B, 2n, 2), in fp32.
+        # Its last layer's gradient is a sum over every key of dz0 = -dz1 = p0 p1 (g0 - g1), a
+        # cancellation-heavy reduction: from a bf16 dz it carried ~10 % error (C1 / C4 parity
+        # reports, round 3); the (B*2n) x C x C GEMMs are ~0.1 GFLOP, so fp32 costs nothing.
         sw = self.get_sample_weight
-        w = F.softmax(self._tok_linear(sw[2], sw[1](self._tok_linear(sw[0], qs.transpose(1, 2)))), dim=-1)
+        with torch.autocast("cuda", enabled=False):
+            h = F.relu(F.linear(qs.transpose(1, 2), sw[0].weight.flatten(1), sw[0].bias))
+            w = F.softmax(F.linear(h, sw[2].weight.flatten(1), sw[2].bias), dim=-1)
         sampled = xs * w[..., 0].unsqueeze(1) + ys * w[..., 1].unsqueeze(1)  # (B, C, 2n) fp32
         s_tok = sampled.transpose(1, 2)
         nH, hc = self.n_heads, self.n_head_channels

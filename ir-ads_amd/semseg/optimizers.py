@@ -3,7 +3,7 @@
 TRAIN_TYPE 'Adapter' trains only parameters whose name contains Adapter /
 extra_patch_embed / head / MPG (optimizers.py:7-30) and freezes the rest.  On GPU the
 AdamW update runs as irads_adamw (irads/optim.py: torch's AdamW object and state, capturable,
-the update in 40-tensor launches sized to the tensors)."""
+the update in launches of up to 72 tensors sized to the tensors, irads_adamw)."""
 import torch
 from torch import nn
 from torch.optim import AdamW, SGD

@@ -250,3 +250,57 @@ def test_fp32_gather_backward_vs_scatter_and_fp64(D, case):
     assert ops.msda_gather_workspace_bytes(value.double(), gout.double(), loc.double()) == 0
     v30 = torch.randn(bs, S, M, 30, device=DEV)
     assert ops.msda_gather_workspace_bytes(v30, torch.randn(bs, Q, M * 30, device=DEV), loc) == 0
+
+
+def _rel(a, b):
+    a, b = a.double().flatten(), b.double().flatten()
+    return float((a - b).norm() / b.norm().clamp_min(1e-300))
+
+
+@pytest.mark.parametrize("Q", [22223, 2200], ids=["encoder", "decoder"])
+def test_c5_size_backward_gather_vs_scatter_and_fp64(Q):
+    """The product backward (irads_msda_bwd_gather) at C5's full sizes (bench.py's MSDA lines,
+    SURVEY §8(d)): bs 2, S = 22 223 over DINO's four levels of an 800x1333 input, M = 8 heads (the
+    M % 8 == 0 head-per-XCD mapping and the coarse-level split pass), D = 32, L = P = 4; the
+    encoder's Q = S and the decoder's 2 000 + 200 queries.  Against the atomic-scatter fp32
+    kernel and the fp64 kernel (pinned to the reference's own fp64 test above,
+    tests/test_ms_deform_attn.py:103-133): relative L2 <= 1e-5 for grad_value, grad_loc and
+    grad_attn_weight; the fp32 forward within 1e-6 of fp64."""
+    from irads import native as N
+    ops = _ops()
+    g = torch.Generator().manual_seed(Q)
+    lv = [(100, 167), (50, 84), (25, 42), (13, 21)]
+    shapes = torch.as_tensor(lv, dtype=torch.long, device=DEV)
+    lsi = torch.cat((shapes.new_zeros((1,)), shapes.prod(1).cumsum(0)[:-1]))
+    S, bs, M, D, L, P = int(shapes.prod(1).sum()), 2, 8, 32, 4, 4
+    assert S == 22223
+    value = torch.randn(bs, S, M, D, generator=g)
+    ref = torch.rand(bs, Q, 1, 1, 1, 2, generator=g)
+    loc = (ref + 0.02 * torch.randn(bs, Q, M, L, P, 2, generator=g)).contiguous()  # ~2 % outside [0, 1]
+    aw = torch.randn(bs, Q, M, L * P, generator=g).softmax(-1).view(bs, Q, M, L, P).contiguous()
+    gout = torch.randn(bs, Q, M * D, generator=g)
+    value, loc, aw, gout = (t.to(DEV) for t in (value, loc, aw, gout))
+    out = ops.MSDAFn.apply(value, shapes, lsi, loc, aw, 64)
+    ws_bytes = ops.msda_gather_workspace_bytes(value, gout, loc)
+    assert ws_bytes > 0
+    ws = torch.empty(ws_bytes, device=DEV, dtype=torch.uint8)
+    gv = torch.full_like(value, float("nan"))
+    gl, ga = torch.empty_like(loc), torch.empty_like(aw)
+    N.call("irads_msda_bwd_gather", N.ptr(value), N.ptr(shapes), N.ptr(lsi), N.ptr(loc), N.ptr(aw), N.ptr(gout),
+           bs, S, M, D, L, Q, P, N.ptr(gv), N.ptr(gl), N.ptr(ga), N.ptr(ws), ws_bytes, N.stream())
+    gv2, gl2, ga2 = torch.zeros_like(value), torch.empty_like(loc), torch.empty_like(aw)
+    N.call("irads_msda_bwd", N.F32, N.ptr(value), N.ptr(shapes), N.ptr(lsi), N.ptr(loc), N.ptr(aw), N.ptr(gout),
+           bs, S, M, D, L, Q, P, N.ptr(gv2), N.ptr(gl2), N.ptr(ga2), N.stream())
+    v64, l64, a64 = (t.double().requires_grad_() for t in (value, loc, aw))
+    o64 = ops.MSDAFn.apply(v64, shapes, lsi, l64, a64, 64)
+    r = torch.autograd.grad((o64 * gout.double()).sum(), (v64, l64, a64))
+    torch.cuda.synchronize()
+    assert torch.isfinite(gv).all()
+    errs = {"out_vs_fp64": _rel(out, o64.detach()),
+            "gvalue_vs_fp64": _rel(gv, r[0]), "gloc_vs_fp64": _rel(gl, r[1]), "gaw_vs_fp64": _rel(ga, r[2]),
+            "gvalue_vs_scatter": _rel(gv, gv2), "gloc_vs_scatter": _rel(gl, gl2), "gaw_vs_scatter": _rel(ga, ga2)}
+    print(Q, errs)
+    assert errs["out_vs_fp64"] <= 1e-6, errs
+    assert all(v <= 1e-5 for k, v in errs.items() if k != "out_vs_fp64"), errs
+    # value cells no sample reaches: exact zeros
+    assert (gv[r[0] == 0] == 0).all()

@@ -94,6 +94,26 @@ def test_adamw_graph_replay_matches_eager():
     assert float(oa.state[a[0]]["step"]) == float(ob.state[b[0]]["step"]) == 1 + 3
 
 
+def test_adamw_capture_refuses_float_lr():
+    """A captured step with a float learning rate would bake the value into the graph (replays
+    never call step(), so a scheduler's later group['lr'] changes would be ignored): refused."""
+    from irads.optim import AdamW
+    a = [torch.nn.Parameter(p.clone()) for p in _tensors(1)]
+    for pa, g in zip(a, _grads(a, 0)):
+        pa.grad = g.clone()
+    oa = AdamW(a, 1e-3, weight_decay=0.01)
+    oa.step()
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(side):
+        with pytest.raises(RuntimeError, match="device tensor"):
+            with torch.cuda.graph(graph, stream=side):
+                oa.step()
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+
+
 def test_get_optimizer_uses_native_adamw():
     from irads.optim import AdamW
     from semseg.optimizers import get_optimizer

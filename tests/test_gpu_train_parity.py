@@ -32,15 +32,20 @@ fp32 (autocast off: the module path with the fp32 kernels), north_star's "fp32 l
   * MMST loss relative 1e-4; logits (stride-8 subsample of y, y_rgb, y_dte) relative L2 <= 1e-3;
   * argmax of y identical wherever the reference's top-2 margin exceeds 1e-2; the product's MMST
     target equal to the reference's on those pixels;
-  * every non-zero trainable gradient vs fp64: norm and 2 seeded projections within
-    max(5e-3, 3 ref32) of the norm; the 14 full tensors relative L2 <= the same.  One class is
-    held looser, DISCONTINUOUS: the DeformMPG offset networks (conv_offset_x / _y) and the
-    Adapters of the stages that feed a DeformMPG block, held at 1e-1.  Their gradients pass through the floor of
-    grid_sample's bilinear cell and the clamp of the sampling positions (swin.py:887-905), so they
-    jump when a position crosses a cell edge: measured on C4, the fp64 REFERENCE block's
-    conv_offset_y gradients move by 3.5e-2 when its depth input is replaced by the product's fp32
-    one, which differs from the fp64 input by 1.0e-6 (scripts/diag_dmpg.py).  What
-    pins those blocks instead is the block-level check:
+  * every non-zero trainable gradient vs fp64 (Adapters included): norm and 2 seeded
+    projections within max(5e-3, 3 ref32) of the norm; the 14 full tensors relative L2 <= the
+    same.  The DeformMPG offset networks (conv_offset_x / _y) are held at 1e-2, and at 1e-1 only
+    where the block-level check below MEASURES a discontinuity for that tensor on that fixture:
+    their gradients pass through the floor of grid_sample's bilinear cell and the clamp of the
+    sampling positions (swin.py:887-905), so they jump when a position crosses a cell edge
+    (measured on C4: the fp64 REFERENCE block's conv_offset_y gradients move by 3.5e-2 when its
+    depth input is replaced by the product's fp32 one, 1.0e-6 away; scripts/diag_dmpg.py,
+    DESIGN.md §3).  A tensor is discontinuous when the oracle's own fp32-vs-fp64 gap on the
+    product's block inputs, or the fp64 oracle's response to a 1e-6 relative perturbation of
+    those inputs (two seeds), exceeds 5e-3.  One named exception, ADAPTER_EXCEPTIONS: the C4
+    stage-2 DTE Adapter of block 16 at 1e-2 (measured 7.0e-3, the rest of C4's Adapters <= 2e-3):
+    it sits two blocks upstream of DeformMPG 2, whose input-gradient sensitivity the report
+    records.  What pins the offset networks is the block-level check:
   * every DeformMPG block re-run on the product's OWN captured inputs and upstream gradient: its
     parameter and input gradients vs the oracle's DeformMPGBlock (oracle/irads_ref.py, pinned to
     the reference by test_oracle_golden.py) in fp64 on the same tensors, relative L2 <= 5e-3, or
@@ -55,10 +60,13 @@ bf16 (autocast, fused Swin stages, bf16 DAttn path; eager and HIP-graph replay):
     to the reference's on >= 99 % of the pixels the margin decides;
   * every non-zero trainable gradient whose reference bf16 error ref16 is at most NOISE16 = 0.3:
       - vs the PRODUCT's own fp32 gradient (full tensors, same inputs, same teacher-forced loss):
-        relative L2 <= tol = max(0.25, K16 ref16) with K16 = 4, i.e. <= BF16_CAP = 0.3 for every
-        tensor whose reference bf16 noise is <= 0.075 (~300 of the 400: "capped"); the fp32 test
-        pins the product's fp32 gradient to fp64, so this bounds the bf16 error vs fp64 too;
-      - vs fp64: the 14 full tensors relative L2 <= tol + 5e-2; the norm/projection estimate
+        relative L2 <= tol = min(BF16_CAP, max(BF16_FLOOR, K16 ref16)) with BF16_CAP = 0.5,
+        BF16_FLOOR = 0.05 and K16 = 4 (round 3 measured <= 0.39 overall; the floor is the
+        ~0.04 median bf16 error); the fp32 test pins the product's fp32 gradient to fp64, so
+        this bounds the bf16 error vs fp64 too;
+      - as an aggregate: the relative L2 over ALL checked tensors together <= max(1e-2, 2x the
+        reference's own aggregate bf16 error);
+      - vs fp64: the 14 full tensors relative L2 <= tol + 0.1; the norm/projection estimate
         (which reads up to ~2.5x the true error) <= 2.5 tol;
       - cosine with the fp32 gradient >= 0.5 and norm ratio in [0.5, 2]: a zeroed or sign-flipped
         gradient fails, whatever its noise level;
@@ -100,11 +108,17 @@ K32 = 3.0
 FP32_DISCONT_TOL = 1e-1
 BLOCK_TOL = 5e-3
 BLOCK_OFFSET_TOL = 5e-2
-DISCONT = re.compile(r"(deform_atten\.conv_offset_[xy]\.|stages\.\d+\.blocks\.\d+\.MLP_(RGB|DTE)_Adapter\.)")
-BF16_CAP = 0.3
+OFFSET_NET = re.compile(r"deform_atten\.conv_offset_[xy]\.")
+OFFSET_TOL = 1e-2
+DISCONT_MEASURED = 5e-3   # block-level gap / perturbation response that marks a discontinuity
+PERTURB_REL = 1e-6        # ~ the product's fp32 block inputs vs the fp64 reference's
+# (fixture tag, parameter-name prefix) -> tolerance, with the evidence in the docstring
+ADAPTER_EXCEPTIONS = {("c4_swinl_480x640", "backbone.stages.2.blocks.16.MLP_DTE_Adapter."): 1e-2}
+BF16_CAP = 0.5
 K16 = 4.0
-BF16_FLOOR = 0.25
+BF16_FLOOR = 0.05
 NOISE16 = 0.3
+FULL_SLACK16 = 1e-1
 
 
 def _rel_l2(a, b):
@@ -231,14 +245,21 @@ def _capture_dmpg(model):
     return cap
 
 
-def _oracle_block_grads(blk, i, args, gout, dtype):
+def _oracle_block_grads(blk, i, args, gout, dtype, perturb_seed=None):
+    """The oracle DeformMPGBlock's parameter and input gradients on the captured inputs; with
+    perturb_seed, both inputs get Gaussian noise of PERTURB_REL x their RMS first."""
     import irads_ref as R
     da = blk.deform_atten
     ref = R.DeformMPGBlock(blk.D_fc1.in_features, da.stride, da.n_groups, da.n_heads, 0.0, i, 1 / 8)
     ref.load_state_dict({k: v.detach().cpu() for k, v in blk.state_dict().items()})
     ref = ref.to(dtype).train()
-    a = args[0].detach().cpu().to(dtype).requires_grad_()
-    b = args[1].detach().cpu().to(dtype).requires_grad_()
+    a = args[0].detach().cpu().to(dtype)
+    b = args[1].detach().cpu().to(dtype)
+    if perturb_seed is not None:
+        gen = torch.Generator().manual_seed(perturb_seed)
+        a = a + PERTURB_REL * a.pow(2).mean().sqrt() * torch.randn(a.shape, generator=gen, dtype=dtype)
+        b = b + PERTURB_REL * b.pow(2).mean().sqrt() * torch.randn(b.shape, generator=gen, dtype=dtype)
+    a, b = a.requires_grad_(), b.requires_grad_()
     ref(a, b, *args[2:]).backward(gout.cpu().to(dtype))
     want = {n: p.grad.double() for n, p in ref.named_parameters() if p.grad is not None}
     want["input x_rgb"], want["input x_dte"] = a.grad.double(), b.grad.double()
@@ -270,24 +291,27 @@ def _check_dmpg_blocks(model, cap, report, fails):
             p.grad = g
         w64 = _oracle_block_grads(blk, i, args, gout, torch.float64)
         w32 = _oracle_block_grads(blk, i, args, gout, torch.float32)
+        wp = [_oracle_block_grads(blk, i, args, gout, torch.float64, perturb_seed=s) for s in (11, 12)]
         for n, g in prod.items():
             full = f"backbone.DeformMPGBlocks.{i}.{n}" if not n.startswith("input") else f"DeformMPGBlocks.{i} {n}"
             if ZERO_GRAD.search(full):
                 continue
             e, gap = _rel_l2(g, w64[n]), _rel_l2(w32[n], w64[n])
+            sens = max(_rel_l2(w[n], w64[n]) for w in wp)
             tol = max(BLOCK_TOL, 2 * gap)
             if "conv_offset_" in n:  # the product's fp32 positions can sit on another side of an edge
                 tol = max(tol, BLOCK_OFFSET_TOL)
-            rows[full] = {"prod32_vs_oracle64": e, "oracle32_vs_oracle64": gap,
-                          "prod32_vs_oracle32": _rel_l2(g, w32[n]), "tol": tol}
+            rows[full] = {"prod32_vs_oracle64": e, "oracle32_vs_oracle64": gap, "perturb_response64": sens,
+                          "prod32_vs_oracle32": _rel_l2(g, w32[n]), "tol": tol,
+                          "discontinuous": max(gap, sens) > DISCONT_MEASURED}
             worst = max(worst, (e / tol, full))
             if not (e <= tol):
                 fails.append(f"fp32 block-level: {full} vs the fp64 oracle on the product's inputs: {e:.3e} > {tol:.3e} "
                              f"(oracle fp32 gap {gap:.2e})")
     report["fp32.dmpg_block_level"] = rows
     report["fp32.dmpg_block_level_worst_frac_of_tol"] = worst
-    report["fp32.dmpg_block_level_discontinuous"] = sorted(n for n, v in rows.items()
-                                                           if v["oracle32_vs_oracle64"] > BLOCK_TOL / 2)
+    report["fp32.dmpg_block_level_discontinuous"] = sorted(n for n, v in rows.items() if v["discontinuous"])
+    return {n for n, v in rows.items() if v["discontinuous"]}
 
 
 def _zero_floor(fx64):
@@ -316,6 +340,7 @@ def _fp32_step(tag):
     report["fp32.bn_running_mean_rel_l2"] = e
     if e > 1e-4:
         fails.append(f"fp32: head BN running mean relative L2 {e:.3e}")
+    discont = _check_dmpg_blocks(model, cap, report, fails)
     floor = _zero_floor(fx64)
     ref32 = fx64["ref32_rel"]
     per, grads = {}, {}
@@ -331,8 +356,11 @@ def _fp32_step(tag):
                 fails.append(f"fp32: mathematically-zero gradient {n} has norm {gn:.2e} > {floor:.2e}")
             continue
         tol = max(FP32_TOL, K32 * float(ref32[k]))
-        if DISCONT.search(n):
-            tol = max(tol, FP32_DISCONT_TOL)
+        if OFFSET_NET.search(n):
+            tol = max(tol, FP32_DISCONT_TOL if n in discont else OFFSET_TOL)
+        for (ftag, prefix), t in ADAPTER_EXCEPTIONS.items():
+            if ftag == tag and n.startswith(prefix):
+                tol = max(tol, t)
         row = {"proj_rel_vs_fp64": rel, "ref32": float(ref32[k]), "tol": tol}
         if not (rel <= tol):
             fails.append(f"fp32: gradient {n}: projection / norm error vs fp64 {rel:.3e} > {tol:.3e}")
@@ -350,7 +378,6 @@ def _fp32_step(tag):
     report["fp32.n_tensors"] = len(per)
     report["fp32.above_5e-3"] = sorted((round(v["proj_rel_vs_fp64"], 5), n) for n, v in per.items()
                                        if v.get("proj_rel_vs_fp64", 0) > FP32_TOL)
-    _check_dmpg_blocks(model, cap, report, fails)
     report["fp32.n_zero_grad"] = sum(1 for v in per.values() if v.get("zero_grad"))
     report["fp32.per_tensor"] = per
     report["fails"] = fails
@@ -379,6 +406,7 @@ def _check_bf16_grads(fx, fx64, model, own32, what, report, fails):
     ref16 = fx64["ref16_rel"]
     floor = _zero_floor(fx64)
     per = {}
+    agg = [0.0, 0.0, 0.0, 0.0]  # sum |g - own32|^2, |own32|^2, (ref16 |g64|)^2, |g64|^2
     for k, (n, g64, rel, absd, nr) in enumerate(_grad_table(fx, fx64, model)):
         if g64 is None:
             fails.append(f"{what}: no gradient for {n}")
@@ -395,7 +423,7 @@ def _check_bf16_grads(fx, fx64, model, own32, what, report, fails):
         own = _rel_l2(g64, o)
         cos = float((g64 * o).sum() / max(gn * on, 1e-300))
         ratio = gn / max(on, 1e-300)
-        tol = max(BF16_FLOOR, K16 * r16)
+        tol = min(BF16_CAP, max(BF16_FLOOR, K16 * r16))
         row = {"proj_rel_vs_fp64": rel, "vs_own_fp32": own, "cos_own_fp32": cos, "norm_ratio_own_fp32": ratio,
                "ref16": r16, "tol": tol}
         if "g." + n in fx64:
@@ -413,15 +441,24 @@ def _check_bf16_grads(fx, fx64, model, own32, what, report, fails):
             fails.append(f"{what}: gradient {n} vs the product's fp32 gradient: relative L2 {own:.3e} > {tol:.3e}")
         if not (cos >= 0.5 and 0.5 <= ratio <= 2.0):
             fails.append(f"{what}: gradient {n} vs the product's fp32 gradient: cosine {cos:.3f}, norm ratio {ratio:.3f}")
-        row["capped"] = tol <= BF16_CAP
         # the projection estimate of the error vs fp64 (max of two Gaussian projections and the
         # norm difference) reads up to ~2.5x the true relative L2; the 14 full tensors are exact
         if not (rel <= 2.5 * tol):
             fails.append(f"{what}: gradient {n}: projection / norm error vs fp64 {rel:.3e} > {2.5 * tol:.3e}")
-        if "full_rel_l2_vs_fp64" in row and not (row["full_rel_l2_vs_fp64"] <= tol + FP32_DISCONT_TOL):
+        if "full_rel_l2_vs_fp64" in row and not (row["full_rel_l2_vs_fp64"] <= tol + FULL_SLACK16):
             fails.append(f"{what}: gradient {n} relative L2 vs fp64 {row['full_rel_l2_vs_fp64']:.3e} > "
-                         f"{tol + FP32_DISCONT_TOL:.3e}")
+                         f"{tol + FULL_SLACK16:.3e}")
+        agg[0] += (own * on) ** 2
+        agg[1] += on * on
+        agg[2] += (r16 * nr) ** 2
+        agg[3] += nr * nr
     rows = [v for v in per.values() if "vs_own_fp32" in v and not v.get("noise_dominated")]
+    agg_own, agg_ref = (agg[0] / agg[1]) ** 0.5, (agg[2] / agg[3]) ** 0.5
+    report[f"{what}.grad_aggregate_vs_own_fp32"] = agg_own
+    report[f"{what}.grad_aggregate_ref16"] = agg_ref
+    if not (agg_own <= max(1e-2, 2 * agg_ref)):
+        fails.append(f"{what}: aggregate bf16 gradient error {agg_own:.3e} > max(1e-2, 2 x the reference's "
+                     f"{agg_ref:.3e})")
     report[f"{what}.grad_vs_own_fp32_median"] = float(np.median([v["vs_own_fp32"] for v in rows]))
     report[f"{what}.grad_vs_own_fp32_worst"] = max((v["vs_own_fp32"], n) for n, v in per.items()
                                                    if "vs_own_fp32" in v and not v.get("noise_dominated"))
@@ -437,7 +474,7 @@ def _check_bf16_grads(fx, fx64, model, own32, what, report, fails):
         fails.append(f"{what}: bf16 gradient error / the reference's bf16 error: median {rs['median']:.2f}, p90 "
                      f"{rs['p90']:.2f} (bounds 1.5, 3)")
     report[f"{what}.n_checked_vs_own_fp32"] = len(rows)
-    report[f"{what}.n_capped_at_0.3"] = sum(1 for v in rows if v.get("capped"))
+    report[f"{what}.n_at_floor"] = sum(1 for v in rows if v["tol"] <= BF16_FLOOR)
     report[f"{what}.n_noise_dominated"] = sum(1 for v in per.values() if v.get("noise_dominated"))
     report[f"{what}.min_cos_own_fp32"] = min((v["cos_own_fp32"], n) for n, v in per.items()
                                              if "cos_own_fp32" in v and not v.get("noise_dominated"))
@@ -523,7 +560,12 @@ def test_train_step_vs_reference(tag):
         fails.append(f"head BN running mean relative L2 {e:.3e}")
     # graph replay, as bench.py / GraphedTrainStep run it.  The eager step's autograd graph is
     # released first: capturing while it is alive ended in a segfault inside capture_end
-    # (hipGraphInstantiate) on ROCm 7.2 / torch 2.10; GraphedTrainStep never holds one.
+    # (hipGraphInstantiate) on ROCm 7.2 / torch 2.10.  The cause is the one torch warns about
+    # (autograd/input_buffer.cpp: "The AccumulateGrad node's stream does not match the stream of
+    # the node that produced the incoming gradient ... break CUDA graph capture"): a live graph
+    # keeps the parameters' AccumulateGrad nodes of the eager step, created on the default
+    # stream, so the captured backward on the side stream syncs with the default stream, which
+    # is not part of the capture.  GraphedTrainStep never holds one.
     del loss, y, yr, yd, own
     torch.cuda.synchronize()
     params = [p for p in model.parameters() if p.requires_grad]

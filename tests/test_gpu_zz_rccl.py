@@ -1,7 +1,8 @@
 """The RCCL-backed overlapped gradient exchange of irads/graph_step.py, in a child process and in
 the last file of the GPU suite (zz): a communicator's background threads then never share a
 process with the other GPU tests.  Two suite runs aborted without a message in this test's RCCL
-section when it ran in the pytest process; the child's output is reported here."""
+section when it ran in the pytest process; the child's whole output is kept in
+$IRADS_REPORT_DIR/rccl_overlap_worker.log (default gpurun_out/)."""
 import os
 import subprocess
 import sys
@@ -31,5 +32,9 @@ def test_graph_step_overlapped_exchange_capture():
         if p.poll() is None:  # our own child only
             p.kill()
             p.wait()
+    log_dir = os.environ.get("IRADS_REPORT_DIR", os.path.join(ROOT, "gpurun_out"))
+    os.makedirs(log_dir, exist_ok=True)
+    with open(os.path.join(log_dir, "rccl_overlap_worker.log"), "w") as f:  # the whole child output
+        f.write(out)
     errs = [ln for ln in out.splitlines() if "error" in ln.lower() and "Traceback" not in ln][:8]
     assert p.returncode == 0 and "OK rel" in out, (p.returncode, errs, out[-3000:])
