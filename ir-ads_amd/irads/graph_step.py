@@ -79,11 +79,9 @@ def capture_group(device):
     g = _CAPTURE_GROUPS.get(key)
     if g is None:
         g = dist.new_group(backend="nccl", device_id=dev, group_desc="irads_graph_capture")
-        if not g._get_backend(dev)._is_initialized():
-            # a lazily connected communicator would be set up by its first collective, which
-            # here is inside a capture
-            raise RuntimeError("irads capture group: the RCCL communicator was not connected eagerly; build the "
-                               "default process group with device_id=torch.device('cuda', local_rank)")
+        # connect now: a lazily connected communicator would be set up by its first collective,
+        # which here is inside a capture (that fails loudly, it is never silently wrong)
+        g._get_backend(dev).eager_connect_single_device(dev)
         _CAPTURE_GROUPS[key] = g
     return g
 

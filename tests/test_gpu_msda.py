@@ -263,9 +263,16 @@ def test_c5_size_backward_gather_vs_scatter_and_fp64(Q):
     SURVEY §8(d)): bs 2, S = 22 223 over DINO's four levels of an 800x1333 input, M = 8 heads (the
     M % 8 == 0 head-per-XCD mapping and the coarse-level split pass), D = 32, L = P = 4; the
     encoder's Q = S and the decoder's 2 000 + 200 queries.  Against the atomic-scatter fp32
-    kernel and the fp64 kernel (pinned to the reference's own fp64 test above,
-    tests/test_ms_deform_attn.py:103-133): relative L2 <= 1e-5 for grad_value, grad_loc and
-    grad_attn_weight; the fp32 forward within 1e-6 of fp64."""
+    kernel (same arithmetic: relative L2 <= 1e-6 for all three gradients) and the fp64 kernel
+    on the same inputs (pinned to the reference's own fp64 test above,
+    tests/test_ms_deform_attn.py:103-133): relative L2 <= 1e-5 for the forward, grad_value and
+    grad_attn_weight.  What sets that bound (measured 2.7e-6): the fractional cell coordinate
+    loc * H - 0.5 is rounded to fp32 before its fraction is taken (ulp 3.8e-6 at H = 100, the
+    reference's CUDA formula, ms_deform_im2col_cuda.cuh:257-262), so every bilinear weight carries
+    ~1e-5 relative error.  grad_loc is the derivative of a piecewise-bilinear function: it jumps
+    where a sample crosses a cell edge, and at 5.7 M encoder samples the fp32 and fp64 positions
+    put ~100 of them in different cells (measured 1.8e-3 over all samples), so grad_loc is held
+    to 1e-5 over the samples whose fp64 position lies more than 1e-4 cells from an edge."""
     from irads import native as N
     ops = _ops()
     g = torch.Generator().manual_seed(Q)
@@ -296,11 +303,21 @@ def test_c5_size_backward_gather_vs_scatter_and_fp64(Q):
     r = torch.autograd.grad((o64 * gout.double()).sum(), (v64, l64, a64))
     torch.cuda.synchronize()
     assert torch.isfinite(gv).all()
+    # distance of each sample's fp64 position to the nearest cell edge, in cells
+    hw = shapes.double()  # (L, 2): H, W
+    pos = torch.stack((l64.detach()[..., 1] * hw[:, 0].view(1, 1, 1, L, 1) - 0.5,
+                       l64.detach()[..., 0] * hw[:, 1].view(1, 1, 1, L, 1) - 0.5), -1)
+    edge = (pos - pos.round()).abs().amin(-1)  # (bs, Q, M, L, P)
+    smooth = (edge > 1e-4).unsqueeze(-1).expand_as(gl)
     errs = {"out_vs_fp64": _rel(out, o64.detach()),
-            "gvalue_vs_fp64": _rel(gv, r[0]), "gloc_vs_fp64": _rel(gl, r[1]), "gaw_vs_fp64": _rel(ga, r[2]),
+            "gvalue_vs_fp64": _rel(gv, r[0]), "gaw_vs_fp64": _rel(ga, r[2]),
+            "gloc_vs_fp64_all": _rel(gl, r[1]), "gloc_vs_fp64_off_edges": _rel(gl[smooth], r[1][smooth]),
+            "samples_near_edges": int((edge <= 1e-4).sum()),
             "gvalue_vs_scatter": _rel(gv, gv2), "gloc_vs_scatter": _rel(gl, gl2), "gaw_vs_scatter": _rel(ga, ga2)}
     print(Q, errs)
-    assert errs["out_vs_fp64"] <= 1e-6, errs
-    assert all(v <= 1e-5 for k, v in errs.items() if k != "out_vs_fp64"), errs
+    for k in ("out_vs_fp64", "gvalue_vs_fp64", "gaw_vs_fp64", "gloc_vs_fp64_off_edges"):
+        assert errs[k] <= 1e-5, (k, errs)
+    for k in ("gvalue_vs_scatter", "gloc_vs_scatter", "gaw_vs_scatter"):
+        assert errs[k] <= 1e-6, (k, errs)
     # value cells no sample reaches: exact zeros
     assert (gv[r[0] == 0] == 0).all()

@@ -250,18 +250,20 @@ def test_wgrad_split_k(K, m, n):
 
 
 @pytest.mark.parametrize("out_features", [16, 2, 5])
-def test_linear_fn_matches_autocast_linear(out_features):
+@pytest.mark.parametrize("x_dtype", [torch.bfloat16, torch.float32])
+def test_linear_fn_matches_autocast_linear(out_features, x_dtype):
     """ops.linear (trainable weight, bf16 autocast): forward is the autocast GEMM bit for bit;
-    dX equals autocast's; dW / db are the fp32 sums autocast rounds to bf16 (tolerance: one
-    bf16 rounding, 2^-8 relative).  out_features < 8 takes the zero-padded weight-gradient
-    path (DAttn's C -> 2 sample-weight projection)."""
+    dX equals autocast's for a bf16 input, and for an fp32 input is the same GEMM's fp32
+    accumulator (autocast rounds it to bf16: tolerance one bf16 rounding); dW / db are the fp32
+    sums autocast rounds to bf16 (tolerance: one bf16 rounding, 2^-8 relative).  out_features < 8
+    takes the zero-padded weight-gradient path."""
     from irads import ops
     from semseg.models.layers.common import TrainLinear
     torch.manual_seed(2)
     lin = torch.nn.Linear(128, out_features).to(DEV)
     tl = TrainLinear(128, out_features).to(DEV)
     tl.load_state_dict(lin.state_dict())
-    x = torch.randn(2, 300, 128, device=DEV)
+    x = torch.randn(2, 300, 128, device=DEV).to(x_dtype)
     g = torch.randn(2, 300, out_features, device=DEV).bfloat16()
     assert ops.wgrad_ok(128, out_features)
     outs = []
@@ -273,7 +275,11 @@ def test_linear_fn_matches_autocast_linear(out_features):
         outs.append((y, gx, gw, gb))
     (y0, gx0, gw0, gb0), (y1, gx1, gw1, gb1) = outs
     assert y1.dtype == torch.bfloat16 and torch.equal(y0, y1)
-    assert torch.equal(gx0, gx1)
+    assert gx1.dtype == x_dtype
+    if x_dtype == torch.bfloat16:
+        assert torch.equal(gx0, gx1)
+    else:
+        assert _rel(gx1, gx0) < 4e-3 and _rel(gx1.bfloat16().float(), gx0) < 4e-3
     assert _rel(gw1, gw0) < 4e-3 and _rel(gb1, gb0) < 4e-3
 
 

