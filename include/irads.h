@@ -89,6 +89,11 @@ int irads_msda_corner_index(int dtype, const void *loc, const int64_t *shapes, i
  * BF16 scores are formed in base-2 units from bf16(q·scale·log2 e); lse holds the base-2
  * log-sum-exp of those scores (the backward's input, from the same library version). */
 long irads_winattn_bias_quads_size(int nH);
+/* Forward kernel selection (tuning / A-B measurements; the default follows IRADS_WINATTN_FWD):
+ * 0 = one workgroup per (window, head); 1 = persistent workgroups of one head, the next window's
+ * q / k / v streamed into LDS by LDS-DMA while the current one computes.  Same arithmetic, same
+ * outputs bit for bit.  Other values only query.  Returns the previous selection. */
+int irads_winattn_fwd_variant(int variant);
 int irads_winattn_bias_quads(const float *rel_table, int nH, float scale, float *bias_quads, void *stream);
 int irads_winattn_fwd(int dtype, const void *qkv, const float *qkv_bias, const float *rel_table,
                       const float *bias_quads, const float *mask, int n_mask, int B, int H, int W, int C, int nH, int shift,

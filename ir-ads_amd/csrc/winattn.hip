@@ -21,6 +21,8 @@
 //   query (dQ) and thread per key (dK, dV).
 #include "common.h"
 #include <type_traits>
+#include <cstdlib>
+#include <cstring>
 
 namespace irads {
 namespace {
@@ -564,6 +566,217 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(MM == 
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Forward, persistent and pipelined: one 3-wave workgroup per (head, chunk of consecutive windows),
+// ~3 per CU.  While a window's scores / softmax / PV run out of one LDS stage, the next window's
+// q / k / v rows stream into the other stage by LDS-DMA (global_load_lds_dwordx4: no VGPRs, no
+// staging instructions), so HBM traffic overlaps the MFMA / VALU work of the previous window
+// instead of alternating with it (the per-item kernel above starts every workgroup with all its
+// loads outstanding and nothing to compute).  The head's bias quads are staged once per
+// workgroup.  LDS: quads 7.4 KB + q 9 KB (one stage: read into registers before the next DMA)
+// + 2 x (k + v) 36 KB + pad rows = 53.6 KB, 3 workgroups per CU.  Arithmetic per window is the
+// per-item kernel's, instruction for instruction (same rounding, same LSE).
+//
+// LDS-DMA writes a wave-uniform base + 16 x lane: the 16 rows x 4 chunks of a row block are
+// contiguous, and the kv_swz chunk swizzle is applied on the GLOBAL side (LDS slot s of row t
+// receives chunk s ^ kv_swz(t)).  Pad tokens (no global row) DMA token 0 of the image and are
+// overwritten from the pad rows by the lane that issued their slot, after its own vmcnt wait.
+// Ordering: each window's DMA is issued after the barrier that ends every wave's reads of the
+// stage and q buffer it overwrites, and waited for (s_waitcnt vmcnt(0)) before the barrier that
+// publishes it; no DMA is in flight across a __syncthreads().
+constexpr int PP_WG_PER_CU = 3;
+constexpr int PP_LDS_BQ = QB * 16, PP_LDS_T = NT * HD * 2;  // bytes: quads, one 144-row tile
+constexpr int PP_LDS = PP_LDS_BQ + 5 * PP_LDS_T + 3 * HD * 2;
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) void glb_void;
+
+__device__ __forceinline__ void dma16(const char *g, unsigned short *lds_block) {
+    __builtin_amdgcn_global_load_lds((glb_void *)g, (lds_void *)lds_block, 16, 0, 0);
+}
+
+template <int MM>
+__global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(3)))
+winattn_fwd_bf16_pp(const unsigned short *__restrict__ qkv, const float *__restrict__ qbias,
+                    const float *__restrict__ quads, const float *__restrict__ mask, Geo g, int cw, float c2,
+                    unsigned short *__restrict__ out, float *__restrict__ lse) {
+    __shared__ __attribute__((aligned(16))) unsigned char smem[PP_LDS];  // ONE array (glds wait trap)
+    f32x4 *Bq = (f32x4 *)smem;
+    unsigned short *Qs = (unsigned short *)(smem + PP_LDS_BQ);
+    unsigned short *KVs = Qs + NT * HD;                      // [stage][k, v][NT * HD]
+    unsigned short *padS = KVs + 4 * NT * HD;                // pad-token q, k, v rows (bf16)
+    const Chunk ck = decode_chunk(g, cw);                    // the heads of one chunk on one XCD
+    const int h = ck.h;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int l16 = lane & 15, grp = lane >> 4;
+    if (ck.w_begin >= ck.w_end) return;
+    const char *base = (const char *)qkv;
+    const unsigned rowb = 6u * (unsigned)g.C, cb = 2u * (unsigned)g.C;
+    // ---- once per workgroup: the head's quads (x c2) and the pad rows
+    {
+        const f32x4 *qsrc = (const f32x4 *)(quads + (long)h * QH);
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+            if (tid + 192 * j < QB) Bq[tid + 192 * j] = qsrc[tid + 192 * j] * c2;  // T / scale -> T·log2 e
+        if (tid < 12) {  // (q, k, v) x 4 chunks of 8 channels
+            const int m = tid >> 2, c = tid & 3;
+            *(u16x8 *)(padS + m * HD + c * 8) = pad_frag(qbias, m * g.C + h * HD + c * 8);
+        }
+    }
+    // DMA slot of this lane: row block rb = 3 wave + j (16 rows), row t = 16 rb + lane / 4, LDS slot
+    // lane % 4 holding global chunk (lane % 4) ^ kv_swz(t)
+    const int dslot = lane & 3;
+    auto issue = [&](int bw, int stage, int (&dtok)[3]) {
+        const WinOrigin wo(g, bw);
+        unsigned short *Kd = KVs + (2 * stage) * NT * HD, *Vd = Kd + NT * HD;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const int rb = 3 * wave + j, t = 16 * rb + (lane >> 2);
+            dtok[j] = wo.tok(g, t);
+            const int c = dslot ^ kv_swz(t);
+            const int src = dtok[j] >= 0 ? dtok[j] : wo.base;  // pad: any valid row, overwritten below
+            const char *p = base + (unsigned)src * rowb + (unsigned)(h * HD + c * 8) * 2u;
+            const int o = rb * 16 * HD;  // wave-uniform LDS base of the row block
+            dma16(p, Qs + o);
+            dma16(p + cb, Kd + o);
+            dma16(p + 2 * cb, Vd + o);
+        }
+    };
+    auto fix_pads = [&](int stage, const int (&dtok)[3]) {  // after this wave's vmcnt wait
+        unsigned short *Kd = KVs + (2 * stage) * NT * HD, *Vd = Kd + NT * HD;
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+            if (dtok[j] < 0) {
+                const int t = 16 * (3 * wave + j) + (lane >> 2), c = dslot ^ kv_swz(t);
+                const int o = t * HD + dslot * 8;
+                *(u16x8 *)(Kd + o) = *(const u16x8 *)(padS + HD + c * 8);
+                *(u16x8 *)(Vd + o) = *(const u16x8 *)(padS + 2 * HD + c * 8);
+            }
+    };
+    int dtok[3];
+    __syncthreads();  // pad rows visible before any fix-up
+    issue(ck.w_begin, 0, dtok);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    fix_pads(0, dtok);
+    __syncthreads();
+    // ---- per-workgroup constants of the arithmetic (the per-item kernel's)
+    int part3[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) part3[j] = QF_STRIDE * ((16 * j + 4 * grp) / WS) + (16 * j + 4 * grp) % WS;
+    unsigned long long hbits = 0, wbits = 0;
+    if (MM == 1) key_class_bits(g.shift, grp, hbits, wbits);
+    const float mneg100 = -100.0f * LOG2E;
+    const bf16x8_t ones = as_bf(u16x8{0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80});
+    const int swz_l = kv_swz(l16);
+    const int vsw = kv_swz(4 * grp), vch = ((l16 & 3) >> 1), vin = (l16 & 1) * 4;
+    const int vrow = 4 * grp + (l16 >> 2);
+    int stage = 0;
+    for (int bw = ck.w_begin; bw < ck.w_end; ++bw, stage ^= 1) {
+        const WinOrigin wo(g, bw);
+        int tok[3];
+        u16x8 qreg[3];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const int t = (3 * wave + j) * 16 + l16;
+            tok[j] = wo.tok(g, t);
+            qreg[j] = tok[j] >= 0 ? *(const u16x8 *)(Qs + t * HD + (grp ^ swz_l) * 8) : *(const u16x8 *)(padS + grp * 8);
+            qreg[j] = scale_frag(qreg[j], c2);
+        }
+        __syncthreads();  // q buffer and the other stage are free
+        const bool more = bw + 1 < ck.w_end;
+        if (more) issue(bw + 1, stage ^ 1, dtok);
+        bool lastH = false, lastW = false;
+        if (MM == 1) {
+            const int wi = bw % g.nW;
+            lastH = wi / g.nWw == g.nWh - 1;
+            lastW = wi % g.nWw == g.nWw - 1;
+        }
+        const unsigned short *Ks = KVs + (2 * stage) * NT * HD, *Vs = Ks + NT * HD;
+        const unsigned short *vb0 = Vs + vrow * HD + ((vch ^ vsw) * 8) + vin;
+        const unsigned short *vb1 = Vs + vrow * HD + (((vch ^ 2) ^ vsw) * 8) + vin;
+        const unsigned short *kb = Ks + l16 * HD + (grp ^ swz_l) * 8;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const int qi = (3 * wave + j) * 16 + l16;
+            const bf16x8_t qf = as_bf(qreg[j]);
+            const f32x4 *bqq = Bq + (QF_STRIDE * 11 + 11 - (QF_STRIDE * (qi / WS) + qi % WS));
+            f32x4 s[9];
+#pragma unroll
+            for (int kt = 0; kt < 9; ++kt) {
+                const f32x4 b4 = bqq[part3[kt % 3] + 4 * QF_STRIDE * (kt / 3)];
+                const bf16x8_t kf = as_bf(*(const u16x8 *)(kb + kt * 16 * HD));
+                s[kt] = mfma16(kf, qf, b4);
+                if (MM == 2) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        s[kt][r] = fmaf(mask[((long)(bw % g.n_mask) * NT + qi) * NT + kt * 16 + grp * 4 + r], LOG2E, s[kt][r]);
+                }
+            }
+            if (MM == 1 && (lastH || lastW)) {
+                unsigned long long mbits = 0;
+                if (lastH) mbits |= hi_row(g, qi) ? ~hbits : hbits;
+                if (lastW) mbits |= hi_col(g, qi) ? ~wbits : wbits;
+#pragma unroll
+                for (int kt = 0; kt < 9; ++kt)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) s[kt][r] += mask_term(mbits, kt * 4 + r, mneg100);
+            }
+            float mx = s[0][0];
+#pragma unroll
+            for (int kt = 0; kt < 9; ++kt)
+#pragma unroll
+                for (int r = (kt == 0); r < 4; ++r) mx = fmaxf(mx, s[kt][r]);
+            mx = max_xor16_32(mx);
+            float shift = 0.f;
+            if (wave_any(!(mx >= -60.f && mx <= 60.f))) {
+                const unsigned short sh = f2bf(-mx * (1.0f / 32.0f));
+                shift = -32.0f * bf2f(sh);
+                const bf16x8_t shb = as_bf(u16x8{sh, sh, sh, sh, sh, sh, sh, sh});
+#pragma unroll
+                for (int kt = 0; kt < 9; ++kt) s[kt] = mfma16(ones, shb, s[kt]);
+            }
+#pragma unroll
+            for (int kt = 0; kt < 9; ++kt)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) s[kt][r] = fast_exp2(s[kt][r]);
+            f32x4 o0 = {0.f, 0.f, 0.f, 0.f}, o1 = o0, os = o0;
+#pragma unroll
+            for (int ks = 0; ks < 5; ++ks) {
+                bf16x8_t pb;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    pb[r] = (__bf16)s[2 * ks][r];
+                    pb[4 + r] = (2 * ks + 1 < 9) ? (__bf16)s[2 * ks + 1][r] : (__bf16)0.f;
+                }
+                const int r0 = 32 * ks * HD, r1 = ks < 4 ? r0 + 16 * HD : r0;
+                const u16x8 a0 = cat4(tr_read(vb0 + r0), tr_read(vb0 + r1));
+                const u16x8 a1 = cat4(tr_read(vb1 + r0), tr_read(vb1 + r1));
+                o0 = mfma16(as_bf(a0), pb, o0);
+                o1 = mfma16(as_bf(a1), pb, o1);
+                os = mfma16(ones, pb, os);
+            }
+            const float inv = __builtin_amdgcn_rcpf(os[0]);
+            if (tok[j] >= 0) {  // stores need no wait: issuing them beside the DMAs is safe
+                u16x4 w0, w1;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    w0[r] = f2bf(o0[r] * inv);
+                    w1[r] = f2bf(o1[r] * inv);
+                }
+                unsigned short *op = out + (long)tok[j] * g.C + h * HD;
+                *(u16x4 *)(op + grp * 4) = w0;
+                *(u16x4 *)(op + 16 + grp * 4) = w1;
+            }
+            if (grp == 0) lse[((long)bw * g.nH + h) * NT + qi] = __log2f(os[0]) + shift;
+        }
+        if (more) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of window bw + 1 landed
+            fix_pads(stage ^ 1, dtok);
+        }
+        __syncthreads();  // publishes the next stage and q rows
+    }
+}
+
 // Backward: persistent-chunk workgroups of 9 waves (one head x a contiguous chunk of windows,
 // ~one workgroup per CU), phase 1 key-on-lane (s' = q·kᵀ + b/scale, dP = dO·Vᵀ - δ; dVᵀ += dOᵀ·P and
 // dKᵀ += qᵀ·dS straight from the accumulators; dS to LDS), phase 2 dQᵀ = Kᵀ·dSᵀ.  The biases are the
@@ -834,6 +1047,30 @@ __global__ void __launch_bounds__(576) winattn_bwd_bf16(
     }
 }
 
+// Forward kernel choice: 0 = one workgroup per (window, head) (winattn_fwd_bf16_rt), 1 = persistent
+// LDS-DMA pipelined (winattn_fwd_bf16_pp).  IRADS_WINATTN_FWD=rt|pp overrides (A/B measurements).
+int g_fwd_variant = -1;  // -1: not chosen yet
+
+int fwd_variant() {
+    if (g_fwd_variant < 0) {
+        const char *e = getenv("IRADS_WINATTN_FWD");
+        g_fwd_variant = (e && !strcmp(e, "pp")) ? 1 : 0;
+    }
+    return g_fwd_variant;
+}
+
+// persistent forward workgroups: PP_WG_PER_CU per CU (LDS-limited), IRADS_WINATTN_PP_WGS overrides
+int pp_slots() {
+    static int n = [] {
+        const char *e = getenv("IRADS_WINATTN_PP_WGS");
+        if (e && atoi(e) > 0) return atoi(e);
+        int dev = 0, cus = 256;
+        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        return PP_WG_PER_CU * cus;
+    }();
+    return n;
+}
+
 int chunk_windows(int total_windows, int nH, long target = 256) {  // target: persistent workgroups
     long cw = ((long)total_windows * nH + target - 1) / target;
     return (int)(cw < 1 ? 1 : cw);
@@ -878,6 +1115,12 @@ extern "C" int irads_winattn_bias_quads(const float *rel_table, int nH, float sc
 
 extern "C" long irads_winattn_bias_quads_size(int nH) { return (long)nH * QH; }
 
+extern "C" int irads_winattn_fwd_variant(int variant) {
+    const int prev = fwd_variant();
+    if (variant == 0 || variant == 1) g_fwd_variant = variant;
+    return prev;
+}
+
 extern "C" int irads_winattn_fwd(int dtype, const void *qkv, const float *qkv_bias, const float *rel_table,
                                  const float *bias_quads, const float *mask, int n_mask, int B, int H, int W, int C, int nH, int shift,
                                  float scale, void *out, float *lse, void *stream) {
@@ -894,10 +1137,21 @@ extern "C" int irads_winattn_fwd(int dtype, const void *qkv, const float *qkv_bi
         IRADS_REQUIRE(bias_quads, "irads_winattn_fwd: bf16 needs bias_quads (irads_winattn_bias_quads)");
         IRADS_REQUIRE(scale > 0.f, "irads_winattn_fwd: scale must be positive (%g)", scale);
         const float c2 = scale * LOG2E;
+        if (fwd_variant() == 1) {  // persistent, LDS-DMA pipelined (winattn_fwd_bf16_pp)
+            const int n_wg = pp_slots();
+            const long items = (long)B * g.nW * nH;
+            const int cw = (int)((items + n_wg - 1) / n_wg);
+            const unsigned nwg = (unsigned)(((B * g.nW + cw - 1) / cw) * nH);
+#define IRADS_WP(M) winattn_fwd_bf16_pp<M><<<nwg, 192, 0, st>>>((const unsigned short *)qkv, qkv_bias, bias_quads, \
+                                                                 mask, g, cw, c2, (unsigned short *)out, lse)
+            if (mm == 0) IRADS_WP(0); else if (mm == 1) IRADS_WP(1); else IRADS_WP(2);
+#undef IRADS_WP
+        } else {
 #define IRADS_WF(M) winattn_fwd_bf16_rt<M><<<nblk, 192, 0, st>>>((const unsigned short *)qkv, qkv_bias, bias_quads, \
                                                                   mask, g, c2, (unsigned short *)out, lse)
-        if (mm == 0) IRADS_WF(0); else if (mm == 1) IRADS_WF(1); else IRADS_WF(2);
+            if (mm == 0) IRADS_WF(0); else if (mm == 1) IRADS_WF(1); else IRADS_WF(2);
 #undef IRADS_WF
+        }
     }
     return check_launch("irads_winattn_fwd");
 }

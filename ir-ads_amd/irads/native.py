@@ -81,6 +81,7 @@ QUERIES = {"irads_wgrad_workspace": (ctypes.c_long, [_i, _i, _i]),
            "irads_ln_bf16_partials": (ctypes.c_long, [_l, _i]),
            "irads_bnact_partials": (ctypes.c_long, [_l, _i]),
            "irads_winattn_bias_quads_size": (ctypes.c_long, [_i]),
+           "irads_winattn_fwd_variant": (ctypes.c_int, [_i]),
            "irads_msda_bwd_workspace_bytes": (ctypes.c_long, [_i, _i, _i, _i, _i, _i, _i, _i]),
            "irads_dattn_attn_bwd_workspace_bytes": (ctypes.c_long, [_i] * 9),
            "irads_dattn_sample_bwd_workspace_bytes": (ctypes.c_long, [_i] * 5)}

@@ -322,10 +322,13 @@ def test_msda_gather_workspace_query(lib):
 
 # kernels allowed to use private (scratch) memory, none of them launched by the Swin-B / Swin-L
 # training steps: the window-attention backward's optional rel-table / pad-bias gradient variant
-# (EX = true; the Adapter step's tables and qkv bias are frozen), the DAttn kernels for head
+# (EX = true; the Adapter step's tables and qkv bias are frozen), the pipelined forward's
+# explicit-mask instance (MM = 2: WindowMSA.forward(x, mask) with a caller's mask; the stages
+# compute the shift mask in-kernel), the DAttn kernels for head
 # channels 16 / 24 (Swin-B and Swin-L DSCF blocks have 8 / 12), the fp64 LightSB kernels (the
 # reference-precision mode).  Every kernel the training steps launch must not.
 SCRATCH_ALLOWED = ("winattn_bwd_bf16ILi0ELb1E", "winattn_bwd_bf16ILi1ELb1E", "winattn_bwd_bf16ILi2ELb1E",
+                   "winattn_fwd_bf16_ppILi2E",
                    "dattn_attn_bwd_k_kernelILi16E", "dattn_attn_bwd_k_kernelILi24E", "dattn_attn_bwd_q_kernelILi24E",
                    "dattn_attn_bwd_k_band_kernelILi24E", "dattn_kpart_reduceILi24E", "dattn_kpart_reduceILi16E",
                    "dattn_sample_bwd_lds_kernelILi16E", "sb_drift_kernelIdE", "sb_em_kernelIdE",
