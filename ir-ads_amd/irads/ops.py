@@ -1040,7 +1040,6 @@ class LinearFn(torch.autograd.Function):
         ctx.save_for_backward(xb, wb)
         ctx.has_bias = bias is not None
         ctx.shape = shape
-        ctx.x_f32 = x.dtype == torch.float32
         return y.view(*shape[:-1], weight.shape[0])
 
     @staticmethod
@@ -1051,9 +1050,7 @@ class LinearFn(torch.autograd.Function):
             g = g.to(torch.bfloat16).contiguous()
         gx = gw = gb = None
         if ctx.needs_input_grad[0]:
-            # an fp32 input (DAttn's sampled features and attention output) gets its gradient
-            # straight from the GEMM's fp32 accumulator, not rounded to bf16 and cast back
-            gx = (torch.mm(g, wb, out_dtype=torch.float32) if ctx.x_f32 else torch.mm(g, wb)).view(ctx.shape)
+            gx = torch.mm(g, wb).view(ctx.shape)  # bf16, as autocast's F.linear backward
         if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
             o = wb.shape[0]
             if o % 8:  # narrow output: zero-pad dY to 8 columns (16-B rows for the kernel)
