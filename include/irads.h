@@ -296,18 +296,6 @@ int irads_resln_bwd(const uint16_t *dy, const float *x, const float *mean, const
  * keyed by seed ^ *seed_dev (seed_dev: one device uint64, or NULL for seed alone) so that a
  * captured HIP graph draws a fresh mask on every replay. */
 int irads_gelu_fwd(const uint16_t *u, uint16_t *g, long n, void *stream);
-/* The mmcv FFN's two GEMMs with the GELU in their epilogues (replace swin.py:586-601's
- * Linear(C, 4C) -> GELU -> and the GELU backward; the fused Swin stage's hidden tensor).
- * C[M x N] = A[M x K] · B[N x K]ᵀ, bf16 operands (K contiguous), fp32 accumulation; K % 64 == 0,
- * N % 128 == 0, 16-byte aligned pointers.
- *   fc1:  x (M, C) · w1 (4C, C)ᵀ + b1 (fp32)  ->  u = bf16(.) and g = bf16(GELU(u))   (K = C, N = 4C)
- *   fc2 dgrad:  dy (M, C) · w2t (4C, C)ᵀ, w2t = the fc2 weight (C, 4C) transposed
- *         ->  du = bf16(bf16(.) * GELU'(u))                                           (K = C, N = 4C)
- * Same element arithmetic as irads_gelu_fwd / irads_gelu_bwd on the GEMM's bf16 result. */
-int irads_ffn_fc1_gelu(const uint16_t *x, const uint16_t *w1, const float *b1, int M, int K, int N, uint16_t *u,
-                       uint16_t *g, void *stream);
-int irads_ffn_fc2_dgrad_dgelu(const uint16_t *dy, const uint16_t *w2t, const uint16_t *u, int M, int K, int N,
-                              uint16_t *du, void *stream);
 int irads_gelu_bwd(const uint16_t *u, const uint16_t *dg, uint16_t *du, long n, void *stream);
 int irads_relu_dropout_fwd(const uint16_t *a, uint16_t *r, long n, float p, uint64_t seed, const uint64_t *seed_dev,
                            void *stream);

@@ -48,8 +48,6 @@ SIGNATURES = {
     "irads_resln_fwd": [_vp, _vp, _vp, _vp, _f, _i, _i, _i, _vp, _vp, _f, _vp, _vp, _vp, _vp, _vp, _vp],
     "irads_resln_bwd": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _vp, _vp, _vp, _vp, _f, _vp],
     "irads_gelu_fwd": [_vp, _vp, _l, _vp],
-    "irads_ffn_fc1_gelu": [_vp, _vp, _vp, _i, _i, _i, _vp, _vp, _vp],
-    "irads_ffn_fc2_dgrad_dgelu": [_vp, _vp, _vp, _i, _i, _i, _vp, _vp],
     "irads_gelu_bwd": [_vp, _vp, _vp, _l, _vp],
     "irads_relu_dropout_fwd": [_vp, _vp, _l, _f, _u64, _vp, _vp],
     "irads_relu_dropout_bwd": [_vp, _vp, _vp, _l, _f, _vp],
