@@ -1,10 +1,9 @@
-"""vCLR DINO deformable transformer on the MI355X MSDeformAttn kernels
-(reference projects/vCLR_deformable_mask/modeling/__init__.py exports these three classes).
-
-The detector around it (ResNet-50 backbone, CDN query generation, Hungarian criteria, mask
-head, detectron2 trainer) is out of scope; ``attach_detection_heads``
-restates the part of ``DINO.__init__`` (dino.py:185-230) that the transformer's two-stage
-selection and box refinement read.
+"""vCLR DINO on the MI355X MSDeformAttn kernels (reference
+projects/vCLR_deformable_mask/modeling/__init__.py): the deformable transformer, the detector
+around it (dino.py: ResNet-50 + ChannelMapper features, contrastive-denoising queries, class /
+box / mask heads) and its criterion (dn_criterion.py / two_stage_criterion.py).
+``attach_detection_heads`` restates the part of ``DINO.__init__`` (dino.py:185-230) that the
+transformer's two-stage selection and box refinement read, for the transformer-only bench.
 """
 import copy
 import math
@@ -13,6 +12,8 @@ import torch.nn as nn
 
 from detrex.layers import MLP
 
+from .criterion import DINOCriterion
+from .dino import DINO
 from .dino_transformer import DINOTransformer, DINOTransformerDecoder, DINOTransformerEncoder
 
 
@@ -30,4 +31,5 @@ def attach_detection_heads(transformer: DINOTransformer, num_classes: int = 1, e
     return transformer
 
 
-__all__ = ["DINOTransformerEncoder", "DINOTransformerDecoder", "DINOTransformer", "attach_detection_heads"]
+__all__ = ["DINOTransformerEncoder", "DINOTransformerDecoder", "DINOTransformer", "attach_detection_heads", "DINO",
+           "DINOCriterion"]

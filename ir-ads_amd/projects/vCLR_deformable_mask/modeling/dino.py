@@ -1,0 +1,287 @@
+"""vCLR DINO detector around the MSDeformAttn transformer (reference
+projects/vCLR_deformable_mask/modeling/dino.py:113-270 (__init__), 727-922 (forward_student),
+974-1149 (aux outputs, contrastive denoising queries, dn post-processing), 1151-1159 and
+1258-1274 (image and target preparation)).
+
+Built: the student's training forward (ResNet-50 -> ChannelMapper -> masks and sine position
+embeddings -> CDN queries -> DINOTransformer on the HIP MSDA kernels -> per-layer class / box /
+ROI / mask heads with the encoder-memory segmentation features -> dn split -> DINOCriterion) and
+the same path without targets for inference outputs.  Not built: the EMA teacher
+and its pseudo-boxes (infer_results / forward_ema), the strong-augmentation mix / erase /
+grayscale of the student input, the consistency criterion they feed, and the NMS post-processing
+to detectron2 Instances.  ``forward(batched_inputs)`` therefore runs forward_student on the
+normalised images with ``siamese_outputs=None`` (the reference's consistency loss is skipped
+exactly in that case, dino.py:914).
+
+Inputs: ``batched_inputs`` as detectron2 passes them: dicts with "image" (3, H, W) unnormalised
+and, in training, "instances" with ``image_size``, ``gt_boxes`` (xyxy pixels, a tensor or an object
+with ``.tensor``), ``gt_classes`` and ``gt_masks`` (n, h, w).  Random draws (label / box noise of
+the denoising queries) go through ``self.rng`` (``torch``)."""
+import copy
+import math
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from detrex.layers import MLP
+from detrex.layers.box_ops import box_xyxy_to_cxcywh
+from detrex.utils import inverse_sigmoid
+
+
+def _boxes_tensor(b):
+    return b.tensor if hasattr(b, "tensor") else b
+
+
+def pad_images(images, size_divisibility=0):
+    """detectron2 ImageList.from_tensors: bottom/right zero padding to the largest image."""
+    H = max(int(i.shape[-2]) for i in images)
+    W = max(int(i.shape[-1]) for i in images)
+    if size_divisibility > 1:
+        H = -(-H // size_divisibility) * size_divisibility
+        W = -(-W // size_divisibility) * size_divisibility
+    out = images[0].new_zeros((len(images), images[0].shape[0], H, W))
+    for o, im in zip(out, images):
+        o[:, :im.shape[-2], :im.shape[-1]].copy_(im)
+    return out, [tuple(int(s) for s in im.shape[-2:]) for im in images]
+
+
+class DINO(nn.Module):
+    def __init__(self, backbone, position_embedding, neck, transformer, embed_dim, num_classes, num_queries,
+                 criterion, pixel_mean=(123.675, 116.280, 103.530), pixel_std=(58.395, 57.120, 57.375),
+                 aux_loss=True, select_box_nums_for_evaluation=300, device="cuda", dn_number=100,
+                 label_noise_ratio=0.2, box_noise_scale=1.0, input_format="RGB", vis_period=0, depth_net=None,
+                 r50_extractor=None, consistency_criterion=None):
+        super().__init__()
+        self.backbone, self.position_embedding, self.neck = backbone, position_embedding, neck
+        self.num_queries, self.embed_dim, self.transformer = num_queries, embed_dim, transformer
+        self.depth_model, self.r50_extractor = depth_net, r50_extractor
+        self.num_classes, self.aux_loss, self.criterion = num_classes, aux_loss, criterion
+        self.consistency_criterion = consistency_criterion
+        self.label_enc = nn.Embedding(num_classes, embed_dim)
+        self.dn_number, self.label_noise_ratio, self.box_noise_scale = dn_number, label_noise_ratio, box_noise_scale
+        self.device = device
+        self.register_buffer("pixel_mean", torch.tensor(pixel_mean).view(-1, 1, 1), persistent=False)
+        self.register_buffer("pixel_std", torch.tensor(pixel_std).view(-1, 1, 1), persistent=False)
+        self.select_box_nums_for_evaluation = select_box_nums_for_evaluation
+        self.input_format, self.vis_period = input_format, vis_period
+        self.rng = torch
+        # heads (dino.py:185-230): shared initialisation, then one copy per decoder layer + encoder
+        class_embed = nn.Linear(embed_dim, num_classes)
+        bbox_embed = MLP(embed_dim, embed_dim, 4, 3)
+        class_embed.bias.data = torch.ones(num_classes) * -math.log((1 - 0.01) / 0.01)
+        nn.init.constant_(bbox_embed.layers[-1].weight.data, 0)
+        nn.init.constant_(bbox_embed.layers[-1].bias.data, 0)
+        for _, layer in self.neck.named_modules():
+            if isinstance(layer, nn.Conv2d):
+                nn.init.xavier_uniform_(layer.weight, gain=1)
+                nn.init.constant_(layer.bias, 0)
+        n = transformer.decoder.num_layers + 1
+        self.class_embed = nn.ModuleList(copy.deepcopy(class_embed) for _ in range(n))
+        self.bbox_embed = nn.ModuleList(copy.deepcopy(bbox_embed) for _ in range(n))
+        nn.init.constant_(self.bbox_embed[0].layers[-1].bias.data[2:], -2.0)
+        self.transformer.decoder.class_embed = self.class_embed
+        self.transformer.decoder.bbox_embed = self.bbox_embed
+        for b in self.bbox_embed:
+            nn.init.constant_(b.layers[-1].bias.data[2:], 0.0)
+        roi = nn.Sequential(MLP(embed_dim, embed_dim, 1024, 3), nn.ReLU())
+        self.ROI_embed = nn.ModuleList(copy.deepcopy(roi) for _ in range(n))
+        if self.r50_extractor is not None:
+            for p in self.r50_extractor.parameters():
+                p.requires_grad = False
+        mask = MLP(embed_dim, embed_dim, 1024, 3)
+        self.mask_embed = nn.ModuleList(copy.deepcopy(mask) for _ in range(n))
+        self.transformer.decoder.mask_embed = self.mask_embed
+        self.mapping_fpn_features_for_seg = nn.Sequential(nn.Conv2d(1024, 2048, 3, 1, 1), nn.BatchNorm2d(2048),
+                                                          nn.ReLU(), nn.Conv2d(2048, 1024, 3, 1, 1))
+        self.post_layernorm = nn.LayerNorm(1024)
+
+    # ---------------------------------------------------------------- inputs
+    def preprocess_image(self, batched_inputs):
+        dev = self.pixel_mean.device
+        ims = [(x["image"].to(dev).to(self.pixel_mean.dtype) - self.pixel_mean) / self.pixel_std for x in batched_inputs]
+        return pad_images(ims)
+
+    def prepare_targets(self, batched_inputs, padded_hw):
+        dev = self.pixel_mean.device
+        h_pad, w_pad = padded_hw
+        out = []
+        for x in batched_inputs:
+            inst = x["instances"]
+            h, w = inst.image_size if hasattr(inst, "image_size") else inst["image_size"]
+            get = (lambda k: getattr(inst, k)) if hasattr(inst, "gt_classes") else (lambda k: inst[k])
+            wh = torch.as_tensor([w, h, w, h], dtype=self.pixel_mean.dtype, device=dev)
+            boxes = box_xyxy_to_cxcywh(_boxes_tensor(get("gt_boxes")).to(dev).to(wh.dtype) / wh)
+            gm = get("gt_masks").to(dev)
+            masks = torch.zeros((gm.shape[0], h_pad, w_pad), dtype=gm.dtype, device=dev)
+            masks[:, :gm.shape[1], :gm.shape[2]] = gm
+            out.append({"labels": get("gt_classes").to(dev), "boxes": boxes, "masks": masks})
+        return out
+
+    # ---------------------------------------------------------------- forward
+    def forward(self, batched_inputs):
+        images, sizes = self.preprocess_image(batched_inputs)
+        B, _, H, W = images.shape
+        if self.training:
+            img_masks = images.new_ones(B, H, W)
+            for i, x in enumerate(batched_inputs):
+                ih, iw = (x["instances"].image_size if hasattr(x["instances"], "image_size")
+                          else x["instances"]["image_size"])
+                img_masks[i, :ih, :iw] = 0
+        else:
+            img_masks = images.new_zeros(B, H, W)
+        return self.forward_student(batched_inputs, images, img_masks)
+
+    def forward_student(self, batched_inputs, images, img_masks, ema_gts=None):
+        targets = self.prepare_targets(batched_inputs, images.shape[-2:]) if self.training else None
+        features = self.backbone(images)
+        feats = self.neck(features)
+        masks, pos = [], []
+        for f in feats:
+            masks.append(F.interpolate(img_masks[None], size=f.shape[-2:]).to(torch.bool).squeeze(0))
+            pos.append(self.position_embedding(masks[-1]))
+        if self.training:
+            if ema_gts is not None:
+                for t, e in zip(targets, ema_gts):
+                    if e["labels"].shape[0]:
+                        t["labels"] = torch.cat([t["labels"], e["labels"]], 0)
+                        t["boxes"] = torch.cat([t["boxes"], e["boxes"]])
+            q_label, q_bbox, attn_mask, dn_meta = self.prepare_for_cdn(targets)
+        else:
+            q_label = q_bbox = attn_mask = dn_meta = None
+        inter_states, init_ref, inter_refs, enc_state, enc_ref, enc_memory = self.transformer(
+            feats, masks, pos, (q_label, q_bbox), attn_masks=[attn_mask, None])
+        inter_states[0] += self.label_enc.weight[0, 0] * 0.0  # every parameter in the graph (dino.py:816)
+        # segmentation features: the encoder memory of every level at the finest level's size
+        rh, rw = feats[0].shape[2:]
+        segs, start = [], 0
+        for f in feats:
+            hh, ww = f.shape[-2:]
+            m = enc_memory[:, start:start + hh * ww, :].reshape(enc_memory.shape[0], hh, ww, -1).permute(0, 3, 1, 2)
+            segs.append(F.interpolate(m, (rh, rw), mode="bilinear", align_corners=True))
+            start += hh * ww
+        seg = torch.cat(segs, dim=1)
+        seg = self.mapping_fpn_features_for_seg(seg) + seg
+        seg = self.post_layernorm(seg.permute(0, 2, 3, 1)).permute(0, 3, 1, 2)
+        seg_flat = seg.flatten(2)
+        classes, coords, rois, queries, pmasks = [], [], [], [], []
+        for lvl in range(inter_states.shape[0]):
+            ref = inverse_sigmoid(init_ref if lvl == 0 else inter_refs[lvl - 1])
+            st = inter_states[lvl]
+            classes.append(self.class_embed[lvl](st))
+            rois.append(self.ROI_embed[lvl](st))
+            me = self.mask_embed[lvl](st)
+            pmasks.append(torch.bmm(me, seg_flat).reshape(me.shape[0], me.shape[1], rh, rw))
+            tmp = self.bbox_embed[lvl](st)
+            if ref.shape[-1] == 4:
+                tmp = tmp + ref
+            else:
+                tmp = torch.cat([tmp[..., :2] + ref, tmp[..., 2:]], -1)
+            coords.append(tmp.sigmoid())
+            queries.append(st)
+        cls, crd, roi, qry, msk = (torch.stack(v) for v in (classes, coords, rois, queries, pmasks))
+        if dn_meta is not None:
+            cls, crd, roi, msk = self.dn_post_process(cls, crd, dn_meta, roi, qry, msk)
+            if dn_meta["single_padding"] > 0:
+                qry = qry[:, :, dn_meta["single_padding"] * dn_meta["dn_num"]:, :]
+        output = {"pred_logits": cls[-1], "pred_boxes": crd[-1], "pred_rois": roi[-1], "pred_queries": qry[-1],
+                  "pred_masks": msk[-1]}
+        if self.aux_loss:
+            output["aux_outputs"] = self._set_aux_loss(cls, crd, roi, qry, msk)
+        enc_cls = self.transformer.decoder.class_embed[-1](enc_state)
+        enc_roi = self.ROI_embed[-1](enc_state)
+        me = self.mask_embed[-1](enc_state)
+        enc_msk = torch.bmm(me, seg_flat).reshape(me.shape[0], me.shape[1], rh, rw)
+        output["enc_outputs"] = {"pred_logits": enc_cls, "pred_boxes": enc_ref, "pred_rois": enc_roi,
+                                 "pred_masks": enc_msk}
+        if not self.training:
+            return output
+        loss_dict = self.criterion(output, targets, dn_meta)
+        for k in loss_dict:
+            if k in self.criterion.weight_dict:
+                loss_dict[k] = loss_dict[k] * self.criterion.weight_dict[k]
+        return loss_dict
+
+    @staticmethod
+    def _set_aux_loss(cls, crd, roi, qry, msk):
+        return [{"pred_logits": a, "pred_boxes": b, "pred_rois": c, "pred_queries": d, "pred_masks": e}
+                for a, b, c, d, e in zip(cls[:-1], crd[:-1], roi[:-1], qry[:-1], msk[:-1])]
+
+    def prepare_for_cdn(self, targets):
+        """Contrastive denoising queries (dino.py:983-1126): dn_number groups of positive and
+        negative noised copies of every GT box / label, and the attention mask that keeps the
+        groups and the matching queries apart."""
+        dn_number = self.dn_number
+        if dn_number <= 0:
+            return None, None, None, None
+        dn_number = dn_number * 2
+        dev = self.label_enc.weight.device
+        known = [torch.ones_like(t["labels"]).to(dev) for t in targets]
+        bs = len(known)
+        known_num = [int(k.sum()) for k in known]
+        if max(known_num) == 0:
+            return None, None, None, None
+        dn_number = max(1, dn_number // (max(known_num) * 2))
+        unmask = torch.cat(known)
+        labels = torch.cat([t["labels"] for t in targets])
+        boxes = torch.cat([t["boxes"] for t in targets])
+        batch_idx = torch.cat([torch.full_like(t["labels"].long(), i) for i, t in enumerate(targets)])
+        known_labels = labels.repeat(2 * dn_number, 1).view(-1)
+        known_bid = batch_idx.repeat(2 * dn_number, 1).view(-1)
+        known_bboxs = boxes.repeat(2 * dn_number, 1)
+        labels_exp = known_labels.clone()
+        bbox_exp = known_bboxs.clone()
+        if self.label_noise_ratio > 0:
+            p = self.rng.rand_like(labels_exp.float())
+            chosen = torch.nonzero(p < (self.label_noise_ratio * 0.5)).view(-1)
+            labels_exp.scatter_(0, chosen, self.rng.randint_like(chosen, 0, self.num_classes))
+        single_padding = max(known_num)
+        pad_size = int(single_padding * 2 * dn_number)
+        pos_idx = torch.arange(len(boxes), device=dev).long().unsqueeze(0).repeat(dn_number, 1)
+        pos_idx += (torch.arange(dn_number, device=dev) * len(boxes) * 2).long().unsqueeze(1)
+        pos_idx = pos_idx.flatten()
+        neg_idx = pos_idx + len(boxes)
+        if self.box_noise_scale > 0:
+            xyxy = torch.cat([known_bboxs[:, :2] - known_bboxs[:, 2:] / 2, known_bboxs[:, :2] + known_bboxs[:, 2:] / 2], 1)
+            diff = torch.cat([known_bboxs[:, 2:] / 2, known_bboxs[:, 2:] / 2], 1)
+            sign = self.rng.randint_like(known_bboxs, low=0, high=2, dtype=torch.float32).to(known_bboxs.dtype) * 2.0 - 1.0
+            part = self.rng.rand_like(known_bboxs)
+            part[neg_idx] += 1.0
+            part *= sign
+            xyxy = (xyxy + part * diff * self.box_noise_scale).clamp(min=0.0, max=1.0)
+            bbox_exp = torch.cat([(xyxy[:, :2] + xyxy[:, 2:]) / 2, xyxy[:, 2:] - xyxy[:, :2]], 1)
+        label_embed = self.label_enc(labels_exp.long().to(dev))
+        bbox_embed = inverse_sigmoid(bbox_exp)
+        q_label = torch.zeros(bs, pad_size, self.embed_dim, device=dev, dtype=label_embed.dtype)
+        q_bbox = torch.zeros(bs, pad_size, 4, device=dev, dtype=bbox_embed.dtype)
+        map_idx = torch.cat([torch.arange(n) for n in known_num])
+        map_idx = torch.cat([map_idx + single_padding * i for i in range(2 * dn_number)]).long().to(dev)
+        if len(known_bid):
+            q_label = q_label.index_put((known_bid.long(), map_idx), label_embed)
+            q_bbox = q_bbox.index_put((known_bid.long(), map_idx), bbox_embed)
+        tgt_size = pad_size + self.num_queries
+        attn = torch.zeros(tgt_size, tgt_size, dtype=torch.bool, device=dev)
+        attn[pad_size:, :pad_size] = True
+        sp2 = single_padding * 2
+        for i in range(dn_number):
+            r = slice(sp2 * i, sp2 * (i + 1))
+            if i == 0:
+                attn[r, sp2 * (i + 1):pad_size] = True
+            if i == dn_number - 1:
+                attn[r, :sp2 * i] = True
+            else:
+                attn[r, sp2 * (i + 1):pad_size] = True
+                attn[r, :sp2 * i] = True
+        return q_label, q_bbox, attn, {"single_padding": sp2, "dn_num": dn_number}
+
+    def dn_post_process(self, cls, crd, dn_meta, roi, qry, msk):
+        if dn_meta and dn_meta["single_padding"] > 0:
+            p = dn_meta["single_padding"] * dn_meta["dn_num"]
+            out = {"pred_logits": cls[-1, :, :p], "pred_boxes": crd[-1, :, :p], "pred_rois": roi[-1, :, :p],
+                   "outputs_query": qry[-1, :, :p], "pred_masks": msk[-1, :, :p]}
+            if self.aux_loss:
+                out["aux_outputs"] = self._set_aux_loss(cls[:, :, :p], crd[:, :, :p], roi[:, :, :p], qry[:, :, :p],
+                                                        msk[:, :, :p])
+            dn_meta["output_known_lbs_bboxes"] = out
+            cls, crd, roi, msk = cls[:, :, p:], crd[:, :, p:], roi[:, :, p:], msk[:, :, p:]
+        return cls, crd, roi, msk

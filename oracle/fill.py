@@ -42,11 +42,21 @@ def _values(name, shape, seed):
 
 
 @torch.no_grad()
-def fill_module(module: torch.nn.Module, seed: int = 0) -> torch.nn.Module:
-    """Overwrite every floating-point parameter/buffer of ``module`` in place."""
-    for name, t in module.state_dict(keep_vars=True).items():
+def fill_module(module: torch.nn.Module, seed: int = 0, dedup: bool = False) -> torch.nn.Module:
+    """Overwrite every floating-point parameter/buffer of ``module`` in place.  dedup: a tensor
+    registered under several names (DINO's heads, shared with its decoder) is filled once, from
+    its alphabetically first name, so the result does not depend on module registration order."""
+    items = module.state_dict(keep_vars=True).items()
+    seen = set()
+    if dedup:
+        items = sorted(items)
+    for name, t in items:
         if any(s in name for s in _SKIP) or not t.is_floating_point() or t.dim() == 0:
             continue
+        if dedup:
+            if id(t) in seen:
+                continue
+            seen.add(id(t))
         v = torch.from_numpy(_values(name, tuple(t.shape), seed)).to(t.dtype)
         t.data.copy_(v.to(t.device))
     return module

@@ -587,6 +587,117 @@ DINO_FULL_GRADS = ("level_embeds", "encoder.layers.0.attentions.0.sampling_offse
                    "decoder.bbox_embed.2.layers.2.bias", "tgt_embed.weight")
 
 
+def _det_reference_model(L, dtype):
+    """The reference detector (dino.py) at the reduced dino_det_case configuration."""
+    from dino_det_case import DET_CFG, DET_FILL_SEED, DET_NUM_POINTS, det_weight_dict
+    S = L.ShapeSpec
+    c = DET_CFG
+    backbone = L.resnet.ResNet(stem=L.resnet.BasicStem(in_channels=3, out_channels=64, norm="FrozenBN"),
+                               stages=L.resnet.ResNet.make_default_stages(depth=50, stride_in_1x1=False, norm="FrozenBN"),
+                               out_features=["res3", "res4", "res5"], freeze_at=1)
+    neck = L.neck.ChannelMapper(input_shapes={"res3": S(channels=512), "res4": S(channels=1024), "res5": S(channels=2048)},
+                                in_features=["res3", "res4", "res5"], out_channels=256, num_outs=4, kernel_size=1,
+                                norm_layer=torch.nn.GroupNorm(num_groups=32, num_channels=256))
+    d = L.dino
+    tr = d.DINOTransformer(
+        encoder=d.DINOTransformerEncoder(embed_dim=256, num_heads=8, feedforward_dim=2048, attn_dropout=0.0,
+                                         ffn_dropout=0.0, num_layers=c["enc_layers"], post_norm=False,
+                                         num_feature_levels=4, use_checkpoint=False),
+        decoder=d.DINOTransformerDecoder(embed_dim=256, num_heads=8, feedforward_dim=2048, attn_dropout=0.0,
+                                         ffn_dropout=0.0, num_layers=c["dec_layers"], return_intermediate=True,
+                                         num_feature_levels=4, use_checkpoint=False),
+        num_feature_levels=4, two_stage_num_proposals=c["num_queries"])
+    matcher = L.matcher.HungarianMatcher(cost_class=2.0, cost_bbox=5.0, cost_giou=2.0,
+                                         cost_class_type="focal_loss_cost", alpha=0.25, gamma=2.0)
+    crit = L.criterion.DINOCriterion(num_classes=c["num_classes"], matcher=matcher,
+                                     weight_dict=det_weight_dict(c["dec_layers"]), loss_class_type="focal_loss",
+                                     alpha=0.25, gamma=2.0, two_stage_binary_cls=False)
+    crit.num_points = DET_NUM_POINTS
+    pe = L.detrex_layers.PositionEmbeddingSine(num_pos_feats=128, temperature=10000, normalize=True, offset=-0.5)
+    model = L.dino_det.DINO(backbone=backbone, position_embedding=pe, neck=neck, transformer=tr, embed_dim=256,
+                            num_classes=c["num_classes"], num_queries=c["num_queries"], criterion=crit, aux_loss=True,
+                            device="cpu", dn_number=c["dn_number"], label_noise_ratio=c["label_noise_ratio"],
+                            box_noise_scale=c["box_noise_scale"])
+    fill_module(model, seed=DET_FILL_SEED, dedup=True)
+    return model.to(dtype).train()
+
+
+def _det_reference_step(L, dtype, rng):
+    """forward_student + the loss sum + backward of the reference on the CPU in `dtype`, with the
+    random draws from `rng`; the reference's .cuda() / .to("cuda") calls are CPU no-ops here."""
+    from dino_det_case import canonical_params, det_inputs
+    model = _det_reference_model(L, dtype)
+    batched = []
+    for img, boxes, cls, masks in det_inputs():
+        inst = L.Instances(tuple(img.shape[1:]), gt_boxes=L.Boxes(t(boxes, dtype)), gt_classes=t(cls),
+                           gt_masks=t(masks))
+        batched.append({"image": t(img, dtype), "instances": inst})
+    orig = {k: getattr(torch, k) for k in ("rand", "rand_like", "randint_like")}
+    orig_cuda, orig_to = torch.Tensor.cuda, torch.Tensor.to
+
+    def to_cpu(self, *a, **k):
+        if a and (a[0] == "cuda" or (isinstance(a[0], torch.device) and a[0].type == "cuda")):
+            a = ("cpu",) + a[1:]
+        if k.get("device") == "cuda":
+            k["device"] = "cpu"
+        return orig_to(self, *a, **k)
+    default = torch.get_default_dtype()
+    try:
+        # the reference allocates its query paddings with the default dtype (dino.py:1079-1080)
+        torch.set_default_dtype(dtype)
+        torch.rand, torch.rand_like, torch.randint_like = rng.rand, rng.rand_like, rng.randint_like
+        torch.Tensor.cuda = lambda self, *a, **k: self
+        torch.Tensor.to = to_cpu
+        images = model.preprocess_image(batched)
+        B, _, H, W = images.tensor.shape
+        img_masks = images.tensor.new_ones(B, H, W)
+        for i, x in enumerate(batched):
+            ih, iw = x["instances"].image_size
+            img_masks[i, :ih, :iw] = 0
+        losses = model.forward_student(batched, images, img_masks)
+        total = sum(losses.values())
+        total.backward()
+    finally:
+        for k, v in orig.items():
+            setattr(torch, k, v)
+        torch.Tensor.cuda, torch.Tensor.to = orig_cuda, orig_to
+        torch.set_default_dtype(default)
+    return losses, total, canonical_params(model)
+
+
+def gen_dino_detector(ref):
+    """vCLR DINO detector training step (reduced, dino_det_case.py) in fp64 and fp32 on the
+    reference; the fp32 run replays the fp64 run's random draws."""
+    from dino_det_case import ReplayRNG, RecordingRNG
+    from train_fixture import N_PROJ, projection
+    L = __import__("ref_import").load_dino_detector()
+    rec = RecordingRNG(2024)
+    l64, tot64, p64 = _det_reference_step(L, torch.float64, rec)
+    l32, tot32, p32 = _det_reference_step(L, torch.float32, ReplayRNG(rec.draws))
+    keys = sorted(l64)
+    res = {"loss_keys": np.array(keys), "loss64": np.array([float(l64[k]) for k in keys]),
+           "loss32": np.array([float(l32[k]) for k in keys]), "total64": float(tot64), "total32": float(tot32),
+           "n_draws": len(rec.draws)}
+    for i, d in enumerate(rec.draws):
+        res[f"draw_{i}"] = d.numpy()
+    names = [n for n, _ in p64]
+    assert names == [n for n, _ in p32]
+    norms, projs, ref32 = [], [], []
+    for (n, p), (_, q) in zip(p64, p32):
+        g = p.grad.numpy() if p.grad is not None else np.zeros(tuple(p.shape))
+        g32 = q.grad.double().numpy() if q.grad is not None else np.zeros(tuple(q.shape))
+        nr = float(np.sqrt((g * g).sum()))
+        norms.append(nr)
+        projs.append([projection(n, g, j) for j in range(N_PROJ)])
+        ref32.append(float(np.sqrt(((g32 - g) ** 2).sum())) / max(nr, 1e-300))
+    res.update(grad_names=np.array(names), grad_norms=np.array(norms), grad_projs=np.array(projs),
+               ref32_rel=np.array(ref32))
+    for n, p in p64:  # a few full gradients (the heads and queries)
+        if p.numel() <= 4096 and p.grad is not None:
+            res["g." + n] = p.grad.numpy()
+    save("dino_detector_step.npz", **res)
+
+
 def gen_dino(ref):
     L = __import__("ref_import").load_dino()
     torch.manual_seed(0)
@@ -711,7 +822,7 @@ if __name__ == "__main__":
     which = sys.argv[1:] or ["msda", "swin", "block", "dattn", "fusion", "cmnext", "sb", "metrics", "train"]
     ref = load_reference()
     torch.manual_seed(0)
-    fns = {"dino": gen_dino, "msda": gen_msda, "swin": gen_swin_wmsa, "block": gen_swin_block, "dattn": gen_dattn,
+    fns = {"dino": gen_dino, "dino_detector": gen_dino_detector, "msda": gen_msda, "swin": gen_swin_wmsa, "block": gen_swin_block, "dattn": gen_dattn,
            "fusion": gen_fusion_small, "cmnext": gen_cmnext, "sb": gen_sb, "metrics": gen_metrics_loss,
            "train": gen_cmnext_train, "train64": gen_cmnext_train_fp64, "msf": gen_msf}
     for w in which:

@@ -233,3 +233,205 @@ def load_val_mm():
 if __name__ == "__main__":
     r = load_reference()
     print(sorted(vars(r)))
+
+
+# ---------------------------------------------------------------------------------------------
+# vCLR DINO detector (projects/vCLR_deformable_mask/modeling/dino.py + its criteria) for the
+# reduced training-step fixture.  Stand-ins, restating the published detectron2 0.6 / fvcore /
+# torchvision pieces the detector path uses (their arithmetic is therefore parity unpinned):
+#   detectron2.layers: Conv2d(norm=, activation=), FrozenBatchNorm2d (eps 1e-5), get_norm,
+#     CNNBlockBase, ShapeSpec; detectron2.modeling.backbone.Backbone;
+#   detectron2.structures: Boxes (.tensor), ImageList.from_tensors (bottom/right zero padding),
+#     Instances (image_size + fields);
+#   detectron2.projects.point_rend.point_features: point_sample (grid_sample of 2p - 1) and
+#     get_uncertain_point_coords_with_randomness (uniform oversampling, top-k uncertainty,
+#     uniform fill);
+#   fvcore.nn.weight_init.c2_msra_fill (the fixture overwrites every weight anyway);
+#   torchvision._is_tracing -> False, torchvision.ops.boxes.box_area ((x1 - x0)(y1 - y0));
+#   detrex.utils dist helpers for one process;
+#   detrex.modeling.ema, NMS, event storage, image-format conversion: unused by the training
+#   forward (None).
+# The reference calls .cuda() / .to("cuda") inside prepare_for_cdn and the dn criterion; for
+# this CPU-only generation those become no-ops (patched only while the fixture is made).
+class _D2Conv2d(nn.Conv2d):
+    def __init__(self, *args, **kwargs):
+        norm = kwargs.pop("norm", None)
+        activation = kwargs.pop("activation", None)
+        super().__init__(*args, **kwargs)
+        self.norm, self.activation = norm, activation
+
+    def forward(self, x):
+        x = torch.nn.functional.conv2d(x, self.weight, self.bias, self.stride, self.padding, self.dilation,
+                                       self.groups)
+        if self.norm is not None:
+            x = self.norm(x)
+        if self.activation is not None:
+            x = self.activation(x)
+        return x
+
+
+class _FrozenBN(nn.Module):
+    def __init__(self, num_features, eps=1e-5):
+        super().__init__()
+        self.num_features, self.eps = num_features, eps
+        self.register_buffer("weight", torch.ones(num_features))
+        self.register_buffer("bias", torch.zeros(num_features))
+        self.register_buffer("running_mean", torch.zeros(num_features))
+        self.register_buffer("running_var", torch.ones(num_features) - eps)
+
+    def forward(self, x):
+        scale = self.weight * (self.running_var + self.eps).rsqrt()
+        bias = self.bias - self.running_mean * scale
+        return x * scale.reshape(1, -1, 1, 1).to(x.dtype) + bias.reshape(1, -1, 1, 1).to(x.dtype)
+
+
+class _CNNBlockBase(nn.Module):
+    def __init__(self, in_channels, out_channels, stride):
+        super().__init__()
+        self.in_channels, self.out_channels, self.stride = in_channels, out_channels, stride
+
+    def freeze(self):
+        for p in self.parameters():
+            p.requires_grad = False
+        return self
+
+
+def _get_norm(norm, out_channels):
+    if norm is None or norm == "":
+        return None
+    return {"FrozenBN": _FrozenBN, "BN": nn.BatchNorm2d}[norm](out_channels)
+
+
+class _Backbone(nn.Module):
+    @property
+    def size_divisibility(self):
+        return 0
+
+
+class _Boxes:
+    def __init__(self, tensor):
+        self.tensor = tensor
+
+
+class _ImageList:
+    def __init__(self, tensor, image_sizes):
+        self.tensor, self.image_sizes = tensor, image_sizes
+
+    @staticmethod
+    def from_tensors(tensors, size_divisibility=0, pad_value=0.0):
+        H = max(t.shape[-2] for t in tensors)
+        W = max(t.shape[-1] for t in tensors)
+        out = tensors[0].new_full((len(tensors), tensors[0].shape[0], H, W), pad_value)
+        for o, t in zip(out, tensors):
+            o[:, :t.shape[-2], :t.shape[-1]].copy_(t)
+        return _ImageList(out, [tuple(t.shape[-2:]) for t in tensors])
+
+
+class _Instances:
+    def __init__(self, image_size, **fields):
+        self.image_size = image_size
+        for k, v in fields.items():
+            setattr(self, k, v)
+
+    def to(self, device):
+        return self
+
+
+def _point_sample(input, point_coords, **kwargs):
+    add_dim = point_coords.dim() == 3
+    if add_dim:
+        point_coords = point_coords.unsqueeze(2)
+    out = torch.nn.functional.grid_sample(input, 2.0 * point_coords - 1.0, **kwargs)
+    return out.squeeze(3) if add_dim else out
+
+
+def _uncertain_points(coarse_logits, uncertainty_func, num_points, oversample_ratio, importance_sample_ratio):
+    num_boxes = coarse_logits.shape[0]
+    num_sampled = int(num_points * oversample_ratio)
+    point_coords = torch.rand(num_boxes, num_sampled, 2, device=coarse_logits.device)
+    point_logits = _point_sample(coarse_logits, point_coords, align_corners=False)
+    point_uncertainties = uncertainty_func(point_logits)
+    num_uncertain = int(importance_sample_ratio * num_points)
+    num_random = num_points - num_uncertain
+    idx = torch.topk(point_uncertainties[:, 0, :], k=num_uncertain, dim=1)[1]
+    shift = num_sampled * torch.arange(num_boxes, dtype=torch.long, device=coarse_logits.device)
+    idx += shift[:, None]
+    point_coords = point_coords.view(-1, 2)[idx.view(-1), :].view(num_boxes, num_uncertain, 2)
+    if num_random > 0:
+        point_coords = torch.cat([point_coords, torch.rand(num_boxes, num_random, 2, device=coarse_logits.device)], 1)
+    return point_coords
+
+
+def _c2_msra_fill(m):
+    nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+    if m.bias is not None:
+        nn.init.constant_(m.bias, 0)
+
+
+def _pkg(name):
+    m = _mod(name)
+    m.__path__ = []
+    return m
+
+
+def load_dino_detector():
+    """The reference DINO detector, its criteria, matcher, ResNet and ChannelMapper (see above)."""
+    import collections
+    ref = load_dino()
+    if "dino_det" in _LOADED:
+        return ref
+    _ShapeSpec = collections.namedtuple("ShapeSpec", ["channels", "height", "width", "stride"],
+                                        defaults=(None, None, None, None))
+    for p in ("detectron2", "detectron2.utils", "detectron2.data", "detectron2.modeling", "detectron2.projects",
+              "detectron2.projects.point_rend"):
+        _pkg(p)
+    _mod("detectron2.layers", Conv2d=_D2Conv2d, FrozenBatchNorm2d=_FrozenBN, get_norm=_get_norm,
+         CNNBlockBase=_CNNBlockBase, ShapeSpec=_ShapeSpec, DeformConv=None, ModulatedDeformConv=None,
+         cat=torch.cat).__path__ = []
+    _mod("detectron2.layers.nms", batched_nms=None)
+    _mod("detectron2.modeling.backbone", Backbone=_Backbone)
+    _mod("detectron2.structures", Boxes=_Boxes, ImageList=_ImageList, Instances=_Instances, ROIMasks=None)
+    _mod("detectron2.utils.events", get_event_storage=None)
+    _mod("detectron2.data.detection_utils", convert_image_to_rgb=None)
+    _mod("detectron2.projects.point_rend.point_features", point_sample=_point_sample,
+         get_uncertain_point_coords_with_randomness=_uncertain_points)
+    _pkg("fvcore")
+    _mod("fvcore.nn.weight_init", c2_msra_fill=_c2_msra_fill)
+    sys.modules["fvcore.nn"].weight_init = sys.modules["fvcore.nn.weight_init"]
+    tv = _mod("torchvision")
+    tv._is_tracing = lambda: False
+    tv.__path__ = []
+    _pkg("torchvision.ops")
+    _mod("torchvision.ops.boxes", box_area=lambda b: (b[:, 2] - b[:, 0]) * (b[:, 3] - b[:, 1]))
+    import torch.distributed as tdist
+    du = sys.modules["detrex.utils"]
+    du.get_world_size = lambda: tdist.get_world_size() if tdist.is_available() and tdist.is_initialized() else 1
+    du.is_dist_avail_and_initialized = lambda: tdist.is_available() and tdist.is_initialized()
+    lay = sys.modules["detrex.layers"]
+    for name, rel in (("box_ops", "box_ops.py"), ("conv", "conv.py"), ("shape_spec", "shape_spec.py")):
+        m = _load(f"detrex.layers.{name}", f"detrex/layers/{rel}")
+        for k in dir(m):
+            if not k.startswith("_"):
+                setattr(lay, k, getattr(m, k))
+    _pkg("detrex.modeling")
+    _mod("detrex.modeling.ema", apply_model_ema_and_restore=None)
+    sys.modules["detrex.modeling"].ema = sys.modules["detrex.modeling.ema"]
+    _pkg("detrex.modeling.criterion")
+    crit = _load("detrex.modeling.criterion.criterion", "detrex/modeling/criterion/criterion.py")
+    sys.modules["detrex.modeling.criterion"].SetCriterion = crit.SetCriterion
+    matcher = _load("detrex.modeling.matcher.matcher", "detrex/modeling/matcher/matcher.py")
+    neck = _load("detrex.modeling.neck.channel_mapper", "detrex/modeling/neck/channel_mapper.py")
+    resnet = _load("detrex.modeling.backbone.resnet", "detrex/modeling/backbone/resnet.py")
+    pkg = _pkg("vclr_modeling")
+    pkg.__path__ = [f"{REF}/projects/vCLR_deformable_mask/modeling"]
+    for name in ("misc", "two_stage_criterion", "dn_criterion", "dino"):
+        spec = importlib.util.spec_from_file_location(f"vclr_modeling.{name}",
+                                                      f"{REF}/projects/vCLR_deformable_mask/modeling/{name}.py")
+        m = importlib.util.module_from_spec(spec)
+        sys.modules[f"vclr_modeling.{name}"] = m
+        spec.loader.exec_module(m)
+        _LOADED[f"vclr_{name}"] = m
+    _LOADED.update(dino_det=sys.modules["vclr_modeling.dino"], matcher=matcher, neck=neck, resnet=resnet,
+                   criterion=sys.modules["vclr_modeling.dn_criterion"], ShapeSpec=_ShapeSpec,
+                   ImageList=_ImageList, Instances=_Instances, Boxes=_Boxes)
+    return types.SimpleNamespace(**_LOADED)

@@ -1,0 +1,118 @@
+"""The vCLR DINO detector's training step (projects/vCLR_deformable_mask/modeling/dino.py,
+forward_student + DINOCriterion) on the GPU against the reference run on the CPU
+(tests/golden/dino_detector_step.npz, oracle/gen_golden.py gen_dino_detector: the reference's own
+dino.py / dn_criterion.py / two_stage_criterion.py / matcher / ChannelMapper / ResNet modules at
+the reduced dino_det_case.py configuration, fp64 and fp32).
+
+Both sides use the same weights (name-hashed fill), the same two padded images with box masks,
+and the same random draws (the denoising queries' label / box noise and the mask losses' point
+sampling, recorded on the reference side and replayed here).  Checked:
+  * every entry of the loss dict (same keys, weighted as the reference weights them): relative
+    error <= 1e-4 in fp32, 1e-9 in fp64 (absolute 1e-6 / 1e-12 where the entry is 0);
+  * every distinct trainable parameter's gradient (norm and two seeded projections, the small
+    tensors in full): error <= max(1e-3, 10 x the reference's own fp32-vs-fp64 error) of the
+    norm in fp32, 1e-7 in fp64; mathematically zero gradients (the conv bias ahead of a
+    training-mode BatchNorm, parameters the weighted loss does not reach) against an absolute
+    floor;
+  * the MSDA calls ran on the HIP kernels (irads_msda_fwd / irads_msda_bwd_gather)."""
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from golden_util import Fixture
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+
+
+def _run(dtype):
+    from dino_det_case import DET_CFG, DET_FILL_SEED, DET_NUM_POINTS, ReplayRNG, canonical_params, det_inputs
+    from fill import fill_module
+    from projects.vCLR_deformable_mask.configs.dino_r50 import build_model
+    fx = Fixture("dino_detector_step.npz")
+    model = build_model(**DET_CFG, device="cuda")
+    model.criterion.num_points = DET_NUM_POINTS
+    fill_module(model, seed=DET_FILL_SEED, dedup=True)
+    model = model.to(DEV).to(dtype).train()
+    rng = ReplayRNG([fx[f"draw_{i}"] for i in range(int(fx["n_draws"]))])
+    model.rng = model.criterion.rng = rng
+    batched = []
+    for img, boxes, cls, masks in det_inputs():
+        inst = {"image_size": tuple(img.shape[1:]), "gt_boxes": torch.as_tensor(boxes, dtype=dtype, device=DEV),
+                "gt_classes": torch.as_tensor(cls, device=DEV), "gt_masks": torch.as_tensor(masks, device=DEV)}
+        batched.append({"image": torch.as_tensor(img, dtype=dtype), "instances": inst})
+    calls = {"fwd": 0, "bwd": 0}
+    from irads import native as N
+    orig = N.call
+
+    def spy(name, *a):
+        if name == "irads_msda_fwd":
+            calls["fwd"] += 1
+        elif name.startswith("irads_msda_bwd"):
+            calls["bwd"] += 1
+        return orig(name, *a)
+    N.call = spy
+    try:
+        images, _ = model.preprocess_image(batched)
+        B, _, H, W = images.shape
+        img_masks = images.new_ones(B, H, W)
+        for i, x in enumerate(batched):
+            ih, iw = x["instances"]["image_size"]
+            img_masks[i, :ih, :iw] = 0
+        losses = model.forward_student(batched, images, img_masks)
+        total = sum(losses.values())
+        total.backward()
+        torch.cuda.synchronize()
+    finally:
+        N.call = orig
+    assert rng.i == len(rng.draws), "every recorded draw replayed"
+    return fx, losses, total, canonical_params(model), calls
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64], ids=["fp32", "fp64"])
+def test_dino_detector_step_vs_reference(dtype):
+    from train_fixture import N_PROJ, projection
+    fx, losses, total, params, calls = _run(dtype)
+    fp32 = dtype == torch.float32
+    assert calls["fwd"] > 0 and calls["bwd"] > 0, calls
+    keys = [str(k) for k in fx["loss_keys"]]
+    assert sorted(losses) == keys
+    rtol, atol = (1e-4, 1e-6) if fp32 else (1e-9, 1e-12)
+    fails = []
+    for k, v64 in zip(keys, fx["loss64"]):
+        got = float(losses[k])
+        if abs(v64) < 1e-12:
+            if abs(got) > atol:
+                fails.append(f"{k}: {got} (reference 0)")
+        elif abs(got - v64) > rtol * abs(v64):
+            fails.append(f"{k}: {got} vs {v64} (rel {abs(got - v64) / abs(v64):.2e})")
+    names = [str(n) for n in fx["grad_names"]]
+    assert [n for n, _ in params] == names
+    norms, projs, ref32 = fx["grad_norms"], fx["grad_projs"], fx["ref32_rel"]
+    floor = 1e-7 * float(norms.max())
+    worst = (0.0, "")
+    for k, (n, p) in enumerate(params):
+        g = (p.grad.detach().double().cpu().numpy() if p.grad is not None else np.zeros(tuple(p.shape)))
+        nr = float(norms[k])
+        d = [projection(n, g, j) - float(projs[k][j]) for j in range(N_PROJ)]
+        d.append(float(np.sqrt((g * g).sum())) - nr)
+        err = max(abs(x) for x in d)
+        if nr <= floor:  # mathematically zero (or unreached) gradient
+            if err > (1e3 if fp32 else 1.0) * floor:
+                fails.append(f"{n}: zero gradient expected, |error| {err:.2e}")
+            continue
+        tol = max(1e-3, 10 * float(ref32[k])) if fp32 else 1e-7
+        rel = err / nr
+        worst = max(worst, (rel / tol, n))
+        if rel > tol:
+            fails.append(f"{n}: gradient error {rel:.2e} of the norm > {tol:.1e}")
+        if "g." + n in fx:
+            ref = fx["g." + n]
+            e = float(np.sqrt(((g - ref) ** 2).sum()) / max(np.sqrt((ref * ref).sum()), 1e-300))
+            if e > tol:
+                fails.append(f"{n}: full gradient relative L2 {e:.2e} > {tol:.1e}")
+    print(dtype, "total", float(total), "vs", float(fx["total64"]), "worst grad / tol", worst)
+    assert not fails, fails[:20]
