@@ -115,3 +115,25 @@ def canonical_params(model):
         if p.requires_grad and (id(p) not in first or n < first[id(p)][0]):
             first[id(p)] = (n, p)
     return sorted(first.values(), key=lambda x: x[0])
+
+
+def seg_probes(model):
+    """Forward hooks on the segmentation-feature branch (the concatenated level features, the
+    mapping convs' output and the post LayerNorm's): (L2 norm, seeded projection) of each, for
+    localising a difference between the reference and the product."""
+    store = {}
+
+    def stat(t):
+        t = t.detach().double().cpu()
+        g = torch.Generator().manual_seed(7)
+        r = torch.randn(t.shape, generator=g, dtype=torch.float64)
+        return [float(t.norm()), float((t * r).sum()), float(t.abs().sum())]
+
+    hs = [model.mapping_fpn_features_for_seg.register_forward_pre_hook(
+              lambda m, a: store.__setitem__("seg_in", stat(a[0]))),
+          model.mapping_fpn_features_for_seg.register_forward_hook(
+              lambda m, a, o: store.__setitem__("seg_mapped", stat(o))),
+          model.mapping_fpn_features_for_seg[1].register_forward_hook(
+              lambda m, a, o: store.__setitem__("seg_bn", stat(o))),
+          model.post_layernorm.register_forward_hook(lambda m, a, o: store.__setitem__("seg_ln", stat(o)))]
+    return store, hs

@@ -648,6 +648,8 @@ def _det_reference_step(L, dtype, rng):
         torch.rand, torch.rand_like, torch.randint_like = rng.rand, rng.rand_like, rng.randint_like
         torch.Tensor.cuda = lambda self, *a, **k: self
         torch.Tensor.to = to_cpu
+        from dino_det_case import seg_probes
+        probes, hooks = seg_probes(model)
         images = model.preprocess_image(batched)
         B, _, H, W = images.tensor.shape
         img_masks = images.tensor.new_ones(B, H, W)
@@ -655,7 +657,10 @@ def _det_reference_step(L, dtype, rng):
             ih, iw = x["instances"].image_size
             img_masks[i, :ih, :iw] = 0
         losses = model.forward_student(batched, images, img_masks)
-        total = sum(losses.values())
+        for h in hooks:
+            h.remove()
+        losses["_probes"] = probes
+        total = sum(v for k, v in losses.items() if k != "_probes")
         total.backward()
     finally:
         for k, v in orig.items():
@@ -674,8 +679,11 @@ def gen_dino_detector(ref):
     rec = RecordingRNG(2024)
     l64, tot64, p64 = _det_reference_step(L, torch.float64, rec)
     l32, tot32, p32 = _det_reference_step(L, torch.float32, ReplayRNG(rec.draws))
+    probes = l64.pop("_probes")
+    l32.pop("_probes")
     keys = sorted(l64)
-    res = {"loss_keys": np.array(keys), "loss64": np.array([float(l64[k]) for k in keys]),
+    res = {"loss_keys": np.array(keys), "probe_keys": np.array(sorted(probes)),
+           "probes": np.array([probes[k] for k in sorted(probes)]), "loss64": np.array([float(l64[k]) for k in keys]),
            "loss32": np.array([float(l32[k]) for k in keys]), "total64": float(tot64), "total32": float(tot32),
            "n_draws": len(rec.draws)}
     for i, d in enumerate(rec.draws):

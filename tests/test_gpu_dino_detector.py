@@ -55,6 +55,8 @@ def _run(dtype):
             calls["bwd"] += 1
         return orig(name, *a)
     N.call = spy
+    from dino_det_case import seg_probes
+    probes, hooks = seg_probes(model)
     try:
         images, _ = model.preprocess_image(batched)
         B, _, H, W = images.shape
@@ -63,12 +65,17 @@ def _run(dtype):
             ih, iw = x["instances"]["image_size"]
             img_masks[i, :ih, :iw] = 0
         losses = model.forward_student(batched, images, img_masks)
+        for h in hooks:
+            h.remove()
         total = sum(losses.values())
         total.backward()
         torch.cuda.synchronize()
     finally:
         N.call = orig
     assert rng.i == len(rng.draws), "every recorded draw replayed"
+    for k, v in zip(fx["probe_keys"], fx["probes"]):
+        got = probes[str(k)]
+        print("probe", k, [f"{(a - b) / max(abs(b), 1e-300):.2e}" for a, b in zip(got, v)])
     return fx, losses, total, canonical_params(model), calls
 
 
@@ -83,7 +90,7 @@ def test_dino_detector_step_vs_reference(dtype):
     rtol, atol = (1e-4, 1e-6) if fp32 else (1e-9, 1e-12)
     fails = []
     for k, v64 in zip(keys, fx["loss64"]):
-        got = float(losses[k])
+        got = float(losses[k].detach())
         if abs(v64) < 1e-12:
             if abs(got) > atol:
                 fails.append(f"{k}: {got} (reference 0)")
@@ -114,5 +121,7 @@ def test_dino_detector_step_vs_reference(dtype):
             e = float(np.sqrt(((g - ref) ** 2).sum()) / max(np.sqrt((ref * ref).sum()), 1e-300))
             if e > tol:
                 fails.append(f"{n}: full gradient relative L2 {e:.2e} > {tol:.1e}")
-    print(dtype, "total", float(total), "vs", float(fx["total64"]), "worst grad / tol", worst)
+    print(dtype, "total", float(total), "vs", float(fx["total64"]), "worst grad / tol", worst, "n_fail", len(fails))
+    for f in fails[:60]:
+        print("  !", f)
     assert not fails, fails[:20]
