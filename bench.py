@@ -427,7 +427,7 @@ def main():
         if rank == 0:
             print(json.dumps({"profile_only": True, "ms_per_step": 1e3 * elapsed / args.steps}))
         if world > 1:
-            dist.destroy_process_group()
+            _teardown()
         return
     images = args.batch * world * args.steps
     result = {
@@ -519,7 +519,13 @@ def main():
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
-        dist.destroy_process_group()
+        _teardown()
+
+
+def _teardown():
+    from irads.graph_step import quiesce_process_groups
+    quiesce_process_groups()  # the captured graph is still alive: leave no eager work to poll
+    dist.destroy_process_group()
 
 
 if __name__ == "__main__":

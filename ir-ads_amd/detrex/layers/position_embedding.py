@@ -5,6 +5,28 @@ import torch
 import torch.nn as nn
 
 
+# The arguments of a fully padded row or column are huge: the normalised cumsum there is
+# (0 - 0.5) / (0 + eps) * 2 pi ~ -3e6 (eps = 1e-6), so one ulp of a frequency moves the sine by up to
+# 0.2.  The GPU's fp32 pow(T, e) differs from the CPU's (the reference run that made
+# tests/golden/dino_detector_step.npz) by an ulp on some frequencies, and its fp32 sin / cos of
+# such arguments is not correctly rounded either; the CPU's are (pow exactly, sin / cos within one
+# ulp of the fp64 result).  So the frequencies are the fp64 pow rounded to fp32 (bit-identical to
+# the CPU's fp32 pow for every T^(2 floor(i/2)/F) used here) and the sines the fp64 sine of the fp32
+# argument, rounded (scripts/dino_det_dump.py localised the round-4 DINO detector mismatch here).
+def _frequencies(num_pos_feats, temperature, device):
+    i = torch.arange(num_pos_feats, dtype=torch.float32, device=device)
+    e = 2 * torch.div(i, 2, rounding_mode="floor") / num_pos_feats  # exact in fp32
+    return (float(temperature) ** e.double()).float()
+
+
+def _sin(t):
+    return t.double().sin().to(t.dtype) if t.dtype == torch.float32 else t.sin()
+
+
+def _cos(t):
+    return t.double().cos().to(t.dtype) if t.dtype == torch.float32 else t.cos()
+
+
 class PositionEmbeddingSine(nn.Module):
     """DETR sine embedding of a padding mask (reference position_embedding.py:28-117)."""
 
@@ -29,13 +51,12 @@ class PositionEmbeddingSine(nn.Module):
         if self.normalize:
             y = (y + self.offset) / (y[:, -1:, :] + self.eps) * self.scale
             x = (x + self.offset) / (x[:, :, -1:] + self.eps) * self.scale
-        dim_t = torch.arange(self.num_pos_feats, dtype=torch.float32, device=mask.device)
-        dim_t = self.temperature ** (2 * torch.div(dim_t, 2, rounding_mode="floor") / self.num_pos_feats)
+        dim_t = _frequencies(self.num_pos_feats, self.temperature, mask.device)
         px = x[:, :, :, None] / dim_t
         py = y[:, :, :, None] / dim_t
         B, H, W = mask.shape
-        px = torch.stack((px[:, :, :, 0::2].sin(), px[:, :, :, 1::2].cos()), dim=4).view(B, H, W, -1)
-        py = torch.stack((py[:, :, :, 0::2].sin(), py[:, :, :, 1::2].cos()), dim=4).view(B, H, W, -1)
+        px = torch.stack((_sin(px[:, :, :, 0::2]), _cos(px[:, :, :, 1::2])), dim=4).view(B, H, W, -1)
+        py = torch.stack((_sin(py[:, :, :, 0::2]), _cos(py[:, :, :, 1::2])), dim=4).view(B, H, W, -1)
         return torch.cat((py, px), dim=3).permute(0, 3, 1, 2)
 
 
@@ -47,13 +68,12 @@ def get_sine_pos_embed(pos_tensor: torch.Tensor, num_pos_feats: int = 128, tempe
     frequencies of ``2π·c / T^(2⌊i/2⌋/F)``, interleaved; with ``exchange_xy`` the first two
     coordinates' blocks swap places (``[pos(y), pos(x), ...]``).
     """
-    dim_t = torch.arange(num_pos_feats, dtype=torch.float32, device=pos_tensor.device)
-    dim_t = temperature ** (2 * torch.div(dim_t, 2, rounding_mode="floor") / num_pos_feats)
+    dim_t = _frequencies(num_pos_feats, temperature, pos_tensor.device)
     scale = 2 * math.pi
 
     def embed(c):
         s = c * scale / dim_t
-        return torch.stack((s[:, :, 0::2].sin(), s[:, :, 1::2].cos()), dim=3).flatten(2)
+        return torch.stack((_sin(s[:, :, 0::2]), _cos(s[:, :, 1::2])), dim=3).flatten(2)
 
     parts = [embed(c) for c in pos_tensor.split([1] * pos_tensor.shape[-1], dim=-1)]
     if exchange_xy:

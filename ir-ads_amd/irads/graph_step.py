@@ -91,6 +91,29 @@ def release_capture_groups():
     _CAPTURE_GROUPS.clear()
 
 
+def quiesce_process_groups():
+    """Block until every RCCL process group's watchdog has retired all of its eager works.
+
+    The watchdog thread polls each eager work's end event (hipEventQuery) every ~100 ms until it
+    sees it complete.  A poll that lands while a capture is open can fail with
+    hipErrorCapturedEvent ("operation not permitted on an event last recorded in a capturing
+    stream": round 4, tests/test_gpu_zz_rccl.py, the DEFAULT group's watchdog during the capture
+    of collectives issued on the capture-only group), and the watchdog rethrows it, which aborts
+    the process.  Which stream the failing event sat on does not matter for the fix: with the
+    work lists empty (ProcessGroup._wait_for_pending_works returns only when the watchdog has
+    removed every work, after a device synchronisation has completed them all) the watchdog has
+    nothing to poll while the capture is open, and nothing adds a work until it closes — captured
+    collectives are never handed to the watchdog, and no eager collective is issued during a
+    capture.  Called before each capture and before destroy_process_group (teardown with graphs
+    alive, round 3)."""
+    if not dist.is_initialized() or dist.get_backend() != "nccl":
+        return
+    torch.cuda.synchronize()
+    groups = [dist.group.WORLD] + list(_CAPTURE_GROUPS.values())
+    for g in groups:
+        g._wait_for_pending_works()
+
+
 # "thread_local": only the capturing thread's capture-unsafe HIP calls are refused.  In the
 # default "global" mode a call from any thread of the process fails while a capture is open,
 # and a process with an RCCL communicator has threads of its own (RCCL's proxy thread, the
@@ -153,6 +176,7 @@ class GraphedTrainStep:
         optimizer.zero_grad(set_to_none=True)
         if before_capture is not None:
             before_capture()
+        quiesce_process_groups()  # no eager work left for a watchdog to poll during the capture
         self.graph = torch.cuda.CUDAGraph()
         self.opt_graph = None
         if self.comm == "split":

@@ -41,7 +41,10 @@ def setup_ddp():
 
 def cleanup_ddp():
     if dist.is_initialized():
+        from irads.graph_step import quiesce_process_groups, release_capture_groups
+        quiesce_process_groups()  # teardown with captured graphs alive: no work left to poll
         dist.destroy_process_group()
+        release_capture_groups()
 
 
 def reduce_tensor(tensor):

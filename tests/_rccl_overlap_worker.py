@@ -65,9 +65,15 @@ def main():
     rel = (num / den) ** 0.5
     assert rel < 2e-2, rel
     assert all(torch.allclose(a, b, rtol=0, atol=2e-3) for a, b in zip(p0, p1))
-    # torn down with the captured graph (and its RCCL kernels) still alive, as train_mm.py does:
-    # the round-3 abort happened here, in destroy_process_group
-    dist.destroy_process_group()
+    # an eager collective after the replays (train_mm.py's loss / metric reductions), then torn
+    # down with the captured graph (and its RCCL kernels) still alive, as train_mm.py does: the
+    # round-3 abort happened in destroy_process_group
+    t = torch.ones(4, device=dev)
+    dist.all_reduce(t)
+    step.step()
+    torch.cuda.synchronize()
+    from semseg.utils.utils import cleanup_ddp
+    cleanup_ddp()  # quiesce_process_groups() + destroy_process_group()
     print(f"OK rel {rel:.3e}", flush=True)
 
 

@@ -8,10 +8,11 @@ Both sides use the same weights (name-hashed fill), the same two padded images w
 and the same random draws (the denoising queries' label / box noise and the mask losses' point
 sampling, recorded on the reference side and replayed here).  Checked:
   * every entry of the loss dict (same keys, weighted as the reference weights them): relative
-    error <= 1e-4 in fp32, 1e-9 in fp64 (absolute 1e-6 / 1e-12 where the entry is 0);
+    error <= 1e-4 in fp32, 1e-7 in fp64 (absolute 1e-6 / 1e-12 where the entry is 0);
   * every distinct trainable parameter's gradient (norm and two seeded projections, the small
     tensors in full): error <= max(1e-3, 10 x the reference's own fp32-vs-fp64 error) of the
-    norm in fp32, 1e-7 in fp64; mathematically zero gradients (the conv bias ahead of a
+    norm in fp32, 1e-5 in fp64 (the reference's fp32 sub-computations, see the test);
+    mathematically zero gradients (the conv bias ahead of a
     training-mode BatchNorm, parameters the weighted loss does not reach) against an absolute
     floor;
   * the MSDA calls ran on the HIP kernels (irads_msda_fwd / irads_msda_bwd_gather)."""
@@ -87,7 +88,12 @@ def test_dino_detector_step_vs_reference(dtype):
     assert calls["fwd"] > 0 and calls["bwd"] > 0, calls
     keys = [str(k) for k in fx["loss_keys"]]
     assert sorted(losses) == keys
-    rtol, atol = (1e-4, 1e-6) if fp32 else (1e-9, 1e-12)
+    # fp64: the reference's fp64 step still evaluates its sine position embeddings, reference
+    # points and proposal grids in fp32 (position_embedding.py:96-104, dino_transformer.py:293,
+    # 342: explicit float32), where the CPU and the GPU agree to one ulp (6e-8), not bit for bit;
+    # carried through the step that is ~1e-8 on the losses and up to 1.1e-6 of the norm on the
+    # most position-sensitive gradient (the decoder's sampling offsets; measured round 4)
+    rtol, atol = (1e-4, 1e-6) if fp32 else (1e-7, 1e-12)
     fails = []
     for k, v64 in zip(keys, fx["loss64"]):
         got = float(losses[k].detach())
@@ -111,7 +117,7 @@ def test_dino_detector_step_vs_reference(dtype):
             if err > (1e3 if fp32 else 1.0) * floor:
                 fails.append(f"{n}: zero gradient expected, |error| {err:.2e}")
             continue
-        tol = max(1e-3, 10 * float(ref32[k])) if fp32 else 1e-7
+        tol = max(1e-3, 10 * float(ref32[k])) if fp32 else 1e-5
         rel = err / nr
         worst = max(worst, (rel / tol, n))
         if rel > tol:
