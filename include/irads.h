@@ -241,6 +241,12 @@ int irads_resize_fwd(int dtype, const void *in, const int64_t *in_strides, int B
  * accumulated).  workspace: B*C*h*W floats. */
 int irads_resize_bwd(int dtype, const void *grad_out, const int64_t *go_strides, int B, int C, int H, int W,
                      void *grad_in, const int64_t *gi_strides, int h, int w, float *workspace, void *stream);
+/* The same adjoint in one pass for channels-last (B, ., ., C) tensors, C % 8 == 0, 16-B aligned,
+ * no workspace (rows reduced in LDS per workgroup of 32 input columns x a channel block).
+ * irads_resize_bwd_cl_fits(C, w, W) says whether the span fits the LDS budget. */
+int irads_resize_bwd_cl(int dtype, const void *grad_out, int B, int C, int H, int W, void *grad_in, int h, int w,
+                        void *stream);
+int irads_resize_bwd_cl_fits(int C, int w, int W);
 
 /* out = base + sum_s resize(src_s) (bilinear, align_corners=False, the resize_fwd taps), all
  * channels-last (B, C, ., .) tensors of one dtype with C % 8 == 0, fp32 sum rounded once.
@@ -265,6 +271,15 @@ int irads_ce_fwd(int dtype, const void *logits, const int64_t *strides, int B, i
 int irads_ce_bwd(int dtype, const void *logits, const int64_t *strides, int B, int C, int H, int W,
                  const int64_t *target, int ignore_index, const float *class_weight, const float *lse,
                  const float *loss, const float *grad_loss, void *grad_logits, void *stream);
+/* The loss gradient taken through the bilinear upsample that produced the logits, in one pass
+ * (replaces irads_ce_bwd + irads_resize_bwd when the logits are F.interpolate(low, (H, W),
+ * 'bilinear', align_corners=False) of a (B, C, h, w) map: cmnext.py:30-32 + train_mm.py:133-148).
+ * logits channels-last (B, H, W, C) contiguous, C % 8 == 0, lse / loss from irads_ce_fwd of the
+ * same logits; grad_low channels-last (B, h, w, C) = resize_adjoint(grad_loss[0] w_t (softmax -
+ * onehot) / loss[1]), the per-pixel gradient kept in fp32. */
+int irads_ce_resize_bwd(int dtype, const void *logits, int B, int C, int H, int W, const int64_t *target,
+                        int ignore_index, const float *class_weight, const float *lse, const float *loss,
+                        const float *grad_loss, int h, int w, void *grad_low, void *stream);
 
 /* ------------------------------------------------------------------ fused Swin block row kernels
  * The non-GEMM work of SwinBlockAdapter.forward under bf16 autocast (swin.py:584-610:

@@ -551,6 +551,93 @@ __global__ void __launch_bounds__(256) ce_bwd_cl8(const T *__restrict__ x, Dims 
     V8<T>::st(gx + (long)r * 8, g);
 }
 
+// ------------------------------------------------------------------ fused CE + resize backward
+// The training loss reads logits that F.interpolate upsampled (cmnext.py:30-32: 1/4 -> full
+// resolution, bilinear, align_corners=False).  Unfused, the backward writes the full-resolution
+// logit gradient (ce_bwd, bf16: 168 MB per C2 head) and the resize adjoint reads it back twice
+// (rows, then columns through an fp32 temporary): ~0.23 ms per head.  Here one workgroup owns
+// the low-resolution gradient of CRX columns of one row yi of one image: it recomputes the
+// loss gradient g = s·(exp(x − lse) − [c = t]) of every full-resolution pixel whose taps reach
+// that row segment (each logit read by the two row workgroups that share it, next to each other
+// on one XCD), reduces over output rows with the row taps into LDS, then over output columns
+// with the column taps, and writes the segment once.  Taps and weights are resize_bwd's; g stays
+// fp32 (the unfused path rounds it to the logits' dtype first).
+constexpr int CRX = 32;  // low-resolution columns per workgroup
+
+template <typename T, bool CE>
+__global__ void __launch_bounds__(256) ce_resize_bwd_cl8(const T *__restrict__ x, Dims d,
+                                                         const int64_t *__restrict__ tgt, int ignore,
+                                                         const float *__restrict__ cw, const float *__restrict__ lse,
+                                                         const float *__restrict__ loss,
+                                                         const float *__restrict__ gloss, T *__restrict__ gin,
+                                                         Dims di, float sh, float sw, float inv_sh, float inv_sw,
+                                                         int nx_max, int CB) {
+    extern __shared__ __attribute__((aligned(16))) float rsm[];  // [nx_max][CB]: row-reduced gradient
+    const int nseg = (di.W + CRX - 1) / CRX, ncb = d.C / CB;
+    int blk = xcd_remap(blockIdx.x, gridDim.x);  // consecutive (channel block, segment, row) items on one XCD
+    const int cb0 = (blk % ncb) * CB;
+    blk /= ncb;
+    const int seg = blk % nseg;
+    blk /= nseg;
+    const int yi = blk % di.H, b = blk / di.H;
+    const int xs0 = seg * CRX, xs1 = min(di.W, xs0 + CRX) - 1;
+    int ylo, yhi, xlo, xhi, dum;
+    reach(yi, inv_sh, d.H, ylo, yhi);
+    reach(xs0, inv_sw, d.W, xlo, dum);
+    reach(xs1, inv_sw, d.W, dum, xhi);
+    xhi = min(xhi, xlo + nx_max - 1);  // the host sized nx_max to cover every segment
+    const int nx = xhi - xlo + 1, C = d.C, C8 = CB >> 3;  // C8: 8-channel groups of this block
+    const float gsc = CE ? gloss[0] / loss[1] : 1.f;
+    for (int it = threadIdx.x; it < nx * C8; it += blockDim.x) {
+        const int xo = it / C8, cl = (it - xo * C8) * 8, c0 = cb0 + cl, X = xlo + xo;
+        float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        for (int Y = ylo; Y <= yhi; ++Y) {
+            const float wy = tap_weight(tap_of(Y, sh, di.H), yi);
+            const long p = ((long)b * d.H + Y) * d.W + X;
+            if (!CE) {  // plain resize adjoint: x is the gradient of the upsampled tensor
+                if (wy == 0.f) continue;
+                float v[8];
+                V8<T>::ld(x + p * C + c0, v);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) acc[j] = fmaf(wy, v[j], acc[j]);
+                continue;
+            }
+            const long t = tgt[p];
+            if (wy == 0.f || t == ignore || t < 0 || t >= C) continue;
+            const float gs = wy * gsc * (cw ? cw[t] : 1.f), l = lse[p];
+            float v[8];
+            V8<T>::ld(x + p * C + c0, v);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc[j] = fmaf(gs, fast_exp2((v[j] - l) * kLog2e) - (c0 + j == t ? 1.f : 0.f), acc[j]);
+        }
+        *(float4 *)(rsm + xo * CB + cl) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+        *(float4 *)(rsm + xo * CB + cl + 4) = make_float4(acc[4], acc[5], acc[6], acc[7]);
+    }
+    __syncthreads();
+    for (int it = threadIdx.x; it < (xs1 - xs0 + 1) * C8; it += blockDim.x) {
+        const int xi = xs0 + it / C8, cl = (it % C8) * 8, c0 = cb0 + cl;
+        int lo, hi;
+        reach(xi, inv_sw, d.W, lo, hi);
+        lo = max(lo, xlo);
+        hi = min(hi, xhi);
+        float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        for (int X = lo; X <= hi; ++X) {
+            const float wx = tap_weight(tap_of(X, sw, di.W), xi);
+            if (wx == 0.f) continue;
+            const float4 a = *(const float4 *)(rsm + (X - xlo) * CB + cl), b4 = *(const float4 *)(rsm + (X - xlo) * CB + cl + 4);
+            acc[0] = fmaf(wx, a.x, acc[0]);
+            acc[1] = fmaf(wx, a.y, acc[1]);
+            acc[2] = fmaf(wx, a.z, acc[2]);
+            acc[3] = fmaf(wx, a.w, acc[3]);
+            acc[4] = fmaf(wx, b4.x, acc[4]);
+            acc[5] = fmaf(wx, b4.y, acc[5]);
+            acc[6] = fmaf(wx, b4.z, acc[6]);
+            acc[7] = fmaf(wx, b4.w, acc[7]);
+        }
+        V8<T>::st(gin + (((long)b * di.H + yi) * di.W + xi) * C + c0, acc);
+    }
+}
+
 // 0 = NCHW-contiguous, 1 = channels-last-contiguous, -1 = neither (strides of size-1
 // dims are ignored, as torch's is_contiguous does)
 int layout_of(const int64_t *s, int B, int C, int H, int W) {
@@ -750,6 +837,92 @@ extern "C" int irads_ce_bwd(int dtype, const void *logits, const int64_t *stride
                                                    grad_loss, (U *)grad_logits);
     }
     return check_launch("irads_ce_bwd");
+}
+
+// host mirror of reach() (an upper bound on a segment's output-column span: +4 covers any
+// rounding difference between the host's and the device's evaluation of the same formula)
+static int ce_resize_nx_max(int w, int W) {
+    const float inv = (float)W / (float)w;
+    int best = 0;
+    for (int xs0 = 0; xs0 < w; xs0 += CRX) {
+        const int xs1 = std::min(w, xs0 + CRX) - 1;
+        int lo = (int)floorf(((float)xs0 - 0.5f) * inv - 0.5f) - 2, hi = (int)ceilf(((float)xs1 + 1.5f) * inv - 0.5f) + 2;
+        lo = std::max(lo, 0);
+        hi = std::min(hi, W - 1);
+        best = std::max(best, hi - lo + 1);
+    }
+    return std::min(best + 4, W);
+}
+
+// channels per workgroup of the plain adjoint: the largest multiple of 8 dividing C whose
+// row-reduced span stays within 32 KB of LDS (several workgroups per CU); 0 if none fits
+static int resize_cl_block(int C, int nx_max) {
+    for (int cb = C; cb >= 8; cb -= 8)
+        if (C % cb == 0 && (size_t)nx_max * cb * sizeof(float) <= 32 * 1024) return cb;
+    return 0;
+}
+
+extern "C" int irads_ce_resize_bwd(int dtype, const void *logits, int B, int C, int H, int W, const int64_t *target,
+                                   int ignore_index, const float *class_weight, const float *lse, const float *loss,
+                                   const float *grad_loss, int h, int w, void *grad_low, void *stream) {
+    IRADS_REQUIRE(dtype == IRADS_F32 || dtype == IRADS_BF16, "ce_resize_bwd: dtype must be float32 or bfloat16");
+    IRADS_REQUIRE(B > 0 && C > 0 && C % 8 == 0 && H > 0 && W > 0 && h > 0 && w > 0,
+                  "ce_resize_bwd: bad sizes (C %% 8 == 0 needed, C=%d)", C);
+    IRADS_REQUIRE(small_enough((long)B * C * H * W), "ce_resize_bwd: tensor too large");
+    IRADS_REQUIRE(logits && target && lse && loss && grad_loss && grad_low, "ce_resize_bwd: null buffer");
+    IRADS_REQUIRE(aligned16(logits, grad_low), "ce_resize_bwd: logits / grad must be 16-byte aligned");
+    const int nx_max = ce_resize_nx_max(w, W);
+    const size_t sm = (size_t)nx_max * C * sizeof(float);
+    IRADS_REQUIRE(sm <= 64 * 1024, "ce_resize_bwd: %d output columns x %d classes exceed the LDS budget", nx_max, C);
+    const Dims d{B, C, H, W}, di{B, C, h, w};
+    const float sh = (float)h / (float)H, sw = (float)w / (float)W;
+    const unsigned grid = (unsigned)((long)B * h * ((w + CRX - 1) / CRX));
+    hipStream_t st = (hipStream_t)stream;
+    if (dtype == IRADS_F32)
+        ce_resize_bwd_cl8<float, true><<<grid, 256, sm, st>>>((const float *)logits, d, target, ignore_index, class_weight,
+                                                        lse, loss, grad_loss, (float *)grad_low, di, sh, sw,
+                                                        (float)H / (float)h, (float)W / (float)w, nx_max, C);
+    else
+        ce_resize_bwd_cl8<unsigned short, true><<<grid, 256, sm, st>>>((const unsigned short *)logits, d, target,
+                                                                 ignore_index, class_weight, lse, loss, grad_loss,
+                                                                 (unsigned short *)grad_low, di, sh, sw,
+                                                                 (float)H / (float)h, (float)W / (float)w, nx_max, C);
+    return check_launch("irads_ce_resize_bwd");
+}
+
+// The resize adjoint of a channels-last map in one pass (ce_resize_bwd_cl8 without the loss):
+// no fp32 row-reduced temporary in HBM, the rows reduced in LDS.  Same taps; the fp32 sums are
+// added in a different order than resize_bwd_rows/cols (rows first within a workgroup's column
+// span, then columns).  Used when C % 8 == 0, both tensors channels-last and 16-B aligned, and
+// the span fits the LDS budget; otherwise irads_resize_bwd.
+extern "C" int irads_resize_bwd_cl(int dtype, const void *grad_out, int B, int C, int H, int W, void *grad_in, int h,
+                                   int w, void *stream) {
+    IRADS_REQUIRE(dtype == IRADS_F32 || dtype == IRADS_BF16, "resize_bwd_cl: dtype must be float32 or bfloat16");
+    IRADS_REQUIRE(B > 0 && C > 0 && C % 8 == 0 && H > 0 && W > 0 && h > 0 && w > 0,
+                  "resize_bwd_cl: bad sizes (C %% 8 == 0 needed, C=%d)", C);
+    IRADS_REQUIRE(small_enough((long)B * C * H * W) && small_enough((long)B * C * h * w), "resize_bwd_cl: too large");
+    IRADS_REQUIRE(grad_out && grad_in && aligned16(grad_out, grad_in), "resize_bwd_cl: null / unaligned buffer");
+    const int nx_max = ce_resize_nx_max(w, W);
+    const int CB = resize_cl_block(C, nx_max);
+    IRADS_REQUIRE(CB > 0, "resize_bwd_cl: %d output columns exceed the LDS budget", nx_max);
+    const size_t sm = (size_t)nx_max * CB * sizeof(float);
+    const Dims d{B, C, H, W}, di{B, C, h, w};
+    const float sh = (float)h / (float)H, sw = (float)w / (float)W;
+    const unsigned grid = (unsigned)((long)B * h * ((w + CRX - 1) / CRX) * (C / CB));
+    hipStream_t st = (hipStream_t)stream;
+    if (dtype == IRADS_F32)
+        ce_resize_bwd_cl8<float, false><<<grid, 256, sm, st>>>((const float *)grad_out, d, nullptr, 0, nullptr,
+                                                               nullptr, nullptr, nullptr, (float *)grad_in, di, sh, sw,
+                                                               (float)H / (float)h, (float)W / (float)w, nx_max, CB);
+    else
+        ce_resize_bwd_cl8<unsigned short, false><<<grid, 256, sm, st>>>(
+            (const unsigned short *)grad_out, d, nullptr, 0, nullptr, nullptr, nullptr, nullptr,
+            (unsigned short *)grad_in, di, sh, sw, (float)H / (float)h, (float)W / (float)w, nx_max, CB);
+    return check_launch("irads_resize_bwd_cl");
+}
+
+extern "C" int irads_resize_bwd_cl_fits(int C, int w, int W) {
+    return C % 8 == 0 && resize_cl_block(C, ce_resize_nx_max(w, W)) > 0;
 }
 
 extern "C" int irads_upsample_sum_fwd(int dtype, const void *base, const void *const *srcs, const int *src_h,

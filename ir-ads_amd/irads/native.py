@@ -43,8 +43,10 @@ SIGNATURES = {
     "irads_sb_log_potential": [_i, _vp, _vp, _vp, _vp, _d, _i, _i, _i, _vp, _vp, _vp],
     "irads_resize_fwd": [_i, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _vp],
     "irads_resize_bwd": [_i, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _vp, _vp],
+    "irads_resize_bwd_cl": [_i, _vp, _i, _i, _i, _i, _vp, _i, _i, _vp],
     "irads_ce_fwd": [_i, _vp, _vp, _i, _i, _i, _i, _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp],
     "irads_ce_bwd": [_i, _vp, _vp, _i, _i, _i, _i, _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp],
+    "irads_ce_resize_bwd": [_i, _vp, _i, _i, _i, _i, _vp, _i, _vp, _vp, _vp, _vp, _i, _i, _vp, _vp],
     "irads_resln_fwd": [_vp, _vp, _vp, _vp, _f, _i, _i, _i, _vp, _vp, _f, _vp, _vp, _vp, _vp, _vp, _vp],
     "irads_resln_bwd": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _vp, _vp, _vp, _vp, _f, _vp],
     "irads_gelu_fwd": [_vp, _vp, _l, _vp],
@@ -83,6 +85,7 @@ QUERIES = {"irads_wgrad_workspace": (ctypes.c_long, [_i, _i, _i]),
            "irads_winattn_bias_quads_size": (ctypes.c_long, [_i]),
            "irads_winattn_fwd_variant": (ctypes.c_int, [_i]),
            "irads_msda_bwd_workspace_bytes": (ctypes.c_long, [_i, _i, _i, _i, _i, _i, _i, _i]),
+           "irads_resize_bwd_cl_fits": (ctypes.c_int, [_i, _i, _i]),
            "irads_dattn_attn_bwd_workspace_bytes": (ctypes.c_long, [_i] * 9),
            "irads_dattn_sample_bwd_workspace_bytes": (ctypes.c_long, [_i] * 5)}
 CE_WORKSPACE = 8192

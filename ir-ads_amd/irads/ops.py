@@ -714,6 +714,13 @@ class ResizeFn(torch.autograd.Function):
 
 
 def _resize_bwd(go, code, B, C, h, w, H, W, nchw):
+    if not nchw and C % 8 == 0 and N.load().irads_resize_bwd_cl_fits(C, w, W):
+        # channels-last: one pass, rows reduced in LDS (irads_resize_bwd_cl), no fp32 temporary
+        go = go.contiguous(memory_format=torch.channels_last)
+        gi = torch.empty((B, C, h, w), device=go.device, dtype=go.dtype, memory_format=torch.channels_last)
+        if go.data_ptr() % 16 == 0:
+            N.call("irads_resize_bwd_cl", code, N.ptr(go), B, C, H, W, N.ptr(gi), h, w, N.stream())
+            return gi
     go = go.contiguous() if nchw or C == 1 else go.contiguous(memory_format=torch.channels_last)
     gs = (ctypes.c_int64 * 4)(*go.stride())
     gi = torch.empty((B, C, h, w), device=go.device, dtype=go.dtype,
@@ -727,7 +734,10 @@ def _resize_bwd(go, code, B, C, h, w, H, W, nchw):
 def resize(x, size):
     if x.dtype == torch.float16:  # fp16 autocast: the fp32 kernel (F.interpolate's upcast precision)
         x = x.float()
-    return ResizeFn.apply(x, tuple(size))
+    out = ResizeFn.apply(x, tuple(size))
+    # cross_entropy() of this output takes its gradient straight to x (irads_ce_resize_bwd)
+    out._irads_resized_from = (x, out._version)
+    return out
 
 
 class UpsampleSumFn(torch.autograd.Function):
@@ -813,9 +823,55 @@ class CrossEntropyFn(torch.autograd.Function):
         return gx, None, None, None, None
 
 
+class ResizeCrossEntropyFn(torch.autograd.Function):
+    """CrossEntropyFn of logits = resize(low) (ops.resize's output, untouched since), with the
+    gradient taken straight to `low`: the forward is CrossEntropyFn's on the materialised logits
+    (the model's output, which the caller may use otherwise), the backward one irads_ce_resize_bwd
+    pass instead of irads_ce_bwd's full-resolution gradient and the resize adjoint reading it back.
+    The per-pixel gradient stays fp32 inside the pass (the unfused path rounds it to the logits'
+    dtype first); the result is the same adjoint with the same taps."""
+
+    @staticmethod
+    def forward(ctx, low, logits, target, ignore_index, weight, want_match):
+        out = CrossEntropyFn.forward(ctx, logits, target, ignore_index, weight, want_match)
+        ctx.low_shape = tuple(low.shape)
+        return out
+
+    @staticmethod
+    def backward(ctx, gloss, *_):
+        if gloss is None:
+            return None, None, None, None, None, None
+        logits, target, w, lse, loss = ctx.saved_tensors
+        code, B, C, H, W, ignore = ctx.cfg
+        _, _, h, w_ = ctx.low_shape
+        g = N.check(gloss.float().reshape(1).contiguous(), "grad")
+        gi = torch.empty((B, C, h, w_), device=logits.device, dtype=logits.dtype, memory_format=torch.channels_last)
+        N.call("irads_ce_resize_bwd", code, N.ptr(logits), B, C, H, W, N.ptr(target), ignore, N.ptr(w), N.ptr(lse),
+               N.ptr(loss), N.ptr(g), h, w_, N.ptr(gi), N.stream())
+        return gi, None, None, None, None, None
+
+
+def _resized_source(logits):
+    """The low-resolution map ops.resize made `logits` from, if the fused loss backward applies:
+    logits unmodified since, both channels-last with C % 8 == 0, same dtype, a gradient wanted."""
+    src = getattr(logits, "_irads_resized_from", None)
+    if src is None or src[1] != logits._version or not torch.is_grad_enabled():
+        return None
+    low = src[0]
+    cl = torch.channels_last
+    if (not low.requires_grad or low.dtype != logits.dtype or logits.dtype not in (torch.float32, torch.bfloat16)
+            or logits.shape[1] % 8 or not logits.is_contiguous(memory_format=cl)
+            or logits.data_ptr() % 16 or logits.shape[:2] != low.shape[:2] or not low.is_contiguous(memory_format=cl)):
+        return None
+    return low
+
+
 def cross_entropy(logits, target, ignore_index=255, weight=None, return_match=False):
     if logits.dtype == torch.float16:  # autocast runs cross-entropy in fp32
         logits = logits.float()
+    low = _resized_source(logits)
+    if low is not None:
+        return ResizeCrossEntropyFn.apply(low, logits.detach(), target, ignore_index, weight, bool(return_match))
     return CrossEntropyFn.apply(logits, target, ignore_index, weight, bool(return_match))
 
 

@@ -293,3 +293,119 @@ def test_head_bnact_tail_matches_module_path(E):
     per_chan = ratio.abs().amax(1)  # (B, E): 0 (dropped) or 2 (kept)
     assert ((per_chan == 0) | ((per_chan - 2).abs() < 1e-2)).all()
     assert 0.2 < (per_chan > 0).float().mean().item() < 0.8
+
+
+RESIZE_CE_CASES = [
+    # (B, C, h, w, H, W): x4 like the CMNeXt heads, ragged widths (segments of 32 low-res columns
+    # with a partial last one), non-integer ratios, one-column / one-row maps
+    (2, 40, 32, 32, 128, 128), (2, 16, 24, 70, 96, 280), (1, 8, 13, 17, 50, 61), (2, 24, 1, 9, 4, 36),
+    (1, 16, 7, 1, 28, 4)]
+
+
+def _spy_calls():
+    from irads import native as N
+    calls, orig = [], N.call
+
+    def spy(name, *a):
+        calls.append(name)
+        return orig(name, *a)
+    return calls, orig, spy
+
+
+@pytest.mark.parametrize("case", RESIZE_CE_CASES)
+def test_ce_through_resize_fused_fp32(case):
+    """cross_entropy(resize(low)) takes its gradient to `low` in one irads_ce_resize_bwd pass:
+    loss and gradient vs autograd through F.interpolate + F.cross_entropy in fp64, with class
+    weights, ignored and out-of-range targets and a scaled loss."""
+    from irads import native as N
+    ops = _ops()
+    B, C, h, w, H, W = case
+    low = (_rand((B, C, h, w), 70 + C) * 2).contiguous(memory_format=torch.channels_last)
+    t = _targets(B, H, W, C, 71 + C)
+    t[0, 0, :2] = C + 3  # out of range: treated as ignored (DESIGN.md §3)
+    t_ref = t.clone()
+    t_ref[t_ref == C + 3] = 255
+    wt = torch.rand(C, generator=torch.Generator().manual_seed(72)) + 0.5
+    ld = low.double().requires_grad_(True)
+    ref = F.cross_entropy(F.interpolate(ld, (H, W), mode="bilinear", align_corners=False), t_ref,
+                          weight=wt.double(), ignore_index=255)
+    (2.5 * ref).backward()
+    calls, orig, spy = _spy_calls()
+    N.call = spy
+    try:
+        lg = low.to(DEV).requires_grad_(True)
+        y = ops.resize(lg, (H, W))
+        loss = ops.cross_entropy(y, t.to(DEV), 255, wt.to(DEV))
+        (2.5 * loss).backward()
+    finally:
+        N.call = orig
+    assert "irads_ce_resize_bwd" in calls and "irads_resize_bwd" not in calls and "irads_ce_bwd" not in calls
+    close(loss, ref, 1e-6, 1e-6, f"CE(resize) fwd {case}")
+    assert lg.grad.is_contiguous(memory_format=torch.channels_last)
+    close(lg.grad, ld.grad, 1e-7, 1e-5, f"CE(resize) bwd {case}")
+
+
+def test_ce_through_resize_fused_bf16_and_fallbacks():
+    """bf16 (the AMP path): the fused gradient against fp64 autograd is at least as close as the
+    unfused one (which rounds the full-resolution gradient to bf16 first); the unfused path still
+    serves NCHW logits, a modified output and no-grad inputs."""
+    from irads import native as N
+    ops = _ops()
+    B, C, h, w, H, W = 2, 40, 32, 40, 128, 160
+    low = (_rand((B, C, h, w), 80) * 3).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    t = _targets(B, H, W, C, 81)
+    ld = low.double().requires_grad_(True)
+    F.cross_entropy(F.interpolate(ld, (H, W), mode="bilinear", align_corners=False), t, ignore_index=255).backward()
+    grads = {}
+    for fused in (True, False):
+        lg = low.to(DEV).requires_grad_(True)
+        y = ops.resize(lg, (H, W))
+        if not fused:
+            y = y * 1  # a new tensor: not ops.resize's output, so the unfused path runs
+        ops.cross_entropy(y, t.to(DEV), 255).backward()
+        assert lg.grad.dtype == torch.bfloat16
+        grads[fused] = lg.grad.double().cpu()
+    ref = ld.grad
+    err = {k: float((g - ref).norm() / ref.norm()) for k, g in grads.items()}
+    assert err[True] <= 4e-3 and err[True] <= err[False] * 1.05, err
+    # fallbacks: NCHW logits, an in-place-modified output, a source that wants no gradient
+    calls, orig, spy = _spy_calls()
+    N.call = spy
+    try:
+        lg = low.float().contiguous().to(DEV).requires_grad_(True)
+        ops.cross_entropy(ops.resize(lg, (H, W)), t.to(DEV), 255).backward()
+        lg2 = low.to(DEV).requires_grad_(True)
+        y2 = ops.resize(lg2, (H, W))
+        y2.mul_(1.0)
+        ops.cross_entropy(y2, t.to(DEV), 255).backward()
+        ops.cross_entropy(ops.resize(low.to(DEV), (H, W)).requires_grad_(), t.to(DEV), 255).backward()
+    finally:
+        N.call = orig
+    assert "irads_ce_resize_bwd" not in calls and calls.count("irads_ce_bwd") == 3
+
+
+@pytest.mark.parametrize("C,h,H", [(512, 64, 128), (256, 32, 128), (512, 16, 128), (40, 13, 50), (24, 9, 36)])
+def test_resize_adjoint_one_pass_vs_two_pass(C, h, H):
+    """Channels-last resize gradients take irads_resize_bwd_cl (rows reduced in LDS, one pass;
+    the SegFormer upsample_sum sources and the CMNeXt logits): against the NCHW two-pass adjoint
+    (irads_resize_bwd) on the same gradient, fp32 to 1e-5 relative and bf16 to one rounding,
+    and fp32 against F.interpolate's autograd in fp64."""
+    from irads import native as N
+    ops = _ops()
+    B = 2
+    assert N.load().irads_resize_bwd_cl_fits(C, h, H)
+    x = _rand((B, C, h, h + 3), 90 + C)
+    go = _rand((B, C, H, H + 12), 91 + C)
+    xd = x.double().requires_grad_(True)
+    F.interpolate(xd, (H, H + 12), mode="bilinear", align_corners=False).backward(go.double())
+    for dt, rtol in ((torch.float32, 1e-5), (torch.bfloat16, 2 ** -7)):
+        grads = []
+        for cl in (True, False):
+            xg = _fmt(x.to(dt), cl).to(DEV).requires_grad_(True)
+            y = ops.resize(xg, (H, H + 12))
+            y.backward(_fmt(go.to(dt), cl).to(DEV))
+            grads.append(xg.grad.float().cpu())
+        scale = float(grads[1].abs().max())
+        close(grads[0], grads[1], rtol * scale, rtol, f"one-pass vs two-pass adjoint C={C} {dt}")
+        if dt == torch.float32:
+            close(grads[0], xd.grad, 1e-5 * scale, 1e-5, f"one-pass adjoint vs fp64 C={C}")
