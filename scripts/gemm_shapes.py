@@ -3,7 +3,7 @@ isolation, with the shipped TunableOp table: time per call, TFLOP/s, and the fra
 shape's own bound max(flops / 2.5 PF, bytes / 8 TB/s).  Forward: y = x Wᵀ + b (F.linear under
 the same bf16 operands autocast produces); backward: dX = dY W (the trunk is frozen: no dW).
 
-    python scripts/gemm_shapes.py
+    python scripts/gemm_shapes.py [--untuned]
 """
 import json
 import os
@@ -35,7 +35,7 @@ def timed(fn, reps=20):
 
 def main():
     from irads.gemm_tuning import use_tuned_gemms
-    print("tuned table:", use_tuned_gemms())
+    print("tuned table:", use_tuned_gemms() if "--untuned" not in sys.argv else "off (hipBLASLt heuristic)")
     dev = torch.device("cuda:0")
     tot = {"us": 0.0, "bound_us": 0.0}
     for C, M, blocks in STAGES:
