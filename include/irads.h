@@ -453,6 +453,26 @@ int irads_adamw(int n, float *const *p, const float *const *g, float *const *m, 
                 const float *const *step, const float *const *lr, const float *wd, const long *numel, double beta1,
                 double beta2, double eps, void *stream);
 
+/* The frozen Swin trunk's projections (swin.py:81-119 qkv / proj, :586-601 mmcv FFN under bf16 autocast),
+ * replacing F.linear's hipBLASLt call and, for the FFN, the GELU element passes:
+ *   C[M x N] = A[M x K] · B[N x K]^T, bf16 operands K-contiguous (B = a Linear weight as stored, or its
+ *   transpose for dX = dY·W), fp32 accumulate;  epilogue 0: C0 = bf16(acc + bias) (bias fp32, may be
+ *   NULL); 1: C0 = U = bf16(acc + bias), C1 = bf16(GELU_erf(U)); 2: C0 = bf16(bf16(acc) · GELU_erf'(U))
+ *   (U read with leading dimension ldu).  N % 128 == 0, K % 64 == 0, leading dimensions multiples of 8,
+ *   16-byte aligned pointers. */
+int irads_gemm_nt(int epilogue, const uint16_t *A, long lda, const uint16_t *B, long ldb, const float *bias,
+                  const uint16_t *U, long ldu, uint16_t *C0, uint16_t *C1, long ldc, int M, int N, int K,
+                  void *stream);
+/* irads_gemm_nt with the tiling chosen (A/B only): 0 = 256 x 128 tiles, 2 LDS buffers; 1 = 256 x 128, 3
+ * buffers; 2 = 128 x 128 tiles, 2 buffers (irads_gemm_nt's); 3 = 128 x 128, 3 buffers. */
+int irads_gemm_nt_variant(int variant, int epilogue, const uint16_t *A, long lda, const uint16_t *B, long ldb,
+                          const float *bias, const uint16_t *U, long ldu, uint16_t *C0, uint16_t *C1, long ldc, int M,
+                          int N, int K, void *stream);
+/* irads_gemm_nt_variant (epilogue 0) logging each workgroup's wall_clock64() (100 MHz) at entry, after every
+ * k-step's barrier, after the main loop and at exit: trace[wg * (K/64 + 3) + i].  A/B only. */
+int irads_gemm_nt_trace(int variant, const uint16_t *A, long lda, const uint16_t *B, long ldb, const float *bias,
+                        uint16_t *C0, long ldc, int M, int N, int K, long long *trace, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

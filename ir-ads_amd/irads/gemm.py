@@ -1,0 +1,90 @@
+"""The frozen Swin trunk's projection GEMMs: irads_gemm_nt (csrc/gemm.hip) where it measured faster
+than hipBLASLt, F.linear / torch.mm elsewhere.
+
+Reference: the Linear layers of ShiftWindowMSA (qkv, proj; swin.py:81-119) and the mmcv FFN
+(swin.py:586-601) under bf16 autocast.  The trunk is frozen (TRAIN_TYPE Adapter), so a layer is
+used as  y = x Wᵀ + b  forward and  dX = dY W  backward, both "NT" products of K-contiguous
+operands once Wᵀ is kept beside W (made once per weight version).
+
+Which kernel serves a shape is a table, not a heuristic: scripts/gemm_tune.py times both on the
+shapes of BASELINE.json's C2 and C4 steps (interleaved rounds in one process) and writes
+tuned/irads_gemm_select_mi355x.json, the (direction, M, N, K) keys where irads_gemm_nt won by
+≥ 5 %.  A shape not in the table, or one the kernel cannot take (N % 128, K % 64), goes to
+hipBLASLt.  IRADS_GEMM=off sends every shape to hipBLASLt, IRADS_GEMM=all every shape the
+kernel takes to irads_gemm_nt (A/B and tests).
+"""
+import json
+import os
+
+import torch
+import torch.nn.functional as F
+
+from . import native as N
+
+_BF16 = torch.bfloat16
+_TABLE_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned", "irads_gemm_select_mi355x.json")
+_table = None
+
+
+def _selected():
+    global _table
+    if _table is None:
+        try:
+            with open(_TABLE_PATH) as fh:
+                _table = {tuple(k) for k in json.load(fh)["irads"]}
+        except FileNotFoundError:
+            _table = set()
+    return _table
+
+
+def kernel_fits(N_out, K):
+    return N_out % 128 == 0 and K % 64 == 0
+
+
+def use_irads(direction, M, N_out, K):
+    mode = os.environ.get("IRADS_GEMM", "table")
+    if mode == "off" or not kernel_fits(N_out, K):
+        return False
+    return mode == "all" or (direction, M, N_out, K) in _selected()
+
+
+def weights(lin):
+    """(W bf16 [N, K], b bf16 [N] or None, Wᵀ bf16 [K, N], b fp32 or None) of a frozen Linear, cached
+    on the module until a parameter's version moves (the fp32 bias is the bf16 one widened: the
+    epilogue adds exactly what hipBLASLt's bias epilogue adds)."""
+    w, b = lin.weight, lin.bias
+    key = (w.data_ptr(), w._version, None if b is None else b._version)
+    cache = lin.__dict__.get("_irads_gemm_cache")
+    if cache is None or cache[0] != key:
+        w16, b16 = lin.amp_weights(_BF16)
+        with torch.no_grad():
+            cache = (key, w16, b16, w16.t().contiguous(), None if b16 is None else b16.float())
+        lin.__dict__["_irads_gemm_cache"] = cache
+    return cache[1:]
+
+
+def _nt(A, B, bias32, M, N_out, K):
+    out = torch.empty((M, N_out), device=A.device, dtype=_BF16)
+    N.call("irads_gemm_nt", 0, N.ptr(A), A.stride(0), N.ptr(B), B.stride(0), N.ptr(bias32), None, 0, N.ptr(out),
+           None, out.stride(0), M, N_out, K, N.stream())
+    return out
+
+
+def linear(x, lw):
+    """y = x Wᵀ + b for x (M, K) bf16 contiguous and lw = weights(lin)."""
+    w16, b16, _, b32 = lw
+    M, K = x.shape
+    N_out = w16.shape[0]
+    if use_irads("fwd", M, N_out, K) and x.is_contiguous():
+        return _nt(x, w16, b32, M, N_out, K)
+    return F.linear(x, w16, b16)
+
+
+def dgrad(dy, lw):
+    """dX = dY W for dY (M, N) bf16 contiguous (the input gradient of a frozen Linear)."""
+    w16, _, wt, _ = lw
+    M, N_in = dy.shape
+    K_out = w16.shape[1]
+    if use_irads("bwd", M, K_out, N_in) and dy.is_contiguous():
+        return _nt(dy, wt, None, M, K_out, N_in)
+    return torch.mm(dy, w16)

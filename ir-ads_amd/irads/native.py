@@ -46,6 +46,9 @@ SIGNATURES = {
     "irads_resize_bwd_cl": [_i, _vp, _i, _i, _i, _i, _vp, _i, _i, _vp],
     "irads_ce_fwd": [_i, _vp, _vp, _i, _i, _i, _i, _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp],
     "irads_ce_bwd": [_i, _vp, _vp, _i, _i, _i, _i, _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp],
+    "irads_gemm_nt": [_i, _vp, _l, _vp, _l, _vp, _vp, _l, _vp, _vp, _l, _i, _i, _i, _vp],
+    "irads_gemm_nt_variant": [_i, _i, _vp, _l, _vp, _l, _vp, _vp, _l, _vp, _vp, _l, _i, _i, _i, _vp],
+    "irads_gemm_nt_trace": [_i, _vp, _l, _vp, _l, _vp, _vp, _l, _i, _i, _i, _vp, _vp],
     "irads_ce_resize_bwd": [_i, _vp, _i, _i, _i, _i, _vp, _i, _vp, _vp, _vp, _vp, _i, _i, _vp, _vp],
     "irads_resln_fwd": [_vp, _vp, _vp, _vp, _f, _i, _i, _i, _vp, _vp, _f, _vp, _vp, _vp, _vp, _vp, _vp],
     "irads_resln_bwd": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _vp, _vp, _vp, _vp, _f, _vp],

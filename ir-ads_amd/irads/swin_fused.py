@@ -13,19 +13,20 @@ stage is a single torch.autograd.Function whose forward and backward are hand-sc
   forward, per block (M = 2B*H*W rows of the rgb+dte batch, C channels)
     h1            = LN1(x)                                 [resln_fwd, fused into the
                                                             previous block's output pass]
-    qkv           = h1 Wqkvᵀ + b                          [hipBLASLt]
+    qkv           = h1 Wqkvᵀ + b                          [irads_gemm_nt | hipBLASLt, irads.gemm]
     a             = shifted-window attention(qkv)         [irads_winattn_fwd]
-    o             = a Wpᵀ + b                             [hipBLASLt]
+    o             = a Wpᵀ + b                             [irads_gemm_nt | hipBLASLt]
     X1, h2, X1b   = x + DP(o), LN2(.), bf16(.)            [resln_fwd]
-    g             = GELU(h2 W1ᵀ + b1)                      [hipBLASLt + gelu_fwd]
-    f             = g W2ᵀ + b2                             [hipBLASLt]
+    g             = GELU(h2 W1ᵀ + b1)                      [irads_gemm_nt | hipBLASLt, + gelu_fwd]
+    f             = g W2ᵀ + b2                             [irads_gemm_nt | hipBLASLt]
     d[rgb|dte]    = Adapter_{rgb|dte}(X1b[rgb|dte])        [adapter_down + adapter_up]
     x'            = (X1 + DP(f)) + 0.5 d ; h1' = LN1'(x')  [resln_fwd]
   backward mirrors it with resln_bwd producing, in one pass, the fp32 residual gradient
   and the bf16 operands of the branches (DropPath-backward, 0.5 * for the adapter).
 
-Rounding is the autocast reference's op by op (see csrc/swinblock.hip); the GEMMs are the
-same hipBLASLt calls F.linear makes under autocast.  Used only when the stage is frozen
+Rounding is the autocast reference's op by op (see csrc/swinblock.hip); each projection GEMM
+is either the hipBLASLt call F.linear makes under autocast or irads_gemm_nt (bf16 operands,
+fp32 accumulate, bf16(acc + bias)), per the measured selection table of irads.gemm.  Used only when the stage is frozen
 (no trunk parameter requires grad) and autocast runs in bf16; any other configuration takes
 the module-by-module path.  Gradient checkpointing (with_cp, Swin-L) is numerically neutral
 and is not re-enacted: the fused stage keeps its activations.
@@ -33,6 +34,7 @@ and is not re-enacted: the fused stage keeps its activations.
 import torch
 import torch.nn.functional as F
 
+from . import gemm as G
 from . import native as N
 from . import ops
 
@@ -206,21 +208,19 @@ class SwinStageFn(torch.autograd.Function):
         cur = x
         for i, blk in enumerate(blocks):
             w_msa = blk.attn.w_msa
-            wq, bq = w_msa.qkv.amp_weights(_BF16)
-            wp, bp = w_msa.proj.amp_weights(_BF16)
-            w1, b1 = blk.ffn.layers[0][0].amp_weights(_BF16)
-            w2, b2 = blk.ffn.layers[1].amp_weights(_BF16)
-            qkv = F.linear(h1, wq, bq).view(S, L, 3 * C)
+            lq, lp = G.weights(w_msa.qkv), G.weights(w_msa.proj)
+            l1, l2 = G.weights(blk.ffn.layers[0][0]), G.weights(blk.ffn.layers[1])
+            qkv = G.linear(h1, lq).view(S, L, 3 * C)
             bias_f = None if w_msa.qkv.bias is None else w_msa.qkv.bias.detach()
             table_f = w_msa.relative_position_bias_table.detach()
             a, lse = ops.winattn_fwd(qkv, bias_f, table_f, None, H, W, w_msa.num_heads, blk.attn.shift_size,
                                      w_msa.scale, table_owner=w_msa.relative_position_bias_table)
-            o = F.linear(a.view(M, C), wp, bp)
+            o = G.linear(a.view(M, C), lp)
             X1, h2, X1b, mean2, rstd2 = _resln_fwd(cur, M, C, L, add1=o, add1_scale=None if dp is None else dp[i, 0],
                                                   norm=blk.norm2, x_out=True, xb_out=True)
-            u = F.linear(h2, w1, b1)
+            u = G.linear(h2, l1)
             g = _elem("irads_gelu_fwd", u, out_like=u)
-            f = F.linear(g, w2, b2)
+            f = G.linear(g, l2)
             d = torch.empty((M, C), device=dev, dtype=_BF16)
             if fast:
                 # both Adapters in two launches: D_fc1 + ReLU + dropout, then D_fc2 (+ bias)
@@ -278,10 +278,8 @@ class SwinStageFn(torch.autograd.Function):
             blk = blocks[i]
             x, mean1, rstd1, qkv, a, lse, X1, mean2, rstd2, u, X1b, rs = ctx.saved[i]
             w_msa = blk.attn.w_msa
-            wq, _ = w_msa.qkv.amp_weights(_BF16)
-            wp, _ = w_msa.proj.amp_weights(_BF16)
-            w1, _ = blk.ffn.layers[0][0].amp_weights(_BF16)
-            w2, _ = blk.ffn.layers[1].amp_weights(_BF16)
+            lq, lp = G.weights(w_msa.qkv), G.weights(w_msa.proj)
+            l1, l2 = G.weights(blk.ffn.layers[0][0]), G.weights(blk.ffn.layers[1])
             # Adapters (per modality half): D_fc2, ReLU+dropout, D_fc1
             dX1b = torch.empty((M, C), device=g.device, dtype=_BF16)
             if fast:
@@ -334,19 +332,19 @@ class SwinStageFn(torch.autograd.Function):
                 ops.wgrad(da1, X1b[rows], gwa1, colsum_a=gba1)
                 torch.mm(da1, wa1, out=dX1b[rows])
             # FFN
-            dgl = torch.mm(df, w2)
+            dgl = G.dgrad(df, l2)
             du = torch.empty_like(dgl)
             N.call("irads_gelu_bwd", N.ptr(u), N.ptr(dgl), N.ptr(du), du.numel(), N.stream())
-            dh2 = torch.mm(du, w1)
+            dh2 = G.dgrad(du, l1)
             dX1, do, _ = _resln_bwd(M, C, L, dy=dh2, x=X1, mean=mean2, rstd=rstd2, norm=blk.norm2, g_res=g,
                                     g_add=dX1b, b1=True, b1_scale=None if dp is None else dp[i, 0])
             # attention
-            da = torch.mm(do, wp).view(S, L, C)
+            da = G.dgrad(do, lp).view(S, L, C)
             bias_f = None if w_msa.qkv.bias is None else w_msa.qkv.bias.detach()
             gqkv, _, _ = ops.winattn_bwd(qkv, bias_f, w_msa.relative_position_bias_table.detach(), None, H, W,
                                          w_msa.num_heads, blk.attn.shift_size, w_msa.scale, a, lse, da,
                                          table_owner=w_msa.relative_position_bias_table)
-            dh1 = torch.mm(gqkv.view(M, 3 * C), wq)
+            dh1 = G.dgrad(gqkv.view(M, 3 * C), lq)
             if i > 0:
                 g, df, dd = _resln_bwd(M, C, L, dy=dh1, x=x, mean=mean1, rstd=rstd1, norm=blk.norm1, g_res=dX1,
                                        b1=True, b2=True, b1_scale=None if dp is None else dp[i - 1, 1])

@@ -385,3 +385,22 @@ def test_native_adamw_refuses_cpu_parameters():
     m = torch.nn.Module()
     m.Adapter = torch.nn.Linear(2, 2)
     assert type(get_optimizer(m, "adamw", 1e-3, "Adapter")) is torch.optim.AdamW
+
+
+def test_gemm_selection_table_and_dispatch_modes(monkeypatch):
+    """irads.gemm's shipped selection table (scripts/gemm_tune.py on an MI355X) holds only shapes the
+    kernel takes (N % 128, K % 64), keyed (direction, M, N_out, K); the dispatch modes honour it."""
+    from irads import gemm as G
+    keys = G._selected()
+    assert keys, "tuned/irads_gemm_select_mi355x.json missing or empty"
+    for d, M, n, k in keys:
+        assert d in ("fwd", "bwd") and M > 0 and G.kernel_fits(n, k), (d, M, n, k)
+    # the C2 step's stage-2 attention projection, the shape it wins most on, is in the table
+    assert ("fwd", 16384, 512, 512) in keys and ("bwd", 16384, 512, 512) in keys
+    some = next(iter(keys))
+    monkeypatch.setenv("IRADS_GEMM", "table")
+    assert G.use_irads(*some) and not G.use_irads("fwd", 16384, 192, 192)
+    monkeypatch.setenv("IRADS_GEMM", "off")
+    assert not G.use_irads(*some)
+    monkeypatch.setenv("IRADS_GEMM", "all")
+    assert G.use_irads("fwd", 5, 256, 128) and not G.use_irads("fwd", 5, 192, 128)
