@@ -35,10 +35,10 @@ typedef __attribute__((address_space(1))) void g_glb_void;
 constexpr int GBN = 128, GBK = 64, G_B_BYTES = GBN * GBK * 2;
 enum { EPI_BIAS = 0, EPI_GELU = 1, EPI_DGELU = 2 };
 
-__device__ __forceinline__ float g_gelu(float x) { return x * 0.5f * (1.f + erff(x * 0.70710678118654752440f)); }
+__device__ __forceinline__ float g_gelu(float x) { return x * 0.5f * (1.f + erf_f32(x * 0.70710678118654752440f)); }
 __device__ __forceinline__ float g_gelu_grad(float x) {
-    const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752440f));
-    const float pdf = expf(-0.5f * x * x) * 0.39894228040143267794f;
+    const float cdf = 0.5f * (1.f + erf_f32(x * 0.70710678118654752440f));
+    const float pdf = __expf(-0.5f * x * x) * 0.39894228040143267794f;
     return cdf + x * pdf;
 }
 

@@ -271,10 +271,10 @@ __device__ __forceinline__ u32x4 pack8(const float *f) {
     return w;
 }
 
-__device__ __forceinline__ float gelu_f(float x) { return x * 0.5f * (1.f + erff(x * 0.70710678118654752440f)); }
+__device__ __forceinline__ float gelu_f(float x) { return x * 0.5f * (1.f + erf_f32(x * 0.70710678118654752440f)); }
 __device__ __forceinline__ float gelu_grad(float x) {
-    const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752440f));
-    const float pdf = expf(-0.5f * x * x) * 0.39894228040143267794f;
+    const float cdf = 0.5f * (1.f + erf_f32(x * 0.70710678118654752440f));
+    const float pdf = __expf(-0.5f * x * x) * 0.39894228040143267794f;
     return cdf + x * pdf;
 }
 
