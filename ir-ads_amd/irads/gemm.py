@@ -9,8 +9,10 @@ operands once Wᵀ is kept beside W (made once per weight version).
 Which kernel serves a shape is a table, not a heuristic: scripts/gemm_tune.py times both on the
 shapes of BASELINE.json's C2 and C4 steps (interleaved rounds in one process) and writes
 tuned/irads_gemm_select_mi355x.json, the (direction, M, N, K) keys where irads_gemm_nt won by
-≥ 5 %.  A shape not in the table, or one the kernel cannot take (N % 128, K % 64), goes to
-hipBLASLt.  IRADS_GEMM=off sends every shape to hipBLASLt, IRADS_GEMM=all every shape the
+≥ 5 %.  Directions: "fwd" (y = x Wᵀ + b), "bwd" (dX = dY W), and the FFN's fused pairs
+"fwd_gelu" (fc1 with the erf GELU in the epilogue, against the better GEMM + gelu pass) and
+"bwd_dgelu" (fc2's dX with GELU' applied in the epilogue, against GEMM + gelu_bwd pass).  A
+shape not in the table, or one the kernel cannot take (N % 128, K % 64), goes to hipBLASLt.  IRADS_GEMM=off sends every shape to hipBLASLt, IRADS_GEMM=all every shape the
 kernel takes to irads_gemm_nt (A/B and tests).
 """
 import json
@@ -78,6 +80,42 @@ def linear(x, lw):
     if use_irads("fwd", M, N_out, K) and x.is_contiguous():
         return _nt(x, w16, b32, M, N_out, K)
     return F.linear(x, w16, b16)
+
+
+def ffn_up(h, lw):
+    """(U, G) = (h W1ᵀ + b1, GELU(U)) of the FFN's first Linear: one irads_gemm_nt launch with the GELU
+    in its epilogue where the table says so ("fwd_gelu"), else the GEMM and the element pass."""
+    w16, _, _, b32 = lw
+    M, K = h.shape
+    N_out = w16.shape[0]
+    if use_irads("fwd_gelu", M, N_out, K) and h.is_contiguous():
+        u = torch.empty((M, N_out), device=h.device, dtype=_BF16)
+        g = torch.empty_like(u)
+        N.call("irads_gemm_nt", 1, N.ptr(h), h.stride(0), N.ptr(w16), w16.stride(0), N.ptr(b32), None, 0,
+               N.ptr(u), N.ptr(g), u.stride(0), M, N_out, K, N.stream())
+        return u, g
+    u = linear(h, lw)
+    g = torch.empty_like(u)
+    N.call("irads_gelu_fwd", N.ptr(u), N.ptr(g), u.numel(), N.stream())
+    return u, g
+
+
+def ffn_down_dgrad_gelu(df, lw, u):
+    """dU = GELU'(U) ⊙ (dF W2) through the FFN's second Linear and the GELU: one irads_gemm_nt launch
+    with the dGELU in its epilogue where the table says so ("bwd_dgelu"; dG never reaches HBM), else
+    the input-gradient GEMM and the element pass."""
+    w16, _, wt, _ = lw
+    M, N_in = df.shape
+    K_out = w16.shape[1]
+    if use_irads("bwd_dgelu", M, K_out, N_in) and df.is_contiguous() and u.is_contiguous():
+        du = torch.empty((M, K_out), device=df.device, dtype=_BF16)
+        N.call("irads_gemm_nt", 2, N.ptr(df), df.stride(0), N.ptr(wt), wt.stride(0), None, N.ptr(u), u.stride(0),
+               N.ptr(du), None, du.stride(0), M, K_out, N_in, N.stream())
+        return du
+    dg = dgrad(df, lw)
+    du = torch.empty_like(dg)
+    N.call("irads_gelu_bwd", N.ptr(u), N.ptr(dg), N.ptr(du), du.numel(), N.stream())
+    return du
 
 
 def dgrad(dy, lw):

@@ -17,7 +17,7 @@ stage is a single torch.autograd.Function whose forward and backward are hand-sc
     a             = shifted-window attention(qkv)         [irads_winattn_fwd]
     o             = a Wpᵀ + b                             [irads_gemm_nt | hipBLASLt]
     X1, h2, X1b   = x + DP(o), LN2(.), bf16(.)            [resln_fwd]
-    g             = GELU(h2 W1ᵀ + b1)                      [irads_gemm_nt | hipBLASLt, + gelu_fwd]
+    g             = GELU(h2 W1ᵀ + b1)                      [irads_gemm_nt GELU epilogue | GEMM + gelu_fwd]
     f             = g W2ᵀ + b2                             [irads_gemm_nt | hipBLASLt]
     d[rgb|dte]    = Adapter_{rgb|dte}(X1b[rgb|dte])        [adapter_down + adapter_up]
     x'            = (X1 + DP(f)) + 0.5 d ; h1' = LN1'(x')  [resln_fwd]
@@ -218,8 +218,7 @@ class SwinStageFn(torch.autograd.Function):
             o = G.linear(a.view(M, C), lp)
             X1, h2, X1b, mean2, rstd2 = _resln_fwd(cur, M, C, L, add1=o, add1_scale=None if dp is None else dp[i, 0],
                                                   norm=blk.norm2, x_out=True, xb_out=True)
-            u = G.linear(h2, l1)
-            g = _elem("irads_gelu_fwd", u, out_like=u)
+            u, g = G.ffn_up(h2, l1)
             f = G.linear(g, l2)
             d = torch.empty((M, C), device=dev, dtype=_BF16)
             if fast:
@@ -332,9 +331,7 @@ class SwinStageFn(torch.autograd.Function):
                 ops.wgrad(da1, X1b[rows], gwa1, colsum_a=gba1)
                 torch.mm(da1, wa1, out=dX1b[rows])
             # FFN
-            dgl = G.dgrad(df, l2)
-            du = torch.empty_like(dgl)
-            N.call("irads_gelu_bwd", N.ptr(u), N.ptr(dgl), N.ptr(du), du.numel(), N.stream())
+            du = G.ffn_down_dgrad_gelu(df, l2, u)
             dh2 = G.dgrad(du, l1)
             dX1, do, _ = _resln_bwd(M, C, L, dy=dh2, x=X1, mean=mean2, rstd=rstd2, norm=blk.norm2, g_res=g,
                                     g_add=dX1b, b1=True, b1_scale=None if dp is None else dp[i, 0])

@@ -3,6 +3,8 @@ on every trunk projection shape of BASELINE.json's C2 (Swin-B, 8 x 512², rgb + 
 (Swin-L, 4 x 480x640) steps, forward y = x Wᵀ + b and backward dX = dY W, in interleaved rounds in
 one process (median of 5 rounds x 10 calls each).  A shape goes to irads_gemm_nt when its median is
 ≥ 5 % below hipBLASLt's and its error against the fp32 product is no worse than 1.5x hipBLASLt's.
+The FFN's fused pairs (fc1 + GELU epilogue, fc2 dX + GELU' epilogue) are timed against the better
+unfused arm (hipBLASLt or irads_gemm_nt, then the element pass) and kept on the same 5 % margin.
 
     python scripts/gemm_tune.py [out.json]    (default gpurun_out/irads_gemm_select_mi355x.json;
                                                copy it to ir-ads_amd/irads/tuned/ to ship it)
@@ -49,6 +51,67 @@ def nt(A, B, bias32):
     return out
 
 
+def gelu(u):
+    g = torch.empty_like(u)
+    N.call("irads_gelu_fwd", N.ptr(u), N.ptr(g), u.numel(), N.stream())
+    return g
+
+
+def gelu_bwd(u, dg):
+    du = torch.empty_like(dg)
+    N.call("irads_gelu_bwd", N.ptr(u), N.ptr(dg), N.ptr(du), du.numel(), N.stream())
+    return du
+
+
+def fused_rows(cfg, M, C, C4, A, W1, b16, b32):
+    """The FFN's fused pairs against the better unfused arm: fc1 + GELU (U, G), and fc2's dX + GELU'
+    (dU; fc2 = W2 (C, 4C), so its dX is (M, 4C) = dF (M, C) · W2 with U of fc1's output shape)."""
+    out, keys = [], []
+    lib_fc1 = lambda: gelu(F.linear(A, W1, b16))  # noqa: E731
+    ir_fc1 = lambda: gelu(nt(A, W1, b32))  # noqa: E731
+
+    def fused_fc1():
+        u = torch.empty((M, C4), device=A.device, dtype=torch.bfloat16)
+        g = torch.empty_like(u)
+        N.call("irads_gemm_nt", 1, N.ptr(A), A.stride(0), N.ptr(W1), W1.stride(0), N.ptr(b32), None, 0, N.ptr(u),
+               N.ptr(g), u.stride(0), M, C4, C, N.stream())
+        return g
+    W2 = (torch.randn(C, C4, device=A.device) * C4 ** -0.5).bfloat16()  # fc2's weight (C, 4C)
+    W2t = W2.t().contiguous()  # (4C, C)
+    dF = torch.randn(M, C, device=A.device).bfloat16()
+    U = (torch.randn(M, C4, device=A.device) * 1.5).bfloat16()
+    lib_fc2 = lambda: gelu_bwd(U, torch.mm(dF, W2))  # noqa: E731
+    ir_fc2 = lambda: gelu_bwd(U, nt(dF, W2t, None))  # noqa: E731
+
+    def fused_fc2():
+        du = torch.empty((M, C4), device=A.device, dtype=torch.bfloat16)
+        N.call("irads_gemm_nt", 2, N.ptr(dF), dF.stride(0), N.ptr(W2t), W2t.stride(0), None, N.ptr(U), U.stride(0),
+               N.ptr(du), None, du.stride(0), M, C4, C, N.stream())
+        return du
+    for d, key, arms in (("fwd_gelu", ("fwd_gelu", M, C4, C), (lib_fc1, ir_fc1, fused_fc1)),
+                         ("bwd_dgelu", ("bwd_dgelu", M, C4, C), (lib_fc2, ir_fc2, fused_fc2))):
+        if not G.kernel_fits(key[2], key[3]):
+            continue
+        ref = arms[0]()
+        e = [rel(a(), ref) for a in arms]
+        for a in arms:
+            a(), a()
+        ts = [[], [], []]
+        for _ in range(5):
+            for j, a in enumerate(arms):
+                ts[j].append(timed(a))
+        med = [statistics.median(t) for t in ts]
+        win = med[2] < 0.95 * min(med[0], med[1]) and e[2] <= 2e-2
+        row = {"cfg": cfg, "op": "fc1+gelu" if d == "fwd_gelu" else "fc2+dgelu", "dir": d, "M": M, "N": C4, "K": C,
+               "lib_plus_pass_us": round(med[0], 2), "irads_plus_pass_us": round(med[1], 2),
+               "fused_us": round(med[2], 2), "fused_vs_lib_rel": round(e[2], 6), "irads": win}
+        print(json.dumps(row), flush=True)
+        out.append(row)
+        if win:
+            keys.append(list(key))
+    return out, keys
+
+
 def main():
     from irads.gemm_tuning import use_tuned_gemms
     use_tuned_gemms()
@@ -90,6 +153,10 @@ def main():
                 rows.append(row)
                 if win:
                     keys.append(list(key))
+            if op == "fc1" and G.kernel_fits(Nn, K):
+                rows_, keys_ = fused_rows(cfg, M, K, Nn, A, W, b16, b32)
+                rows += rows_
+                keys += keys_
             del A, W, Wt, dY
             torch.cuda.empty_cache()
     os.makedirs(os.path.dirname(out_path) or ".", exist_ok=True)

@@ -1,0 +1,9 @@
+#!/bin/bash
+# Bench line + kernel trace + step breakdown only (no test suite).   bash scripts/gpu_r04_p.sh <tag>
+cd "$(dirname "$0")/.."
+tag=${1:-r04p}
+mkdir -p gpurun_out
+timeout -k 10 500 python bench.py --steps 20 --warmup 5 > gpurun_out/bench_$tag.log 2>&1 || { echo bench failed; tail gpurun_out/bench_$tag.log; exit 1; }
+tail -1 gpurun_out/bench_$tag.log | cut -c1-300
+PROFILE_TIMEOUT=300 bash scripts/profile_bench.sh prof_$tag --steps 4 --warmup 4 --no-cpu-baseline --profile-only || exit $?
+f=$(find gpurun_out/prof_$tag -name "*kernel_trace.csv.gz" | head -1); python3 scripts/trace_summary.py "$f" --steps 4 --match winattn > gpurun_out/step_breakdown_$tag.txt 2>&1; head -45 gpurun_out/step_breakdown_$tag.txt

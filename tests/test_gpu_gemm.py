@@ -126,3 +126,36 @@ def test_dispatch_linear_and_dgrad(mode, monkeypatch):
         lin.weight.mul_(2)
     lw2 = G.weights(lin)
     assert torch.equal(lw2[2], lin.amp_weights(torch.bfloat16)[0].t())
+
+
+@pytest.mark.parametrize("mode", ["all", "off"])
+def test_ffn_fused_gelu_paths(mode, monkeypatch):
+    """irads.gemm.ffn_up / ffn_down_dgrad_gelu (GELU and GELU' in irads_gemm_nt's epilogue) against the
+    unfused GEMM + element passes: bit for bit given the same GEMM (mode all: both arms irads_gemm_nt),
+    and within hipBLASLt's own rounding of the fp32 result (mode off: the hipBLASLt arm)."""
+    from irads import gemm as G
+    from semseg.models.layers.common import Linear
+    N = _N()
+    torch.manual_seed(13)
+    C, M = 256, 4096
+    fc1 = Linear(C, 4 * C).to(DEV).requires_grad_(False)
+    fc2 = Linear(4 * C, C).to(DEV).requires_grad_(False)
+    l1, l2 = G.weights(fc1), G.weights(fc2)
+    h = torch.randn(M, C, device=DEV).bfloat16()
+    df = torch.randn(M, C, device=DEV).bfloat16()
+    monkeypatch.setenv("IRADS_GEMM", mode)
+    u, g = G.ffn_up(h, l1)
+    du = G.ffn_down_dgrad_gelu(df, l2, u)
+    # unfused arms with the same GEMM kernel
+    u2 = G.linear(h, l1)
+    g2 = torch.empty_like(u2)
+    N.call("irads_gelu_fwd", N.ptr(u2), N.ptr(g2), u2.numel(), N.stream())
+    dg2 = G.dgrad(df, l2)
+    du2 = torch.empty_like(dg2)
+    N.call("irads_gelu_bwd", N.ptr(u), N.ptr(dg2), N.ptr(du2), du2.numel(), N.stream())
+    assert torch.equal(u, u2) and torch.equal(g, g2) and torch.equal(du, du2)
+    # and against fp32 math on the same operands
+    w1, b1 = fc1.amp_weights(torch.bfloat16)
+    ref_u = torch.addmm(b1.float(), h.float(), w1.float().t())
+    assert _rel(u, ref_u) < 4e-3
+    assert _rel(g, F.gelu(ref_u)) < 4e-3
