@@ -32,7 +32,7 @@ typedef __attribute__((ext_vector_type(4))) unsigned short gu16x4;
 typedef __attribute__((address_space(3))) void g_lds_void;
 typedef __attribute__((address_space(1))) void g_glb_void;
 
-constexpr int GBN = 128, GBK = 64, G_B_BYTES = GBN * GBK * 2;
+constexpr int GBN = 128, GBK = 64;  // GBN: the column granule every tiling takes (N % 128 == 0)
 enum { EPI_BIAS = 0, EPI_GELU = 1, EPI_DGELU = 2 };
 
 __device__ __forceinline__ float g_gelu(float x) { return x * 0.5f * (1.f + erf_f32(x * 0.70710678118654752440f)); }
@@ -67,8 +67,9 @@ __device__ __forceinline__ gbf16x8 g_frag(const unsigned char *img, int rb, int 
     return *(const gbf16x8 *)(img + row * 128 + ((c ^ (row & 7)) << 4));
 }
 
-template <int EPI, int NS, int BMT, bool TR = false>
-__global__ void __launch_bounds__(BMT * 2) gemm_nt_bf16(const unsigned short *__restrict__ A, long lda,
+// BMT x BNT tile on (BMT / WR) x (BNT / 64) waves, each WR x 64 (WR / 16 x 4 MFMA blocks)
+template <int EPI, int NS, int BMT, int BNT, int WR, bool TR = false>
+__global__ void __launch_bounds__((BMT / WR) * (BNT / 64) * 64) gemm_nt_bf16(const unsigned short *__restrict__ A, long lda,
                                                     const unsigned short *__restrict__ B, long ldb,
                                                     const float *__restrict__ bias,
                                                     const unsigned short *__restrict__ U, long ldu,
@@ -76,21 +77,21 @@ __global__ void __launch_bounds__(BMT * 2) gemm_nt_bf16(const unsigned short *__
                                                     long ldc, int M, int N, int K, long long *trace = nullptr) {
     // TR: wave 0 of every workgroup logs wall_clock64() at entry, after each k-step's barrier, after the
     // main loop and at exit into trace[blockIdx.x * (K / 64 + 3) ...] (irads_gemm_nt_trace, A/B only)
-    constexpr int NW = BMT / 32;  // (BMT / 64) x 2 waves of 64 x 64
-    constexpr int G_A_BYTES = BMT * GBK * 2, G_STAGE = G_A_BYTES + G_B_BYTES;
+    constexpr int NWN = BNT / 64, NW = (BMT / WR) * NWN, MI = WR / 16;
+    constexpr int G_A_BYTES = BMT * GBK * 2, G_STAGE = G_A_BYTES + BNT * GBK * 2;
     long long *tr = TR ? trace + (long)blockIdx.x * (K / GBK + 3) : nullptr;
     if (TR && threadIdx.x == 0) tr[0] = wall_clock64();
     __shared__ __attribute__((aligned(16))) unsigned char smem[NS * G_STAGE];  // ONE array (glds wait trap)
-    const int nbn = N / GBN;
+    const int nbn = N / BNT;
     const int lid = xcd_remap(blockIdx.x, gridDim.x);  // the N tiles of an M row-band on one XCD
     const int bm = lid / nbn, bn = lid - bm * nbn;
-    const int m0 = bm * BMT, n0 = bn * GBN;
+    const int m0 = bm * BMT, n0 = bn * BNT;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const int wm = wave >> 1, wn = wave & 1;
+    const int wm = wave / NWN, wn = wave % NWN;
     const int grp = lane >> 4;
-    f32x4 acc[4][4];
+    f32x4 acc[MI][4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     const int nk = K / GBK;
@@ -105,12 +106,12 @@ __global__ void __launch_bounds__(BMT * 2) gemm_nt_bf16(const unsigned short *__
     // NS-buffer ring, NS - 1 k-steps in flight: step ks waits (counted vmcnt, G_LOADS global_load_lds per
     // wave and stage) for its own stage only, the barrier after it publishes every wave's DMA and retires
     // every read of buffer (ks - 1) % NS, which then takes stage ks + NS - 1.
-    constexpr int G_LOADS = (BMT + GBN) / (8 * NW);
+    constexpr int G_LOADS = (BMT + BNT) / (8 * NW);
 #pragma unroll
     for (int s = 0; s < NS - 1; ++s)
         if (s < nk) {
             g_stage<BMT, NW>(A, lda, m0, M - 1, s * GBK, smem + s * G_STAGE, wave, lane);
-            g_stage<GBN, NW>(B, ldb, n0, N - 1, s * GBK, smem + s * G_STAGE + G_A_BYTES, wave, lane);
+            g_stage<BNT, NW>(B, ldb, n0, N - 1, s * GBK, smem + s * G_STAGE + G_A_BYTES, wave, lane);
         }
     for (int ks = 0; ks < nk; ++ks) {
         if (NS == 3 && ks + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G_LOADS) : "memory");
@@ -122,26 +123,31 @@ __global__ void __launch_bounds__(BMT * 2) gemm_nt_bf16(const unsigned short *__
         if (ks + NS - 1 < nk) {
             unsigned char *nx = smem + ((ks + NS - 1) % NS) * G_STAGE;
             g_stage<BMT, NW>(A, lda, m0, M - 1, (ks + NS - 1) * GBK, nx, wave, lane);
-            g_stage<GBN, NW>(B, ldb, n0, N - 1, (ks + NS - 1) * GBK, nx + G_A_BYTES, wave, lane);
+            g_stage<BNT, NW>(B, ldb, n0, N - 1, (ks + NS - 1) * GBK, nx + G_A_BYTES, wave, lane);
         }
-        // all 16 fragment reads of the step up front: the second half's land under the first half's MFMAs
-        gbf16x8 af[2][4], bf[2][4];
+        // 64 x 64 waves: all 16 fragment reads of the step up front (the second half's land under the
+        // first half's MFMAs); 128 x 64 waves (128 accumulator registers) read one half at a time
+        constexpr int KU = MI == 4 ? 2 : 1;
 #pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {
+        for (int k0 = 0; k0 < 2; k0 += KU) {
+            gbf16x8 af[KU][MI], bf[KU][4];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) bf[kk][j] = g_frag(Bs, wn * 64 + j * 16, kk * 4 + grp, lane);
+            for (int kk = 0; kk < KU; ++kk) {
 #pragma unroll
-            for (int i = 0; i < 4; ++i) af[kk][i] = g_frag(As, wm * 64 + i * 16, kk * 4 + grp, lane);
+                for (int j = 0; j < 4; ++j) bf[kk][j] = g_frag(Bs, wn * 64 + j * 16, (k0 + kk) * 4 + grp, lane);
+#pragma unroll
+                for (int i = 0; i < MI; ++i) af[kk][i] = g_frag(As, wm * WR + i * 16, (k0 + kk) * 4 + grp, lane);
+            }
+            __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+            for (int kk = 0; kk < KU; ++kk)
+#pragma unroll
+                for (int i = 0; i < MI; ++i)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[kk][j], af[kk][i], acc[i][j], 0, 0, 0);
+            __builtin_amdgcn_s_setprio(0);
         }
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-                for (int j = 0; j < 4; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[kk][j], af[kk][i], acc[i][j], 0, 0, 0);
-        __builtin_amdgcn_s_setprio(0);
     }
     // Epilogue through LDS: the wave's 64 x 64 tile, rounded to bf16 in the MFMA layout (lane: row
     // 16 i + (lane & 15), columns 16 j + 4 grp .. + 3), goes to its own 8 KiB LDS region, then back as
@@ -149,63 +155,73 @@ __global__ void __launch_bounds__(BMT * 2) gemm_nt_bf16(const unsigned short *__
     // EPI_DGELU, full-line loads of U).  Rows of the region: 128 B with 16-B chunk c at slot
     // c ^ (row & 7), so the row-wise reads are conflict free.
     // EPI_DGELU: this lane's 8 rows x 8 columns of U (the row-wise layout below), issued before the LDS
-    // round trip so their latency hides under it (rows past M clamped: loaded, never stored)
+    // round trip so their latency hides under it (rows past M clamped: loaded, never stored).
+    // (WR = 128: two 64-row halves through the same region, one after the other)
     const int lr = lane >> 3, lc = lane & 7;
-    gu16x8 uq[8];
-    if (EPI == EPI_DGELU) {
-#pragma unroll
-        for (int it = 0; it < 8; ++it) {
-            const int m = min(m0 + wm * 64 + it * 8 + lr, M - 1);
-            uq[it] = *(const gu16x8 *)(U + (long)m * ldu + n0 + wn * 64 + lc * 8);
-        }
-    }
     // every wave's last fragment reads of the main loop are done (consumed by its MFMAs); a raw barrier,
     // as __syncthreads() would also wait for the U loads in flight
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    if (TR && tid == 0) tr[1 + nk] = wall_clock64();
     unsigned char *reg = smem + wave * 8192;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int nl = j * 16 + grp * 4;  // column within the wave tile
-        const f32x4 b4 = hasb ? bq[j] : f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int h = 0; h < WR / 64; ++h) {
+        const int mh = m0 + wm * WR + h * 64;  // first row of this half
+        gu16x8 uq[8];
+        if (EPI == EPI_DGELU) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int row = i * 16 + (lane & 15);
-            gu16x4 w;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) w[r] = f2bf(acc[i][j][r] + b4[r]);  // EPI_DGELU: b4 = 0, bf16(acc)
-            const int c = nl >> 3, half = (nl >> 2) & 1;  // 16-B chunk and its 8-B half
-            *(gu16x4 *)(reg + row * 128 + ((c ^ (row & 7)) << 4) + half * 8) = w;
-        }
-    }
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes are done (own region only)
-    __builtin_amdgcn_wave_barrier();
-    gu16x8 v[8];
-#pragma unroll
-    for (int it = 0; it < 8; ++it) {
-        const int row = it * 8 + lr;
-        v[it] = *(const gu16x8 *)(reg + row * 128 + ((lc ^ (row & 7)) << 4));
-    }
-#pragma unroll
-    for (int it = 0; it < 8; ++it) {
-        const int m = m0 + wm * 64 + it * 8 + lr;
-        const long o = (long)m * ldc + n0 + wn * 64 + lc * 8;
-        if (EPI == EPI_BIAS) {
-            if (m < M) *(gu16x8 *)(C0 + o) = v[it];
-        } else if (EPI == EPI_GELU) {
-            gu16x8 g;
-#pragma unroll
-            for (int e = 0; e < 8; ++e) g[e] = f2bf(g_gelu(bf2f(v[it][e])));
-            if (m < M) {
-                *(gu16x8 *)(C0 + o) = v[it];
-                *(gu16x8 *)(C1 + o) = g;
+            for (int it = 0; it < 8; ++it) {
+                const int m = min(mh + it * 8 + lr, M - 1);
+                uq[it] = *(const gu16x8 *)(U + (long)m * ldu + n0 + wn * 64 + lc * 8);
             }
+        }
+        if (h == 0) {
+            __builtin_amdgcn_s_barrier();
+            __builtin_amdgcn_sched_barrier(0);
+            if (TR && tid == 0) tr[1 + nk] = wall_clock64();
         } else {
-            gu16x8 d;
+            __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the previous half's row reads are done
+            __builtin_amdgcn_wave_barrier();
+        }
 #pragma unroll
-            for (int e = 0; e < 8; ++e) d[e] = f2bf(bf2f(v[it][e]) * g_gelu_grad(bf2f(uq[it][e])));
-            if (m < M) *(gu16x8 *)(C0 + o) = d;
+        for (int j = 0; j < 4; ++j) {
+            const int nl = j * 16 + grp * 4;  // column within the wave tile
+            const f32x4 b4 = hasb ? bq[j] : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int row = i * 16 + (lane & 15);
+                gu16x4 w;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) w[r] = f2bf(acc[h * 4 + i][j][r] + b4[r]);  // EPI_DGELU: b4 = 0
+                const int c = nl >> 3, half = (nl >> 2) & 1;  // 16-B chunk and its 8-B half
+                *(gu16x4 *)(reg + row * 128 + ((c ^ (row & 7)) << 4) + half * 8) = w;
+            }
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes are done (own region only)
+        __builtin_amdgcn_wave_barrier();
+        gu16x8 v[8];
+#pragma unroll
+        for (int it = 0; it < 8; ++it) {
+            const int row = it * 8 + lr;
+            v[it] = *(const gu16x8 *)(reg + row * 128 + ((lc ^ (row & 7)) << 4));
+        }
+#pragma unroll
+        for (int it = 0; it < 8; ++it) {
+            const int m = mh + it * 8 + lr;
+            const long o = (long)m * ldc + n0 + wn * 64 + lc * 8;
+            if (EPI == EPI_BIAS) {
+                if (m < M) *(gu16x8 *)(C0 + o) = v[it];
+            } else if (EPI == EPI_GELU) {
+                gu16x8 g;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) g[e] = f2bf(g_gelu(bf2f(v[it][e])));
+                if (m < M) {
+                    *(gu16x8 *)(C0 + o) = v[it];
+                    *(gu16x8 *)(C1 + o) = g;
+                }
+            } else {
+                gu16x8 d;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) d[e] = f2bf(bf2f(v[it][e]) * g_gelu_grad(bf2f(uq[it][e])));
+                if (m < M) *(gu16x8 *)(C0 + o) = d;
+            }
         }
     }
     if (TR) {
@@ -220,14 +236,16 @@ __global__ void __launch_bounds__(BMT * 2) gemm_nt_bf16(const unsigned short *__
 using namespace irads;
 
 // variant: 0 = 256 x 128 tiles, 2 buffers; 1 = 256 x 128, 3 buffers (1 workgroup per CU either way);
-// 2 = 128 x 128 tiles on 4 waves, 2 buffers (64 KiB: 2 workgroups per CU); 3 = 128 x 128, 3 buffers
+// 2 = 128 x 128 tiles on 4 waves, 2 buffers (64 KiB: 2 workgroups per CU); 3 = 128 x 128, 3 buffers;
+// 4 = 256 x 256 tiles on 8 waves of 128 x 64, 2 buffers (128 KiB; N % 256 == 0)
 template <int EPI, int V, bool TR = false>
 static void gemm_launch(const uint16_t *A, long lda, const uint16_t *B, long ldb, const float *bias, const uint16_t *U,
                         long ldu, uint16_t *C0, uint16_t *C1, long ldc, int M, int N, int K, long long *trace,
                         hipStream_t st) {
-    constexpr int BMT = V < 2 ? 256 : 128, NS = (V & 1) ? 3 : 2;
-    const unsigned nwg = (unsigned)(((M + BMT - 1) / BMT) * (N / GBN));
-    gemm_nt_bf16<EPI, NS, BMT, TR><<<nwg, BMT * 2, 0, st>>>(
+    constexpr int BMT = (V < 2 || V == 4) ? 256 : 128, NS = (V & 1) ? 3 : 2, BNT = V == 4 ? 256 : 128;
+    constexpr int WR = V == 4 ? 128 : 64;
+    const unsigned nwg = (unsigned)(((M + BMT - 1) / BMT) * (N / BNT));
+    gemm_nt_bf16<EPI, NS, BMT, BNT, WR, TR><<<nwg, (BMT / WR) * (BNT / 64) * 64, 0, st>>>(
         (const unsigned short *)A, lda, (const unsigned short *)B, ldb, bias, (const unsigned short *)U, ldu,
         (unsigned short *)C0, (unsigned short *)C1, ldc, M, N, K, trace);
 }
@@ -240,7 +258,8 @@ static void gemm_dispatch(int variant, const uint16_t *A, long lda, const uint16
     case 0: gemm_launch<EPI, 0>(A, lda, B, ldb, bias, U, ldu, C0, C1, ldc, M, N, K, nullptr, st); break;
     case 1: gemm_launch<EPI, 1>(A, lda, B, ldb, bias, U, ldu, C0, C1, ldc, M, N, K, nullptr, st); break;
     case 2: gemm_launch<EPI, 2>(A, lda, B, ldb, bias, U, ldu, C0, C1, ldc, M, N, K, nullptr, st); break;
-    default: gemm_launch<EPI, 3>(A, lda, B, ldb, bias, U, ldu, C0, C1, ldc, M, N, K, nullptr, st); break;
+    case 3: gemm_launch<EPI, 3>(A, lda, B, ldb, bias, U, ldu, C0, C1, ldc, M, N, K, nullptr, st); break;
+    default: gemm_launch<EPI, 4>(A, lda, B, ldb, bias, U, ldu, C0, C1, ldc, M, N, K, nullptr, st); break;
     }
 }
 
@@ -248,7 +267,8 @@ extern "C" int irads_gemm_nt_variant(int variant, int epilogue, const uint16_t *
                                      long ldb, const float *bias, const uint16_t *U, long ldu, uint16_t *C0,
                                      uint16_t *C1, long ldc, int M, int N, int K, void *stream) {
     IRADS_REQUIRE(epilogue >= 0 && epilogue <= 2, "irads_gemm_nt: epilogue %d", epilogue);
-    IRADS_REQUIRE(variant >= 0 && variant <= 3, "irads_gemm_nt: variant %d", variant);
+    IRADS_REQUIRE(variant >= 0 && variant <= 4, "irads_gemm_nt: variant %d", variant);
+    IRADS_REQUIRE(variant != 4 || N % 256 == 0, "irads_gemm_nt: the 256 x 256 tiling needs N %% 256 == 0 (N=%d)", N);
     IRADS_REQUIRE(M >= 0 && N > 0 && K > 0 && N % GBN == 0 && K % GBK == 0,
                   "irads_gemm_nt: needs N %% 128 == 0 and K %% 64 == 0 (M=%d N=%d K=%d)", M, N, K);
     IRADS_REQUIRE(A && B && C0 && (epilogue != 1 || C1) && (epilogue != 2 || U), "irads_gemm_nt: null pointer");
@@ -275,14 +295,16 @@ extern "C" int irads_gemm_nt(int epilogue, const uint16_t *A, long lda, const ui
 extern "C" int irads_gemm_nt_trace(int variant, const uint16_t *A, long lda, const uint16_t *B, long ldb,
                                    const float *bias, uint16_t *C0, long ldc, int M, int N, int K, long long *trace,
                                    void *stream) {
-    IRADS_REQUIRE(M > 0 && N > 0 && K > 0 && N % GBN == 0 && K % GBK == 0 && trace && variant >= 0 && variant <= 3,
+    IRADS_REQUIRE(M > 0 && N > 0 && K > 0 && N % GBN == 0 && K % GBK == 0 && trace && variant >= 0 && variant <= 4 &&
+                      (variant != 4 || N % 256 == 0),
                   "irads_gemm_nt_trace: shape / variant");
     hipStream_t st = (hipStream_t)stream;
     switch (variant) {
     case 0: gemm_launch<EPI_BIAS, 0, true>(A, lda, B, ldb, bias, nullptr, 0, C0, nullptr, ldc, M, N, K, trace, st); break;
     case 1: gemm_launch<EPI_BIAS, 1, true>(A, lda, B, ldb, bias, nullptr, 0, C0, nullptr, ldc, M, N, K, trace, st); break;
     case 2: gemm_launch<EPI_BIAS, 2, true>(A, lda, B, ldb, bias, nullptr, 0, C0, nullptr, ldc, M, N, K, trace, st); break;
-    default: gemm_launch<EPI_BIAS, 3, true>(A, lda, B, ldb, bias, nullptr, 0, C0, nullptr, ldc, M, N, K, trace, st); break;
+    case 3: gemm_launch<EPI_BIAS, 3, true>(A, lda, B, ldb, bias, nullptr, 0, C0, nullptr, ldc, M, N, K, trace, st); break;
+    default: gemm_launch<EPI_BIAS, 4, true>(A, lda, B, ldb, bias, nullptr, 0, C0, nullptr, ldc, M, N, K, trace, st); break;
     }
     return check_launch("irads_gemm_nt_trace");
 }

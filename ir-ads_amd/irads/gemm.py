@@ -9,7 +9,8 @@ operands once Wᵀ is kept beside W (made once per weight version).
 Which kernel serves a shape is a table, not a heuristic: scripts/gemm_tune.py times both on the
 shapes of BASELINE.json's C2 and C4 steps (interleaved rounds in one process) and writes
 tuned/irads_gemm_select_mi355x.json, the (direction, M, N, K) keys where irads_gemm_nt won by
-≥ 5 %.  Directions: "fwd" (y = x Wᵀ + b), "bwd" (dX = dY W), and the FFN's fused pairs
+≥ 5 %, each with the tiling that won (variant 2: 128 x 128 tiles, 2 workgroups per CU; 4: 256 x 256
+tiles on 8 waves, N % 256 == 0).  Directions: "fwd" (y = x Wᵀ + b), "bwd" (dX = dY W), and the FFN's fused pairs
 "fwd_gelu" (fc1 with the erf GELU in the epilogue, against the better GEMM + gelu pass) and
 "bwd_dgelu" (fc2's dX with GELU' applied in the epilogue, against GEMM + gelu_bwd pass).  A
 shape not in the table, or one the kernel cannot take (N % 128, K % 64), goes to hipBLASLt.  IRADS_GEMM=off sends every shape to hipBLASLt, IRADS_GEMM=all every shape the
@@ -28,26 +29,34 @@ _TABLE_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned", 
 _table = None
 
 
+DEFAULT_VARIANT = 2  # 128 x 128 tiles, 2 workgroups per CU (csrc/gemm.hip)
+
+
 def _selected():
+    """{(direction, M, N, K): tiling variant} of the shipped table (entries [dir, M, N, K, variant])."""
     global _table
     if _table is None:
         try:
             with open(_TABLE_PATH) as fh:
-                _table = {tuple(k) for k in json.load(fh)["irads"]}
+                _table = {tuple(k[:4]): (k[4] if len(k) > 4 else DEFAULT_VARIANT) for k in json.load(fh)["irads"]}
         except FileNotFoundError:
-            _table = set()
+            _table = {}
     return _table
 
 
-def kernel_fits(N_out, K):
-    return N_out % 128 == 0 and K % 64 == 0
+def kernel_fits(N_out, K, variant=DEFAULT_VARIANT):
+    return N_out % (256 if variant == 4 else 128) == 0 and K % 64 == 0
 
 
 def use_irads(direction, M, N_out, K):
+    """The irads_gemm_nt tiling variant serving this shape, or None for hipBLASLt."""
     mode = os.environ.get("IRADS_GEMM", "table")
     if mode == "off" or not kernel_fits(N_out, K):
-        return False
-    return mode == "all" or (direction, M, N_out, K) in _selected()
+        return None
+    if mode == "all":
+        return DEFAULT_VARIANT
+    v = _selected().get((direction, M, N_out, K))
+    return v if v is not None and kernel_fits(N_out, K, v) else None
 
 
 def weights(lin):
@@ -65,10 +74,10 @@ def weights(lin):
     return cache[1:]
 
 
-def _nt(A, B, bias32, M, N_out, K):
+def _nt(A, B, bias32, M, N_out, K, variant):
     out = torch.empty((M, N_out), device=A.device, dtype=_BF16)
-    N.call("irads_gemm_nt", 0, N.ptr(A), A.stride(0), N.ptr(B), B.stride(0), N.ptr(bias32), None, 0, N.ptr(out),
-           None, out.stride(0), M, N_out, K, N.stream())
+    N.call("irads_gemm_nt_variant", variant, 0, N.ptr(A), A.stride(0), N.ptr(B), B.stride(0), N.ptr(bias32), None, 0,
+           N.ptr(out), None, out.stride(0), M, N_out, K, N.stream())
     return out
 
 
@@ -77,8 +86,9 @@ def linear(x, lw):
     w16, b16, _, b32 = lw
     M, K = x.shape
     N_out = w16.shape[0]
-    if use_irads("fwd", M, N_out, K) and x.is_contiguous():
-        return _nt(x, w16, b32, M, N_out, K)
+    v = use_irads("fwd", M, N_out, K)
+    if v is not None and x.is_contiguous():
+        return _nt(x, w16, b32, M, N_out, K, v)
     return F.linear(x, w16, b16)
 
 
@@ -88,10 +98,11 @@ def ffn_up(h, lw):
     w16, _, _, b32 = lw
     M, K = h.shape
     N_out = w16.shape[0]
-    if use_irads("fwd_gelu", M, N_out, K) and h.is_contiguous():
+    v = use_irads("fwd_gelu", M, N_out, K)
+    if v is not None and h.is_contiguous():
         u = torch.empty((M, N_out), device=h.device, dtype=_BF16)
         g = torch.empty_like(u)
-        N.call("irads_gemm_nt", 1, N.ptr(h), h.stride(0), N.ptr(w16), w16.stride(0), N.ptr(b32), None, 0,
+        N.call("irads_gemm_nt_variant", v, 1, N.ptr(h), h.stride(0), N.ptr(w16), w16.stride(0), N.ptr(b32), None, 0,
                N.ptr(u), N.ptr(g), u.stride(0), M, N_out, K, N.stream())
         return u, g
     u = linear(h, lw)
@@ -107,9 +118,10 @@ def ffn_down_dgrad_gelu(df, lw, u):
     w16, _, wt, _ = lw
     M, N_in = df.shape
     K_out = w16.shape[1]
-    if use_irads("bwd_dgelu", M, K_out, N_in) and df.is_contiguous() and u.is_contiguous():
+    v = use_irads("bwd_dgelu", M, K_out, N_in)
+    if v is not None and df.is_contiguous() and u.is_contiguous():
         du = torch.empty((M, K_out), device=df.device, dtype=_BF16)
-        N.call("irads_gemm_nt", 2, N.ptr(df), df.stride(0), N.ptr(wt), wt.stride(0), None, N.ptr(u), u.stride(0),
+        N.call("irads_gemm_nt_variant", v, 2, N.ptr(df), df.stride(0), N.ptr(wt), wt.stride(0), None, N.ptr(u), u.stride(0),
                N.ptr(du), None, du.stride(0), M, K_out, N_in, N.stream())
         return du
     dg = dgrad(df, lw)
@@ -123,6 +135,7 @@ def dgrad(dy, lw):
     w16, _, wt, _ = lw
     M, N_in = dy.shape
     K_out = w16.shape[1]
-    if use_irads("bwd", M, K_out, N_in) and dy.is_contiguous():
-        return _nt(dy, wt, None, M, K_out, N_in)
+    v = use_irads("bwd", M, K_out, N_in)
+    if v is not None and dy.is_contiguous():
+        return _nt(dy, wt, None, M, K_out, N_in, v)
     return torch.mm(dy, w16)

@@ -71,6 +71,8 @@ def main():
             row["lib_us"] = timed(lambda: F.linear(A, W, bias))
             row["irads_us"] = timed(lambda: gemm(0, A, W, bias32))
             for v in VARIANTS:
+                if v == 4 and Nn % 256:
+                    continue
                 row[f"irads_v{v}_us"] = timed(lambda: gemm(0, A, W, bias32, variant=v))
                 assert torch.equal(gemm(0, A, W, bias32, variant=v), mine)
             if op == "fc1":  # fused GELU epilogue: bit-identical to the element kernel on the same U
@@ -97,6 +99,8 @@ def main():
             row["lib_us"] = timed(lambda: torch.mm(dY, W))
             row["irads_us"] = timed(lambda: gemm(0, dY, Wt))
             for v in VARIANTS:
+                if v == 4 and K % 256:
+                    continue
                 row[f"irads_v{v}_us"] = timed(lambda: gemm(0, dY, Wt, variant=v))
                 assert torch.equal(gemm(0, dY, Wt, variant=v), mine)
             if op == "fc2":  # dGELU epilogue (dU of fc1's output U) against irads_gelu_bwd on the same dG

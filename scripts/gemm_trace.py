@@ -29,8 +29,9 @@ def main():
         C = torch.empty(M, Nn, device=dev, dtype=torch.bfloat16)
         nk = K // 64
         variant = int(os.environ.get("GEMM_VARIANT", "2"))
-        bmt = 256 if variant < 2 else 128
-        nwg = (M + bmt - 1) // bmt * (Nn // 128)
+        bmt = 256 if variant in (0, 1, 4) else 128
+        bnt = 256 if variant == 4 else 128
+        nwg = (M + bmt - 1) // bmt * (Nn // bnt)
         tr = torch.zeros(nwg * (nk + 3), dtype=torch.int64, device=dev)
         args = (variant, N.ptr(A), A.stride(0), N.ptr(W), W.stride(0), N.ptr(bias), N.ptr(C), C.stride(0), M, Nn, K,
                 N.ptr(tr), N.stream())

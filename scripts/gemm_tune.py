@@ -5,6 +5,7 @@ one process (median of 5 rounds x 10 calls each).  A shape goes to irads_gemm_nt
 ≥ 5 % below hipBLASLt's and its error against the fp32 product is no worse than 1.5x hipBLASLt's.
 The FFN's fused pairs (fc1 + GELU epilogue, fc2 dX + GELU' epilogue) are timed against the better
 unfused arm (hipBLASLt or irads_gemm_nt, then the element pass) and kept on the same 5 % margin.
+Each irads arm tries the tilings in VARIANTS and the table keeps the winner's: [dir, M, N, K, variant].
 
     python scripts/gemm_tune.py [out.json]    (default gpurun_out/irads_gemm_select_mi355x.json;
                                                copy it to ir-ads_amd/irads/tuned/ to ship it)
@@ -43,11 +44,14 @@ def rel(a, b):
     return float((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-30))
 
 
-def nt(A, B, bias32):
+VARIANTS = (2, 4)  # irads_gemm_nt_variant tilings tried per shape (4 only where N % 256 == 0)
+
+
+def nt(A, B, bias32, v=2):
     M, K = A.shape
     out = torch.empty((M, B.shape[0]), device=A.device, dtype=torch.bfloat16)
-    N.call("irads_gemm_nt", 0, N.ptr(A), A.stride(0), N.ptr(B), B.stride(0), N.ptr(bias32), None, 0, N.ptr(out),
-           None, out.stride(0), M, B.shape[0], K, N.stream())
+    N.call("irads_gemm_nt_variant", v, 0, N.ptr(A), A.stride(0), N.ptr(B), B.stride(0), N.ptr(bias32), None, 0,
+           N.ptr(out), None, out.stride(0), M, B.shape[0], K, N.stream())
     return out
 
 
@@ -67,14 +71,15 @@ def fused_rows(cfg, M, C, C4, A, W1, b16, b32):
     """The FFN's fused pairs against the better unfused arm: fc1 + GELU (U, G), and fc2's dX + GELU'
     (dU; fc2 = W2 (C, 4C), so its dX is (M, 4C) = dF (M, C) · W2 with U of fc1's output shape)."""
     out, keys = [], []
+    vs = [v for v in VARIANTS if G.kernel_fits(C4, C, v)]
     lib_fc1 = lambda: gelu(F.linear(A, W1, b16))  # noqa: E731
     ir_fc1 = lambda: gelu(nt(A, W1, b32))  # noqa: E731
 
-    def fused_fc1():
+    def fused_fc1(v):
         u = torch.empty((M, C4), device=A.device, dtype=torch.bfloat16)
         g = torch.empty_like(u)
-        N.call("irads_gemm_nt", 1, N.ptr(A), A.stride(0), N.ptr(W1), W1.stride(0), N.ptr(b32), None, 0, N.ptr(u),
-               N.ptr(g), u.stride(0), M, C4, C, N.stream())
+        N.call("irads_gemm_nt_variant", v, 1, N.ptr(A), A.stride(0), N.ptr(W1), W1.stride(0), N.ptr(b32), None, 0,
+               N.ptr(u), N.ptr(g), u.stride(0), M, C4, C, N.stream())
         return g
     W2 = (torch.randn(C, C4, device=A.device) * C4 ** -0.5).bfloat16()  # fc2's weight (C, 4C)
     W2t = W2.t().contiguous()  # (4C, C)
@@ -83,32 +88,35 @@ def fused_rows(cfg, M, C, C4, A, W1, b16, b32):
     lib_fc2 = lambda: gelu_bwd(U, torch.mm(dF, W2))  # noqa: E731
     ir_fc2 = lambda: gelu_bwd(U, nt(dF, W2t, None))  # noqa: E731
 
-    def fused_fc2():
+    def fused_fc2(v):
         du = torch.empty((M, C4), device=A.device, dtype=torch.bfloat16)
-        N.call("irads_gemm_nt", 2, N.ptr(dF), dF.stride(0), N.ptr(W2t), W2t.stride(0), None, N.ptr(U), U.stride(0),
-               N.ptr(du), None, du.stride(0), M, C4, C, N.stream())
+        N.call("irads_gemm_nt_variant", v, 2, N.ptr(dF), dF.stride(0), N.ptr(W2t), W2t.stride(0), None, N.ptr(U),
+               U.stride(0), N.ptr(du), None, du.stride(0), M, C4, C, N.stream())
         return du
-    for d, key, arms in (("fwd_gelu", ("fwd_gelu", M, C4, C), (lib_fc1, ir_fc1, fused_fc1)),
-                         ("bwd_dgelu", ("bwd_dgelu", M, C4, C), (lib_fc2, ir_fc2, fused_fc2))):
-        if not G.kernel_fits(key[2], key[3]):
+    for d, key, lib_arm, ir_arm, fused in (("fwd_gelu", ("fwd_gelu", M, C4, C), lib_fc1, ir_fc1, fused_fc1),
+                                           ("bwd_dgelu", ("bwd_dgelu", M, C4, C), lib_fc2, ir_fc2, fused_fc2)):
+        if not vs:
             continue
+        arms = [lib_arm, ir_arm] + [lambda v=v: fused(v) for v in vs]
         ref = arms[0]()
         e = [rel(a(), ref) for a in arms]
         for a in arms:
             a(), a()
-        ts = [[], [], []]
+        ts = [[] for _ in arms]
         for _ in range(5):
             for j, a in enumerate(arms):
                 ts[j].append(timed(a))
         med = [statistics.median(t) for t in ts]
-        win = med[2] < 0.95 * min(med[0], med[1]) and e[2] <= 2e-2
+        jb = 2 + min(range(len(vs)), key=lambda j: med[2 + j])
+        win = med[jb] < 0.95 * min(med[0], med[1]) and e[jb] <= 2e-2
         row = {"cfg": cfg, "op": "fc1+gelu" if d == "fwd_gelu" else "fc2+dgelu", "dir": d, "M": M, "N": C4, "K": C,
                "lib_plus_pass_us": round(med[0], 2), "irads_plus_pass_us": round(med[1], 2),
-               "fused_us": round(med[2], 2), "fused_vs_lib_rel": round(e[2], 6), "irads": win}
+               **{f"fused_v{v}_us": round(med[2 + j], 2) for j, v in enumerate(vs)},
+               "variant": vs[jb - 2], "fused_vs_lib_rel": round(e[jb], 6), "irads": win}
         print(json.dumps(row), flush=True)
         out.append(row)
         if win:
-            keys.append(list(key))
+            keys.append(list(key) + [vs[jb - 2]])
     return out, keys
 
 
@@ -128,31 +136,35 @@ def main():
             Wt = W.t().contiguous()
             dY = torch.randn(M, Nn, device=dev).bfloat16()
             for d, key, lib, mine, ref in (
-                    ("fwd", ("fwd", M, Nn, K), lambda: F.linear(A, W, b16), lambda: nt(A, W, b32),
+                    ("fwd", ("fwd", M, Nn, K), lambda: F.linear(A, W, b16), lambda v: nt(A, W, b32, v),
                      lambda: torch.addmm(b32, A.float(), W.float().t())),
-                    ("bwd", ("bwd", M, K, Nn), lambda: torch.mm(dY, W), lambda: nt(dY, Wt, None),
+                    ("bwd", ("bwd", M, K, Nn), lambda: torch.mm(dY, W), lambda v: nt(dY, Wt, None, v),
                      lambda: dY.float() @ W.float())):
                 if key in seen or not G.kernel_fits(key[2], key[3]):
                     continue
                 seen.add(key)
+                vs = [v for v in VARIANTS if G.kernel_fits(key[2], key[3], v)]
+                arms = [lib] + [lambda v=v, mine=mine: mine(v) for v in vs]
                 r32 = ref()
-                e_lib, e_ir = rel(lib(), r32), rel(mine(), r32)
+                e = [rel(a(), r32) for a in arms]
                 del r32
                 for _ in range(2):
-                    lib(), mine()
-                t_lib, t_ir = [], []
+                    for a in arms:
+                        a()
+                ts = [[] for _ in arms]
                 for _ in range(5):
-                    t_lib.append(timed(lib))
-                    t_ir.append(timed(mine))
-                ml, mi = statistics.median(t_lib), statistics.median(t_ir)
-                win = mi < 0.95 * ml and e_ir <= 1.5 * e_lib + 1e-4
-                row = {"cfg": cfg, "op": op, "dir": d, "M": key[1], "N": key[2], "K": key[3], "lib_us": round(ml, 2),
-                       "irads_us": round(mi, 2), "err_lib": round(e_lib, 6), "err_irads": round(e_ir, 6),
-                       "irads": win}
+                    for j, a in enumerate(arms):
+                        ts[j].append(timed(a))
+                med = [statistics.median(t) for t in ts]
+                jb = 1 + min(range(len(vs)), key=lambda j: med[1 + j])
+                win = med[jb] < 0.95 * med[0] and e[jb] <= 1.5 * e[0] + 1e-4
+                row = {"cfg": cfg, "op": op, "dir": d, "M": key[1], "N": key[2], "K": key[3], "lib_us": round(med[0], 2),
+                       **{f"irads_v{v}_us": round(med[1 + j], 2) for j, v in enumerate(vs)}, "variant": vs[jb - 1],
+                       "err_lib": round(e[0], 6), "err_irads": round(e[jb], 6), "irads": win}
                 print(json.dumps(row), flush=True)
                 rows.append(row)
                 if win:
-                    keys.append(list(key))
+                    keys.append(list(key) + [vs[jb - 1]])
             if op == "fc1" and G.kernel_fits(Nn, K):
                 rows_, keys_ = fused_rows(cfg, M, K, Nn, A, W, b16, b32)
                 rows += rows_

@@ -389,12 +389,14 @@ def test_native_adamw_refuses_cpu_parameters():
 
 def test_gemm_selection_table_and_dispatch_modes(monkeypatch):
     """irads.gemm's shipped selection table (scripts/gemm_tune.py on an MI355X) holds only shapes the
-    kernel takes (N % 128, K % 64), keyed (direction, M, N_out, K); the dispatch modes honour it."""
+    chosen tiling takes (N % 128, or % 256 for variant 4; K % 64), keyed (direction, M, N_out, K); the
+    dispatch modes honour it."""
     from irads import gemm as G
     keys = G._selected()
     assert keys, "tuned/irads_gemm_select_mi355x.json missing or empty"
-    for d, M, n, k in keys:
-        assert d in ("fwd", "bwd") and M > 0 and G.kernel_fits(n, k), (d, M, n, k)
+    for (d, M, n, k), v in keys.items():
+        assert d in ("fwd", "bwd", "fwd_gelu", "bwd_dgelu") and M > 0 and v in (2, 4) and G.kernel_fits(n, k, v), \
+            (d, M, n, k, v)
     # the C2 step's stage-2 attention projection, the shape it wins most on, is in the table
     assert ("fwd", 16384, 512, 512) in keys and ("bwd", 16384, 512, 512) in keys
     some = next(iter(keys))

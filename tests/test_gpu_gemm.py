@@ -54,7 +54,9 @@ def test_gemm_nt_bias_vs_fp32_and_hipblaslt(M, Nn, K):
     # no bias, and every tile variant bit for bit
     nob = _gemm(0, A, W)
     assert _rel(nob, A.float() @ W.float().t()) <= 1.5 * _rel(lib, ref) + 1e-4
-    for v in range(4):
+    for v in range(5):
+        if v == 4 and Nn % 256:
+            continue
         assert torch.equal(_gemm(0, A, W, b16.float(), variant=v), mine), v
 
 
