@@ -18,6 +18,40 @@ class MLP(nn.Module):
         return self.proj(x.flatten(2).transpose(1, 2))
 
 
+class _ComposeFn(torch.autograd.Function):
+    """The branch weights of SegFormerHead.forward: A_i = W_i M_i and c_i = W_i b_i, W_i the column
+    block of linear_fuse's weight that branch i's MLP feeds (blocks in [c4 | c3 | c2 | c1] order),
+    all in fp32 in one autograd node.  As separate autocast ops each branch cost a weight cast each
+    way, a bf16 product, a slice backward (zero fill + copy) and a gradient add on the shared fuse
+    weight; here the fuse weight's gradient is the concatenation of its blocks', written once."""
+
+    @staticmethod
+    def forward(ctx, Wf, E, *mb):
+        n = len(mb) // 2
+        outs = []
+        for i in range(n):
+            Wi = Wf[:, (n - 1 - i) * E:(n - i) * E]
+            outs += [Wi @ mb[2 * i], Wi @ mb[2 * i + 1]]
+        ctx.save_for_backward(Wf, *mb)
+        ctx.E = E
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *g):
+        Wf, *mb = ctx.saved_tensors
+        E, n = ctx.E, len(mb) // 2
+        blocks, dmb = [None] * n, []
+        for i in range(n):
+            Wi = Wf[:, (n - 1 - i) * E:(n - i) * E]
+            M, b = mb[2 * i], mb[2 * i + 1]
+            gA = g[2 * i] if g[2 * i] is not None else torch.zeros((E, M.shape[1]), device=Wf.device)
+            gc = g[2 * i + 1] if g[2 * i + 1] is not None else torch.zeros((E,), device=Wf.device)
+            blocks[n - 1 - i] = torch.addr(gA @ M.t(), gc, b)
+            dmb += [Wi.t() @ gA, Wi.t() @ gc]
+        dWf = torch.cat(blocks, dim=1) if ctx.needs_input_grad[0] else None
+        return (dWf, None, *dmb)
+
+
 class ConvModule(nn.Module):
     def __init__(self, c1, c2):
         super().__init__()
@@ -48,20 +82,26 @@ class SegFormerHead(nn.Module):
         where W_i is linear_fuse's column block for branch i and (M_i, b_i) the MLP: resize and a
         1x1 projection commute, so each branch is ONE GEMM at its own resolution (1/4 ... 1/32)
         into E channels, and the 4E-channel concatenation at 1/4 resolution never exists.  The
-        composed weights W_i M_i are formed each call (E x E x dim_i flops), so gradients reach
-        linear_fuse.conv.weight and every MLP through autograd.  Parameters and keys unchanged."""
+        composed weights W_i M_i are formed each call in fp32 (E x E x dim_i flops, _ComposeFn), so
+        gradients reach linear_fuse.conv.weight and every MLP through autograd.  Parameters and
+        keys unchanged."""
         B, _, H, W = features[0].shape
         E = self.linear_fuse.conv.weight.shape[0]
         Wf = self.linear_fuse.conv.weight.view(E, -1)  # column blocks: [c4 | c3 | c2 | c1]
         n = len(features)
+        mlps = [getattr(self, f"linear_c{i + 1}").proj for i in range(n)]
+        if mlps[0].bias is not None and Wf.dtype == torch.float32:
+            # the branch weights (E, dim_i) and biases in fp32, one node (ops.linear casts A to bf16)
+            with torch.autocast("cuda", enabled=False):
+                Ac = _ComposeFn.apply(Wf, E, *[t for m in mlps for t in (m.weight, m.bias)])
+        else:
+            Ac = []
+            for i, mlp in enumerate(mlps):
+                Wi = Wf[:, (n - 1 - i) * E:(n - i) * E]
+                Ac += [Wi @ mlp.weight, None if mlp.bias is None else Wi @ mlp.bias]
         zs = []
         for i, f in enumerate(features):
-            mlp = getattr(self, f"linear_c{i + 1}").proj
-            Wi = Wf[:, (n - 1 - i) * E:(n - i) * E]
-            A = Wi @ mlp.weight  # (E, dim_i): under autocast a bf16 GEMM, as the two Linears' own operands
-            with torch.autocast("cuda", enabled=False):
-                c = Wi @ mlp.bias  # bias in fp32
-            z = ops.linear(f.flatten(2).transpose(1, 2), A, c)  # (B, h*w, E)
+            z = ops.linear(f.flatten(2).transpose(1, 2), Ac[2 * i], Ac[2 * i + 1])  # (B, h*w, E)
             zs.append(z.transpose(1, 2).reshape(B, E, *f.shape[-2:]))  # channels-last (B, E, h, w) view
         seg = ops.upsample_sum(zs[0], zs[1:])
         if self.training and seg.dtype == torch.bfloat16 and seg.is_cuda:

@@ -406,3 +406,20 @@ def test_gemm_selection_table_and_dispatch_modes(monkeypatch):
     assert not G.use_irads(*some)
     monkeypatch.setenv("IRADS_GEMM", "all")
     assert G.use_irads("fwd", 5, 256, 128) and not G.use_irads("fwd", 5, 192, 128)
+
+
+def test_segformer_branch_composition_gradients():
+    """SegFormerHead's _ComposeFn (A_i = W_i M_i, c_i = W_i b_i over the column blocks of
+    linear_fuse's weight, one autograd node) against autograd of the plain products, fp64 gradcheck."""
+    from semseg.models.heads.segformer import _ComposeFn
+    torch.manual_seed(0)
+    E, dims = 4, [3, 5, 2, 6]
+    Wf = torch.randn(E, 4 * E, dtype=torch.float64, requires_grad=True)
+    mb = [t.requires_grad_() for d in dims for t in (torch.randn(E, d, dtype=torch.float64),
+                                                      torch.randn(E, dtype=torch.float64))]
+    out = _ComposeFn.apply(Wf, E, *mb)
+    for i in range(4):
+        Wi = Wf[:, (3 - i) * E:(4 - i) * E]
+        torch.testing.assert_close(out[2 * i], Wi @ mb[2 * i])
+        torch.testing.assert_close(out[2 * i + 1], Wi @ mb[2 * i + 1])
+    assert torch.autograd.gradcheck(lambda W, *m: _ComposeFn.apply(W, E, *m), (Wf, *mb))
