@@ -14,7 +14,7 @@ d = collections.defaultdict(list)
 for r in csv.DictReader(open(sys.argv[1])):
     n = r["Kernel_Name"]
     if "dattn_attn" not in n and "dattn_rpe" not in n: continue
-    k = (n.split("(")[0].split("::")[-1][:40], r["Grid_Size_X"], r["Grid_Size_Y"])
+    k = (n.replace("(anonymous namespace)::", "").split("(")[0].split("::")[-1][:40], r["Grid_Size_X"], r["Grid_Size_Y"])
     d[k].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
 for k, v in sorted(d.items()):
     v.sort()
