@@ -10,7 +10,8 @@ BASELINE.json), bf16 autocast, TRAIN_TYPE Adapter (optimizers.py:7-30), MMST los
 timing (data loading excluded).  Data parallel over RCCL (DDP, one process per GPU),
 weak scaling.  Rank 0 prints one JSON line.
 
-Extra fields: ``roofline`` for the dominant hot-path kernel (Swin window-attention
+Extra fields: ``roofline_gemm`` (irads_gemm_nt at the stage-2 trunk shapes it serves, against
+the bf16 MFMA peak); ``roofline`` for the dominant hot-path kernel (Swin window-attention
 forward, bf16), with per-launch durations measured by HIP events on the launch stream
 over the timed region; ``cpu_baseline`` = the CPU restatement (oracle/, the checker)
 timed on this host on a bounded sample of the same workload.
@@ -309,6 +310,57 @@ def dino_stack_line(device, msda, reps=5):
     return res
 
 
+MFMA_BF16_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md; no sparsity)
+GEMM_SHAPES = (("fwd", 16384, 512, 512, "stage-2 attention proj"), ("bwd", 16384, 512, 1536, "stage-2 qkv dX"),
+               ("bwd", 16384, 512, 2048, "stage-2 fc1 dX"))
+
+
+def gemm_roofline(device, reps=20, sets=4):
+    """irads_gemm_nt at the C2 step's stage-2 shapes it serves (18 blocks each, irads.gemm's table
+    picks the tiling), against the dense bf16 MFMA peak; hipBLASLt (shipped TunableOp table) on the
+    same operands beside it.  `reps` launches per event pair, cycling over `sets` operand sets."""
+    from irads import gemm as G
+    from irads import native as N
+    out = {}
+    tot_f = tot_ms = 0.0
+    for d, M, Nn, K, what in GEMM_SHAPES:
+        v = G.use_irads(d, M, Nn, K) or G.DEFAULT_VARIANT
+        g = torch.Generator(device="cpu").manual_seed(1)
+        A = [torch.randn(M, K, generator=g).bfloat16().to(device) for _ in range(sets)]
+        B = [(torch.randn(Nn, K, generator=g) * K ** -0.5).bfloat16().to(device) for _ in range(sets)]
+        C = torch.empty(M, Nn, device=device, dtype=torch.bfloat16)
+
+        def mine(i):
+            N.call("irads_gemm_nt_variant", v, 0, N.ptr(A[i]), K, N.ptr(B[i]), K, None, None, 0, N.ptr(C), None, Nn,
+                   M, Nn, K, N.stream())
+
+        def lib(i):
+            torch.mm(A[i], B[i].t(), out=C)
+        ms = {}
+        for name, fn in (("irads", mine), ("hipblaslt", lib)):
+            for i in range(sets):
+                fn(i)
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda.synchronize()
+            a.record()
+            for r in range(reps):
+                fn(r % sets)
+            b.record()
+            torch.cuda.synchronize()
+            ms[name] = a.elapsed_time(b) / reps
+        tf = 2.0 * M * Nn * K / (ms["irads"] * 1e-3) / 1e12
+        tot_f += 2.0 * M * Nn * K
+        tot_ms += ms["irads"]
+        out[f"{d}_{M}x{Nn}x{K}"] = {"what": what, "variant": v, "avg_launch_ms": round(ms["irads"], 5),
+                                    "tflops": round(tf, 1), "frac": round(tf / MFMA_BF16_PEAK_TFLOPS, 4),
+                                    "hipblaslt_nt_ms": round(ms["hipblaslt"], 5)}  # torch.mm(A, Bᵀ), same operands
+    tf = tot_f / (tot_ms * 1e-3) / 1e12
+    return {"kernel": "irads_gemm_nt (bf16 NT GEMM, frozen Swin trunk projections)", "bound": "mfma",
+            "achieved": round(tf, 1), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(tf / MFMA_BF16_PEAK_TFLOPS, 4),
+            "timing": f"{reps} launches per HIP event pair, cycling over {sets} operand sets", "shapes": out}
+
+
 def traffic_from_profile():
     """HBM bytes per forward launch from the newest committed PMC passes of the same 24 launches
     (scripts/pmc_winattn_kind.sh: FETCH_SIZE x2 + WRITE_SIZE, separate rocprofv3 passes); PMC
@@ -502,6 +554,10 @@ def main():
         result["data"] = ("synthetic (RGB N(0,1), %s U[0,1), labels U{0..%d} with 10%% ignore=255; random-init "
                           "weights)" % ({"c3": "HHA"}.get(args.workload, "thermal"), wl["n_cls"] - 1))
     if rank == 0 and not args.no_kernels and args.workload == "c2":
+        try:
+            result["roofline_gemm"] = gemm_roofline(device)
+        except Exception as e:  # report, never fake
+            result["roofline_gemm"] = {"error": repr(e)[:200]}
         try:
             result["kernels"] = msda_rooflines(device)
         except Exception as e:  # report, never fake
