@@ -143,6 +143,16 @@ int irads_dattn_gate_fwd(const void *out_tok, const void *xy, const float *defor
 int irads_dattn_gate_bwd(const float *grad_y, const void *out_tok, const void *xy, const float *deform_weight,
                          const float *identity_weight, int B, int C, int HW, void *grad_out, void *grad_xy,
                          float *partials, void *stream);
+/* DAttentionMM's modality mix of the sampled features (swin.py:946-949) with the transpose and bf16
+ * cast of its token-major consumers: out (B, n2, C) bf16 = bf16(xs·w[..., 0] + ys·w[..., 1]), xs /
+ * ys (B, C, n2) fp32, w (B, n2, 2) fp32 (the 2-way softmax); fp32 rounding of each product and the
+ * sum as the reference's separate ops.  Backward from grad_tok (B, n2, C) bf16: grad_xs / grad_ys
+ * (B, C, n2) = g·w0 / g·w1, grad_w (B, n2, 2) = channel sums of g·xs, g·ys.  C a multiple of 8,
+ * out / grad_tok 16-B aligned. */
+int irads_dattn_mix_fwd(const float *xs, const float *ys, const float *w, int B, int C, int n2, void *out,
+                        void *stream);
+int irads_dattn_mix_bwd(const void *grad_tok, const float *xs, const float *ys, const float *w, int B, int C, int n2,
+                        float *grad_xs, float *grad_ys, float *grad_w, void *stream);
 /* Fused attention with on-the-fly bilinear rpe bias (swin.py:950-1016):
  *   q (B*nH, hc, HW)  k, v KEY-MAJOR (B*nH, 2n, hc)  rpe (nH, Ht, Wt)  qgrid_y (H), qgrid_x (W)
  *   (the reference's _get_q_grid values)  out (B*nH, hc, HW)  lse (B*nH, HW).

@@ -1384,6 +1384,64 @@ __global__ void __launch_bounds__(256) dattn_gate_bwd_kernel(const float *__rest
     }
 }
 }  // namespace
+// ---------------------------------------------------------------- sampled-feature mix
+typedef __attribute__((ext_vector_type(4))) unsigned int mix_u32x4;
+// DAttentionMM's modality mix (swin.py:946-949: sum over the stacked (x, y) samples weighted by
+// the 2-way softmax) fused with the transpose and the bf16 cast its consumers (proj_k / proj_v as
+// token-major Linears under autocast) apply: s_tok[b, j, c] = bf16(xs[b, c, j]·w[b, j, 0] +
+// ys[b, c, j]·w[b, j, 1]), each product and the sum rounded in fp32 as the reference's separate
+// elementwise ops (this file builds without FMA contraction).  Thread per (b, j): the channel loop
+// reads xs / ys coalesced across the wave's consecutive j and writes 16-B runs of 8 channels.
+__global__ void __launch_bounds__(256) dattn_mix_fwd_kernel(const float *__restrict__ xs, const float *__restrict__ ys,
+                                                          const float *__restrict__ w, int B, int C, int n2,
+                                                          unsigned short *__restrict__ out) {
+    const long t = (long)blockIdx.x * 256 + threadIdx.x;
+    if (t >= (long)B * n2) return;
+    const int b = (int)(t / n2), j = (int)(t - (long)b * n2);
+    const float w0 = w[t * 2], w1 = w[t * 2 + 1];
+    const float *xb = xs + (long)b * C * n2 + j, *yb = ys + (long)b * C * n2 + j;
+    for (int c8 = 0; c8 < C; c8 += 8) {
+        mix_u32x4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const long c0 = (long)(c8 + 2 * e) * n2, c1 = c0 + n2;
+            const float p0 = xb[c0] * w0, q0 = yb[c0] * w1, p1 = xb[c1] * w0, q1 = yb[c1] * w1;
+            o[e] = (unsigned)f2bf(p0 + q0) | ((unsigned)f2bf(p1 + q1) << 16);
+        }
+        *reinterpret_cast<mix_u32x4 *>(out + t * C + c8) = o;
+    }
+}
+
+// backward: g (B, n2, C) bf16 (the sum of the proj_k and proj_v input gradients) -> grad_xs =
+// g·w0, grad_ys = g·w1 (fp32, (B, C, n2)) and grad_w[b, j] = (Σ_c g·xs, Σ_c g·ys) summed over c
+// in order.
+__global__ void __launch_bounds__(256) dattn_mix_bwd_kernel(const unsigned short *__restrict__ g,
+                                                          const float *__restrict__ xs, const float *__restrict__ ys,
+                                                          const float *__restrict__ w, int B, int C, int n2,
+                                                          float *__restrict__ gxs, float *__restrict__ gys,
+                                                          float *__restrict__ gw) {
+    const long t = (long)blockIdx.x * 256 + threadIdx.x;
+    if (t >= (long)B * n2) return;
+    const int b = (int)(t / n2), j = (int)(t - (long)b * n2);
+    const float w0 = w[t * 2], w1 = w[t * 2 + 1];
+    const long base = (long)b * C * n2 + j;
+    float a0 = 0.f, a1 = 0.f;
+    for (int c8 = 0; c8 < C; c8 += 8) {
+        const mix_u32x4 gv = *reinterpret_cast<const mix_u32x4 *>(g + t * C + c8);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const float gf = bf2f((unsigned short)(gv[e >> 1] >> (16 * (e & 1))));
+            const long o = base + (long)(c8 + e) * n2;
+            gxs[o] = gf * w0;
+            gys[o] = gf * w1;
+            a0 += gf * xs[o];
+            a1 += gf * ys[o];
+        }
+    }
+    gw[t * 2] = a0;
+    gw[t * 2 + 1] = a1;
+}
+
 }  // namespace irads
 
 extern "C" int irads_dattn_gate_fwd(const void *out_tok, const void *xy, const float *deform_weight,
@@ -1413,4 +1471,28 @@ extern "C" int irads_dattn_gate_bwd(const float *grad_y, const void *out_tok, co
                        grad_y, (const unsigned short *)out_tok, (const unsigned short *)xy, deform_weight,
                        identity_weight, B, C, HW, (unsigned short *)grad_out, (unsigned short *)grad_xy, partials);
     return check_launch("irads_dattn_gate_bwd");
+}
+
+extern "C" int irads_dattn_mix_fwd(const float *xs, const float *ys, const float *w, int B, int C, int n2, void *out,
+                                   void *stream) {
+    IRADS_REQUIRE(xs && ys && w && out, "dattn_mix: null pointer");
+    IRADS_REQUIRE(B >= 0 && n2 >= 0 && C > 0 && C % 8 == 0 && ((uintptr_t)out % 16) == 0,
+                  "dattn_mix: C=%d must be a multiple of 8, out 16-B aligned", C);
+    const long n = (long)B * n2;
+    if (n == 0) return IRADS_OK;
+    hipLaunchKernelGGL(dattn_mix_fwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, xs,
+                       ys, w, B, C, n2, (unsigned short *)out);
+    return check_launch("irads_dattn_mix_fwd");
+}
+
+extern "C" int irads_dattn_mix_bwd(const void *grad_tok, const float *xs, const float *ys, const float *w, int B, int C,
+                                   int n2, float *grad_xs, float *grad_ys, float *grad_w, void *stream) {
+    IRADS_REQUIRE(grad_tok && xs && ys && w && grad_xs && grad_ys && grad_w, "dattn_mix: null pointer");
+    IRADS_REQUIRE(B >= 0 && n2 >= 0 && C > 0 && C % 8 == 0 && ((uintptr_t)grad_tok % 16) == 0,
+                  "dattn_mix: C=%d must be a multiple of 8, grad_tok 16-B aligned", C);
+    const long n = (long)B * n2;
+    if (n == 0) return IRADS_OK;
+    hipLaunchKernelGGL(dattn_mix_bwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       (const unsigned short *)grad_tok, xs, ys, w, B, C, n2, grad_xs, grad_ys, grad_w);
+    return check_launch("irads_dattn_mix_bwd");
 }

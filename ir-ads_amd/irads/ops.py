@@ -358,6 +358,39 @@ def dattn_gate_ok(out_tok, xy):
             and out_tok.shape[1] == xy.shape[2] * xy.shape[3] and xy.shape[1] % 8 == 0 and xy.shape[1] <= 128)
 
 
+def dattn_mix_ok(xs, ys, w):
+    """Whether DAttnMixFn serves the modality mix: fp32 (B, C, 2n) samples, (B, 2n, 2) weights, C % 8."""
+    return (xs.is_cuda and xs.dtype == ys.dtype == w.dtype == torch.float32 and xs.dim() == 3
+            and xs.shape == ys.shape and tuple(w.shape) == (xs.shape[0], xs.shape[2], 2) and xs.shape[1] % 8 == 0
+            and xs.is_contiguous() and ys.is_contiguous())
+
+
+class DAttnMixFn(torch.autograd.Function):
+    """sampled = xs·w[..., 0] + ys·w[..., 1] (swin.py:946-949), returned as the token-major bf16
+    operand (B, 2n, C) of proj_k / proj_v (what the transpose and autocast's cast would make of it),
+    in one pass each way (irads_dattn_mix_fwd/bwd)."""
+
+    @staticmethod
+    def forward(ctx, xs, ys, w):
+        B, C, n2 = xs.shape
+        w = w.contiguous()
+        out = torch.empty((B, n2, C), device=xs.device, dtype=torch.bfloat16)
+        N.call("irads_dattn_mix_fwd", N.ptr(xs), N.ptr(ys), N.ptr(w), B, C, n2, N.ptr(out), N.stream())
+        ctx.save_for_backward(xs, ys, w)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        xs, ys, w = ctx.saved_tensors
+        B, C, n2 = xs.shape
+        g = g.to(torch.bfloat16).contiguous()
+        gxs, gys = torch.empty_like(xs), torch.empty_like(ys)
+        gw = torch.empty_like(w)
+        N.call("irads_dattn_mix_bwd", N.ptr(g), N.ptr(xs), N.ptr(ys), N.ptr(w), B, C, n2, N.ptr(gxs), N.ptr(gys),
+               N.ptr(gw), N.stream())
+        return gxs, gys, gw
+
+
 class DAttnGateFn(torch.autograd.Function):
     """deform_weight[c] * out + identity_weight[c] * xy (DAttentionMM's last op, swin.py:1016)
     in one pass each way (irads_dattn_gate_fwd/bwd).  out_tok: (B, HW, C) bf16; xy: (B, C, H, W)

@@ -444,8 +444,11 @@ class DAttentionMM(nn.Module):
         with torch.autocast("cuda", enabled=False):
             h = F.relu(F.linear(qs.transpose(1, 2), sw[0].weight.flatten(1), sw[0].bias))
             w = F.softmax(F.linear(h, sw[2].weight.flatten(1), sw[2].bias), dim=-1)
-        sampled = xs * w[..., 0].unsqueeze(1) + ys * w[..., 1].unsqueeze(1)  # (B, C, 2n) fp32
-        s_tok = sampled.transpose(1, 2)
+        if ops.dattn_mix_ok(xs, ys, w):  # the mix, its transpose and the bf16 cast in one pass each way
+            s_tok = ops.DAttnMixFn.apply(xs, ys, w)  # (B, 2n, C) bf16
+        else:
+            sampled = xs * w[..., 0].unsqueeze(1) + ys * w[..., 1].unsqueeze(1)  # (B, C, 2n) fp32
+            s_tok = sampled.transpose(1, 2)
         nH, hc = self.n_heads, self.n_head_channels
 
         def key_major(conv_):  # (B, 2n, C) bf16 -> (B*nH, 2n, hc) fp32, viewed as (B*nH, hc, 2n)
