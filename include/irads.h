@@ -424,6 +424,9 @@ int irads_wgrad_batched(int count, const irads_wgrad_problem *problems, int K, i
 int irads_wgrad(const uint16_t *A, long lda, const uint16_t *B, long ldb, int K, int m, int n, float alpha,
                 int accumulate, int transpose_out, float *D, float *colsum_a, float *colsum_b, float *workspace,
                 void *stream);
+/* out[e] = sum_r ws[r * count + e], rows summed in a fixed order (deterministic): the per-workgroup
+ * partial sums several backward kernels leave for the small parameter gradients. */
+int irads_sum_rows(const float *ws, int rows, long count, float *out, void *stream);
 
 /* SegFormer head tail in training mode (segformer.py:22-48: ConvModule BatchNorm2d (batch
  * statistics) + ReLU, then Dropout2d) on the fused map held token-major: x (M x E) bf16, M =

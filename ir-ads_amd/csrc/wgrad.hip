@@ -380,3 +380,21 @@ extern "C" int irads_wgrad(const uint16_t *A, long lda, const uint16_t *B, long 
     const irads_wgrad_problem p{A, lda, B, ldb, D, colsum_a, colsum_b, transpose_out};
     return irads_wgrad_batched(1, &p, K, m, n, alpha, accumulate, workspace, stream);
 }
+
+// out[e] = sum over r of ws[r * count + e] (e < count), rows summed in a fixed order: the per-workgroup
+// partials of the small gradient reductions (gates, LayerNorm / BN affine parameters, offset networks)
+// that torch's sum(0) ran as a fill + a few-block reduction.
+extern "C" int irads_sum_rows(const float *ws, int rows, long count, float *out, void *stream) {
+    IRADS_REQUIRE(ws && out && rows >= 1 && count >= 0, "irads_sum_rows: null pointer / rows=%d", rows);
+    if (count == 0) return IRADS_OK;
+    Segs segs;
+    segs.nseg = 1;
+    segs.s[0] = Seg{ws, out, count, (int)((count + 63) / 64), 0};
+    const dim3 grid((unsigned)((count + 63) / 64));
+    hipStream_t st = (hipStream_t)stream;
+    if (rows >= 128) hipLaunchKernelGGL(wgrad_reduce_kernel<16>, grid, dim3(64 * 16), 0, st, segs, rows, 1.f, 0, 1, 1);
+    else if (rows >= 32) hipLaunchKernelGGL(wgrad_reduce_kernel<4>, grid, dim3(64 * 4), 0, st, segs, rows, 1.f, 0, 1, 1);
+    else hipLaunchKernelGGL(wgrad_reduce_kernel<1>, grid, dim3(64), 0, st, segs, rows, 1.f, 0, 1, 1);
+    return check_launch("irads_sum_rows");
+}
+

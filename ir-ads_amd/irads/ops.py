@@ -418,8 +418,17 @@ class DAttnGateFn(torch.autograd.Function):
         part = torch.empty((nblk, 2, C), device=xy.device, dtype=torch.float32)
         N.call("irads_dattn_gate_bwd", N.ptr(g), N.ptr(out_tok), N.ptr(xy), N.ptr(dw32), N.ptr(iw32), B, C, H * W,
                N.ptr(gout), N.ptr(gxy), N.ptr(part), N.stream())
-        s = part.sum(0)  # fixed-order tree reduction over the workgroups
+        s = sum_rows(part, 2 * C).view(2, C)  # fixed-order reduction over the workgroups
         return gout, gxy, s[0].to(ctx.dtypes[0]), s[1].to(ctx.dtypes[1])
+
+
+def sum_rows(parts, cols):
+    """parts (contiguous fp32, rows x cols flattened).sum(0) in one fixed-order launch (irads_sum_rows):
+    torch's sum(0) of these per-workgroup partials ran as a fill and a few-workgroup reduction."""
+    rows = parts.numel() // cols
+    out = torch.empty((cols,), device=parts.device, dtype=torch.float32)
+    N.call("irads_sum_rows", N.ptr(parts), rows, cols, N.ptr(out), N.stream())
+    return out
 
 
 def zeros_like_many(*ts):
@@ -943,7 +952,7 @@ class BNActFn(torch.autograd.Function):
         n_part = N.load().irads_bnact_partials(M, E)
         parts = torch.empty((n_part,), device=x.device, dtype=torch.float32)
         N.call("irads_bnact_stats", N.ptr(xb), M, E, N.ptr(parts), N.stream())
-        s = parts.view(-1, 2, E).sum(0)
+        s = sum_rows(parts, 2 * E).view(2, E)
         shift = xb.view(M, E)[0].float()
         m1 = s[0] / M
         mean = shift + m1
@@ -971,7 +980,7 @@ class BNActFn(torch.autograd.Function):
         parts = torch.empty((N.load().irads_bnact_partials(M, E),), device=g.device, dtype=torch.float32)
         N.call("irads_bnact_bwd", N.ptr(g), N.ptr(xb), M, E, L, N.ptr(mean), N.ptr(invstd), N.ptr(w), N.ptr(b),
                N.ptr(mask), N.ptr(parts), None, None, None, N.stream())
-        s = parts.view(-1, 2, E).sum(0)  # (sum d, sum d * xhat)
+        s = sum_rows(parts, 2 * E).view(2, E)  # (sum d, sum d * xhat)
         md, mdx = s[0] / M, s[1] / M
         dx = torch.empty_like(xb)
         N.call("irads_bnact_bwd", N.ptr(g), N.ptr(xb), M, E, L, N.ptr(mean), N.ptr(invstd), N.ptr(w), N.ptr(b),
@@ -1024,7 +1033,7 @@ class MPGResidualFn(torch.autograd.Function):
         parts = torch.empty((N.load().irads_mpg_partials(R, C),), device=g.device, dtype=torch.float32)
         N.call("irads_mpg_bwd", N.ptr(g), N.ptr(xb), N.ptr(g_rgb), N.ptr(g_dte), R, C, N.ptr(gx), N.ptr(parts),
                N.stream())
-        s = parts.view(-1, 4, C).sum(0)
+        s = sum_rows(parts, 4 * C).view(4, C)
         return gx, g[:B], g[B:], s[0], s[1], s[2], s[3]
 
 
@@ -1280,7 +1289,7 @@ class LayerNormFromBF16Fn(torch.autograd.Function):
         parts = torch.empty((N.load().irads_ln_bf16_partials(M, C),), device=g.device, dtype=torch.float32)
         N.call("irads_ln_bf16_bwd", N.ptr(g), N.ptr(x2), N.ptr(mean), N.ptr(rstd), N.ptr(w), M, C, N.ptr(dx),
                N.ptr(parts), N.stream())
-        s = parts.view(-1, 2, C).sum(0)
+        s = sum_rows(parts, 2 * C).view(2, C)
         return dx.view(ctx.shape), s[0], s[1], None
 
 

@@ -571,7 +571,9 @@ class DeformMPGBlock(nn.Module):
         xr = xr.reshape(B, H, W, c).permute(0, 3, 1, 2).contiguous()
         xd = xd.reshape(B, H, W, c).permute(0, 3, 1, 2).contiguous()
         fused = self.deform_atten(xr, xd)
-        return self.U_fc1(fused.reshape(B, c, -1).permute(0, 2, 1))
+        # (B, HW, c) token-major: a view when the attention returned its output channels-last (the
+        # fused gate does), where reshape(B, c, -1).permute(0, 2, 1) copied it to NCHW and back
+        return self.U_fc1(fused.permute(0, 2, 3, 1).reshape(B, -1, c))
 
 
 def apply_mask(rgb, dte):

@@ -1,6 +1,6 @@
 """Produce the hipBLASLt selection table for the bench step (PyTorch TunableOp), on an MI355X.
 
-    python scripts/tune_gemms.py --out gpurun_out/tunableop_mi355x0.csv
+    python scripts/tune_gemms.py --out gpurun_out/tunableop_mi355x0.csv [--workload c4] [--merge <table>]
 then copy the file to ir-ads_amd/irads/tuned/tunableop_mi355x0.csv (read by
 irads.gemm_tuning.use_tuned_gemms, which bench.py calls).  Runs eager training steps of the
 bench configuration with tuning on, so every GEMM shape of the step is benchmarked once.
@@ -24,18 +24,40 @@ def main():
     ap.add_argument("--out", required=True)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--max-ms", type=int, default=30)
+    ap.add_argument("--workload", default="c2", help="bench.py workload whose step is tuned (c2, c3, c4)")
+    ap.add_argument("--merge", default=None, help="existing table whose entries are kept where this run has none")
     a = ap.parse_args()
     start_tuning(a.out, a.max_ms)
     dev = torch.device("cuda", 0)
     torch.backends.cudnn.benchmark = True
-    model, opt, sched, loss_fn = bench.build(dev, 1, 0, 1000)
+    wl = dict(bench.WORKLOADS[a.workload])
+    model, opt, sched, loss_fn = bench.build(dev, 1, 0, 1000, wl=wl)
     model.train()
-    batch = bench.synthetic_batch(8, 512, dev, 3407)
+    batch = bench.synthetic_batch(wl["batch"], wl["hw"], dev, 3407, wl["n_cls"])
     for i in range(a.steps):
         bench.train_step(model, opt, sched, loss_fn, batch)
         torch.cuda.synchronize()
         print(f"tuning step {i} done, {len(torch.cuda.tunable.get_results())} GEMM results", flush=True)
-    print("TunableOp writes", a.out, "at exit")
+    torch.cuda.tunable.write_file()
+    print("TunableOp wrote", a.out, flush=True)
+    if a.merge:
+        merge_tables(a.out, a.merge)
+
+
+def merge_tables(new, old):
+    """Rewrite `new` as its entries over `old`'s (keys: op and shape columns), validators from `new`."""
+    def rows(path):
+        with open(path) as f:
+            return [l.rstrip("\n") for l in f if l.strip()]
+    import glob
+    new = sorted(glob.glob(new.replace(".csv", "*.csv")))[0]
+    nl, ol = rows(new), rows(old)
+    val = [l for l in nl if l.startswith("Validator")]
+    ent = {tuple(l.split(",")[:2]): l for l in ol if not l.startswith("Validator")}
+    ent.update({tuple(l.split(",")[:2]): l for l in nl if not l.startswith("Validator")})
+    with open(new, "w") as f:
+        f.write("\n".join(val + list(ent.values())) + "\n")
+    print("merged", len(ent), "entries into", new)
 
 
 if __name__ == "__main__":
