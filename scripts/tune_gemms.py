@@ -1,6 +1,7 @@
 """Produce the hipBLASLt selection table for the bench step (PyTorch TunableOp), on an MI355X.
 
-    python scripts/tune_gemms.py --out gpurun_out/tunableop_mi355x0.csv [--workload c4] [--merge <table>]
+    python scripts/tune_gemms.py --out gpurun_out/tunableop_mi355x0.csv [--workload c4]
+    python scripts/tune_gemms.py --out gpurun_out/tunableop_c4.csv --merge-into ir-ads_amd/irads/tuned/tunableop_mi355x0.csv
 then copy the file to ir-ads_amd/irads/tuned/tunableop_mi355x0.csv (read by
 irads.gemm_tuning.use_tuned_gemms, which bench.py calls).  Runs eager training steps of the
 bench configuration with tuning on, so every GEMM shape of the step is benchmarked once.
@@ -25,8 +26,12 @@ def main():
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--max-ms", type=int, default=30)
     ap.add_argument("--workload", default="c2", help="bench.py workload whose step is tuned (c2, c3, c4)")
-    ap.add_argument("--merge", default=None, help="existing table whose entries are kept where this run has none")
+    ap.add_argument("--merge-into", default=None,
+                    help="no tuning: rewrite this table as its entries overlaid by --out's (a finished run's)")
     a = ap.parse_args()
+    if a.merge_into:
+        merge_tables(a.out, a.merge_into)
+        return
     start_tuning(a.out, a.max_ms)
     dev = torch.device("cuda", 0)
     torch.backends.cudnn.benchmark = True
@@ -38,14 +43,12 @@ def main():
         bench.train_step(model, opt, sched, loss_fn, batch)
         torch.cuda.synchronize()
         print(f"tuning step {i} done, {len(torch.cuda.tunable.get_results())} GEMM results", flush=True)
-    torch.cuda.tunable.write_file()
-    print("TunableOp wrote", a.out, flush=True)
-    if a.merge:
-        merge_tables(a.out, a.merge)
+    print("TunableOp writes", a.out, "at exit; merge it over a shipped table with", flush=True)
+    print(f"    python scripts/tune_gemms.py --merge-into <table> --out {a.out}", flush=True)
 
 
 def merge_tables(new, old):
-    """Rewrite `new` as its entries over `old`'s (keys: op and shape columns), validators from `new`."""
+    """Rewrite `old` as its entries overlaid by `new`'s (keys: op and shape columns), validators from `new`."""
     def rows(path):
         with open(path) as f:
             return [l.rstrip("\n") for l in f if l.strip()]
@@ -55,9 +58,9 @@ def merge_tables(new, old):
     val = [l for l in nl if l.startswith("Validator")]
     ent = {tuple(l.split(",")[:2]): l for l in ol if not l.startswith("Validator")}
     ent.update({tuple(l.split(",")[:2]): l for l in nl if not l.startswith("Validator")})
-    with open(new, "w") as f:
+    with open(old, "w") as f:
         f.write("\n".join(val + list(ent.values())) + "\n")
-    print("merged", len(ent), "entries into", new)
+    print("merged", len(ent), "entries into", old)
 
 
 if __name__ == "__main__":
