@@ -1,6 +1,6 @@
 """Build irads.gemm's selection table: irads_gemm_nt against hipBLASLt (the shipped TunableOp table)
-on every trunk projection shape of BASELINE.json's C2 (Swin-B, 8 x 512², rgb + dte batched) and C4
-(Swin-L, 4 x 480x640) steps, forward y = x Wᵀ + b and backward dX = dY W, in interleaved rounds in
+on every trunk projection shape of BASELINE.json's C2 (Swin-B, 8 x 512², rgb + dte batched), C4
+(Swin-L, 4 x 480x640) and C3 (Swin-B, 4 x 512²) steps, forward y = x Wᵀ + b and backward dX = dY W, in interleaved rounds in
 one process (median of 5 rounds x 10 calls each).  A shape goes to irads_gemm_nt when its median is
 ≥ 5 % below hipBLASLt's and its error against the fp32 product is no worse than 1.5x hipBLASLt's.
 The FFN's fused pairs (fc1 + GELU epilogue, fc2 dX + GELU' epilogue) are timed against the better
@@ -26,7 +26,8 @@ from irads import native as N  # noqa: E402
 
 # (config, C, tokens of the batched rgb + dte stage input)
 STAGES = [("c2", 128 * 2 ** s, 262144 // 4 ** s) for s in range(4)] + \
-         [("c4", 192 * 2 ** s, 153600 // 4 ** s) for s in range(4)]
+         [("c4", 192 * 2 ** s, 153600 // 4 ** s) for s in range(4)] + \
+         [("c3", 128 * 2 ** s, 131072 // 4 ** s) for s in range(4)]  # C3: Swin-B 512², 4 per GPU
 
 
 def timed(fn, reps=10):
