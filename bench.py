@@ -180,10 +180,7 @@ def msda_inputs(device, bs=2, Q=None, seed=0):
     return [t.to(device) for t in (value, shapes, lsi, loc, aw)]
 
 
-TIMED_KERNELS = ("winattn_fwd", "winattn_bwd", "dattn_fwd", "dattn_bwd")
-TIMER_REPS = 1  # launches per event pair in the eager timing pass: one, so no launch re-reads the
-#                previous one's q/k/v from the 256 MB Infinity Cache (round-3 verdict: 4 back-to-back
-#                repeats read 10 % faster than the same kernels in the traced step)
+TIMED_KERNELS = ("winattn_fwd", "winattn_bwd", "dattn_fwd", "dattn_bwd")  # stamped in the step (ops.STAMPS)
 MSDA_SETS = 4  # rotating input sets in msda_rooflines: > 2x the Infinity Cache between reuses
 FP32_PEAK_TFLOPS = 157.3  # MI355X fp32 vector peak (MI355X_MICROARCH.md)
 GATHER_PEAK_GBS = 18800.0  # L2-resident random-row gather rate (upper end), MI355X_MICROARCH.md
@@ -403,23 +400,20 @@ def main():
     batch = synthetic_batch(args.batch, wl["hw"], device, 3407 + rank, wl["n_cls"])
 
     from irads import ops
-    timer_in_graph = False
     if graph:
         # W warm-up iterations run eagerly inside the capture helper, then one captured step
-        # is replayed: the timed region is K graph replays (+ the host-side LR update each)
-        from irads.graph_step import GraphedTrainStep, events_capturable
-        timer_in_graph = events_capturable(device)
+        # is replayed: the timed region is K graph replays (+ the host-side LR update each).
+        # The captured window-attention / DAttn launches carry wall-clock stamp slots (ops.STAMPS).
+        from irads.graph_step import GraphedTrainStep
 
-        def arm_timer():  # per-launch HIP events captured around the window-attention kernels
-            if timer_in_graph:
-                ops.TIMER.records.clear()
-                ops.TIMER.enabled = set(TIMED_KERNELS)
+        def arm_stamps():
+            ops.STAMPS.arm(TIMED_KERNELS, device)
         if world > 1:  # DDP's construction broadcast (the graph path has no DDP wrapper)
             from irads.graph_step import broadcast_module
             broadcast_module(model)
         runner = GraphedTrainStep(model.parameters(), lambda: fwd_bwd(model, loss_fn, batch), opt, world=world,
-                                  warmup=max(args.warmup, 1), before_capture=arm_timer)
-        ops.TIMER.enabled = set()
+                                  warmup=max(args.warmup, 1), before_capture=arm_stamps)
+        ops.STAMPS.disarm()
 
         def step():
             loss = runner.step()
@@ -433,11 +427,6 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    if not graph:
-        ops.TIMER.enabled = set(TIMED_KERNELS)
-    if not timer_in_graph:
-        ops.TIMER.records.clear()
-    torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step()
@@ -445,36 +434,26 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    ops.TIMER.enabled = set()
-    timer_steps = 1 if graph else args.steps  # steps the recorded launches cover
-    if graph and not timer_in_graph:
-        # HIP events cannot be captured on this stack: time the same kernels in one eager step, each
-        # timed launch behind a GPU spin so that its event pair brackets the kernel alone
-        ops.TIMER.records.clear()
-        ops.TIMER.enabled = set(TIMED_KERNELS)
-        ops.TIMER.keep = {"winattn_fwd", "winattn_bwd"}
-        ops.TIMER.lead_cycles = 200_000
-        ops.TIMER.reps = TIMER_REPS
-        fwd_bwd(model, loss_fn, batch)  # gradients land in the graph's buffer, re-zeroed by the next replay
-        ops.TIMER.enabled = set()
-        ops.TIMER.keep = set()
-        ops.TIMER.lead_cycles = 0
-        ops.TIMER.reps = 1
-    # the step's window-attention launches again, back to back, each on its own layer's inputs
-    group = {k: ops.TIMER.replay_group(k) for k in ("winattn_fwd", "winattn_bwd")}
-    ops.TIMER.kept.clear()
+    # In-step kernel spans: ONE more step after the timed region, identical to the timed ones (the
+    # same graph replay; eager: the same step with stamp slots armed), whose window-attention and
+    # DAttn kernels stamp their first-workgroup start / last-workgroup end on the device clock.
+    # Nothing is re-run on the side, and no eager step writes into the graph's buffers.
+    if args.profile_only:  # a kernel trace of exactly K steps: no extra step
+        pass
+    elif graph:
+        ops.STAMPS.reset()
+        step()
+    else:
+        ops.STAMPS.arm(TIMED_KERNELS, device)
+        step()
+        ops.STAMPS.disarm()
+    spans = ops.STAMPS.read() if not args.profile_only else {}
     if world > 1:
         t = torch.tensor([elapsed], device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     loss_val = float(loss.item())
-    fwd = ops.TIMER.summary("winattn_fwd")
-    bwd = ops.TIMER.summary("winattn_bwd")
-    per_call = {"fwd": fwd, "bwd": bwd}  # one event pair per launch (includes its dispatch latency)
-    if graph and not timer_in_graph and group.get("winattn_fwd"):
-        fwd = dict(group["winattn_fwd"], calls=group["winattn_fwd"]["launches"])
-        if group.get("winattn_bwd"):
-            bwd = dict(group["winattn_bwd"], calls=group["winattn_bwd"]["launches"])
+    fwd, bwd = spans.get("winattn_fwd"), spans.get("winattn_bwd")
     if args.profile_only:
         if rank == 0:
             print(json.dumps({"profile_only": True, "ms_per_step": 1e3 * elapsed / args.steps}))
@@ -499,53 +478,52 @@ def main():
                    "miopen": "deterministic solvers" if args.deterministic else "benchmark (fastest) solvers"},
         "loss": round(loss_val, 5),
     }
+    step_ms = 1e3 * elapsed / args.steps
+    stamp_timing = ("in-kernel wall-clock stamps (s_memrealtime, first workgroup start to last workgroup end per "
+                    "launch) of one " + ("graph replay" if graph else "eager step") + " after the timed region, "
+                    "identical to the timed steps: the kernels' spans inside the real step, beside the other "
+                    "streams' work (what rocprofv3's kernel trace reports)")
     if fwd:
         avg_ms = fwd["total_ms"] / fwd["launches"]
         per_launch_bytes = fwd["bytes"] / fwd["launches"]
         achieved = fwd["bytes"] / (fwd["total_ms"] * 1e-3) / 1e9
-        achieved_real = (per_call["fwd"]["real_bytes"] / per_call["fwd"]["bytes"]) * achieved if per_call["fwd"] else None
         traffic, traffic_src = traffic_from_profile()
         result["roofline"] = {
             "kernel": "irads_winattn_fwd (bf16, Swin-B shifted-window attention, all 4 stages x 2 streams)",
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
             "traffic_source": (f"from committed PMC {traffic_src} (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE per launch, "
-                               f"not measured in this run)" if traffic_src else None),
-            "launches": fwd["calls"], "timed_launches": fwd["launches"], "avg_launch_ms": round(avg_ms, 5),
+                               f"separate passes over the same 24 launches; not measurable from inside this run)"
+                               if traffic_src else None),
+            "launches": fwd["launches"], "avg_launch_ms": round(avg_ms, 5),
             "algorithmic_bytes_per_launch": round(per_launch_bytes),
-            "timing": ("HIP events captured in the graph, last timed replay" if timer_in_graph else
-                       "HIP events on the launch stream" + (" (one eager step after the timed region keeps every "
-                                                            "window-attention launch with its inputs; the step's "
-                                                            "launches are then re-issued back to back inside ONE "
-                                                            "event pair behind a GPU spin, each reading its own "
-                                                            "layer's tensors: no launch reuses cached operands)"
-                                                            if graph else "")),
-            "per_launch_event_pairs_avg_ms": (round(per_call["fwd"]["total_ms"] / per_call["fwd"]["launches"], 5)
-                                              if per_call["fwd"] else None),
+            "timing": stamp_timing,
+            "span_ms_min_max": [round(min(fwd["spans_ms"]), 5), round(max(fwd["spans_ms"]), 5)],
             "bytes_definition": "SURVEY §8(d): read q,k,v + write o per padded token (8·Np·C bytes, bf16)",
-            "achieved_real_tokens_gbs": None if achieved_real is None else round(achieved_real, 1),
-            "mfma_tflops": round(fwd["flops"] / (fwd["total_ms"] * 1e-3) / 1e12, 2)}
+            "achieved_real_tokens_gbs": round(fwd["real_bytes"] / (fwd["total_ms"] * 1e-3) / 1e9, 1),
+            "mfma_tflops": round(fwd["flops"] / (fwd["total_ms"] * 1e-3) / 1e12, 2),
+            "share_of_step": round(fwd["total_ms"] / step_ms, 4)}
         if bwd:
             ab = bwd["bytes"] / (bwd["total_ms"] * 1e-3) / 1e9
-            result["roofline_bwd"] = {"kernel": "irads_winattn_bwd (bf16)", "achieved": round(ab, 1),
-                                      "unit": "GB/s", "frac": round(ab / HBM_PEAK_GBS, 4),
+            result["roofline_bwd"] = {"kernel": "irads_winattn_bwd (bf16)", "bound": "hbm", "achieved": round(ab, 1),
+                                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ab / HBM_PEAK_GBS, 4),
+                                      "launches": bwd["launches"],
                                       "avg_launch_ms": round(bwd["total_ms"] / bwd["launches"], 5),
-                                      "share_of_step": round(bwd["total_ms"] * bwd["calls"] / bwd["launches"] / timer_steps
-                                                             / (1e3 * elapsed / args.steps), 4)}
-            result["roofline"]["share_of_step"] = round(fwd["total_ms"] * fwd["calls"] / fwd["launches"] / timer_steps
-                                                        / (1e3 * elapsed / args.steps), 4)
+                                      "timing": "as roofline",
+                                      "share_of_step": round(bwd["total_ms"] / step_ms, 4)}
     for tag in ("fwd", "bwd"):
-        d = ops.TIMER.summary(f"dattn_{tag}")
+        d = spans.get(f"dattn_{tag}")
         if d:
             tf = d["flops"] / (d["total_ms"] * 1e-3) / 1e12
             result[f"roofline_dattn_{tag}"] = {
-                "kernel": f"irads_dattn_attn_{tag} (DSCF deformable attention core, fp32, 4 stages)",
+                "kernel": f"irads_dattn_attn_{tag} (DSCF deformable attention core, fp32, 4 stages)"
+                          + (" (pass Q + pass K + the fixed-order reduces: the entry's span)" if tag == "bwd" else ""),
                 "bound": "fp32-valu", "achieved": round(tf, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(tf / FP32_PEAK_TFLOPS, 4), "launches": d["launches"],
-                "avg_launch_ms": round(d["total_ms"] / d["launches"], 5),
+                "avg_launch_ms": round(d["total_ms"] / d["launches"], 5), "timing": "as roofline",
                 "flops_definition": "SURVEY §8(d): 44 FLOP per (query, key) pair forward, 88 backward; "
                                     "pairs = B·heads·H·W·2n per stage",
-                "share_of_step": round(d["total_ms"] / timer_steps / (1e3 * elapsed / args.steps), 4)}
+                "share_of_step": round(d["total_ms"] / step_ms, 4)}
     if args.workload != "c2":  # a separate line for another BASELINE config, not the headline metric
         result["metric"] = {"c4": "train images/sec @480x640 RGB-T Swin-L, SB hook on (BASELINE.json config C4), "
                                   "1 MI355X",
@@ -579,9 +557,10 @@ def main():
 
 
 def _teardown():
-    from irads.graph_step import quiesce_process_groups
+    from irads.graph_step import quiesce_process_groups, release_capture_groups
     quiesce_process_groups()  # the captured graph is still alive: leave no eager work to poll
     dist.destroy_process_group()
+    release_capture_groups()
 
 
 if __name__ == "__main__":

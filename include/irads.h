@@ -33,6 +33,15 @@ extern "C" {
 
 const char *irads_last_error(void);
 int irads_version(void);
+/* Measurement (bench.py, no reference counterpart): arm `region` (IRADS_STAMP_CAP x 2 uint64,
+ * caller-zeroed) for the calling thread's next window-attention or DAttn-core launch entry
+ * (irads_winattn_fwd/bwd, irads_dattn_attn_fwd/bwd(_ws)), which takes and disarms it: workgroup w
+ * of its kernels (w < IRADS_STAMP_CAP) writes its start / end clock to region[2w] / region[2w+1] on
+ * the device wall clock, also from inside a captured graph; the launch's span is min(start) ..
+ * max(end).  NULL disarms.  irads_wall_clock_khz: that clock's rate. */
+#define IRADS_STAMP_CAP 16384
+void irads_stamp_next(unsigned long long *slot);
+int irads_wall_clock_khz(void);
 
 /* ------------------------------------------------------------------ MSDeformAttn
  * Replaces detrex._C.ms_deform_attn_forward / _backward
@@ -146,13 +155,15 @@ int irads_dattn_gate_bwd(const float *grad_y, const void *out_tok, const void *x
 /* DAttentionMM's modality mix of the sampled features (swin.py:946-949) with the transpose and bf16
  * cast of its token-major consumers: out (B, n2, C) bf16 = bf16(xs·w[..., 0] + ys·w[..., 1]), xs /
  * ys (B, C, n2) fp32, w (B, n2, 2) fp32 (the 2-way softmax); fp32 rounding of each product and the
- * sum as the reference's separate ops.  Backward from grad_tok (B, n2, C) bf16: grad_xs / grad_ys
- * (B, C, n2) = g·w0 / g·w1, grad_w (B, n2, 2) = channel sums of g·xs, g·ys.  C a multiple of 8,
- * out / grad_tok 16-B aligned. */
+ * sum as the reference's separate ops.  out2 (nullable): a second copy, the second consumer's
+ * operand (proj_k reads out, proj_v out2).  Backward from grad_tok (B, n2, C) bf16 and grad_tok2
+ * (nullable, the second consumer's), added in fp32 as g: grad_xs / grad_ys (B, C, n2) = g·w0 /
+ * g·w1, grad_w (B, n2, 2) = channel sums of g·xs, g·ys.  C a multiple of 8, every bf16 operand
+ * 16-B aligned. */
 int irads_dattn_mix_fwd(const float *xs, const float *ys, const float *w, int B, int C, int n2, void *out,
-                        void *stream);
-int irads_dattn_mix_bwd(const void *grad_tok, const float *xs, const float *ys, const float *w, int B, int C, int n2,
-                        float *grad_xs, float *grad_ys, float *grad_w, void *stream);
+                        void *out2, void *stream);
+int irads_dattn_mix_bwd(const void *grad_tok, const void *grad_tok2, const float *xs, const float *ys, const float *w,
+                        int B, int C, int n2, float *grad_xs, float *grad_ys, float *grad_w, void *stream);
 /* Fused attention with on-the-fly bilinear rpe bias (swin.py:950-1016):
  *   q (B*nH, hc, HW)  k, v KEY-MAJOR (B*nH, 2n, hc)  rpe (nH, Ht, Wt)  qgrid_y (H), qgrid_x (W)
  *   (the reference's _get_q_grid values)  out (B*nH, hc, HW)  lse (B*nH, HW).

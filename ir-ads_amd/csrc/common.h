@@ -11,6 +11,9 @@
 namespace irads {
 
 void set_error(const char *fmt, ...);
+// In-step kernel spans (bench.py's roofline lines): the slot irads_stamp_next() armed for the
+// calling thread's next stamped launch, or null; taking it disarms.
+unsigned long long *take_stamp();
 
 #define IRADS_REQUIRE(cond, ...)          \
     do {                                  \
@@ -109,6 +112,35 @@ __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
+}
+
+// Kernel span stamps (bench.py's in-step roofline): a stamped launch gets a region of STAMP_CAP
+// (start, end) pairs; workgroup w (linear block id) writes its entry clock to region[2w] and its exit
+// clock to region[2w + 1] on the device's constant-rate wall clock (s_memrealtime); the host reads
+// min(start) .. max(end) = the launch's span inside the step.  Plain vector stores, one lane per
+// workgroup, no shared address (a single min/max atomic address serialised every workgroup across
+// the 8 XCDs: ~14 ns each, doubling the window-attention forward).  A null region (every launch but
+// the stamped ones) is a uniform branch.  stamp_end has a workgroup barrier: call it where every
+// thread arrives.
+constexpr unsigned STAMP_CAP = IRADS_STAMP_CAP;
+__device__ __forceinline__ unsigned stamp_wg() { return blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z); }
+__device__ __forceinline__ void stamp_begin(unsigned long long *s) {
+    if (s && threadIdx.x == 0) {
+        const unsigned w = stamp_wg();
+        if (w < STAMP_CAP) s[2 * w] = (unsigned long long)wall_clock64();
+    }
+}
+__device__ __forceinline__ void stamp_end_lane0(unsigned long long *s) {  // no barrier: one-pass kernels
+    if (s && threadIdx.x == 0) {
+        const unsigned w = stamp_wg();
+        if (w < STAMP_CAP) s[2 * w + 1] = (unsigned long long)wall_clock64();
+    }
+}
+__device__ __forceinline__ void stamp_end(unsigned long long *s) {
+    if (s) {
+        __syncthreads();
+        stamp_end_lane0(s);
+    }
 }
 
 // counter-based dropout draw: splitmix64 of (seed, element index) -> uniform [0, 1)

@@ -333,6 +333,7 @@ struct AttnArgs {
     const float *q, *k, *v, *px, *py, *rpe, *qgy, *qgx;
     int B, nH, G, hc, H, W, n, Ht, Wt;
     float scale;
+    unsigned long long *stamp;  // irads_stamp_next's slot for this entry's launches, or null
 };
 
 // ---------------------------------------------------------------- shared pieces
@@ -483,6 +484,7 @@ __global__ void __launch_bounds__(1024) dattn_attn_bwd_q_kernel(AttnArgs a, int 
                                                                 float *__restrict__ delta, float *__restrict__ gq,
                                                                 float *__restrict__ grpe, float *__restrict__ dq_part,
                                                                 float *__restrict__ rpe_part) {
+    stamp_begin(a.stamp);  // the entry's span ends in its last kernel (kpart reduce)
     extern __shared__ __attribute__((aligned(16))) float sm[];
     __shared__ float red[16], vmx[16][HC];
     const int n2 = 2 * a.n, HW = a.H * a.W, PC = pad_cells(a.Ht, a.Wt);
@@ -834,7 +836,8 @@ __global__ void __launch_bounds__(1024) dattn_attn_bwd_k_band_kernel(AttnArgs a,
 template <int HC>
 __global__ void __launch_bounds__(256) dattn_kpart_reduce(const float *__restrict__ part, int chunks, int B, int nH,
                                                           int G, int n, float *__restrict__ gk, float *__restrict__ gv,
-                                                          float *__restrict__ gpx, float *__restrict__ gpy) {
+                                                          float *__restrict__ gpx, float *__restrict__ gpy,
+                                                          unsigned long long *__restrict__ stamp) {
     constexpr int F = 2 * HC + 2;
     const int n2 = 2 * n, hpg = nH / G;
     const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -863,6 +866,7 @@ __global__ void __launch_bounds__(256) dattn_kpart_reduce(const float *__restric
             pos += acc;
     }
     if (f >= 2 * HC) ((j < n ? gpx : gpy) + ((long)bg * n + (j % n)) * 2)[f - 2 * HC] = pos;
+    stamp_end_lane0(stamp);
 }
 
 // ---------------------------------------------------------------- forward (banded)
@@ -879,6 +883,7 @@ __global__ void __launch_bounds__(64 * NWAVE) dattn_attn_fwd_band_kernel(AttnArg
                                                                   const float *__restrict__ pxg,
                                                                   const float *__restrict__ pyg,
                                                                   float *__restrict__ out, float *__restrict__ lse) {
+    stamp_begin(a.stamp);
     static_assert(HC % 2 == 0, "packed fp32 needs an even head size");
     extern __shared__ __attribute__((aligned(16))) float sm[];
     const int n2 = 2 * a.n, HW = a.H * a.W, TP = a.Wt + 1;
@@ -985,6 +990,7 @@ __global__ void __launch_bounds__(64 * NWAVE) dattn_attn_fwd_band_kernel(AttnArg
         }
         lse[(long)bh * HW + qi] = m * kLn2 + logf(l);
     }
+    stamp_end(a.stamp);
 }
 
 // table rows a contiguous range of `nq` queries can reach (see band_rows), for LDS sizing
@@ -1147,7 +1153,7 @@ extern "C" int irads_dattn_attn_fwd(const float *q, const float *k, const float 
                                     const float *pos_y, const float *rpe, const float *qgrid_y, const float *qgrid_x,
                                     int B, int nH, int G, int hc, int H, int W, int n, int Ht, int Wt, float scale,
                                     float *out, float *lse, void *stream) {
-    AttnArgs a{q, k, v, pos_x, pos_y, rpe, qgrid_y, qgrid_x, B, nH, G, hc, H, W, n, Ht, Wt, scale};
+    AttnArgs a{q, k, v, pos_x, pos_y, rpe, qgrid_y, qgrid_x, B, nH, G, hc, H, W, n, Ht, Wt, scale, take_stamp()};
     if (int e = check_attn(a)) return e;
     IRADS_REQUIRE(hc <= 16, "dattn_attn: head channels %d > 16", hc);
     if (B == 0) return IRADS_OK;
@@ -1209,7 +1215,7 @@ static int attn_bwd(const float *q, const float *k, const float *v, const float 
                     int W, int n, int Ht, int Wt, float scale, const float *out, const float *lse,
                     const float *grad_out, float *delta, float *grad_q, float *grad_k, float *grad_v, float *grad_rpe,
                     float *grad_pos_x, float *grad_pos_y, char *ws, void *stream) {
-    AttnArgs a{q, k, v, pos_x, pos_y, rpe, qgrid_y, qgrid_x, B, nH, G, hc, H, W, n, Ht, Wt, scale};
+    AttnArgs a{q, k, v, pos_x, pos_y, rpe, qgrid_y, qgrid_x, B, nH, G, hc, H, W, n, Ht, Wt, scale, take_stamp()};
     if (int e = check_attn(a)) return e;
     IRADS_REQUIRE(hc <= 16, "dattn_attn: head channels %d > 16", hc);
     if (B == 0) return IRADS_OK;
@@ -1255,7 +1261,8 @@ static int attn_bwd(const float *q, const float *k, const float *v, const float 
         if (part) {
             const long t = (long)B * G * (2 * HC + 2) * 2 * n;
             dattn_kpart_reduce<HC><<<(unsigned)((t + 255) / 256), 256, 0, st>>>(part, chunks, B, nH, G, n, grad_k,
-                                                                                 grad_v, grad_pos_x, grad_pos_y);
+                                                                                 grad_v, grad_pos_x, grad_pos_y,
+                                                                                 a.stamp);
         }
     })
     return check_launch("irads_dattn_attn_bwd");
@@ -1392,9 +1399,12 @@ typedef __attribute__((ext_vector_type(4))) unsigned int mix_u32x4;
 // ys[b, c, j]·w[b, j, 1]), each product and the sum rounded in fp32 as the reference's separate
 // elementwise ops (this file builds without FMA contraction).  Thread per (b, j): the channel loop
 // reads xs / ys coalesced across the wave's consecutive j and writes 16-B runs of 8 channels.
+// out2 (optional) receives the same values: the second consumer's own operand, so autograd hands
+// the backward each consumer's bf16 gradient separately (the reference adds them in fp32).
 __global__ void __launch_bounds__(256) dattn_mix_fwd_kernel(const float *__restrict__ xs, const float *__restrict__ ys,
                                                           const float *__restrict__ w, int B, int C, int n2,
-                                                          unsigned short *__restrict__ out) {
+                                                          unsigned short *__restrict__ out,
+                                                          unsigned short *__restrict__ out2) {
     const long t = (long)blockIdx.x * 256 + threadIdx.x;
     if (t >= (long)B * n2) return;
     const int b = (int)(t / n2), j = (int)(t - (long)b * n2);
@@ -1409,13 +1419,16 @@ __global__ void __launch_bounds__(256) dattn_mix_fwd_kernel(const float *__restr
             o[e] = (unsigned)f2bf(p0 + q0) | ((unsigned)f2bf(p1 + q1) << 16);
         }
         *reinterpret_cast<mix_u32x4 *>(out + t * C + c8) = o;
+        if (out2) *reinterpret_cast<mix_u32x4 *>(out2 + t * C + c8) = o;
     }
 }
 
-// backward: g (B, n2, C) bf16 (the sum of the proj_k and proj_v input gradients) -> grad_xs =
-// g·w0, grad_ys = g·w1 (fp32, (B, C, n2)) and grad_w[b, j] = (Σ_c g·xs, Σ_c g·ys) summed over c
-// in order.
+// backward: g (B, n2, C) bf16, the proj_k input gradient, and g2 (optional) the proj_v one; their
+// sum in fp32 (gf = g + g2: what autograd forms from the two bf16 cast-backward outputs of the
+// reference's fp32 `sampled`, swin.py:948-952) -> grad_xs = gf·w0, grad_ys = gf·w1 (fp32,
+// (B, C, n2)) and grad_w[b, j] = (Σ_c gf·xs, Σ_c gf·ys) summed over c in order.
 __global__ void __launch_bounds__(256) dattn_mix_bwd_kernel(const unsigned short *__restrict__ g,
+                                                          const unsigned short *__restrict__ g2,
                                                           const float *__restrict__ xs, const float *__restrict__ ys,
                                                           const float *__restrict__ w, int B, int C, int n2,
                                                           float *__restrict__ gxs, float *__restrict__ gys,
@@ -1428,9 +1441,12 @@ __global__ void __launch_bounds__(256) dattn_mix_bwd_kernel(const unsigned short
     float a0 = 0.f, a1 = 0.f;
     for (int c8 = 0; c8 < C; c8 += 8) {
         const mix_u32x4 gv = *reinterpret_cast<const mix_u32x4 *>(g + t * C + c8);
+        mix_u32x4 gv2 = {0u, 0u, 0u, 0u};
+        if (g2) gv2 = *reinterpret_cast<const mix_u32x4 *>(g2 + t * C + c8);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-            const float gf = bf2f((unsigned short)(gv[e >> 1] >> (16 * (e & 1))));
+            float gf = bf2f((unsigned short)(gv[e >> 1] >> (16 * (e & 1))));
+            if (g2) gf = gf + bf2f((unsigned short)(gv2[e >> 1] >> (16 * (e & 1))));
             const long o = base + (long)(c8 + e) * n2;
             gxs[o] = gf * w0;
             gys[o] = gf * w1;
@@ -1474,25 +1490,27 @@ extern "C" int irads_dattn_gate_bwd(const float *grad_y, const void *out_tok, co
 }
 
 extern "C" int irads_dattn_mix_fwd(const float *xs, const float *ys, const float *w, int B, int C, int n2, void *out,
-                                   void *stream) {
+                                   void *out2, void *stream) {
     IRADS_REQUIRE(xs && ys && w && out, "dattn_mix: null pointer");
-    IRADS_REQUIRE(B >= 0 && n2 >= 0 && C > 0 && C % 8 == 0 && ((uintptr_t)out % 16) == 0,
+    IRADS_REQUIRE(B >= 0 && n2 >= 0 && C > 0 && C % 8 == 0 && (((uintptr_t)out | (uintptr_t)out2) % 16) == 0,
                   "dattn_mix: C=%d must be a multiple of 8, out 16-B aligned", C);
     const long n = (long)B * n2;
     if (n == 0) return IRADS_OK;
     hipLaunchKernelGGL(dattn_mix_fwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, xs,
-                       ys, w, B, C, n2, (unsigned short *)out);
+                       ys, w, B, C, n2, (unsigned short *)out, (unsigned short *)out2);
     return check_launch("irads_dattn_mix_fwd");
 }
 
-extern "C" int irads_dattn_mix_bwd(const void *grad_tok, const float *xs, const float *ys, const float *w, int B, int C,
-                                   int n2, float *grad_xs, float *grad_ys, float *grad_w, void *stream) {
+extern "C" int irads_dattn_mix_bwd(const void *grad_tok, const void *grad_tok2, const float *xs, const float *ys,
+                                   const float *w, int B, int C, int n2, float *grad_xs, float *grad_ys, float *grad_w,
+                                   void *stream) {
     IRADS_REQUIRE(grad_tok && xs && ys && w && grad_xs && grad_ys && grad_w, "dattn_mix: null pointer");
-    IRADS_REQUIRE(B >= 0 && n2 >= 0 && C > 0 && C % 8 == 0 && ((uintptr_t)grad_tok % 16) == 0,
+    IRADS_REQUIRE(B >= 0 && n2 >= 0 && C > 0 && C % 8 == 0 && (((uintptr_t)grad_tok | (uintptr_t)grad_tok2) % 16) == 0,
                   "dattn_mix: C=%d must be a multiple of 8, grad_tok 16-B aligned", C);
     const long n = (long)B * n2;
     if (n == 0) return IRADS_OK;
     hipLaunchKernelGGL(dattn_mix_bwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
-                       (const unsigned short *)grad_tok, xs, ys, w, B, C, n2, grad_xs, grad_ys, grad_w);
+                       (const unsigned short *)grad_tok, (const unsigned short *)grad_tok2, xs, ys, w, B, C, n2, grad_xs,
+                       grad_ys, grad_w);
     return check_launch("irads_dattn_mix_bwd");
 }

@@ -36,6 +36,7 @@ typedef __attribute__((ext_vector_type(4))) unsigned short u16x4;
 struct Geo {
     int B, H, W, C, nH, shift, Hp, Wp, nWh, nWw, nW, n_mask;
     float scale;
+    unsigned long long *stamp;  // irads_stamp_next's slot for this launch, or null
 };
 
 // token t (0..143) of window w -> global token index (or -1 for a pad token) and region id
@@ -420,6 +421,7 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(MM == 
     __shared__ __attribute__((aligned(16))) unsigned short Ks[NT * HD];  // swizzled 64-B rows (kv_swz)
     __shared__ __attribute__((aligned(16))) unsigned short Vs[NT * HD];
     __shared__ __attribute__((aligned(16))) f32x4 Bq[QB];  // forward quads of this head x c2
+    stamp_begin(g.stamp);
     const int lid = xcd_remap(blockIdx.x, gridDim.x);      // the heads of one window on one XCD
     const int h = lid % g.nH, bw = lid / g.nH;
     const WinOrigin wo(g, bw);
@@ -564,6 +566,7 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(MM == 
         }
         if (grp == 0) lse[((long)bw * g.nH + h) * NT + qi] = __log2f(os[0]) + shift;  // base-2 LSE of s''
     }
+    stamp_end(g.stamp);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -809,6 +812,7 @@ __global__ void __launch_bounds__(576) winattn_bwd_bf16(
     __shared__ int tokS[NT];
     __shared__ __attribute__((aligned(16))) unsigned short padS[3 * HD];  // pad-token q, k, v (bf16)
     __shared__ float tgS[EX ? TBL : 1];  // EX: this workgroup's rel-table gradient, flushed once
+    stamp_begin(g.stamp);
     const Chunk ck = decode_chunk(g, cw);
     const int h = ck.h;
     const float mneg100 = -100.0f * LOG2E;  // the region mask in s'' units
@@ -1045,6 +1049,7 @@ __global__ void __launch_bounds__(576) winattn_bwd_bf16(
         __syncthreads();
         for (int i = tid; i < TBL; i += 576) atomicAdd(&gtable[i * g.nH + h], tgS[i]);
     }
+    stamp_end(g.stamp);
 }
 
 // Forward kernel choice: 0 = one workgroup per (window, head) (winattn_fwd_bf16_rt), 1 = persistent
@@ -1078,6 +1083,7 @@ int chunk_windows(int total_windows, int nH, long target = 256) {  // target: pe
 
 int make_geo(Geo &g, int dtype, int B, int H, int W, int C, int nH, int shift, float scale, const float *mask,
              int n_mask) {
+    g.stamp = take_stamp();  // taken (disarmed) whatever follows; the bf16 kernels write it
     IRADS_REQUIRE(dtype == IRADS_F32 || dtype == IRADS_BF16, "winattn: dtype must be float32 or bfloat16");
     IRADS_REQUIRE(B >= 0 && H > 0 && W > 0 && nH > 0, "winattn: bad sizes");
     IRADS_REQUIRE(C == nH * HD, "winattn: head_dim must be 32 (embed_dims %d, heads %d)", C, nH);

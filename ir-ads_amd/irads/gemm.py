@@ -13,8 +13,10 @@ tuned/irads_gemm_select_mi355x.json, the (direction, M, N, K) keys where irads_g
 tiles on 8 waves, N % 256 == 0).  Directions: "fwd" (y = x Wᵀ + b), "bwd" (dX = dY W), and the FFN's fused pairs
 "fwd_gelu" (fc1 with the erf GELU in the epilogue, against the better GEMM + gelu pass) and
 "bwd_dgelu" (fc2's dX with GELU' applied in the epilogue, against GEMM + gelu_bwd pass).  A
-shape not in the table, or one the kernel cannot take (N % 128, K % 64), goes to hipBLASLt.  IRADS_GEMM=off sends every shape to hipBLASLt, IRADS_GEMM=all every shape the
-kernel takes to irads_gemm_nt (A/B and tests).
+shape not in the table, or one the kernel cannot take (N % 128, K % 64, an operand not 16-byte aligned
+or with a leading dimension not a multiple of 8), goes to hipBLASLt.  IRADS_GEMM=off sends every shape
+to hipBLASLt, IRADS_GEMM=all every shape the kernel takes to irads_gemm_nt (A/B and tests), on the
+tiling IRADS_GEMM_VARIANT names (default 2; variant 4 where N % 256 == 0, else 2).
 """
 import json
 import os
@@ -54,9 +56,16 @@ def use_irads(direction, M, N_out, K):
     if mode == "off" or not kernel_fits(N_out, K):
         return None
     if mode == "all":
-        return DEFAULT_VARIANT
+        v = int(os.environ.get("IRADS_GEMM_VARIANT", DEFAULT_VARIANT))
+        return v if kernel_fits(N_out, K, v) else DEFAULT_VARIANT
     v = _selected().get((direction, M, N_out, K))
     return v if v is not None and kernel_fits(N_out, K, v) else None
+
+
+def _aligned(*ts):
+    """Every operand as the C entry point takes it: rows contiguous, 16-byte aligned base, leading
+    dimension a multiple of 8 elements (a contiguous view at an odd offset goes to hipBLASLt)."""
+    return all(t.stride(-1) == 1 and t.data_ptr() % 16 == 0 and t.stride(0) % 8 == 0 for t in ts)
 
 
 def weights(lin):
@@ -87,7 +96,7 @@ def linear(x, lw):
     M, K = x.shape
     N_out = w16.shape[0]
     v = use_irads("fwd", M, N_out, K)
-    if v is not None and x.is_contiguous():
+    if v is not None and x.is_contiguous() and _aligned(x, w16):
         return _nt(x, w16, b32, M, N_out, K, v)
     return F.linear(x, w16, b16)
 
@@ -99,7 +108,7 @@ def ffn_up(h, lw):
     M, K = h.shape
     N_out = w16.shape[0]
     v = use_irads("fwd_gelu", M, N_out, K)
-    if v is not None and h.is_contiguous():
+    if v is not None and h.is_contiguous() and _aligned(h, w16):
         u = torch.empty((M, N_out), device=h.device, dtype=_BF16)
         g = torch.empty_like(u)
         N.call("irads_gemm_nt_variant", v, 1, N.ptr(h), h.stride(0), N.ptr(w16), w16.stride(0), N.ptr(b32), None, 0,
@@ -119,7 +128,7 @@ def ffn_down_dgrad_gelu(df, lw, u):
     M, N_in = df.shape
     K_out = w16.shape[1]
     v = use_irads("bwd_dgelu", M, K_out, N_in)
-    if v is not None and df.is_contiguous() and u.is_contiguous():
+    if v is not None and df.is_contiguous() and u.is_contiguous() and _aligned(df, wt, u):
         du = torch.empty((M, K_out), device=df.device, dtype=_BF16)
         N.call("irads_gemm_nt_variant", v, 2, N.ptr(df), df.stride(0), N.ptr(wt), wt.stride(0), None, N.ptr(u), u.stride(0),
                N.ptr(du), None, du.stride(0), M, K_out, N_in, N.stream())
@@ -136,6 +145,6 @@ def dgrad(dy, lw):
     M, N_in = dy.shape
     K_out = w16.shape[1]
     v = use_irads("bwd", M, K_out, N_in)
-    if v is not None and dy.is_contiguous():
+    if v is not None and dy.is_contiguous() and _aligned(dy, wt):
         return _nt(dy, wt, None, M, K_out, N_in, v)
     return torch.mm(dy, w16)

@@ -53,7 +53,7 @@ def rccl_capture_env():
     os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
 
 
-_CAPTURE_GROUPS = {}  # (default group, device) -> process group used only inside captures
+_CAPTURE_GROUPS = {}  # device -> (the default group it was made under, process group used only inside captures)
 
 
 def capture_group(device):
@@ -75,14 +75,16 @@ def capture_group(device):
     if not dist.is_initialized() or dist.get_backend() != "nccl":
         return None
     dev = torch.device(device)
-    key = (id(dist.group.WORLD), dev)
-    g = _CAPTURE_GROUPS.get(key)
-    if g is None:
-        g = dist.new_group(backend="nccl", device_id=dev, group_desc="irads_graph_capture")
-        # connect now: a lazily connected communicator would be set up by its first collective,
-        # which here is inside a capture (that fails loudly, it is never silently wrong)
-        g._get_backend(dev).eager_connect_single_device(dev)
-        _CAPTURE_GROUPS[key] = g
+    # the entry holds the default group OBJECT it was made under (an identity check, not its id():
+    # a re-initialised default group can never match an entry of a destroyed one)
+    ent = _CAPTURE_GROUPS.get(dev)
+    if ent is not None and ent[0] is dist.group.WORLD:
+        return ent[1]
+    g = dist.new_group(backend="nccl", device_id=dev, group_desc="irads_graph_capture")
+    # connect now: a lazily connected communicator would be set up by its first collective,
+    # which here is inside a capture (that fails loudly, it is never silently wrong)
+    g._get_backend(dev).eager_connect_single_device(dev)
+    _CAPTURE_GROUPS[dev] = (dist.group.WORLD, g)
     return g
 
 
@@ -109,7 +111,7 @@ def quiesce_process_groups():
     if not dist.is_initialized() or dist.get_backend() != "nccl":
         return
     torch.cuda.synchronize()
-    groups = [dist.group.WORLD] + list(_CAPTURE_GROUPS.values())
+    groups = [dist.group.WORLD] + [g for w, g in _CAPTURE_GROUPS.values() if w is dist.group.WORLD]
     for g in groups:
         g._wait_for_pending_works()
 

@@ -34,8 +34,8 @@ SIGNATURES = {
     "irads_dattn_gate_fwd": [_vp] * 4 + [_i] * 3 + [_vp, _vp],
     "irads_dattn_gate_bwd": [_vp] * 5 + [_i] * 3 + [_vp] * 4,
     "irads_sum_rows": [_vp, _i, _l, _vp, _vp],
-    "irads_dattn_mix_fwd": [_vp] * 3 + [_i] * 3 + [_vp, _vp],
-    "irads_dattn_mix_bwd": [_vp] * 4 + [_i] * 3 + [_vp] * 4,
+    "irads_dattn_mix_fwd": [_vp] * 3 + [_i] * 3 + [_vp] * 3,
+    "irads_dattn_mix_bwd": [_vp] * 5 + [_i] * 3 + [_vp] * 4,
     "irads_dattn_attn_fwd": [_vp] * 8 + [_i] * 9 + [_f, _vp, _vp, _vp],
     "irads_dattn_attn_bwd": [_vp] * 8 + [_i] * 9 + [_f] + [_vp] * 10 + [_vp],
     "irads_dattn_attn_bwd_ws": [_vp] * 8 + [_i] * 9 + [_f] + [_vp] * 10 + [_vp, _l, _vp],
@@ -93,7 +93,9 @@ QUERIES = {"irads_wgrad_workspace": (ctypes.c_long, [_i, _i, _i]),
            "irads_msda_bwd_workspace_bytes": (ctypes.c_long, [_i, _i, _i, _i, _i, _i, _i, _i]),
            "irads_resize_bwd_cl_fits": (ctypes.c_int, [_i, _i, _i]),
            "irads_dattn_attn_bwd_workspace_bytes": (ctypes.c_long, [_i] * 9),
-           "irads_dattn_sample_bwd_workspace_bytes": (ctypes.c_long, [_i] * 5)}
+           "irads_dattn_sample_bwd_workspace_bytes": (ctypes.c_long, [_i] * 5),
+           "irads_stamp_next": (None, [_vp]),
+           "irads_wall_clock_khz": (ctypes.c_int, [])}
 CE_WORKSPACE = 8192
 
 _lib = None

@@ -97,6 +97,78 @@ class LaunchTimer:
 TIMER = LaunchTimer()
 
 
+class StepStamps:
+    """In-step kernel spans from in-kernel wall-clock stamps (irads_stamp_next, include/irads.h).
+
+    While armed for a kernel name, each of its launch entries gets its own region of STAMP_CAP
+    (start, end) pairs, which its workgroups fill with their entry / exit clocks on the device's
+    constant-rate wall clock; the launch's span is the first start to the last end.  The region
+    pointer is a kernel argument, so a captured graph keeps it: after `reset()` one replay of the
+    graph refills every region with that replay's clocks — the kernels' durations inside the real
+    step, beside the other streams' work (what rocprofv3's kernel trace reports), with no events and
+    no eager re-run.  bench.py reads its roofline lines here."""
+
+    CAPACITY = 96       # stamped launches (the C2 step has 24 + 24 window-attention, 4 + 4 DAttn)
+    STAMP_CAP = 16384   # workgroups per region (IRADS_STAMP_CAP)
+
+    def __init__(self):
+        self.armed = set()
+        self.buf = None
+        self.slots = []  # (name, algorithmic bytes, flops, real-token bytes)
+
+    def arm(self, names, device):
+        if self.buf is None or self.buf.device != torch.device(device):
+            self.buf = torch.zeros((self.CAPACITY, self.STAMP_CAP, 2), device=device, dtype=torch.int64)
+        self.slots = []
+        self.armed = set(names)
+        self.reset()
+
+    def disarm(self):
+        self.armed = set()
+
+    def reset(self):
+        if self.buf is not None:
+            self.buf.zero_()
+
+    def take(self, name, nbytes, flops, real_bytes=None):
+        """Arm the next stamped launch entry of this thread for `name` (call right before it)."""
+        if name not in self.armed or len(self.slots) >= self.CAPACITY:
+            return
+        i = len(self.slots)
+        self.slots.append((name, nbytes, flops, nbytes if real_bytes is None else real_bytes))
+        N.load().irads_stamp_next(ctypes.c_void_p(self.buf[i].data_ptr()))
+
+    def read(self):
+        """{name: {"launches", "total_ms", "bytes", "flops", "real_bytes", "spans_ms"}} of the filled slots."""
+        torch.cuda.synchronize()
+        if not self.slots:
+            return {}
+        khz = N.load().irads_wall_clock_khz()
+        if khz <= 0:
+            raise RuntimeError("irads_wall_clock_khz: device wall-clock rate unavailable")
+        reg = self.buf[:len(self.slots)]
+        st = reg[..., 0]
+        first = torch.where(st > 0, st, torch.full_like(st, torch.iinfo(torch.int64).max)).amin(1)
+        last = reg[..., 1].amax(1)
+        out = {}
+        for (name, nb, fl, rb), s, e in zip(self.slots, first.cpu().tolist(), last.cpu().tolist()):
+            if e <= 0 or e <= s:  # not launched in the replay (or not stamped)
+                continue
+            d = out.setdefault(name, {"launches": 0, "total_ms": 0.0, "bytes": 0, "flops": 0, "real_bytes": 0,
+                                      "spans_ms": []})
+            ms = (e - s) / khz
+            d["launches"] += 1
+            d["total_ms"] += ms
+            d["bytes"] += nb
+            d["flops"] += fl
+            d["real_bytes"] += rb
+            d["spans_ms"].append(ms)
+        return out
+
+
+STAMPS = StepStamps()
+
+
 # ------------------------------------------------------------------ window attention
 def _winattn_geometry(H, W):
     Hp, Wp = -(-H // WINDOW) * WINDOW, -(-W // WINDOW) * WINDOW
@@ -147,18 +219,19 @@ def winattn_fwd(qkv, bias_f, table_f, mask_f, H, W, num_heads, shift, scale, tab
     Hp, Wp, nW = _winattn_geometry(H, W)
     lse = torch.empty((B * nW * num_heads * WINDOW * WINDOW,), device=qkv.device, dtype=torch.float32)
     quads = bias_quads(table_f, num_heads, scale, table_owner) if code == N.BF16 else None
+    # algorithmic work (SURVEY §8(d)): read q, k, v and write o for every PADDED token
+    # (8·Np·C bytes in bf16); 4·N²·32 flops per (window, head).  Real-token bytes kept too.
+    es = qkv.element_size()
+    nbytes, flops = B * Hp * Wp * 4 * C * es, 4 * (WINDOW * WINDOW) ** 2 * HEAD_DIM * B * nW * num_heads
     ev = TIMER.start("winattn_fwd")
     reps = TIMER.launches("winattn_fwd")  # idempotent: out and lse are overwritten
 
     def launch():
         N.call("irads_winattn_fwd", code, N.ptr(qkv), N.ptr(bias_f), N.ptr(table_f), N.ptr(quads), N.ptr(mask_f),
                n_mask, B, H, W, C, num_heads, shift, float(scale), N.ptr(out), N.ptr(lse), N.stream())
+    STAMPS.take("winattn_fwd", nbytes, flops, B * L * 4 * C * es)
     for _ in range(reps):
         launch()
-    # algorithmic work (SURVEY §8(d)): read q, k, v and write o for every PADDED token
-    # (8·Np·C bytes in bf16); 4·N²·32 flops per (window, head).  Real-token bytes kept too.
-    es = qkv.element_size()
-    nbytes, flops = B * Hp * Wp * 4 * C * es, 4 * (WINDOW * WINDOW) ** 2 * HEAD_DIM * B * nW * num_heads
     TIMER.stop("winattn_fwd", ev, nbytes, flops, B * L * 4 * C * es, reps)
     TIMER.keep_launch("winattn_fwd", launch, nbytes, flops)
     return out, lse
@@ -176,6 +249,11 @@ def winattn_bwd(qkv, bias_f, table_f, mask_f, H, W, nH, shift, scale, out, lse, 
     gtable = torch.zeros_like(table_f) if need_table else None
     gbias = torch.zeros((3 * C,), device=qkv.device, dtype=torch.float32) if need_bias else None
     quads = bias_quads(table_f, nH, scale, table_owner) if code == N.BF16 else None
+    # algorithmic (SURVEY §8(d)): read q, k, v, o, dO and write dq, dk, dv per padded token;
+    # 8·N²·32 flops per (window, head)
+    Hp, Wp, nW = _winattn_geometry(H, W)
+    es = qkv.element_size()
+    nbytes, flops = B * Hp * Wp * 8 * C * es, 8 * (WINDOW * WINDOW) ** 2 * HEAD_DIM * B * nW * nH
     ev = TIMER.start("winattn_bwd")
     # idempotent unless the table / pad-bias gradients are accumulated
     reps = 1 if (need_bias or need_table) else TIMER.launches("winattn_bwd")
@@ -184,13 +262,9 @@ def winattn_bwd(qkv, bias_f, table_f, mask_f, H, W, nH, shift, scale, out, lse, 
         N.call("irads_winattn_bwd", code, N.ptr(qkv), N.ptr(bias_f), N.ptr(table_f), N.ptr(quads), N.ptr(mask_f),
                n_mask, B, H, W, C, nH, shift, float(scale), N.ptr(out), N.ptr(lse), N.ptr(gout), N.ptr(gqkv),
                N.ptr(gtable), N.ptr(gbias), N.stream())
+    STAMPS.take("winattn_bwd", nbytes, flops)
     for _ in range(reps):
         launch()
-    # algorithmic (SURVEY §8(d)): read q, k, v, o, dO and write dq, dk, dv per padded token;
-    # 8·N²·32 flops per (window, head)
-    Hp, Wp, nW = _winattn_geometry(H, W)
-    es = qkv.element_size()
-    nbytes, flops = B * Hp * Wp * 8 * C * es, 8 * (WINDOW * WINDOW) ** 2 * HEAD_DIM * B * nW * nH
     TIMER.stop("winattn_bwd", ev, nbytes, flops, B * L * 8 * C * es, reps)
     if not (need_bias or need_table):
         TIMER.keep_launch("winattn_bwd", launch, nbytes, flops)
@@ -368,26 +442,37 @@ def dattn_mix_ok(xs, ys, w):
 class DAttnMixFn(torch.autograd.Function):
     """sampled = xs·w[..., 0] + ys·w[..., 1] (swin.py:946-949), returned as the token-major bf16
     operand (B, 2n, C) of proj_k / proj_v (what the transpose and autocast's cast would make of it),
-    in one pass each way (irads_dattn_mix_fwd/bwd)."""
+    in one pass each way (irads_dattn_mix_fwd/bwd).  Two outputs with the same values, one per
+    consumer: autograd then hands the backward proj_k's and proj_v's bf16 input gradients
+    separately, and the kernel adds them in fp32 — the reference's arithmetic, where `sampled` is
+    fp32 and each autocast cast's backward returns its consumer's gradient to fp32 before the add
+    (one shared bf16 output would have autograd add them in bf16, an extra rounding)."""
 
     @staticmethod
     def forward(ctx, xs, ys, w):
         B, C, n2 = xs.shape
         w = w.contiguous()
         out = torch.empty((B, n2, C), device=xs.device, dtype=torch.bfloat16)
-        N.call("irads_dattn_mix_fwd", N.ptr(xs), N.ptr(ys), N.ptr(w), B, C, n2, N.ptr(out), N.stream())
+        out2 = torch.empty_like(out)
+        N.call("irads_dattn_mix_fwd", N.ptr(xs), N.ptr(ys), N.ptr(w), B, C, n2, N.ptr(out), N.ptr(out2), N.stream())
         ctx.save_for_backward(xs, ys, w)
-        return out
+        return out, out2
 
     @staticmethod
-    def backward(ctx, g):
+    def backward(ctx, g, g2):
         xs, ys, w = ctx.saved_tensors
         B, C, n2 = xs.shape
+        if g is None:
+            g, g2 = g2, None
+        if g is None:
+            return None, None, None
         g = g.to(torch.bfloat16).contiguous()
+        if g2 is not None:
+            g2 = g2.to(torch.bfloat16).contiguous()
         gxs, gys = torch.empty_like(xs), torch.empty_like(ys)
         gw = torch.empty_like(w)
-        N.call("irads_dattn_mix_bwd", N.ptr(g), N.ptr(xs), N.ptr(ys), N.ptr(w), B, C, n2, N.ptr(gxs), N.ptr(gys),
-               N.ptr(gw), N.stream())
+        N.call("irads_dattn_mix_bwd", N.ptr(g), N.ptr(g2), N.ptr(xs), N.ptr(ys), N.ptr(w), B, C, n2, N.ptr(gxs),
+               N.ptr(gys), N.ptr(gw), N.stream())
         return gxs, gys, gw
 
 
@@ -550,14 +635,15 @@ class DAttnAttentionFn(torch.autograd.Function):
         Ht, Wt = rpe_table.shape[1], rpe_table.shape[2]
         out = torch.empty_like(ts[0])
         lse = torch.empty((B * n_heads, H * W), device=q.device, dtype=torch.float32)
-        ev = TIMER.start("dattn_fwd")
-        N.call("irads_dattn_attn_fwd", *[N.ptr(t) for t in ts], B, n_heads, groups, hc, H, W, n, Ht, Wt,
-               float(scale), N.ptr(out), N.ptr(lse), N.stream())
         # algorithmic work: B·h·HW·2n (query, key) pairs at 44 FLOP each (4·hc for
         # q·k and p·v with hc = 8, plus 12 for the bilinear rpe bias); bytes: q, out, k, v, pos, table
         pairs = B * n_heads * H * W * 2 * n
-        TIMER.stop("dattn_fwd", ev, 4 * (2 * q.numel() + 2 * k.numel() + 2 * pos_x.numel() + rpe_table.numel()),
-                   44 * pairs)
+        nbytes = 4 * (2 * q.numel() + 2 * k.numel() + 2 * pos_x.numel() + rpe_table.numel())
+        ev = TIMER.start("dattn_fwd")
+        STAMPS.take("dattn_fwd", nbytes, 44 * pairs)
+        N.call("irads_dattn_attn_fwd", *[N.ptr(t) for t in ts], B, n_heads, groups, hc, H, W, n, Ht, Wt,
+               float(scale), N.ptr(out), N.ptr(lse), N.stream())
+        TIMER.stop("dattn_fwd", ev, nbytes, 44 * pairs)
         ctx.save_for_backward(*ts, out, lse)
         ctx.cfg = (B, n_heads, groups, hc, H, W, n, Ht, Wt, float(scale))
         return out
@@ -575,13 +661,15 @@ class DAttnAttentionFn(torch.autograd.Function):
         gpx, gpy = torch.empty_like(px), torch.empty_like(py)
         ws_bytes = N.load().irads_dattn_attn_bwd_workspace_bytes(B, nH, G, hc, H, W, n, Ht, Wt)
         ws = torch.empty((max(ws_bytes, 4) // 4,), device=q.device, dtype=torch.float32)
+        nbytes = 8 * (2 * q.numel() + 2 * k.numel() + 2 * px.numel() + rpe.numel())
+        flops = 88 * B * nH * H * W * 2 * n  # backward = 2x the forward's 44 FLOP / pair
         ev = TIMER.start("dattn_bwd")
+        STAMPS.take("dattn_bwd", nbytes, flops)
         N.call("irads_dattn_attn_bwd_ws", N.ptr(q), N.ptr(k), N.ptr(v), N.ptr(px), N.ptr(py), N.ptr(rpe), N.ptr(qgy),
                N.ptr(qgx), B, nH, G, hc, H, W, n, Ht, Wt, scale, N.ptr(out), N.ptr(lse), N.ptr(gout), N.ptr(delta),
                N.ptr(gq), N.ptr(gk), N.ptr(gv), N.ptr(grpe), N.ptr(gpx), N.ptr(gpy), N.ptr(ws), ws_bytes,
                N.stream())
-        TIMER.stop("dattn_bwd", ev, 8 * (2 * q.numel() + 2 * k.numel() + 2 * px.numel() + rpe.numel()),
-                   88 * B * nH * H * W * 2 * n)  # backward = 2x the forward's 44 FLOP / pair
+        TIMER.stop("dattn_bwd", ev, nbytes, flops)
         return (gq, gk.transpose(1, 2), gv.transpose(1, 2), gpx, gpy, grpe, None, None, None, None, None, None, None,
                 None)
 

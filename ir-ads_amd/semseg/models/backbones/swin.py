@@ -445,16 +445,16 @@ class DAttentionMM(nn.Module):
             h = F.relu(F.linear(qs.transpose(1, 2), sw[0].weight.flatten(1), sw[0].bias))
             w = F.softmax(F.linear(h, sw[2].weight.flatten(1), sw[2].bias), dim=-1)
         if ops.dattn_mix_ok(xs, ys, w):  # the mix, its transpose and the bf16 cast in one pass each way
-            s_tok = ops.DAttnMixFn.apply(xs, ys, w)  # (B, 2n, C) bf16
+            s_k, s_v = ops.DAttnMixFn.apply(xs, ys, w)  # (B, 2n, C) bf16, one operand per consumer
         else:
             sampled = xs * w[..., 0].unsqueeze(1) + ys * w[..., 1].unsqueeze(1)  # (B, C, 2n) fp32
-            s_tok = sampled.transpose(1, 2)
+            s_k = s_v = sampled.transpose(1, 2)
         nH, hc = self.n_heads, self.n_head_channels
 
-        def key_major(conv_):  # (B, 2n, C) bf16 -> (B*nH, 2n, hc) fp32, viewed as (B*nH, hc, 2n)
+        def key_major(conv_, s_tok):  # (B, 2n, C) bf16 -> (B*nH, 2n, hc) fp32, viewed as (B*nH, hc, 2n)
             t = self._tok_linear(conv_, s_tok).view(B, 2 * n, nH, hc).permute(0, 2, 1, 3)
             return t.to(torch.float32, memory_format=torch.contiguous_format).view(B * nH, 2 * n, hc).transpose(1, 2)
-        k, v = key_major(self.proj_k), key_major(self.proj_v)
+        k, v = key_major(self.proj_k, s_k), key_major(self.proj_v, s_v)
         out = ops.DAttnAttentionFn.apply(q32.view(B * nH, hc, H * W), k, v, pos_x, pos_y, self.rpe_table.float(),
                                          gy, gx, B, nH, g, H, W, self.scale)
         out_tok = self._tok_linear(self.proj_out, out.view(B, C, H * W).transpose(1, 2))  # (B, HW, C) bf16

@@ -24,7 +24,7 @@ def lib():
 
 def declared_symbols():
     txt = open(os.path.join(ROOT, "include", "irads.h")).read()
-    return sorted(set(re.findall(r"^(?:int|long|const char \*)\s*(irads_\w+)\s*\(", txt, re.M)))
+    return sorted(set(re.findall(r"^(?:int|long|void|const char \*)\s*(irads_\w+)\s*\(", txt, re.M)))
 
 
 def test_library_exports_every_declared_symbol(lib):

@@ -276,24 +276,34 @@ def test_dattn_attention_core_many_keys_vs_fp64(Hk, Wk):
 @pytest.mark.parametrize("B,C,n2", [(8, 128, 512), (8, 64, 512), (3, 16, 74)])
 def test_dattn_modality_mix_fused(B, C, n2):
     """DAttnMixFn (irads_dattn_mix_fwd/bwd): the modality mix of swin.py:946-949 with the transpose and
-    bf16 cast of its token-major consumers.  Forward bit-identical to the torch expression (fp32 products
-    and sum, then the cast); grad_xs / grad_ys bit-identical (one product each); grad_w against fp64
-    within 1e-6 relative (a channel sum in another order)."""
+    bf16 cast of its two token-major consumers (proj_k, proj_v).  Forward bit-identical to the torch
+    expression (fp32 products and sum, then the cast) in both outputs.  Backward with TWO consumers,
+    as the model runs it, against the reference's arithmetic: `sampled` fp32, each consumer's bf16
+    gradient cast back to fp32 and added in fp32 (autograd through two separate casts):
+    grad_xs / grad_ys bit-identical (one fp32 add, one product each); grad_w against fp64 within
+    1e-6 relative (a channel sum in another order)."""
     from irads import ops
     torch.manual_seed(C + n2)
     xs = torch.randn(B, C, n2, device=DEV, requires_grad=True)
     ys = torch.randn(B, C, n2, device=DEV, requires_grad=True)
     w = torch.softmax(torch.randn(B, n2, 2, device=DEV), -1).requires_grad_()
     assert ops.dattn_mix_ok(xs, ys, w)
-    out = ops.DAttnMixFn.apply(xs, ys, w)
-    ref = (xs * w[..., 0].unsqueeze(1) + ys * w[..., 1].unsqueeze(1)).transpose(1, 2)
-    assert out.shape == (B, n2, C) and out.dtype == torch.bfloat16 and out.is_contiguous()
-    assert torch.equal(out, ref.to(torch.bfloat16))
-    g = torch.randn(B, n2, C, device=DEV).bfloat16()
-    gx, gy, gw = torch.autograd.grad(out, (xs, ys, w), g)
-    rx, ry, rw = torch.autograd.grad(ref, (xs, ys, w), g.float())
+    out_k, out_v = ops.DAttnMixFn.apply(xs, ys, w)
+    sampled = (xs * w[..., 0].unsqueeze(1) + ys * w[..., 1].unsqueeze(1)).transpose(1, 2)
+    ref_k, ref_v = sampled.to(torch.bfloat16), sampled.to(torch.bfloat16)
+    for out in (out_k, out_v):
+        assert out.shape == (B, n2, C) and out.dtype == torch.bfloat16 and out.is_contiguous()
+        assert torch.equal(out, ref_k)
+    gk = torch.randn(B, n2, C, device=DEV).bfloat16()
+    gv = torch.randn(B, n2, C, device=DEV).bfloat16()
+    gx, gy, gw = torch.autograd.grad((out_k, out_v), (xs, ys, w), (gk, gv))
+    rx, ry, rw = torch.autograd.grad((ref_k, ref_v), (xs, ys, w), (gk, gv))
     assert torch.equal(gx, rx) and torch.equal(gy, ry)
-    gf = g.double().transpose(1, 2)
+    gf = (gk.double() + gv.double()).transpose(1, 2)
     exact = torch.stack([(gf * xs.double()).sum(1), (gf * ys.double()).sum(1)], -1)
     assert ((gw.double() - exact).norm() / exact.norm()).item() < 1e-6
     assert ((rw.double() - exact).norm() / exact.norm()).item() < 1e-6
+    # one consumer only (the other output unused): the single gradient, no add
+    out_k, _ = ops.DAttnMixFn.apply(xs, ys, w)
+    gx1, = torch.autograd.grad(out_k, (xs,), gk)
+    assert torch.equal(gx1, gk.float().transpose(1, 2) * w[..., 0].unsqueeze(1))

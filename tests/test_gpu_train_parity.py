@@ -544,6 +544,21 @@ def _check_dmpg_blocks_bf16(model, cap, report, fails):
     report["eager.dmpg_block_level_bf16_worst_frac_of_tol"] = worst
 
 
+def _count_gemm_nt_calls(monkeypatch):
+    """Count irads_gemm_nt_variant launches per (epilogue, variant) through the native entry."""
+    import collections
+    from irads import native as N
+    counts = collections.Counter()
+    orig = N.call
+
+    def call(name, *args):
+        if name == "irads_gemm_nt_variant":
+            counts[(int(args[1]), int(args[0]))] += 1
+        return orig(name, *args)
+    monkeypatch.setattr(N, "call", call)
+    return counts
+
+
 def _check_ratio_to_noise(report, fails, bound=5.0):
     """Per-tensor bf16 error over the bf16 noise of the reference's arithmetic.  ref16 is ONE
     realisation of the reference's bf16 error; for a tensor that is effectively one scalar (the
@@ -567,16 +582,28 @@ def _check_ratio_to_noise(report, fails, bound=5.0):
                                                "median": float(np.median(list(ratios.values())))}
 
 
-@pytest.mark.parametrize("tag", list(TRAIN_FIXTURES))
-def test_train_step_vs_reference(tag):
+# IRADS_GEMM modes of the bf16 step: "table" (the shipped selection: at B = 2 no (M, N, K) key of the
+# B = 8 / B = 4 table matches, so the trunk runs on hipBLASLt), "all" (every trunk projection the
+# kernel takes on irads_gemm_nt's 128 x 128 tiling, fused GELU / GELU' epilogues included) and
+# "all4" (the 256 x 256 tiling wherever N % 256 == 0: the tiling the table ships for the FFN pairs)
+GEMM_MODES = [(t, "table") for t in TRAIN_FIXTURES] + [(t, "all") for t in TRAIN_FIXTURES] + [("c2_swinb_512", "all4")]
+
+
+@pytest.mark.parametrize("tag,gemm", GEMM_MODES)
+def test_train_step_vs_reference(tag, gemm, monkeypatch):
     from semseg.losses import get_loss
+    from irads import gemm as G
     from irads import swin_fused  # noqa: F401  (the fused stage must be the path that runs)
     own32, _ = _fp32(tag)
+    monkeypatch.setenv("IRADS_GEMM", gemm[:3] if gemm != "table" else "table")
+    if gemm == "all4":
+        monkeypatch.setenv("IRADS_GEMM_VARIANT", "4")
+    launched = _count_gemm_nt_calls(monkeypatch)
     fx, fx64 = Fixture(f"train_{tag}.npz"), Fixture(f"train_{tag}_fp64.npz")
     model, batch = _build(fx)
     loss_fn = get_loss("CrossEntropy", 255)
     aux = _ref_mask(fx, batch[2])
-    report, fails = {"tag": tag, "mode": "bf16"}, []
+    report, fails = {"tag": tag, "mode": "bf16", "gemm": gemm}, []
 
     def logit_tol(name):
         return max(1e-2, 2 * float(fx[f"bf16_{name}_rel_l2"]))
@@ -634,8 +661,13 @@ def test_train_step_vs_reference(tag):
     report["eager_own_mmst.loss_rel"] = abs(float(l_own.detach()) - float(fx["loss"][0])) / abs(float(fx["loss"][0]))
     if not (report["eager_own_mmst.loss_rel"] <= 1e-2):
         fails.append(f"own MMST loss relative error {report['eager_own_mmst.loss_rel']:.3e}")
+    report["irads_gemm_nt_launches"] = {f"epilogue{e}_variant{v}": n for (e, v), n in launched.items()}
+    if gemm != "table":  # the mode must really have put the trunk on the kernel, every epilogue
+        need = {(0, 2 if gemm == "all" else 4), (1, 2 if gemm == "all" else 4), (2, 2 if gemm == "all" else 4)}
+        if not need <= set(launched):
+            fails.append(f"IRADS_GEMM={gemm}: irads_gemm_nt (epilogue, variant) launches {dict(launched)}")
     report["fails"] = fails
-    _write_report(f"train_{tag}_bf16", report)
+    _write_report(f"train_{tag}_bf16" + ("" if gemm == "table" else "_gemm_" + gemm), report)
     print(tag, {k: (round(v, 6) if isinstance(v, float) else v) for k, v in report.items()
                 if not k.endswith("per_tensor")})
     assert not fails, fails
