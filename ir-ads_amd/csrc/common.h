@@ -120,26 +120,37 @@ __device__ __forceinline__ float wave_sum(float v) {
 // min(start) .. max(end) = the launch's span inside the step.  Plain vector stores, one lane per
 // workgroup, no shared address (a single min/max atomic address serialised every workgroup across
 // the 8 XCDs: ~14 ns each, doubling the window-attention forward).  A null region (every launch but
-// the stamped ones) is a uniform branch.  stamp_end has a workgroup barrier: call it where every
-// thread arrives.
+// the stamped ones) is a uniform branch.
 constexpr unsigned STAMP_CAP = IRADS_STAMP_CAP;
+// The entry clock is READ at entry (stamp_clock: a scalar clock read, no memory write) and written
+// with the exit clock at the end: a global store at entry would count as clobbering every later
+// load, so the compiler would stop fetching the kernels' wave-uniform data through scalar loads
+// (measured: DAttn forward 54 -> 130 VGPRs, 7 -> 3 waves per SIMD).
 __device__ __forceinline__ unsigned stamp_wg() { return blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z); }
-__device__ __forceinline__ void stamp_begin(unsigned long long *s) {
+__device__ __forceinline__ unsigned long long stamp_clock(const unsigned long long *s) {
+    return s ? (unsigned long long)wall_clock64() : 0ull;
+}
+__device__ __forceinline__ void stamp_write(unsigned long long *s, unsigned long long t0, bool with_end) {
     if (s && threadIdx.x == 0) {
         const unsigned w = stamp_wg();
-        if (w < STAMP_CAP) s[2 * w] = (unsigned long long)wall_clock64();
+        if (w < STAMP_CAP) {
+            s[2 * w] = t0;
+            if (with_end) s[2 * w + 1] = (unsigned long long)wall_clock64();
+        }
     }
 }
-__device__ __forceinline__ void stamp_end_lane0(unsigned long long *s) {  // no barrier: one-pass kernels
+// exit stamp after a workgroup barrier: call it where every thread arrives
+__device__ __forceinline__ void stamp_end(unsigned long long *s, unsigned long long t0) {
+    if (s) {
+        __syncthreads();
+        stamp_write(s, t0, true);
+    }
+}
+// exit clock only, lane 0 of the workgroup, no barrier (one-pass kernels ending a stamped entry)
+__device__ __forceinline__ void stamp_end_lane0(unsigned long long *s) {
     if (s && threadIdx.x == 0) {
         const unsigned w = stamp_wg();
         if (w < STAMP_CAP) s[2 * w + 1] = (unsigned long long)wall_clock64();
-    }
-}
-__device__ __forceinline__ void stamp_end(unsigned long long *s) {
-    if (s) {
-        __syncthreads();
-        stamp_end_lane0(s);
     }
 }
 

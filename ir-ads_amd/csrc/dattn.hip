@@ -333,7 +333,6 @@ struct AttnArgs {
     const float *q, *k, *v, *px, *py, *rpe, *qgy, *qgx;
     int B, nH, G, hc, H, W, n, Ht, Wt;
     float scale;
-    unsigned long long *stamp;  // irads_stamp_next's slot for this entry's launches, or null
 };
 
 // ---------------------------------------------------------------- shared pieces
@@ -358,7 +357,10 @@ struct BiasPk {
     f2 t0, t1;    // taps (nw, ne), (sw, se)
     float v;
 };
-__device__ __forceinline__ BiasPk rpe_bias_pk(const float *tab, int Ht, int Wt, f2 qg, f2 pk, f2 sc) {
+// tab holds table rows from t_lo on (a band, or the whole padded table with t_lo = 0); the corner
+// row is clamped into [ylo, yhi] (the band's rows whose +1 tap row is staged too).
+__device__ __forceinline__ BiasPk rpe_bias_pk(const float *tab, int Wt, int ylo, int yhi, int t_lo, f2 qg, f2 pk,
+                                              f2 sc) {
     BiasPk b;
     const f2 d = (qg - pk) * (f2){0.5f, 0.5f};
     const f2 ii = (d + (f2){1.f, 1.f}) * sc;
@@ -367,12 +369,12 @@ __device__ __forceinline__ BiasPk rpe_bias_pk(const float *tab, int Ht, int Wt, 
     // positions are clamped to [-1, 1] by DAttentionMM (swin.py:905-906) and the query grid
     // lies in [-1, 1], so the corner is on the table; the clamp only guards the addresses
     // (branch-free: the four keys of an unrolled step schedule together)
-    const int x0 = min(max((int)fl.x, 0), Wt - 1), y0 = min(max((int)fl.y, 0), Ht - 1), TP = Wt + 1;
+    const int x0 = min(max((int)fl.x, 0), Wt - 1), y0 = min(max((int)fl.y, ylo), yhi), TP = Wt + 1;
     const f2 om = (f2){1.f, 1.f} - b.fr;
     const f2 wx = {om.x, b.fr.x};
     b.wt = wx * (f2){om.y, om.y};
     b.wb = wx * (f2){b.fr.y, b.fr.y};
-    b.o = y0 * TP + x0;
+    b.o = (y0 - t_lo) * TP + x0;
     b.t0 = (f2){tab[b.o], tab[b.o + 1]};
     b.t1 = (f2){tab[b.o + TP], tab[b.o + TP + 1]};
     const f2 v = pk_fma(b.t1, b.wb, b.t0 * b.wt);
@@ -460,21 +462,51 @@ __device__ __forceinline__ f2 key_pos(const KeyRef &r, int n, int j) {
 // four keys per step, and the KSP partial states of a query are merged through LDS.
 __device__ __forceinline__ int uniform_int(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
+// Table rows a contiguous query range [qa, qb) can reach: floor((0.5·(qgy − py) + 1)·(Ht−1)/2) for
+// qgy in the range and py in [−1, 1], plus the +1 tap row (the forward, pass Q and pass K stage only
+// this band).
+__device__ __forceinline__ void band_rows(const float *__restrict__ qgy, int W, int Ht, float scy, int qa, int qb,
+                                          int nr_max, int &t_lo, int &nr) {
+    const float ya = qgy[qa / W], yb = qgy[(qb - 1) / W];
+    const float ylo = fminf(ya, yb), yhi = fmaxf(ya, yb);
+    const float lo = (0.5f * (ylo - 1.f) + 1.f) * scy, hi = (0.5f * (yhi + 1.f) + 1.f) * scy;
+    t_lo = max(0, (int)floorf(lo) - 1);
+    const int t_hi = min(Ht, (int)floorf(hi) + 2);  // y0 + 1 at most; row Ht is the zero pad row
+    nr = min(nr_max, t_hi - t_lo + 1);
+}
+
+__device__ __forceinline__ void load_table_band(float *tab, const float *__restrict__ src, int Ht, int Wt, int t_lo,
+                                                int nr) {
+    load_table_rows(tab, src, Ht, Wt, t_lo, nr);
+}
+
 // ---------------------------------------------------------------- backward, pass Q
 // dq (key splits add into the zero-filled gq with float atomics, one per query channel and
 // split), delta = dO·O, and the rpe-table gradient.  The table gradient is accumulated per
 // workgroup in LDS in FIXED POINT with integer atomics (on gfx950 ds_add_f32 retires ~0.3
-// lanes/clk/CU whatever the address pattern, ds_add_u32 ~4: scripts/microbench/lds_atomic.hip);
+// lanes/clk/CU whatever the address pattern, ds_add_u32 ~4, ds_add_u64 ~1.8 at this kernel's
+// ~0.6 cells per lane: scripts/microbench/lds_atomic.hip, profiles/r05_lds_atomic.log);
 // a wave's lanes are consecutive queries of one key, so their four taps are neighbouring
 // cells.  The scale is a power of two chosen from a bound on the workgroup's total
 // contribution: Σ_k |ds_qk| = Σ_k p_qk |dp_qk − δ_q| ≤ |δ_q| + Σ_c |dO_qc| · max_k |v_kc|, and
-// the four bilinear weights of a sample sum to 1, so no cell exceeds B = Σ_q bound_q;
-// scale = 2^(30 − ⌈log2 B⌉) keeps every partial sum inside int32 (resolution B·2^-31; fp32
-// accumulation of the same sums carries 2^-24 relative error).  The workgroup flushes its
+// the four bilinear weights of a sample sum to 1, so no cell exceeds B = Σ_q bound_q.
+//   W64 (the product's shapes): 48-bit fixed point in 64-bit cells, scale 2^(46 − ⌈log2 B⌉),
+//     resolution B·2^-47 — exact to far below fp32's 2^-24 (the bound is loose by ~9x, which in 32
+//     bits left B·2^-31 steps per term and 3-5e-4 relative error in the table gradient).  Each
+//     tap converts with ONE fp64 fma against a magic constant (no float -> int64 instruction
+//     exists: the compiler's emulation cost ~11 VALU per tap, +44 % pass-Q time); the cells add
+//     with ds_add_u64.  The 64-bit cells need 12 B per table cell (fp32 table + int64 gradient), so
+//     only the BAND of rows the workgroup's contiguous query range reaches is staged (band_rows,
+//     as the forward): <= 81 of 120 rows at every C1-C5 stage;
+//   !W64 (bands too tall for 160 KB of LDS: tiny feature maps): the whole table, 32-bit cells,
+//     scale 2^(30 − ⌈log2 B⌉).
+// The workgroup writes its cells (in-band; zero elsewhere) to its partial table, or flushes its
 // non-zero cells with one float atomic each.
-// LDS: table[pad] (float) | tgi[pad] (int)
-template <int HC>
-__global__ void __launch_bounds__(1024) dattn_attn_bwd_q_kernel(AttnArgs a, int KSP, const float *__restrict__ kg,
+// LDS: W64: table band [nr_max][Wt+1] (float) | gradient band [nr_max][Wt+1] (int64)
+//      !W64: table[pad] (float) | tgi[pad] (int)
+template <int HC, bool W64>
+__global__ void __launch_bounds__(1024) dattn_attn_bwd_q_kernel(AttnArgs a, int KSP, int nr_max,
+                                                                const float *__restrict__ kg,
                                                                 const float *__restrict__ vg,
                                                                 const float *__restrict__ pxg,
                                                                 const float *__restrict__ pyg,
@@ -483,21 +515,46 @@ __global__ void __launch_bounds__(1024) dattn_attn_bwd_q_kernel(AttnArgs a, int 
                                                                 const float *__restrict__ gout,
                                                                 float *__restrict__ delta, float *__restrict__ gq,
                                                                 float *__restrict__ grpe, float *__restrict__ dq_part,
-                                                                float *__restrict__ rpe_part) {
-    stamp_begin(a.stamp);  // the entry's span ends in its last kernel (kpart reduce)
+                                                                float *__restrict__ rpe_part,
+                                                                unsigned long long *__restrict__ stamp) {
+    const unsigned long long t_entry = stamp_clock(stamp);  // the entry's span ends in its last kernel
     extern __shared__ __attribute__((aligned(16))) float sm[];
     __shared__ float red[16], vmx[16][HC];
-    const int n2 = 2 * a.n, HW = a.H * a.W, PC = pad_cells(a.Ht, a.Wt);
-    float *tab = sm;
-    int *tgi = reinterpret_cast<int *>(sm + PC);
+    const int n2 = 2 * a.n, HW = a.H * a.W, PC = pad_cells(a.Ht, a.Wt), TP = a.Wt + 1;
     const int bh = blockIdx.y, b = bh / a.nH, h = bh % a.nH;
     const int gi = h / (a.nH / a.G);
-    load_table_padded(tab, a.rpe + (long)h * a.Ht * a.Wt, a.Ht, a.Wt);
-    for (int i = threadIdx.x; i < PC; i += blockDim.x) tgi[i] = 0;
+    const f2 sc = {((float)a.Wt - 1.0f) / 2.0f, ((float)a.Ht - 1.0f) / 2.0f};
+    float *tab = sm;
+    int *tgi = reinterpret_cast<int *>(sm + PC);
+    // W64: one contiguous query range per workgroup (the grid covers HW exactly once) and its band
+    const int QW16 = 16 / KSP;
+    const int q_begin = uniform_int(blockIdx.x * QW16 * 64), q_end = uniform_int(min(HW, q_begin + QW16 * 64));
+    int t_lo = 0, nr = a.Ht + 1;
+    const int BC = ((nr_max * TP + 1) & ~1);  // table-band floats (even: the int64 cells follow)
+    unsigned long long *tgl = reinterpret_cast<unsigned long long *>(sm + BC);
+    if (W64) {
+        band_rows(a.qgy, a.W, a.Ht, sc.y, q_begin, q_end, nr_max, t_lo, nr);
+        t_lo = uniform_int(t_lo);
+        nr = uniform_int(nr);
+        load_table_band(tab, a.rpe + (long)h * a.Ht * a.Wt, a.Ht, a.Wt, t_lo, nr);
+        for (int i = threadIdx.x; i < nr * TP; i += blockDim.x) tgl[i] = 0ull;
+    } else {
+        load_table_padded(tab, a.rpe + (long)h * a.Ht * a.Wt, a.Ht, a.Wt);
+        for (int i = threadIdx.x; i < PC; i += blockDim.x) tgi[i] = 0;
+    }
+    const int ylo = W64 ? t_lo : 0, yhi = W64 ? t_lo + nr - 2 : a.Ht - 1;
     const KeyRef kr = key_ref(a, kg, vg, pxg, pyg, bh, b, gi, HC);
     const int wave = uniform_int(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int QW = 16 / KSP, qw = wave % QW, sp = wave / QW;
     const int kb = uniform_int(sp * n2 / KSP), ke = uniform_int((sp + 1) * n2 / KSP);
+    // W64 and less than one table column per query column ((Wt−1)/(W−1) < 2 cells per 2 queries:
+    // stage 0 at 512², 0.62): a wave's lanes take every OTHER query of a 128-query run (wave pair
+    // 2m: even queries, 2m + 1: odd), so in each of the four tap atomics the 64 lanes hit distinct
+    // cells — ds_add_u64 retires 3.2 lanes/clk/CU on distinct addresses, 1.8 when ~40 % of a
+    // wave's lanes share a cell with their neighbour (profiles/r05_lds_atomic.log)
+    const bool ilv = W64 && (QW & 1) == 0 && 2 * (a.W - 1) > (a.Wt - 1);
+    int tq = qw * 64 + lane;
+    if (ilv) tq = (tq & ~127) | ((tq & 63) << 1) | ((tq >> 6) & 1);
     // max_k |v_kc| over this (b, head)'s keys
     float vm[HC];
 #pragma unroll
@@ -520,7 +577,7 @@ __global__ void __launch_bounds__(1024) dattn_attn_bwd_q_kernel(AttnArgs a, int 
     // bound over the queries this workgroup visits (each counted once: split 0's lanes)
     float bound = 0.f;
     for (int q0 = blockIdx.x * QW * 64; q0 < HW; q0 += gridDim.x * QW * 64) {
-        const int qi = q0 + qw * 64 + lane;
+        const int qi = q0 + tq;
         if (sp == 0 && qi < HW) {
             float dl = 0.f, bq = 0.f;
 #pragma unroll
@@ -536,13 +593,17 @@ __global__ void __launch_bounds__(1024) dattn_attn_bwd_q_kernel(AttnArgs a, int 
     const float btot = block_sum_f(bound, red);
     // non-finite bound (inf / NaN upstream gradient): NaN scales, so this workgroup's table
     // partial, and hence the table gradient, comes out NaN instead of finite and wrong
-    const int e = btot > 0.f ? max(-100, min(100, 30 - (int)ceilf(log2f(btot)))) : 0;
+    const int e = btot > 0.f ? max(-100, min(100, (W64 ? 46 : 30) - (int)ceilf(log2f(btot)))) : 0;
     const bool fin = btot <= 3.0e38f;
     const float fxs = fin ? ldexpf(1.f, e) : __builtin_nanf(""), inv_fx = fin ? ldexpf(1.f, -e) : __builtin_nanf("");
-    const f2 sc = {((float)a.Wt - 1.0f) / 2.0f, ((float)a.Ht - 1.0f) / 2.0f};
-    const int TP = a.Wt + 1;
+    // W64 taps: bits(fma(w, ds·2^e, M)) with M = 1.5·2^52 = M's bits + round(w·ds·2^e) exactly (the
+    // sum stays in M's binade, where the fp64 ulp is 1), so ONE fp64 fma per tap is the fixed-point
+    // conversion; the low 48 bits of M's bits are 0, so the low 48 bits of a cell's 64-bit sum are
+    // the sum of the rounded terms (|sum| <= B·2^e <= 2^46, sign-extended from bit 47 at the flush)
+    const double dfx = fin ? ldexp(1.0, e) : __builtin_nan("");
+    constexpr double kMagic = 6755399441055744.0;  // 1.5 * 2^52
     for (int q0 = blockIdx.x * QW * 64; q0 < HW; q0 += gridDim.x * QW * 64) {
-        const int qi = q0 + qw * 64 + lane;
+        const int qi = q0 + tq;
         const bool valid = qi < HW;
         const int qc = valid ? qi : HW - 1;
         const f2 qg = {a.qgx[qc % a.W], a.qgy[qc / a.W]};
@@ -568,7 +629,7 @@ __global__ void __launch_bounds__(1024) dattn_attn_bwd_q_kernel(AttnArgs a, int 
                 d = pk_fma(qv[c], kk[c], d);
                 dp = pk_fma(dov[c], vv[c], dp);
             }
-            const BiasPk bi = rpe_bias_pk(tab, a.Ht, a.Wt, qg, key_pos(kr, a.n, j), sc);
+            const BiasPk bi = rpe_bias_pk(tab, a.Wt, ylo, yhi, t_lo, qg, key_pos(kr, a.n, j), sc);
             const float s = (d.x + d.y) * a.scale + bi.v;
             const float p = __expf(s - ls);
             const float ds = p * ((dp.x + dp.y) - dl) * dsv;
@@ -576,10 +637,19 @@ __global__ void __launch_bounds__(1024) dattn_attn_bwd_q_kernel(AttnArgs a, int 
 #pragma unroll
             for (int c = 0; c < HC / 2; ++c) dq[c] = pk_fma((f2){dss, dss}, kk[c], dq[c]);
             const float dsq = ds * fxs;
-            atomicAdd(&tgi[bi.o], __float2int_rn(bi.wt.x * dsq));
-            atomicAdd(&tgi[bi.o + 1], __float2int_rn(bi.wt.y * dsq));
-            atomicAdd(&tgi[bi.o + TP], __float2int_rn(bi.wb.x * dsq));
-            atomicAdd(&tgi[bi.o + TP + 1], __float2int_rn(bi.wb.y * dsq));
+            if (W64) {  // (a non-finite bound makes garbage bits here: the flush below writes NaN then)
+                const double D = (double)ds * dfx;
+                atomicAdd(&tgl[bi.o], (unsigned long long)__double_as_longlong(fma((double)bi.wt.x, D, kMagic)));
+                atomicAdd(&tgl[bi.o + 1], (unsigned long long)__double_as_longlong(fma((double)bi.wt.y, D, kMagic)));
+                atomicAdd(&tgl[bi.o + TP], (unsigned long long)__double_as_longlong(fma((double)bi.wb.x, D, kMagic)));
+                atomicAdd(&tgl[bi.o + TP + 1],
+                          (unsigned long long)__double_as_longlong(fma((double)bi.wb.y, D, kMagic)));
+            } else {
+                atomicAdd(&tgi[bi.o], __float2int_rn(bi.wt.x * dsq));
+                atomicAdd(&tgi[bi.o + 1], __float2int_rn(bi.wt.y * dsq));
+                atomicAdd(&tgi[bi.o + TP], __float2int_rn(bi.wb.x * dsq));
+                atomicAdd(&tgi[bi.o + TP + 1], __float2int_rn(bi.wb.y * dsq));
+            }
         }
         if (valid) {
             if (KSP > 1 && dq_part) {  // this key split's dq, summed in split order by dattn_qpart_reduce
@@ -606,18 +676,29 @@ __global__ void __launch_bounds__(1024) dattn_attn_bwd_q_kernel(AttnArgs a, int 
         }
     }
     __syncthreads();
+    stamp_write(stamp, t_entry, false);
+    // cell value of table cell (r, c): W64 outside the band is zero
+    auto cell = [&](int r, int c) -> float {
+        if (W64) {
+            const int br = r - t_lo;
+            if (br < 0 || br >= nr) return fin ? 0.f : inv_fx;
+            const long long v = (long long)(tgl[br * TP + c] << 16) >> 16;  // low 48 bits, sign-extended
+            return fin ? (float)((double)v * ldexp(1.0, -e)) : inv_fx;
+        }
+        return (float)tgi[r * TP + c] * inv_fx;
+    };
     if (rpe_part) {  // this workgroup's table gradient, every cell, summed by dattn_rpe_reduce in order
         float *rp = rpe_part + ((long)blockIdx.y * gridDim.x + blockIdx.x) * a.Ht * a.Wt;
         for (int i = threadIdx.x; i < a.Ht * a.Wt; i += blockDim.x) {
             const int r = i / a.Wt, c = i - r * a.Wt;
-            rp[i] = (float)tgi[r * TP + c] * inv_fx;
+            rp[i] = cell(r, c);
         }
         return;
     }
     for (int i = threadIdx.x; i < a.Ht * a.Wt; i += blockDim.x) {
         const int r = i / a.Wt, c = i - r * a.Wt;
-        const int v = tgi[r * TP + c];
-        if (v != 0 || !fin) atomicAdd(&grpe[(long)h * a.Ht * a.Wt + i], (float)v * inv_fx);
+        const float v = cell(r, c);
+        if (v != 0.f || !fin) atomicAdd(&grpe[(long)h * a.Ht * a.Wt + i], v);
     }
 }
 
@@ -675,21 +756,6 @@ constexpr int QCH = 64;
 //    once at the end); the dot products and accumulations use packed fp32.
 // Positions must lie in [−1, 1] and qgy must be the module's query grid (monotone in [−1, 1]):
 // the band is derived from that (include/irads.h); rows are clamped into the band regardless.
-__device__ __forceinline__ void band_rows(const float *__restrict__ qgy, int W, int Ht, float scy, int qa, int qb,
-                                          int nr_max, int &t_lo, int &nr) {
-    const float ya = qgy[qa / W], yb = qgy[(qb - 1) / W];
-    const float ylo = fminf(ya, yb), yhi = fmaxf(ya, yb);
-    const float lo = (0.5f * (ylo - 1.f) + 1.f) * scy, hi = (0.5f * (yhi + 1.f) + 1.f) * scy;
-    t_lo = max(0, (int)floorf(lo) - 1);
-    const int t_hi = min(Ht, (int)floorf(hi) + 2);  // y0 + 1 at most; row Ht is the zero pad row
-    nr = min(nr_max, t_hi - t_lo + 1);
-}
-
-__device__ __forceinline__ void load_table_band(float *tab, const float *__restrict__ src, int Ht, int Wt, int t_lo,
-                                                int nr) {
-    load_table_rows(tab, src, Ht, Wt, t_lo, nr);
-}
-
 template <int HC>
 __global__ void __launch_bounds__(1024) dattn_attn_bwd_k_band_kernel(AttnArgs a, const float *__restrict__ kg,
                                                                      const float *__restrict__ vg,
@@ -882,8 +948,9 @@ __global__ void __launch_bounds__(64 * NWAVE) dattn_attn_fwd_band_kernel(AttnArg
                                                                   const float *__restrict__ vg,
                                                                   const float *__restrict__ pxg,
                                                                   const float *__restrict__ pyg,
-                                                                  float *__restrict__ out, float *__restrict__ lse) {
-    stamp_begin(a.stamp);
+                                                                  float *__restrict__ out, float *__restrict__ lse,
+                                                                  unsigned long long *__restrict__ stamp) {
+    const unsigned long long t_entry = stamp_clock(stamp);
     static_assert(HC % 2 == 0, "packed fp32 needs an even head size");
     extern __shared__ __attribute__((aligned(16))) float sm[];
     const int n2 = 2 * a.n, HW = a.H * a.W, TP = a.Wt + 1;
@@ -990,7 +1057,7 @@ __global__ void __launch_bounds__(64 * NWAVE) dattn_attn_fwd_band_kernel(AttnArg
         }
         lse[(long)bh * HW + qi] = m * kLn2 + logf(l);
     }
-    stamp_end(a.stamp);
+    stamp_end(stamp, t_entry);
 }
 
 // table rows a contiguous range of `nq` queries can reach (see band_rows), for LDS sizing
@@ -1153,7 +1220,8 @@ extern "C" int irads_dattn_attn_fwd(const float *q, const float *k, const float 
                                     const float *pos_y, const float *rpe, const float *qgrid_y, const float *qgrid_x,
                                     int B, int nH, int G, int hc, int H, int W, int n, int Ht, int Wt, float scale,
                                     float *out, float *lse, void *stream) {
-    AttnArgs a{q, k, v, pos_x, pos_y, rpe, qgrid_y, qgrid_x, B, nH, G, hc, H, W, n, Ht, Wt, scale, take_stamp()};
+    unsigned long long *stamp = take_stamp();  // irads_stamp_next's region for this entry, or null
+    AttnArgs a{q, k, v, pos_x, pos_y, rpe, qgrid_y, qgrid_x, B, nH, G, hc, H, W, n, Ht, Wt, scale};
     if (int e = check_attn(a)) return e;
     IRADS_REQUIRE(hc <= 16, "dattn_attn: head channels %d > 16", hc);
     if (B == 0) return IRADS_OK;
@@ -1172,7 +1240,8 @@ extern "C" int irads_dattn_attn_fwd(const float *q, const float *k, const float 
     IRADS_HC_DISPATCH(hc, {
         (void)hipFuncSetAttribute((const void *)dattn_attn_fwd_band_kernel<HC, NWF>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
-        dattn_attn_fwd_band_kernel<HC, NWF><<<grid, 64 * NWF, sh, st>>>(a, ksp, nr_max, k, v, pos_x, pos_y, out, lse);
+        dattn_attn_fwd_band_kernel<HC, NWF><<<grid, 64 * NWF, sh, st>>>(a, ksp, nr_max, k, v, pos_x, pos_y, out, lse,
+                                                                         stamp);
     })
     return check_launch("irads_dattn_attn_fwd");
 }
@@ -1215,17 +1284,25 @@ static int attn_bwd(const float *q, const float *k, const float *v, const float 
                     int W, int n, int Ht, int Wt, float scale, const float *out, const float *lse,
                     const float *grad_out, float *delta, float *grad_q, float *grad_k, float *grad_v, float *grad_rpe,
                     float *grad_pos_x, float *grad_pos_y, char *ws, void *stream) {
-    AttnArgs a{q, k, v, pos_x, pos_y, rpe, qgrid_y, qgrid_x, B, nH, G, hc, H, W, n, Ht, Wt, scale, take_stamp()};
+    unsigned long long *stamp = take_stamp();  // irads_stamp_next's region for this entry, or null
+    AttnArgs a{q, k, v, pos_x, pos_y, rpe, qgrid_y, qgrid_x, B, nH, G, hc, H, W, n, Ht, Wt, scale};
     if (int e = check_attn(a)) return e;
     IRADS_REQUIRE(hc <= 16, "dattn_attn: head channels %d > 16", hc);
     if (B == 0) return IRADS_OK;
     hipStream_t st = (hipStream_t)stream;
     const int HW = H * W;
-    const size_t sh_q = 2 * pad_cells_h(Ht, Wt) * sizeof(float);
-    IRADS_REQUIRE(sh_q <= 160 * 1024, "dattn_attn_bwd: LDS request exceeds 160 KiB");
     int ksp, blocks;
     split_plan(HW, B * nH, ksp, blocks);
     dim3 gq_grid(blocks, B * nH);
+    // pass Q: 64-bit table-gradient cells on the band of its query range where that fits in LDS
+    // beside the pass's static arrays (red, vmx), else 32-bit cells on the whole table
+    const int q_nr_max = band_rows_max(H, W, Ht, (16 / ksp) * 64);
+    const size_t sh_q64 = ((((size_t)q_nr_max * (Wt + 1) + 1) & ~(size_t)1) * sizeof(float) +
+                           (size_t)q_nr_max * (Wt + 1) * sizeof(unsigned long long));
+    const size_t q_static = (16 + 16 * (size_t)hc) * sizeof(float);
+    const bool w64 = sh_q64 + q_static <= 160 * 1024;
+    const size_t sh_q = w64 ? sh_q64 : 2 * pad_cells_h(Ht, Wt) * sizeof(float);
+    IRADS_REQUIRE(sh_q <= 160 * 1024, "dattn_attn_bwd: LDS request exceeds 160 KiB");
     // pass K: one thread per key over a contiguous query range (band_rows bounds its table rows);
     // more than 1024 keys (MSF evaluation scales >= 1.4 at 480x640) take several key blocks
     const int kblocks = (2 * n + 1023) / 1024;
@@ -1241,12 +1318,19 @@ static int attn_bwd(const float *q, const float *k, const float *v, const float 
     float *dq_part = (ws && ksp > 1) ? (float *)(ws + wl.dqpart) : nullptr;
     float *rpe_part = ws ? (float *)(ws + wl.rpepart) : nullptr;
     IRADS_HC_DISPATCH(hc, {
-        (void)hipFuncSetAttribute((const void *)dattn_attn_bwd_q_kernel<HC>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)sh_q);
+        (void)hipFuncSetAttribute(w64 ? (const void *)dattn_attn_bwd_q_kernel<HC, true>
+                                      : (const void *)dattn_attn_bwd_q_kernel<HC, false>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh_q);
         (void)hipFuncSetAttribute((const void *)dattn_attn_bwd_k_band_kernel<HC>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh_kb);
-        dattn_attn_bwd_q_kernel<HC><<<gq_grid, 1024, sh_q, st>>>(a, ksp, k, v, pos_x, pos_y, out, lse, grad_out, delta,
-                                                                 grad_q, grad_rpe, dq_part, rpe_part);
+        if (w64)
+            dattn_attn_bwd_q_kernel<HC, true><<<gq_grid, 1024, sh_q, st>>>(a, ksp, q_nr_max, k, v, pos_x, pos_y, out,
+                                                                           lse, grad_out, delta, grad_q, grad_rpe,
+                                                                           dq_part, rpe_part, stamp);
+        else
+            dattn_attn_bwd_q_kernel<HC, false><<<gq_grid, 1024, sh_q, st>>>(a, ksp, q_nr_max, k, v, pos_x, pos_y, out,
+                                                                            lse, grad_out, delta, grad_q, grad_rpe,
+                                                                            dq_part, rpe_part, stamp);
         if (dq_part) {
             const long per = (long)B * nH * HC * HW;
             dattn_qpart_reduce<<<(unsigned)((per + 255) / 256), 256, 0, st>>>(dq_part, ksp, per, grad_q);
@@ -1262,7 +1346,7 @@ static int attn_bwd(const float *q, const float *k, const float *v, const float 
             const long t = (long)B * G * (2 * HC + 2) * 2 * n;
             dattn_kpart_reduce<HC><<<(unsigned)((t + 255) / 256), 256, 0, st>>>(part, chunks, B, nH, G, n, grad_k,
                                                                                  grad_v, grad_pos_x, grad_pos_y,
-                                                                                 a.stamp);
+                                                                                 stamp);
         }
     })
     return check_launch("irads_dattn_attn_bwd");

@@ -421,7 +421,7 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(MM == 
     __shared__ __attribute__((aligned(16))) unsigned short Ks[NT * HD];  // swizzled 64-B rows (kv_swz)
     __shared__ __attribute__((aligned(16))) unsigned short Vs[NT * HD];
     __shared__ __attribute__((aligned(16))) f32x4 Bq[QB];  // forward quads of this head x c2
-    stamp_begin(g.stamp);
+    const unsigned long long t_entry = stamp_clock(g.stamp);
     const int lid = xcd_remap(blockIdx.x, gridDim.x);      // the heads of one window on one XCD
     const int h = lid % g.nH, bw = lid / g.nH;
     const WinOrigin wo(g, bw);
@@ -566,7 +566,7 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(MM == 
         }
         if (grp == 0) lse[((long)bw * g.nH + h) * NT + qi] = __log2f(os[0]) + shift;  // base-2 LSE of s''
     }
-    stamp_end(g.stamp);
+    stamp_end(g.stamp, t_entry);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -812,7 +812,7 @@ __global__ void __launch_bounds__(576) winattn_bwd_bf16(
     __shared__ int tokS[NT];
     __shared__ __attribute__((aligned(16))) unsigned short padS[3 * HD];  // pad-token q, k, v (bf16)
     __shared__ float tgS[EX ? TBL : 1];  // EX: this workgroup's rel-table gradient, flushed once
-    stamp_begin(g.stamp);
+    const unsigned long long t_entry = stamp_clock(g.stamp);
     const Chunk ck = decode_chunk(g, cw);
     const int h = ck.h;
     const float mneg100 = -100.0f * LOG2E;  // the region mask in s'' units
@@ -1049,7 +1049,7 @@ __global__ void __launch_bounds__(576) winattn_bwd_bf16(
         __syncthreads();
         for (int i = tid; i < TBL; i += 576) atomicAdd(&gtable[i * g.nH + h], tgS[i]);
     }
-    stamp_end(g.stamp);
+    stamp_end(g.stamp, t_entry);
 }
 
 // Forward kernel choice: 0 = one workgroup per (window, head) (winattn_fwd_bf16_rt), 1 = persistent

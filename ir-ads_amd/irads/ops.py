@@ -6,6 +6,7 @@ graph-capturable.  Gradient accumulators that the kernels add into atomically ar
 zero-filled here.  There is no CPU fallback: CPU tensors raise.
 """
 import ctypes
+import os
 
 import weakref
 
@@ -117,6 +118,9 @@ class StepStamps:
         self.slots = []  # (name, algorithmic bytes, flops, real-token bytes)
 
     def arm(self, names, device):
+        if os.environ.get("IRADS_NO_STAMPS"):  # A/B: the same step with no stamp regions captured
+            self.armed, self.slots = set(), []
+            return
         if self.buf is None or self.buf.device != torch.device(device):
             self.buf = torch.zeros((self.CAPACITY, self.STAMP_CAP, 2), device=device, dtype=torch.int64)
         self.slots = []
@@ -127,7 +131,7 @@ class StepStamps:
         self.armed = set()
 
     def reset(self):
-        if self.buf is not None:
+        if self.buf is not None and self.slots:
             self.buf.zero_()
 
     def take(self, name, nbytes, flops, real_bytes=None):

