@@ -479,10 +479,12 @@ def main():
         "loss": round(loss_val, 5),
     }
     step_ms = 1e3 * elapsed / args.steps
-    stamp_timing = ("in-kernel wall-clock stamps (s_memrealtime, first workgroup start to last workgroup end per "
-                    "launch) of one " + ("graph replay" if graph else "eager step") + " after the timed region, "
-                    "identical to the timed steps: the kernels' spans inside the real step, beside the other "
-                    "streams' work (what rocprofv3's kernel trace reports)")
+    stamp_timing = ("in-kernel wall-clock stamps (s_memrealtime) of one " + ("graph replay" if graph else "eager step")
+                    + " after the timed region, identical to the timed steps: per launch, its first workgroup's "
+                    "start to the first workgroup start of the irads_gemm_nt launch that follows it on the stream "
+                    "(the proj GEMM after the forward, the qkv dX GEMM after the backward: the launch's period, "
+                    "= its dispatch-to-completion time as rocprofv3 traces it, end-of-kernel write-back included; "
+                    "`periods` of `launches`), else its own first-start-to-last-end span")
     if fwd:
         avg_ms = fwd["total_ms"] / fwd["launches"]
         per_launch_bytes = fwd["bytes"] / fwd["launches"]
@@ -497,7 +499,8 @@ def main():
                                if traffic_src else None),
             "launches": fwd["launches"], "avg_launch_ms": round(avg_ms, 5),
             "algorithmic_bytes_per_launch": round(per_launch_bytes),
-            "timing": stamp_timing,
+            "timing": stamp_timing, "periods": fwd["periods"],
+            "own_span_avg_ms": round(sum(fwd["own_spans_ms"]) / len(fwd["own_spans_ms"]), 5),
             "span_ms_min_max": [round(min(fwd["spans_ms"]), 5), round(max(fwd["spans_ms"]), 5)],
             "bytes_definition": "SURVEY §8(d): read q,k,v + write o per padded token (8·Np·C bytes, bf16)",
             "achieved_real_tokens_gbs": round(fwd["real_bytes"] / (fwd["total_ms"] * 1e-3) / 1e9, 1),
@@ -509,7 +512,9 @@ def main():
                                       "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ab / HBM_PEAK_GBS, 4),
                                       "launches": bwd["launches"],
                                       "avg_launch_ms": round(bwd["total_ms"] / bwd["launches"], 5),
-                                      "timing": "as roofline",
+                                      "timing": "as roofline", "periods": bwd["periods"],
+                                      "own_span_avg_ms": round(sum(bwd["own_spans_ms"]) / len(bwd["own_spans_ms"]),
+                                                               5),
                                       "share_of_step": round(bwd["total_ms"] / step_ms, 4)}
     for tag in ("fwd", "bwd"):
         d = spans.get(f"dattn_{tag}")

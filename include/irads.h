@@ -34,8 +34,9 @@ extern "C" {
 const char *irads_last_error(void);
 int irads_version(void);
 /* Measurement (bench.py, no reference counterpart): arm `region` (IRADS_STAMP_CAP x 2 uint64,
- * caller-zeroed) for the calling thread's next window-attention or DAttn-core launch entry
- * (irads_winattn_fwd/bwd, irads_dattn_attn_fwd/bwd(_ws)), which takes and disarms it: workgroup w
+ * caller-zeroed) for the calling thread's next window-attention, DAttn-core or irads_gemm_nt launch
+ * entry (irads_winattn_fwd/bwd, irads_dattn_attn_fwd/bwd(_ws), irads_gemm_nt(_variant); the GEMM
+ * writes start clocks only), which takes and disarms it: workgroup w
  * of its kernels (w < IRADS_STAMP_CAP) writes its start / end clock to region[2w] / region[2w+1] on
  * the device wall clock, also from inside a captured graph; the launch's span is min(start) ..
  * max(end).  NULL disarms.  irads_wall_clock_khz: that clock's rate. */

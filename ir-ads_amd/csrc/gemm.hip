@@ -81,6 +81,10 @@ __global__ void __launch_bounds__((BMT / WR) * (BNT / 64) * 64) gemm_nt_bf16(con
     constexpr int G_A_BYTES = BMT * GBK * 2, G_STAGE = G_A_BYTES + BNT * GBK * 2;
     long long *tr = TR ? trace + (long)blockIdx.x * (K / GBK + 3) : nullptr;
     if (TR && threadIdx.x == 0) tr[0] = wall_clock64();
+    // !TR: `trace` is irads_stamp_next's region (or null): this workgroup's entry clock, written at its
+    // exit (bench.py times the window-attention launch before this GEMM up to this GEMM's start)
+    unsigned long long *stamp = TR ? nullptr : (unsigned long long *)trace;
+    const unsigned long long t_entry = stamp_clock(stamp);
     __shared__ __attribute__((aligned(16))) unsigned char smem[NS * G_STAGE];  // ONE array (glds wait trap)
     const int nbn = N / BNT;
     const int lid = xcd_remap(blockIdx.x, gridDim.x);  // the N tiles of an M row-band on one XCD
@@ -228,6 +232,7 @@ __global__ void __launch_bounds__((BMT / WR) * (BNT / 64) * 64) gemm_nt_bf16(con
         __syncthreads();
         if (tid == 0) tr[2 + nk] = wall_clock64();
     }
+    stamp_write(stamp, t_entry, false);
 }
 
 }  // namespace
@@ -253,19 +258,20 @@ static void gemm_launch(const uint16_t *A, long lda, const uint16_t *B, long ldb
 template <int EPI>
 static void gemm_dispatch(int variant, const uint16_t *A, long lda, const uint16_t *B, long ldb, const float *bias,
                           const uint16_t *U, long ldu, uint16_t *C0, uint16_t *C1, long ldc, int M, int N, int K,
-                          hipStream_t st) {
+                          long long *stamp, hipStream_t st) {
     switch (variant) {
-    case 0: gemm_launch<EPI, 0>(A, lda, B, ldb, bias, U, ldu, C0, C1, ldc, M, N, K, nullptr, st); break;
-    case 1: gemm_launch<EPI, 1>(A, lda, B, ldb, bias, U, ldu, C0, C1, ldc, M, N, K, nullptr, st); break;
-    case 2: gemm_launch<EPI, 2>(A, lda, B, ldb, bias, U, ldu, C0, C1, ldc, M, N, K, nullptr, st); break;
-    case 3: gemm_launch<EPI, 3>(A, lda, B, ldb, bias, U, ldu, C0, C1, ldc, M, N, K, nullptr, st); break;
-    default: gemm_launch<EPI, 4>(A, lda, B, ldb, bias, U, ldu, C0, C1, ldc, M, N, K, nullptr, st); break;
+    case 0: gemm_launch<EPI, 0>(A, lda, B, ldb, bias, U, ldu, C0, C1, ldc, M, N, K, stamp, st); break;
+    case 1: gemm_launch<EPI, 1>(A, lda, B, ldb, bias, U, ldu, C0, C1, ldc, M, N, K, stamp, st); break;
+    case 2: gemm_launch<EPI, 2>(A, lda, B, ldb, bias, U, ldu, C0, C1, ldc, M, N, K, stamp, st); break;
+    case 3: gemm_launch<EPI, 3>(A, lda, B, ldb, bias, U, ldu, C0, C1, ldc, M, N, K, stamp, st); break;
+    default: gemm_launch<EPI, 4>(A, lda, B, ldb, bias, U, ldu, C0, C1, ldc, M, N, K, stamp, st); break;
     }
 }
 
 extern "C" int irads_gemm_nt_variant(int variant, int epilogue, const uint16_t *A, long lda, const uint16_t *B,
                                      long ldb, const float *bias, const uint16_t *U, long ldu, uint16_t *C0,
                                      uint16_t *C1, long ldc, int M, int N, int K, void *stream) {
+    long long *stamp = (long long *)take_stamp();  // irads_stamp_next's region for this launch, or null
     IRADS_REQUIRE(epilogue >= 0 && epilogue <= 2, "irads_gemm_nt: epilogue %d", epilogue);
     IRADS_REQUIRE(variant >= 0 && variant <= 4, "irads_gemm_nt: variant %d", variant);
     IRADS_REQUIRE(variant != 4 || N % 256 == 0, "irads_gemm_nt: the 256 x 256 tiling needs N %% 256 == 0 (N=%d)", N);
@@ -280,9 +286,12 @@ extern "C" int irads_gemm_nt_variant(int variant, int epilogue, const uint16_t *
     IRADS_REQUIRE((long)((M + 127) / 128) * (N / GBN) < (1L << 31), "irads_gemm_nt: grid too large");
     if (M == 0) return IRADS_OK;
     hipStream_t st = (hipStream_t)stream;
-    if (epilogue == EPI_BIAS) gemm_dispatch<EPI_BIAS>(variant, A, lda, B, ldb, bias, U, ldu, C0, C1, ldc, M, N, K, st);
-    else if (epilogue == EPI_GELU) gemm_dispatch<EPI_GELU>(variant, A, lda, B, ldb, bias, U, ldu, C0, C1, ldc, M, N, K, st);
-    else gemm_dispatch<EPI_DGELU>(variant, A, lda, B, ldb, bias, U, ldu, C0, C1, ldc, M, N, K, st);
+    if (epilogue == EPI_BIAS)
+        gemm_dispatch<EPI_BIAS>(variant, A, lda, B, ldb, bias, U, ldu, C0, C1, ldc, M, N, K, stamp, st);
+    else if (epilogue == EPI_GELU)
+        gemm_dispatch<EPI_GELU>(variant, A, lda, B, ldb, bias, U, ldu, C0, C1, ldc, M, N, K, stamp, st);
+    else
+        gemm_dispatch<EPI_DGELU>(variant, A, lda, B, ldb, bias, U, ldu, C0, C1, ldc, M, N, K, stamp, st);
     return check_launch("irads_gemm_nt");
 }
 

@@ -25,6 +25,7 @@ import torch
 import torch.nn.functional as F
 
 from . import native as N
+from .stamps import STAMPS
 
 _BF16 = torch.bfloat16
 _TABLE_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned", "irads_gemm_select_mi355x.json")
@@ -96,7 +97,9 @@ def linear(x, lw):
     M, K = x.shape
     N_out = w16.shape[0]
     v = use_irads("fwd", M, N_out, K)
-    if v is not None and x.is_contiguous() and _aligned(x, w16):
+    ok = v is not None and x.is_contiguous() and _aligned(x, w16)
+    STAMPS.follow(ok)
+    if ok:
         return _nt(x, w16, b32, M, N_out, K, v)
     return F.linear(x, w16, b16)
 
@@ -145,6 +148,8 @@ def dgrad(dy, lw):
     M, N_in = dy.shape
     K_out = w16.shape[1]
     v = use_irads("bwd", M, K_out, N_in)
-    if v is not None and dy.is_contiguous() and _aligned(dy, wt):
+    ok = v is not None and dy.is_contiguous() and _aligned(dy, wt)
+    STAMPS.follow(ok)
+    if ok:
         return _nt(dy, wt, None, M, K_out, N_in, v)
     return torch.mm(dy, w16)

@@ -6,7 +6,6 @@ graph-capturable.  Gradient accumulators that the kernels add into atomically ar
 zero-filled here.  There is no CPU fallback: CPU tensors raise.
 """
 import ctypes
-import os
 
 import weakref
 
@@ -98,79 +97,7 @@ class LaunchTimer:
 TIMER = LaunchTimer()
 
 
-class StepStamps:
-    """In-step kernel spans from in-kernel wall-clock stamps (irads_stamp_next, include/irads.h).
-
-    While armed for a kernel name, each of its launch entries gets its own region of STAMP_CAP
-    (start, end) pairs, which its workgroups fill with their entry / exit clocks on the device's
-    constant-rate wall clock; the launch's span is the first start to the last end.  The region
-    pointer is a kernel argument, so a captured graph keeps it: after `reset()` one replay of the
-    graph refills every region with that replay's clocks — the kernels' durations inside the real
-    step, beside the other streams' work (what rocprofv3's kernel trace reports), with no events and
-    no eager re-run.  bench.py reads its roofline lines here."""
-
-    CAPACITY = 96       # stamped launches (the C2 step has 24 + 24 window-attention, 4 + 4 DAttn)
-    STAMP_CAP = 16384   # workgroups per region (IRADS_STAMP_CAP)
-
-    def __init__(self):
-        self.armed = set()
-        self.buf = None
-        self.slots = []  # (name, algorithmic bytes, flops, real-token bytes)
-
-    def arm(self, names, device):
-        if os.environ.get("IRADS_NO_STAMPS"):  # A/B: the same step with no stamp regions captured
-            self.armed, self.slots = set(), []
-            return
-        if self.buf is None or self.buf.device != torch.device(device):
-            self.buf = torch.zeros((self.CAPACITY, self.STAMP_CAP, 2), device=device, dtype=torch.int64)
-        self.slots = []
-        self.armed = set(names)
-        self.reset()
-
-    def disarm(self):
-        self.armed = set()
-
-    def reset(self):
-        if self.buf is not None and self.slots:
-            self.buf.zero_()
-
-    def take(self, name, nbytes, flops, real_bytes=None):
-        """Arm the next stamped launch entry of this thread for `name` (call right before it)."""
-        if name not in self.armed or len(self.slots) >= self.CAPACITY:
-            return
-        i = len(self.slots)
-        self.slots.append((name, nbytes, flops, nbytes if real_bytes is None else real_bytes))
-        N.load().irads_stamp_next(ctypes.c_void_p(self.buf[i].data_ptr()))
-
-    def read(self):
-        """{name: {"launches", "total_ms", "bytes", "flops", "real_bytes", "spans_ms"}} of the filled slots."""
-        torch.cuda.synchronize()
-        if not self.slots:
-            return {}
-        khz = N.load().irads_wall_clock_khz()
-        if khz <= 0:
-            raise RuntimeError("irads_wall_clock_khz: device wall-clock rate unavailable")
-        reg = self.buf[:len(self.slots)]
-        st = reg[..., 0]
-        first = torch.where(st > 0, st, torch.full_like(st, torch.iinfo(torch.int64).max)).amin(1)
-        last = reg[..., 1].amax(1)
-        out = {}
-        for (name, nb, fl, rb), s, e in zip(self.slots, first.cpu().tolist(), last.cpu().tolist()):
-            if e <= 0 or e <= s:  # not launched in the replay (or not stamped)
-                continue
-            d = out.setdefault(name, {"launches": 0, "total_ms": 0.0, "bytes": 0, "flops": 0, "real_bytes": 0,
-                                      "spans_ms": []})
-            ms = (e - s) / khz
-            d["launches"] += 1
-            d["total_ms"] += ms
-            d["bytes"] += nb
-            d["flops"] += fl
-            d["real_bytes"] += rb
-            d["spans_ms"].append(ms)
-        return out
-
-
-STAMPS = StepStamps()
+from .stamps import STAMPS  # noqa: E402  (in-step kernel spans, bench.py)
 
 
 # ------------------------------------------------------------------ window attention

@@ -375,7 +375,7 @@ def test_hot_kernels_use_no_scratch(tmp_path):
     # store at a kernel's entry once moved the DAttn cores' wave-uniform key loads off the scalar
     # path (forward 7 -> 3 waves per SIMD, 0.45 -> 0.76 ms per step)
     floors = {"winattn_fwd_bf16_rtILi0": 5, "winattn_fwd_bf16_rtILi1": 5, "winattn_bwd_bf16ILi0ELb0": 3,
-              "dattn_attn_fwd_band_kernelILi8ELi8": 7, "dattn_attn_bwd_q_kernelILi8": 6,
+              "dattn_attn_fwd_band_kernelILi8ELi8": 7, "dattn_attn_bwd_q_kernelILi8": 4,  # 1024-thread workgroups: 4 per SIMD at most
               "dattn_attn_bwd_k_band_kernelILi8": 6, "gemm_nt_bf16ILi0ELi2ELi128ELi128ELi64": 2}
     for pat, lo in floors.items():
         got = [v for k, v in occ.items() if pat in k]
