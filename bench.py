@@ -307,6 +307,56 @@ def dino_stack_line(device, msda, reps=5):
     return res
 
 
+def dino_detector_line(device, warmup=2, steps=3):
+    """The vCLR DINO-R50 detector's full training step at BASELINE config C5 per GPU (SURVEY §8(f)
+    row 4): 2 images of 800x1333 and 750x1200 (the second padded), 2000 two-stage queries, 100
+    denoising groups' budget, 1 class (deformable_train_voc_eval_nonvoc.py:139-155), 6 synthetic box
+    instances with masks per image.  One step = train_net.run_step: the EMA teacher's no-grad pass
+    on the weak view, the strong view's mix / erase / grayscale, the student's forward + backward
+    with the DINO and consistency criteria (Hungarian matching on the host, scipy), gradient
+    clipping at 0.1, AdamW (backbone lr x 0.1) and the EMA update.  fp32, random init."""
+    from projects.vCLR_deformable_mask import train_net
+    from projects.vCLR_deformable_mask.configs.dino_r50 import build_model
+    torch.manual_seed(0)
+    model = build_model(num_classes=1, num_queries=2000, dn_number=100, device="cuda").to(device).train()
+    updater = train_net.build_ema(model, decay=0.999)
+    bb = [p for n, p in model.named_parameters() if p.requires_grad and n.startswith("backbone")]
+    rest = [p for n, p in model.named_parameters() if p.requires_grad and not n.startswith("backbone")]
+    opt = torch.optim.AdamW([{"params": bb, "lr": 1e-5}, {"params": rest, "lr": 1e-4}], lr=1e-4, betas=(0.9, 0.999),
+                            weight_decay=1e-4)
+    g = torch.Generator(device="cpu").manual_seed(5)
+    batched = []
+    for h, w in ((800, 1333), (750, 1200)):
+        n = 6
+        x0 = (torch.rand(n, generator=g) * 0.6 * w).floor()
+        y0 = (torch.rand(n, generator=g) * 0.6 * h).floor()
+        x1 = torch.minimum(x0 + 32 + (torch.rand(n, generator=g) * 0.35 * w).floor(), torch.tensor(float(w)))
+        y1 = torch.minimum(y0 + 32 + (torch.rand(n, generator=g) * 0.35 * h).floor(), torch.tensor(float(h)))
+        masks = torch.zeros(n, h, w, dtype=torch.bool)
+        for k in range(n):
+            masks[k, int(y0[k]):int(y1[k]), int(x0[k]):int(x1[k])] = True
+        inst = {"image_size": (h, w), "gt_boxes": torch.stack([x0, y0, x1, y1], 1).to(device),
+                "gt_classes": torch.zeros(n, dtype=torch.long, device=device), "gt_masks": masks.to(device)}
+        batched.append({"image": (torch.rand(3, h, w, generator=g) * 255).floor().to(device),
+                        "image_rgb": (torch.rand(3, h, w, generator=g) * 255).floor().to(device), "instances": inst})
+    clip = {"max_norm": 0.1, "norm_type": 2}
+    for _ in range(warmup):
+        train_net.run_step(model, opt, batched, clip, updater)
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(steps):
+        total, losses = train_net.run_step(model, opt, batched, clip, updater)
+    b.record()
+    torch.cuda.synchronize()
+    ms = a.elapsed_time(b) / steps
+    return {"workload": "C5 vCLR DINO-R50 detector training step (EMA teacher on the weak view + student on the "
+                        "strong view, DINO + consistency criteria, clip 0.1, AdamW, EMA update), fp32, random init",
+            "shape": "bs=2 (800x1333, 750x1200 padded), 2000 queries + 100 dn, 1 class, 6 boxes/image",
+            "ms_per_step": round(ms, 2), "images_per_s": round(2 / (ms * 1e-3), 3), "steps": steps,
+            "warmup": warmup, "loss": round(float(total), 4), "loss_sim": round(float(losses["loss_sim"]), 4)}
+
+
 MFMA_BF16_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md; no sparsity)
 GEMM_SHAPES = (("fwd", 16384, 512, 512, "stage-2 attention proj"), ("bwd", 16384, 512, 1536, "stage-2 qkv dX"),
                ("bwd", 16384, 512, 2048, "stage-2 fc1 dX"))
@@ -550,6 +600,10 @@ def main():
                 result["kernels"]["dino_transformer_c5"] = dino_stack_line(device, result["kernels"])
             except Exception as e:  # report, never fake
                 result["kernels"]["dino_transformer_c5"] = {"error": repr(e)[:200]}
+            try:
+                result["kernels"]["dino_detector_c5"] = dino_detector_line(device)
+            except Exception as e:  # report, never fake
+                result["kernels"]["dino_detector_c5"] = {"error": repr(e)[:300]}
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == "c2":
         try:
             result["cpu_baseline"] = cpu_baseline(args)

@@ -11,6 +11,7 @@ import torch.nn as nn
 from detrex.layers import PositionEmbeddingSine
 from detrex.modeling import BasicStem, ChannelMapper, HungarianMatcher, ResNet
 
+from ..modeling.consistency import ConsisCriterion
 from ..modeling.criterion import DINOCriterion
 from ..modeling.dino import DINO
 from ..modeling.dino_transformer import DINOTransformer, DINOTransformerDecoder, DINOTransformerEncoder
@@ -28,7 +29,7 @@ def weight_dict(dec_layers):
 
 
 def build_model(num_classes=80, num_queries=900, enc_layers=6, dec_layers=6, dn_number=100, label_noise_ratio=0.5,
-                box_noise_scale=1.0, device="cuda"):
+                box_noise_scale=1.0, device="cuda", consistency=True):
     backbone = ResNet(stem=BasicStem(in_channels=3, out_channels=64, norm="FrozenBN"),
                       stages=ResNet.make_default_stages(depth=50, stride_in_1x1=False, norm="FrozenBN"),
                       out_features=["res3", "res4", "res5"], freeze_at=1)
@@ -46,9 +47,14 @@ def build_model(num_classes=80, num_queries=900, enc_layers=6, dec_layers=6, dn_
                                alpha=0.25, gamma=2.0)
     criterion = DINOCriterion(num_classes=num_classes, matcher=matcher, weight_dict=copy.deepcopy(weight_dict(dec_layers)),
                               loss_class_type="focal_loss", alpha=0.25, gamma=2.0, two_stage_binary_cls=False)
+    # the siamese consistency loss with its own matcher (dino_r50.py:110-130); the teacher it compares
+    # against is the model's EMA (ema.may_build_model_ema + train_net.run_step's update)
+    consis = ConsisCriterion(matcher=HungarianMatcher(cost_class=2.0, cost_bbox=5.0, cost_giou=2.0,
+                                                      cost_class_type="focal_loss_cost", alpha=0.25, gamma=2.0),
+                             weight_dict=copy.deepcopy(BASE_WEIGHTS)) if consistency else None
     return DINO(backbone=backbone,
                 position_embedding=PositionEmbeddingSine(num_pos_feats=128, temperature=10000, normalize=True,
                                                          offset=-0.5),
                 neck=neck, transformer=transformer, embed_dim=256, num_classes=num_classes, num_queries=num_queries,
                 criterion=criterion, aux_loss=True, dn_number=dn_number, label_noise_ratio=label_noise_ratio,
-                box_noise_scale=box_noise_scale, device=device)
+                box_noise_scale=box_noise_scale, device=device, consistency_criterion=consis)

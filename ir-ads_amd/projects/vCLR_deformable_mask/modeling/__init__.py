@@ -12,6 +12,7 @@ import torch.nn as nn
 
 from detrex.layers import MLP
 
+from .consistency import ConsisCriterion
 from .criterion import DINOCriterion
 from .dino import DINO
 from .dino_transformer import DINOTransformer, DINOTransformerDecoder, DINOTransformerEncoder
@@ -32,4 +33,4 @@ def attach_detection_heads(transformer: DINOTransformer, num_classes: int = 1, e
 
 
 __all__ = ["DINOTransformerEncoder", "DINOTransformerDecoder", "DINOTransformer", "attach_detection_heads", "DINO",
-           "DINOCriterion"]
+           "DINOCriterion", "ConsisCriterion"]

@@ -1,24 +1,30 @@
 """vCLR DINO detector around the MSDeformAttn transformer (reference
-projects/vCLR_deformable_mask/modeling/dino.py:113-270 (__init__), 727-922 (forward_student),
-974-1149 (aux outputs, contrastive denoising queries, dn post-processing), 1151-1159 and
-1258-1274 (image and target preparation)).
+projects/vCLR_deformable_mask/modeling/dino.py:113-270 (__init__), 278-303 (forward), 306-415
+(infer_results), 472-561 (weak images and the strong view's mix / erase / grayscale), 727-922
+(forward_student), 974-1149 (aux outputs, contrastive denoising queries, dn post-processing),
+1151-1159 and 1258-1274 (image and target preparation)).
 
-Built: the student's training forward (ResNet-50 -> ChannelMapper -> masks and sine position
-embeddings -> CDN queries -> DINOTransformer on the HIP MSDA kernels -> per-layer class / box /
-ROI / mask heads with the encoder-memory segmentation features -> dn split -> DINOCriterion) and
-the same path without targets for inference outputs.  Not built: the EMA teacher
-and its pseudo-boxes (infer_results / forward_ema), the strong-augmentation mix / erase /
-grayscale of the student input, the consistency criterion they feed, and the NMS post-processing
-to detectron2 Instances.  ``forward(batched_inputs)`` therefore runs forward_student on the
-normalised images with ``siamese_outputs=None`` (the reference's consistency loss is skipped
-exactly in that case, dino.py:914).
+The training forward is the reference's: the student runs on the strong view (the normalised
+"image", randomly mixed with an up-sampled patch of itself, erased in a random rectangle and, with
+probability 1/2, turned grey), the EMA teacher (``self.ema_state``, detrex/modeling/ema.py, kept up
+to date by train_net.run_step) runs without gradients on the weak view (the normalised
+"image_rgb"), and the consistency criterion (consistency.py) adds the cosine loss between the two
+views' matched queries to the DINO criterion's losses.  ResNet-50 -> ChannelMapper -> masks and
+sine position embeddings -> CDN queries -> DINOTransformer on the HIP MSDA kernels -> per-layer
+class / box / ROI / mask heads with the encoder-memory segmentation features -> dn split ->
+DINOCriterion.  Without a teacher state or a consistency criterion the forward is
+forward_student on the normalised images, as the reference's is when ``siamese_outputs`` is None
+(dino.py:914).  Not built: NMS post-processing to detectron2 Instances (evaluation only).
 
-Inputs: ``batched_inputs`` as detectron2 passes them: dicts with "image" (3, H, W) unnormalised
-and, in training, "instances" with ``image_size``, ``gt_boxes`` (xyxy pixels, a tensor or an object
-with ``.tensor``), ``gt_classes`` and ``gt_masks`` (n, h, w).  Random draws (label / box noise of
-the denoising queries) go through ``self.rng`` (``torch``)."""
+Inputs: ``batched_inputs`` as detectron2 passes them: dicts with "image" (3, H, W) unnormalised,
+"image_rgb" (the weak view, same size) and, in training, "instances" with ``image_size``,
+``gt_boxes`` (xyxy pixels, a tensor or an object with ``.tensor``), ``gt_classes`` and
+``gt_masks`` (n, h, w).  Random draws go through ``self.rng`` (torch-like: the denoising noise and
+the mix patch) and ``self.pyrng`` (Python-``random``-like: erase and grayscale), so tests replay
+the reference's recorded draws."""
 import copy
 import math
+import random
 
 import torch
 import torch.nn as nn
@@ -26,6 +32,7 @@ import torch.nn.functional as F
 
 from detrex.layers import MLP
 from detrex.layers.box_ops import box_xyxy_to_cxcywh
+from detrex.modeling import ema
 from detrex.utils import inverse_sigmoid
 
 
@@ -66,6 +73,8 @@ class DINO(nn.Module):
         self.select_box_nums_for_evaluation = select_box_nums_for_evaluation
         self.input_format, self.vis_period = input_format, vis_period
         self.rng = torch
+        self.pyrng = random
+        self.ema_state = None  # the EMA teacher (detrex/modeling/ema.py); None: no siamese pass
         # heads (dino.py:185-230): shared initialisation, then one copy per decoder layer + encoder
         class_embed = nn.Linear(embed_dim, num_classes)
         bbox_embed = MLP(embed_dim, embed_dim, 4, 3)
@@ -119,27 +128,124 @@ class DINO(nn.Module):
         return out
 
     # ---------------------------------------------------------------- forward
+    def preprocess_image_strong(self, batched_inputs):
+        # the reference normalises the same "image" for the strong view (dino.py:1156-1159)
+        return self.preprocess_image(batched_inputs)
+
+    def prepare_weak_images(self, batched_inputs, padded_hw):
+        """The normalised "image_rgb" of each input, zero-padded bottom / right to the batch's
+        padded size (dino.py:472-481)."""
+        H, W = padded_hw
+        dev = self.pixel_mean.device
+        out = []
+        for x in batched_inputs:
+            im = (x["image_rgb"].to(dev).to(self.pixel_mean.dtype) - self.pixel_mean) / self.pixel_std
+            out.append(F.pad(im, (0, W - im.shape[2], 0, H - im.shape[1]), value=0.0))
+        return pad_images(out)[0]
+
+    @staticmethod
+    def _image_size(x):
+        inst = x["instances"]
+        return tuple(inst.image_size if hasattr(inst, "image_size") else inst["image_size"])
+
+    # ---------------------------------------------------------------- the strong view (dino.py:484-561)
+    def random_mix(self, batched_inputs, images):
+        """Blend each image with a bilinearly up-sampled random (h/8 x w/8) patch of itself, by a
+        ratio drawn from U[0.5, 1)."""
+        for i, x in enumerate(batched_inputs):
+            h, w = self._image_size(x)
+            bh, bw = h // 8, w // 8
+            x0 = int(self.rng.randint(0, w - bw, (1,)))
+            y0 = int(self.rng.randint(0, h - bh, (1,)))
+            patch = F.interpolate(images[i:i + 1, :, y0:y0 + bh, x0:x0 + bw], (h, w), mode="bilinear")
+            ratio = torch.abs(self.rng.rand(1).to(images.device) - 0.5) + 0.5
+            images[i, :, :h, :w] = images[i, :, :h, :w] * ratio + patch[0] * (1.0 - ratio)
+        return images
+
+    def random_erase(self, batched_inputs, images):
+        """Zero a rectangle of area U[0.02, 1/3] of the image, log-aspect U[log 0.3, log 0.7]
+        (half the image when it does not fit)."""
+        lo, hi = math.log(0.3), math.log(0.7)
+        for i, x in enumerate(batched_inputs):
+            h, w = self._image_size(x)
+            area = self.pyrng.uniform(0.02, 1.0 / 3.0) * h * w
+            aspect = math.exp(self.pyrng.uniform(lo, hi))
+            eh, ew = int(round(math.sqrt(area * aspect))), int(round(math.sqrt(area / aspect)))
+            if not (eh < h and ew < w):
+                eh, ew = int(h / 2.0), int(w / 2.0)
+            top = self.pyrng.randint(0, h - eh)
+            left = self.pyrng.randint(0, w - ew)
+            images[i, :, top:top + eh, left:left + ew] = 0.0
+        return images
+
+    def random_grayscale(self, images):
+        """With probability 1/2, the whole batch (padding included) to ITU-R 601 luma, re-normalised."""
+        if self.pyrng.random() > 0.5:
+            mean, std = self.pixel_mean.view(1, 3, 1, 1), self.pixel_std.view(1, 3, 1, 1)
+            raw = images * std + mean
+            grey = (0.299 * raw[:, 0] + 0.587 * raw[:, 1] + raw[:, 2] * 0.114).unsqueeze(1).repeat(1, 3, 1, 1)
+            images = (grey - mean) / std
+        return images
+
+    def image_transform(self, batched_inputs, images):
+        images = self.random_mix(batched_inputs, images)
+        images = self.random_erase(batched_inputs, images)
+        return self.random_grayscale(images)
+
+    # ---------------------------------------------------------------- forward
     def forward(self, batched_inputs):
         images, sizes = self.preprocess_image(batched_inputs)
         B, _, H, W = images.shape
-        if self.training:
-            img_masks = images.new_ones(B, H, W)
-            for i, x in enumerate(batched_inputs):
-                ih, iw = (x["instances"].image_size if hasattr(x["instances"], "image_size")
-                          else x["instances"]["image_size"])
-                img_masks[i, :ih, :iw] = 0
-        else:
-            img_masks = images.new_zeros(B, H, W)
-        return self.forward_student(batched_inputs, images, img_masks)
+        if not self.training:
+            return self.forward_student(batched_inputs, images, images.new_zeros(B, H, W))
+        img_masks = images.new_ones(B, H, W)
+        for i, x in enumerate(batched_inputs):
+            ih, iw = self._image_size(x)
+            img_masks[i, :ih, :iw] = 0
+        if self.ema_state is None or not self.ema_state.has_inited() or self.consistency_criterion is None:
+            return self.forward_student(batched_inputs, images, img_masks)
+        strong, _ = self.preprocess_image_strong(batched_inputs)
+        weak = self.prepare_weak_images(batched_inputs, (H, W))
+        siamese = self.infer_results(batched_inputs, weak, img_masks)
+        strong = self.image_transform(batched_inputs, strong)
+        return self.forward_student(batched_inputs, strong, img_masks, ema_gts=None, weak_images=images,
+                                    siamese_outputs=siamese)
 
-    def forward_student(self, batched_inputs, images, img_masks, ema_gts=None):
-        targets = self.prepare_targets(batched_inputs, images.shape[-2:]) if self.training else None
-        features = self.backbone(images)
-        feats = self.neck(features)
+    def _features(self, images, img_masks):
+        feats = self.neck(self.backbone(images))
         masks, pos = [], []
         for f in feats:
             masks.append(F.interpolate(img_masks[None], size=f.shape[-2:]).to(torch.bool).squeeze(0))
             pos.append(self.position_embedding(masks[-1]))
+        return feats, masks, pos
+
+    @torch.no_grad()
+    def infer_results(self, batched_inputs, images, img_masks):
+        """The EMA teacher on the weak view, no denoising queries, no gradients (dino.py:306-415):
+        last-layer logits, boxes, ROI embeddings and the detached query features, plus the
+        encoder proposals; the student's weights are restored afterwards."""
+        with ema.apply_model_ema_and_restore(self, self.ema_state):
+            feats, masks, pos = self._features(images, img_masks)
+            inter_states, init_ref, inter_refs, enc_state, enc_ref, _ = self.transformer(
+                feats, masks, pos, (None, None), attn_masks=[None, None])
+            last = inter_states.shape[0] - 1  # only the last layer's outputs are returned
+            st = inter_states[last]
+            ref = inverse_sigmoid(init_ref if last == 0 else inter_refs[last - 1])
+            tmp = self.bbox_embed[last](st)
+            if ref.shape[-1] == 4:
+                tmp = tmp + ref
+            else:
+                tmp = torch.cat([tmp[..., :2] + ref, tmp[..., 2:]], -1)
+            out = {"pred_logits": self.class_embed[last](st), "pred_boxes": tmp.sigmoid(),
+                   "pred_rois": self.ROI_embed[last](st), "pred_query": st.clone().detach()}
+            out["enc_outputs"] = {"pred_logits": self.transformer.decoder.class_embed[-1](enc_state),
+                                  "pred_boxes": enc_ref, "pred_rois": self.ROI_embed[-1](enc_state),
+                                  "pred_query": enc_state}
+        return out
+
+    def forward_student(self, batched_inputs, images, img_masks, ema_gts=None, weak_images=None, siamese_outputs=None):
+        targets = self.prepare_targets(batched_inputs, images.shape[-2:]) if self.training else None
+        feats, masks, pos = self._features(images, img_masks)
         if self.training:
             if ema_gts is not None:
                 for t, e in zip(targets, ema_gts):
@@ -197,6 +303,8 @@ class DINO(nn.Module):
         if not self.training:
             return output
         loss_dict = self.criterion(output, targets, dn_meta)
+        if siamese_outputs is not None and self.consistency_criterion is not None:
+            loss_dict.update(self.consistency_criterion(output, siamese_outputs, targets, dn_meta))
         for k in loss_dict:
             if k in self.criterion.weight_dict:
                 loss_dict[k] = loss_dict[k] * self.criterion.weight_dict[k]

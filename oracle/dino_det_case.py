@@ -69,6 +69,57 @@ class RecordingRNG:
         t = self._keep(_RANDINT(low, high, tuple(x.shape), generator=self.g, dtype=torch.int64))
         return t.to(device=x.device, dtype=dtype or x.dtype)
 
+    def randint(self, low=0, high=None, size=None, dtype=None, device=None, **kw):
+        if high is None:
+            low, high = 0, low
+        t = self._keep(_RANDINT(low, high, tuple(size), generator=self.g, dtype=torch.int64))
+        return t.to(device=device, dtype=dtype or torch.int64)
+
+
+class RecordingPyRandom:
+    """random.uniform / randint / random from a seeded random.Random; every result is kept."""
+
+    def __init__(self, seed):
+        import random
+        self.r = random.Random(seed)
+        self.draws = []
+
+    def _keep(self, v):
+        self.draws.append(float(v))
+        return v
+
+    def uniform(self, a, b):
+        return self._keep(self.r.uniform(a, b))
+
+    def randint(self, a, b):
+        return self._keep(self.r.randint(a, b))
+
+    def random(self):
+        return self._keep(self.r.random())
+
+
+class ReplayPyRandom:
+    """The recorded Python-random results, in order (randint's as ints)."""
+
+    def __init__(self, draws):
+        self.draws, self.i = [float(d) for d in draws], 0
+
+    def _next(self):
+        v = self.draws[self.i]
+        self.i += 1
+        return v
+
+    def uniform(self, a, b):
+        return self._next()
+
+    def randint(self, a, b):
+        v = self._next()
+        assert v == int(v) and a <= v <= b, (v, a, b)
+        return int(v)
+
+    def random(self):
+        return self._next()
+
 
 class ReplayRNG:
     """The recorded draws, in order, on the caller's device and dtype."""
@@ -92,6 +143,40 @@ class ReplayRNG:
 
     def randint_like(self, x, low=0, high=None, dtype=None, **kw):
         return self._next(x.shape).to(device=x.device, dtype=dtype or x.dtype)
+
+    def randint(self, low=0, high=None, size=None, dtype=None, device=None, **kw):
+        return self._next(tuple(size)).to(device=device, dtype=dtype or torch.int64)
+
+
+TRAIN_PY_SEED = 0  # python-random seed of the training-forward case (its grayscale draw is > 0.5)
+EMA_MIX = (0.9, 0.1, 1)  # teacher = 0.9 * the model's fill + 0.1 * the fill at DET_FILL_SEED + 1
+
+
+def det_train_inputs():
+    """det_inputs() plus each image's weak view "image_rgb" (its own seeded image, same size)."""
+    out = []
+    for i, (img, boxes, cls, masks) in enumerate(det_inputs()):
+        rgb = np.floor(seeded(img.shape, 330 + i, "uniform") * 255.0)
+        out.append((img, rgb, boxes, cls, masks))
+    return out
+
+
+@torch.no_grad()
+def ema_teacher_state(model, fill_module, seed):
+    """name -> value for every parameter and buffer of ``model`` as the EMA state iterates them: a
+    mix of the model's own (name-hashed) fill and the fill at ``seed + EMA_MIX[2]`` for every
+    entry the fill touches (identical on the reference and the product, whatever their module
+    registration order), the model's own value elsewhere."""
+    import copy
+    a, b, ds = EMA_MIX
+    other = fill_module(copy.deepcopy(model), seed=seed + ds, dedup=True)
+    mine = dict(list(model.named_parameters()) + list(model.named_buffers()))
+    theirs = dict(list(other.named_parameters()) + list(other.named_buffers()))
+    out = {}
+    for n, v in mine.items():
+        w = theirs[n]
+        out[n] = v.detach().clone() if (not v.is_floating_point() or torch.equal(v, w)) else a * v.detach() + b * w.detach()
+    return out
 
 
 BASE_WEIGHTS = {"loss_class": 1, "loss_bbox": 5.0, "loss_giou": 2.0, "loss_class_dn": 0, "loss_bbox_dn": 0.0,

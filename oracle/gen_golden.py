@@ -706,6 +706,87 @@ def gen_dino_detector(ref):
     save("dino_detector_step.npz", **res)
 
 
+def _det_train_reference_step(L, dtype, rng, pyrng):
+    """The reference's FULL training forward (DINO.forward, dino.py:278-303: EMA teacher on the weak
+    view, strong view mix / erase / grayscale, forward_student with the consistency criterion) +
+    the loss sum + backward, on the CPU in `dtype`, draws from `rng` (torch) and `pyrng` (random)."""
+    from dino_det_case import BASE_WEIGHTS, DET_FILL_SEED, canonical_params, det_train_inputs, ema_teacher_state
+    model = _det_reference_model(L, dtype)
+    matcher = L.matcher.HungarianMatcher(cost_class=2.0, cost_bbox=5.0, cost_giou=2.0,
+                                         cost_class_type="focal_loss_cost", alpha=0.25, gamma=2.0)
+    model.consistency_criterion = L.consis.ConsisCriterion(matcher=matcher, weight_dict=dict(BASE_WEIGHTS))
+    model.ema_state = L.ema.EMAState()
+    model.ema_state.state = ema_teacher_state(model, fill_module, DET_FILL_SEED)
+    batched = []
+    for img, rgb, boxes, cls, masks in det_train_inputs():
+        inst = L.Instances(tuple(img.shape[1:]), gt_boxes=L.Boxes(t(boxes, dtype)), gt_classes=t(cls),
+                           gt_masks=t(masks))
+        batched.append({"image": t(img, dtype), "image_rgb": t(rgb, dtype), "instances": inst})
+    orig = {k: getattr(torch, k) for k in ("rand", "rand_like", "randint_like", "randint")}
+    orig_cuda, orig_to = torch.Tensor.cuda, torch.Tensor.to
+    orig_random = L.dino_det.random
+
+    def to_cpu(self, *a, **k):
+        if a and (a[0] == "cuda" or (isinstance(a[0], torch.device) and a[0].type == "cuda")):
+            a = ("cpu",) + a[1:]
+        if k.get("device") == "cuda":
+            k["device"] = "cpu"
+        return orig_to(self, *a, **k)
+    default = torch.get_default_dtype()
+    try:
+        torch.set_default_dtype(dtype)
+        torch.rand, torch.rand_like, torch.randint_like, torch.randint = (rng.rand, rng.rand_like, rng.randint_like,
+                                                                           rng.randint)
+        torch.Tensor.cuda = lambda self, *a, **k: self
+        torch.Tensor.to = to_cpu
+        L.dino_det.random = pyrng
+        losses = model(batched)
+        total = sum(losses.values())
+        total.backward()
+    finally:
+        for k, v in orig.items():
+            setattr(torch, k, v)
+        torch.Tensor.cuda, torch.Tensor.to = orig_cuda, orig_to
+        L.dino_det.random = orig_random
+        torch.set_default_dtype(default)
+    return losses, total, canonical_params(model)
+
+
+def gen_dino_train(ref):
+    """The vCLR DINO detector's full training forward (reduced case) in fp64 and fp32 on the
+    reference; the fp32 run replays the fp64 run's draws (torch and Python random)."""
+    from dino_det_case import (TRAIN_PY_SEED, RecordingPyRandom, RecordingRNG, ReplayPyRandom, ReplayRNG)
+    from train_fixture import N_PROJ, projection
+    L = __import__("ref_import").load_dino_train()
+    rec, prec = RecordingRNG(2025), RecordingPyRandom(TRAIN_PY_SEED)
+    l64, tot64, p64 = _det_train_reference_step(L, torch.float64, rec, prec)
+    l32, tot32, p32 = _det_train_reference_step(L, torch.float32, ReplayRNG(rec.draws), ReplayPyRandom(prec.draws))
+    assert prec.draws[-1] > 0.5, "the case is meant to take the grayscale branch: pick another TRAIN_PY_SEED"
+    keys = sorted(l64)
+    assert "loss_sim" in keys, keys
+    res = {"loss_keys": np.array(keys), "loss64": np.array([float(l64[k]) for k in keys]),
+           "loss32": np.array([float(l32[k]) for k in keys]), "total64": float(tot64), "total32": float(tot32),
+           "n_draws": len(rec.draws), "pydraws": np.array(prec.draws)}
+    for i, d in enumerate(rec.draws):
+        res[f"draw_{i}"] = d.numpy()
+    names = [n for n, _ in p64]
+    assert names == [n for n, _ in p32]
+    norms, projs, ref32 = [], [], []
+    for (n, p), (_, q) in zip(p64, p32):
+        g = p.grad.numpy() if p.grad is not None else np.zeros(tuple(p.shape))
+        g32 = q.grad.double().numpy() if q.grad is not None else np.zeros(tuple(q.shape))
+        nr = float(np.sqrt((g * g).sum()))
+        norms.append(nr)
+        projs.append([projection(n, g, j) for j in range(N_PROJ)])
+        ref32.append(float(np.sqrt(((g32 - g) ** 2).sum())) / max(nr, 1e-300))
+    res.update(grad_names=np.array(names), grad_norms=np.array(norms), grad_projs=np.array(projs),
+               ref32_rel=np.array(ref32))
+    for n, p in p64:
+        if p.numel() <= 4096 and p.grad is not None:
+            res["g." + n] = p.grad.numpy()
+    save("dino_train_step.npz", **res)
+
+
 def gen_dino(ref):
     L = __import__("ref_import").load_dino()
     torch.manual_seed(0)
@@ -830,7 +911,7 @@ if __name__ == "__main__":
     which = sys.argv[1:] or ["msda", "swin", "block", "dattn", "fusion", "cmnext", "sb", "metrics", "train"]
     ref = load_reference()
     torch.manual_seed(0)
-    fns = {"dino": gen_dino, "dino_detector": gen_dino_detector, "msda": gen_msda, "swin": gen_swin_wmsa, "block": gen_swin_block, "dattn": gen_dattn,
+    fns = {"dino": gen_dino, "dino_detector": gen_dino_detector, "dino_train": gen_dino_train, "msda": gen_msda, "swin": gen_swin_wmsa, "block": gen_swin_block, "dattn": gen_dattn,
            "fusion": gen_fusion_small, "cmnext": gen_cmnext, "sb": gen_sb, "metrics": gen_metrics_loss,
            "train": gen_cmnext_train, "train64": gen_cmnext_train_fp64, "msf": gen_msf}
     for w in which:

@@ -435,3 +435,29 @@ def load_dino_detector():
                    criterion=sys.modules["vclr_modeling.dn_criterion"], ShapeSpec=_ShapeSpec,
                    ImageList=_ImageList, Instances=_Instances, Boxes=_Boxes)
     return types.SimpleNamespace(**_LOADED)
+
+
+class _HookBase:
+    """detectron2.engine.train_loop.HookBase (the EMA module subclasses it; never driven here)."""
+
+
+def load_dino_train():
+    """load_dino_detector() plus the pieces of the reference's full training forward (DINO.forward,
+    dino.py:278-303): detrex/modeling/ema.py itself (EMAState, apply_model_ema_and_restore; its
+    detectron2 HookBase import stood in) bound as the `ema` module dino.py calls, and
+    ConsisCriterion.py."""
+    ref = load_dino_detector()
+    if "consis" in _LOADED:
+        return types.SimpleNamespace(**_LOADED)
+    _pkg("detectron2.engine")
+    _mod("detectron2.engine.train_loop", HookBase=_HookBase)
+    ema = _load("detrex.modeling.ema_reference", "detrex/modeling/ema.py")
+    _LOADED["dino_det"].ema = ema
+    spec = importlib.util.spec_from_file_location(
+        "vclr_modeling.ConsisCriterion", f"{REF}/projects/vCLR_deformable_mask/modeling/ConsisCriterion.py")
+    m = importlib.util.module_from_spec(spec)
+    sys.modules["vclr_modeling.ConsisCriterion"] = m
+    spec.loader.exec_module(m)
+    _LOADED.update(ema=ema, consis=m)
+    del ref
+    return types.SimpleNamespace(**_LOADED)

@@ -15,7 +15,16 @@ def main():
     op = gzip.open if path.endswith(".gz") else open
     d = collections.defaultdict(list)
     with op(path, "rt") as fh:
-        for r in csv.DictReader(fh):
+        rows = [r for r in csv.DictReader(fh) if r.get("Kind", "KERNEL_DISPATCH") == "KERNEL_DISPATCH"]
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    # the last `steps` training steps only (bench traces: cut at the fused AdamW launch, one per step)
+    adam = [i for i, r in enumerate(rows) if "adam" in r["Kernel_Name"].lower()]
+    if adam:
+        firsts = [adam[0]] + [b for a_, b in zip(adam, adam[1:]) if b - a_ > 50]
+        if len(firsts) > steps:
+            rows = rows[firsts[-steps - 1] + 1:firsts[-1] + 1]
+    if True:
+        for r in rows:
             n = r["Kernel_Name"]
             if not pat.search(n):
                 continue

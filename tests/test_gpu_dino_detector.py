@@ -80,10 +80,79 @@ def _run(dtype):
     return fx, losses, total, canonical_params(model), calls
 
 
+def _run_train(dtype):
+    """The full training forward, model(batched_inputs), as the reference's DINO.forward runs it."""
+    from dino_det_case import (DET_CFG, DET_FILL_SEED, DET_NUM_POINTS, ReplayPyRandom, ReplayRNG, canonical_params,
+                               det_train_inputs, ema_teacher_state)
+    from fill import fill_module
+    from detrex.modeling.ema import EMAState
+    from projects.vCLR_deformable_mask.configs.dino_r50 import build_model
+    fx = Fixture("dino_train_step.npz")
+    model = build_model(**DET_CFG, device="cuda")
+    model.criterion.num_points = DET_NUM_POINTS
+    fill_module(model, seed=DET_FILL_SEED, dedup=True)
+    model = model.to(DEV).to(dtype).train()
+    model.ema_state = EMAState(ema_teacher_state(model, fill_module, DET_FILL_SEED))
+    rng = ReplayRNG([fx[f"draw_{i}"] for i in range(int(fx["n_draws"]))])
+    pyrng = ReplayPyRandom(fx["pydraws"])
+    model.rng = model.criterion.rng = rng
+    model.pyrng = pyrng
+    batched = []
+    for img, rgb, boxes, cls, masks in det_train_inputs():
+        inst = {"image_size": tuple(img.shape[1:]), "gt_boxes": torch.as_tensor(boxes, dtype=dtype, device=DEV),
+                "gt_classes": torch.as_tensor(cls, device=DEV), "gt_masks": torch.as_tensor(masks, device=DEV)}
+        batched.append({"image": torch.as_tensor(img, dtype=dtype), "image_rgb": torch.as_tensor(rgb, dtype=dtype),
+                        "instances": inst})
+    student = {n: p.detach().clone() for n, p in model.named_parameters()}
+    calls = {"fwd": 0, "bwd": 0}
+    from irads import native as N
+    orig = N.call
+
+    def spy(name, *a):
+        if name == "irads_msda_fwd":
+            calls["fwd"] += 1
+        elif name.startswith("irads_msda_bwd"):
+            calls["bwd"] += 1
+        return orig(name, *a)
+    N.call = spy
+    try:
+        losses = model(batched)
+        total = sum(losses.values())
+        total.backward()
+        torch.cuda.synchronize()
+    finally:
+        N.call = orig
+    assert rng.i == len(rng.draws) and pyrng.i == len(pyrng.draws), "every recorded draw replayed"
+    # the teacher pass swapped the EMA weights in and the student's back out, bit for bit
+    for n, p in model.named_parameters():
+        assert torch.equal(p.detach(), student[n]), n
+    return fx, losses, total, canonical_params(model), calls
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float64], ids=["fp32", "fp64"])
 def test_dino_detector_step_vs_reference(dtype):
+    _check(dtype, *_run(dtype))
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64], ids=["fp32", "fp64"])
+def test_dino_training_forward_vs_reference(dtype):
+    """DINO.forward in training mode (dino.py:278-303) on the reduced case against the reference's
+    own (tests/golden/dino_train_step.npz, oracle/gen_golden.py gen_dino_train): the EMA teacher
+    (detrex/modeling/ema.py, a fixed teacher state mixed from two fills) on the weak "image_rgb"
+    view without gradients, the strong view's random mix / erase / grayscale (the case takes the
+    grayscale branch) with the reference's recorded torch and Python random draws, forward_student
+    with the siamese consistency loss (ConsisCriterion: loss_sim = -cosine of the matched queries,
+    -0.70 here).  Same tolerances as the forward_student test; the student's weights are restored
+    bit for bit after the teacher pass."""
+    fx, losses, total, params, calls = _run_train(dtype)
+    assert "loss_sim" in losses
+    # the teacher's MSDA calls ran on the kernels too (forward only: no gradients through it)
+    assert calls["fwd"] >= 2 * (1 + 1) and calls["bwd"] > 0, calls
+    _check(dtype, fx, losses, total, params, calls)
+
+
+def _check(dtype, fx, losses, total, params, calls):
     from train_fixture import N_PROJ, projection
-    fx, losses, total, params, calls = _run(dtype)
     fp32 = dtype == torch.float32
     assert calls["fwd"] > 0 and calls["bwd"] > 0, calls
     keys = [str(k) for k in fx["loss_keys"]]
