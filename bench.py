@@ -498,6 +498,8 @@ def main():
         step()
         ops.STAMPS.disarm()
     spans = ops.STAMPS.read() if not args.profile_only else {}
+    if os.environ.get("IRADS_STAMP_DUMP") and not args.profile_only and rank == 0:
+        ops.STAMPS.dump(os.environ["IRADS_STAMP_DUMP"])
     if world > 1:
         t = torch.tensor([elapsed], device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

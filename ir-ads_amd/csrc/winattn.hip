@@ -246,6 +246,18 @@ __device__ __forceinline__ f32x4 mfma16(const bf16x8_t &a, const bf16x8_t &b, co
 
 __device__ __forceinline__ bf16x8_t as_bf(u16x8 v) { return __builtin_bit_cast(bf16x8_t, v); }
 
+typedef __attribute__((ext_vector_type(8))) float f32x8;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4_t;
+// fp32 -> bf16 (round to nearest even, as f2bf) as whole vectors: one v_cvt_pk_bf16_f32 per PAIR.
+// Element-by-element f2bf made hipcc convert every value alone and v_perm the halves together
+// (108 cvt + 54 perm per lane in the forward instead of 54 cvt).
+__device__ __forceinline__ bf16x8_t pack_bf16(f32x4 lo, f32x4 hi) {
+    return __builtin_convertvector((f32x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]}, bf16x8_t);
+}
+__device__ __forceinline__ u16x4 pack_bf16x4(f32x4 v) {
+    return __builtin_bit_cast(u16x4, __builtin_convertvector(v, bf16x4_t));
+}
+
 typedef __attribute__((ext_vector_type(4))) short i16x4;
 typedef __attribute__((ext_vector_type(4))) short s16x4;
 typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
@@ -395,10 +407,13 @@ __device__ __forceinline__ u16x8 pad_frag(const float *qbias, int c0) {
 
 // bf16 fragment x c2, rounded to bf16
 __device__ __forceinline__ u16x8 scale_frag(u16x8 v, float c) {
-    u16x8 r;
+    f32x4 lo, hi;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) r[e] = f2bf(bf2f(v[e]) * c);
-    return r;
+    for (int e = 0; e < 4; ++e) {
+        lo[e] = bf2f(v[e]) * c;
+        hi[e] = bf2f(v[4 + e]) * c;
+    }
+    return __builtin_bit_cast(u16x8, pack_bf16(lo, hi));
 }
 
 // Forward, one workgroup per (window, head): 3 waves, wave w owns query tiles 3w..3w+2.  All global
@@ -538,12 +553,7 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(MM == 
         f32x4 o0 = {0.f, 0.f, 0.f, 0.f}, o1 = o0, os = o0;
 #pragma unroll
         for (int ks = 0; ks < 5; ++ks) {
-            bf16x8_t pb;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                pb[r] = (__bf16)s[2 * ks][r];
-                pb[4 + r] = (2 * ks + 1 < 9) ? (__bf16)s[2 * ks + 1][r] : (__bf16)0.f;
-            }
+            const bf16x8_t pb = pack_bf16(s[2 * ks], (2 * ks + 1 < 9) ? s[2 * ks + 1] : f32x4{0.f, 0.f, 0.f, 0.f});
             // keys 144..159 do not exist: their P is 0, so any finite rows serve (tile 8 again)
             const int r0 = 32 * ks * HD, r1 = ks < 4 ? r0 + 16 * HD : r0;
             const u16x8 a0 = cat4(tr_read(vb0 + r0), tr_read(vb0 + r1));
@@ -554,12 +564,7 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(MM == 
         }
         const float inv = __builtin_amdgcn_rcpf(os[0]);
         if (tok[j] >= 0) {
-            u16x4 w0, w1;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                w0[r] = f2bf(o0[r] * inv);
-                w1[r] = f2bf(o1[r] * inv);
-            }
+            const u16x4 w0 = pack_bf16x4(o0 * inv), w1 = pack_bf16x4(o1 * inv);
             unsigned short *op = out + (long)tok[j] * g.C + h * HD;
             *(u16x4 *)(op + grp * 4) = w0;
             *(u16x4 *)(op + 16 + grp * 4) = w1;

@@ -80,6 +80,16 @@ class StepStamps:
         self.follows[i] = j
         N.load().irads_stamp_next(ctypes.c_void_p(self.buf[j].data_ptr()))
 
+    def dump(self, path):
+        """The raw per-workgroup (start, end) clocks of every filled slot, with the slot names and the
+        clock rate, to an .npz (workgroup timelines: scripts/stamp_timeline.py)."""
+        import numpy as np
+        torch.cuda.synchronize()
+        n = len(self.slots)
+        np.savez_compressed(path, regions=self.buf[:n].cpu().numpy(), names=np.array([s[0] for s in self.slots]),
+                            bytes=np.array([s[1] for s in self.slots]), khz=N.load().irads_wall_clock_khz(),
+                            follows=np.array(sorted(self.follows.items()), dtype=np.int64).reshape(-1, 2))
+
     def read(self):
         """{name: {"launches", "total_ms", "bytes", "flops", "real_bytes", "spans_ms", "own_spans_ms",
         "periods"}} of the filled slots: total_ms / spans_ms are the launch's period where an irads GEMM

@@ -166,16 +166,19 @@ def ema_teacher_state(model, fill_module, seed):
     """name -> value for every parameter and buffer of ``model`` as the EMA state iterates them: a
     mix of the model's own (name-hashed) fill and the fill at ``seed + EMA_MIX[2]`` for every
     entry the fill touches (identical on the reference and the product, whatever their module
-    registration order), the model's own value elsewhere."""
-    import copy
+    registration order), the model's own value elsewhere.  The second fill is made in place and
+    the model's values are put back (no deepcopy: the product model holds module references)."""
     a, b, ds = EMA_MIX
-    other = fill_module(copy.deepcopy(model), seed=seed + ds, dedup=True)
-    mine = dict(list(model.named_parameters()) + list(model.named_buffers()))
-    theirs = dict(list(other.named_parameters()) + list(other.named_buffers()))
+    items = list(model.named_parameters()) + list(model.named_buffers())
+    mine = {n: v.detach().clone() for n, v in items}
+    fill_module(model, seed=seed + ds, dedup=True)
+    theirs = {n: v.detach().clone() for n, v in items}
+    for n, v in items:
+        v.data.copy_(mine[n])
     out = {}
     for n, v in mine.items():
         w = theirs[n]
-        out[n] = v.detach().clone() if (not v.is_floating_point() or torch.equal(v, w)) else a * v.detach() + b * w.detach()
+        out[n] = v if (not v.is_floating_point() or torch.equal(v, w)) else a * v + b * w
     return out
 
 

@@ -6,7 +6,9 @@
 
 `run` issues exactly the 24 irads_winattn_fwd launches of one bench step (Swin-B at 512²,
 rgb+dte batched: B = 16; depths 2/2/18/2, shift 0/6 alternating), on the same synthetic
-scale as bench.py, after one untimed pass of the same sequence.  `parse` takes the last 24
+scale as bench.py, after one untimed pass of the same sequence.  Every launch reads its OWN qkv
+tensor, as the step's blocks do (round 3's runner reused one per stage, so the 18 stage-2
+launches found their inputs in the 256 MB Infinity Cache: FETCH read low).  `parse` takes the last 24
 dispatches of the kernel and applies MI355X_MICROARCH.md's gfx950 corrections: FETCH_SIZE
 counts half the bytes of wide (16 B/lane) streaming reads, so it is doubled; WRITE_SIZE is
 exact for 16 B/lane stores.  Both counters are in KiB.  FETCH_SIZE and WRITE_SIZE need
@@ -31,21 +33,21 @@ def run():
     ins = []
     for side, C, nH, depth in STAGES:
         L = side * side
-        qkv = (torch.randn(B, L, 3 * C, device="cuda") * 0.5).bfloat16()
+        qkvs = [(torch.randn(B, L, 3 * C, device="cuda") * 0.5).bfloat16() for _ in range(depth)]
         bias = torch.randn(3 * C, device="cuda") * 0.1
         table = torch.randn(23 * 23, nH, device="cuda") * 0.1
-        ins.append((qkv, bias, table, side, nH, depth))
+        ins.append((qkvs, bias, table, side, nH, depth))
 
     def step():
-        for qkv, bias, table, side, nH, depth in ins:
+        for qkvs, bias, table, side, nH, depth in ins:
             for blk in range(depth):
-                ops.winattn_fwd(qkv, bias, table, None, side, side, nH, 6 if blk % 2 else 0, 32 ** -0.5)
+                ops.winattn_fwd(qkvs[blk], bias, table, None, side, side, nH, 6 if blk % 2 else 0, 32 ** -0.5)
 
     def step_bwd():  # the 24 backward launches, each on its own forward's output and LSE
-        for qkv, bias, table, side, nH, depth in ins:
+        for qkvs, bias, table, side, nH, depth in ins:
             for blk in range(depth):
                 shift = 6 if blk % 2 else 0
-                qq = qkv.clone().requires_grad_()
+                qq = qkvs[blk].clone().requires_grad_()
                 o = ops.window_attention(qq, bias, table, None, side, side, nH, shift, 32 ** -0.5)
                 o.backward(torch.ones_like(o))
     if KIND == "bwd":
