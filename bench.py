@@ -412,12 +412,17 @@ def traffic_from_profile():
     """HBM bytes per forward launch from the newest committed PMC passes of the same 24 launches
     (scripts/pmc_winattn_kind.sh: FETCH_SIZE x2 + WRITE_SIZE, separate rocprofv3 passes); PMC
     counters cannot be read from inside this process.  Returns (bytes, source file)."""
-    for tag in ("r04", "r03", "r02"):
+    for tag in ("r05", "r04", "r03", "r02"):
         rel = os.path.join("profiles", f"{tag}_pmc_winattn_fwd.json")
         if os.path.exists(os.path.join(ROOT, rel)):
             with open(os.path.join(ROOT, rel)) as f:
                 return json.load(f).get("hbm_bytes_per_launch"), rel
     return None, None
+
+
+def _progress(msg):
+    """A progress line on stderr (the one JSON result line stays alone on stdout)."""
+    print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
 
 def main():
@@ -484,6 +489,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    _progress(f"timed {args.steps} steps: {1e3 * elapsed / args.steps:.3f} ms/step")
     # In-step kernel spans: ONE more step after the timed region, identical to the timed ones (the
     # same graph replay; eager: the same step with stamp slots armed), whose window-attention and
     # DAttn kernels stamp their first-workgroup start / last-workgroup end on the device clock.
@@ -589,6 +595,7 @@ def main():
         result["data"] = ("synthetic (RGB N(0,1), %s U[0,1), labels U{0..%d} with 10%% ignore=255; random-init "
                           "weights)" % ({"c3": "HHA"}.get(args.workload, "thermal"), wl["n_cls"] - 1))
     if rank == 0 and not args.no_kernels and args.workload == "c2":
+        _progress("kernel lines: trunk GEMMs, MSDA, DINO transformer / detector (C5)")
         try:
             result["roofline_gemm"] = gemm_roofline(device)
         except Exception as e:  # report, never fake
@@ -602,11 +609,13 @@ def main():
                 result["kernels"]["dino_transformer_c5"] = dino_stack_line(device, result["kernels"])
             except Exception as e:  # report, never fake
                 result["kernels"]["dino_transformer_c5"] = {"error": repr(e)[:200]}
+            _progress("DINO detector line (C5)")
             try:
                 result["kernels"]["dino_detector_c5"] = dino_detector_line(device)
             except Exception as e:  # report, never fake
                 result["kernels"]["dino_detector_c5"] = {"error": repr(e)[:300]}
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == "c2":
+        _progress("cpu_baseline (oracle on the host cores)")
         try:
             result["cpu_baseline"] = cpu_baseline(args)
         except Exception as e:  # report, never fake

@@ -235,172 +235,6 @@ __global__ void __launch_bounds__((BMT / WR) * (BNT / 64) * 64) gemm_nt_bf16(con
     stamp_write(stamp, t_entry, false);
 }
 
-// ---------------------------------------------------------------------------------------------
-// Pipelined variant (5 / 6): 64 x 64 wave tiles (4 x 4 MFMA blocks), NS LDS stages, and the NEXT
-// k-step's fragments read from LDS while this k-step's MFMAs run (two register sets, f0 / f1).
-// The round-4 stamps put the 2-buffer loop's k-step at 2.3x its MFMA time: every k-step issued its
-// 16 fragment reads, waited for all of them, then ran its 32 MFMAs, then met a barrier — LDS latency
-// and the barrier skew sat on the critical path, whatever the staging depth.  Here, per k-step ks:
-//   wait (counted vmcnt) for stage ks+1, lgkmcnt(0) for this k-step's fragments, ONE raw barrier,
-//   issue stage ks+NS into the buffer of tile ks (its fragments are in registers), issue the
-//   fragment reads of tile ks+1, then the 32 MFMAs on tile ks (s_setprio 1 around them).
-// Stage t is issued NS - 1 k-steps before it is waited for; the buffers hold tiles ks+1 .. ks+NS.
-struct GFrags {
-    gbf16x8 a[2][4], b[2][4];  // [k half][A row block / B column block] of a 64 x 64 wave tile
-};
-
-__device__ __forceinline__ void g_read_frags(GFrags &f, const unsigned char *As, const unsigned char *Bs, int wm,
-                                             int wn, int grp, int lane) {
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) f.b[kk][j] = g_frag(Bs, wn * 64 + j * 16, kk * 4 + grp, lane);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) f.a[kk][i] = g_frag(As, wm * 64 + i * 16, kk * 4 + grp, lane);
-    }
-}
-
-__device__ __forceinline__ void g_mfma_step(f32x4 (&acc)[4][4], const GFrags &f) {
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.b[kk][j], f.a[kk][i], acc[i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-}
-
-template <int EPI, int BMT, int BNT, int NS>
-__global__ void __launch_bounds__((BMT / 64) * (BNT / 64) * 64, 2) gemm_nt_bf16_pf(
-    const unsigned short *__restrict__ A, long lda, const unsigned short *__restrict__ B, long ldb,
-    const float *__restrict__ bias, const unsigned short *__restrict__ U, long ldu, unsigned short *__restrict__ C0,
-    unsigned short *__restrict__ C1, long ldc, int M, int N, int K, unsigned long long *stamp) {
-    static_assert(NS >= 2 && NS <= 4, "stages");
-    constexpr int NWN = BNT / 64, NW = (BMT / 64) * NWN;
-    constexpr int G_A_BYTES = BMT * GBK * 2, G_STAGE = G_A_BYTES + BNT * GBK * 2;
-    constexpr int G_LOADS = (BMT + BNT) / (8 * NW);  // global_load_lds per wave and stage
-    static_assert(NS * G_STAGE >= NW * 8192, "the epilogue reuses the stage memory: 8 KiB per wave");
-    const unsigned long long t_entry = stamp_clock(stamp);
-    __shared__ __attribute__((aligned(16))) unsigned char smem[NS * G_STAGE];  // ONE array (glds wait trap)
-    const int nbn = N / BNT;
-    const int lid = xcd_remap(blockIdx.x, gridDim.x);
-    const int bm = lid / nbn, bn = lid - bm * nbn;
-    const int m0 = bm * BMT, n0 = bn * BNT;
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const int wm = wave / NWN, wn = wave % NWN;
-    const int grp = lane >> 4;
-    f32x4 acc[4][4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const int nk = K / GBK;
-    const bool hasb = EPI != EPI_DGELU && bias;
-    const float *bsrc = hasb ? bias : (const float *)B;
-    f32x4 bq[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) bq[j] = *(const f32x4 *)(bsrc + n0 + wn * 64 + j * 16 + grp * 4);
-    auto stage = [&](int t) {
-        unsigned char *dst = smem + (t % NS) * G_STAGE;
-        g_stage<BMT, NW>(A, lda, m0, M - 1, t * GBK, dst, wave, lane);
-        g_stage<BNT, NW>(B, ldb, n0, N - 1, t * GBK, dst + G_A_BYTES, wave, lane);
-    };
-    // prologue: every buffer in flight; wait for tile 0 (the later NS - 1 stages may still fly)
-#pragma unroll
-    for (int s = 0; s < NS; ++s)
-        if (s < nk) stage(s);
-    if (nk >= NS) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G_LOADS * (NS - 1)) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    GFrags f0, f1;
-    g_read_frags(f0, smem, smem + G_A_BYTES, wm, wn, grp, lane);
-    // one k-step: tile ks's fragments in `cur`, tile ks + 1's read into `nxt`
-    auto kstep = [&](int ks, GFrags &cur, GFrags &nxt) {
-        if (ks + 1 < nk) {
-            // stage ks + 1 landed; the stages after it (up to ks + NS - 1) may still be in flight
-            const int later = min(NS - 2, nk - 2 - ks);
-            if (NS >= 4 && later >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G_LOADS * 2) : "memory");
-            else if (NS >= 3 && later >= 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G_LOADS) : "memory");
-            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this k-step's fragments are in registers
-        __builtin_amdgcn_s_barrier();        // every wave: tile ks read out of LDS, stage ks + 1 published
-        __builtin_amdgcn_sched_barrier(0);
-        if (ks + NS < nk) stage(ks + NS);    // into tile ks's buffer
-        if (ks + 1 < nk) {
-            const unsigned char *As = smem + ((ks + 1) % NS) * G_STAGE;
-            g_read_frags(nxt, As, As + G_A_BYTES, wm, wn, grp, lane);
-        }
-        g_mfma_step(acc, cur);
-    };
-    for (int ks = 0; ks < nk; ks += 2) {
-        kstep(ks, f0, f1);
-        if (ks + 1 < nk) kstep(ks + 1, f1, f0);
-    }
-    // epilogue (as gemm_nt_bf16's, one 64-row half): the wave's tile through its own 8 KiB of LDS
-    // for whole-row stores; a raw barrier first (every wave's last MFMAs have consumed their reads)
-    const int lr = lane >> 3, lc = lane & 7;
-    unsigned char *reg = smem + wave * 8192;
-    const int mh = m0 + wm * 64;
-    gu16x8 uq[8];
-    if (EPI == EPI_DGELU) {
-#pragma unroll
-        for (int it = 0; it < 8; ++it) {
-            const int m = min(mh + it * 8 + lr, M - 1);
-            uq[it] = *(const gu16x8 *)(U + (long)m * ldu + n0 + wn * 64 + lc * 8);
-        }
-    }
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int nl = j * 16 + grp * 4;
-        const f32x4 b4 = hasb ? bq[j] : f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int row = i * 16 + (lane & 15);
-            gu16x4 w;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) w[r] = f2bf(acc[i][j][r] + b4[r]);
-            const int c = nl >> 3, half = (nl >> 2) & 1;
-            *(gu16x4 *)(reg + row * 128 + ((c ^ (row & 7)) << 4) + half * 8) = w;
-        }
-    }
-    __builtin_amdgcn_s_waitcnt(0xc07f);
-    __builtin_amdgcn_wave_barrier();
-    gu16x8 v[8];
-#pragma unroll
-    for (int it = 0; it < 8; ++it) {
-        const int row = it * 8 + lr;
-        v[it] = *(const gu16x8 *)(reg + row * 128 + ((lc ^ (row & 7)) << 4));
-    }
-#pragma unroll
-    for (int it = 0; it < 8; ++it) {
-        const int m = mh + it * 8 + lr;
-        const long o = (long)m * ldc + n0 + wn * 64 + lc * 8;
-        if (EPI == EPI_BIAS) {
-            if (m < M) *(gu16x8 *)(C0 + o) = v[it];
-        } else if (EPI == EPI_GELU) {
-            gu16x8 g;
-#pragma unroll
-            for (int e = 0; e < 8; ++e) g[e] = f2bf(g_gelu(bf2f(v[it][e])));
-            if (m < M) {
-                *(gu16x8 *)(C0 + o) = v[it];
-                *(gu16x8 *)(C1 + o) = g;
-            }
-        } else {
-            gu16x8 d;
-#pragma unroll
-            for (int e = 0; e < 8; ++e) d[e] = f2bf(bf2f(v[it][e]) * g_gelu_grad(bf2f(uq[it][e])));
-            if (m < M) *(gu16x8 *)(C0 + o) = d;
-        }
-    }
-    stamp_write(stamp, t_entry, false);
-}
-
 }  // namespace
 }  // namespace irads
 
@@ -408,9 +242,7 @@ using namespace irads;
 
 // variant: 0 = 256 x 128 tiles, 2 buffers; 1 = 256 x 128, 3 buffers (1 workgroup per CU either way);
 // 2 = 128 x 128 tiles on 4 waves, 2 buffers (64 KiB: 2 workgroups per CU); 3 = 128 x 128, 3 buffers;
-// 4 = 256 x 256 tiles on 8 waves of 128 x 64, 2 buffers (128 KiB; N % 256 == 0);
-// 5 = pipelined (gemm_nt_bf16_pf) 256 x 128 on 8 waves of 64 x 64, 3 stages (144 KiB, 1 per CU);
-// 6 = pipelined 128 x 128 on 4 waves, 2 stages (64 KiB, 2 per CU)
+// 4 = 256 x 256 tiles on 8 waves of 128 x 64, 2 buffers (128 KiB; N % 256 == 0)
 template <int EPI, int V, bool TR = false>
 static void gemm_launch(const uint16_t *A, long lda, const uint16_t *B, long ldb, const float *bias, const uint16_t *U,
                         long ldu, uint16_t *C0, uint16_t *C1, long ldc, int M, int N, int K, long long *trace,
@@ -423,16 +255,6 @@ static void gemm_launch(const uint16_t *A, long lda, const uint16_t *B, long ldb
         (unsigned short *)C0, (unsigned short *)C1, ldc, M, N, K, trace);
 }
 
-template <int EPI, int BMT, int BNT, int NS>
-static void gemm_launch_pf(const uint16_t *A, long lda, const uint16_t *B, long ldb, const float *bias,
-                           const uint16_t *U, long ldu, uint16_t *C0, uint16_t *C1, long ldc, int M, int N, int K,
-                           long long *stamp, hipStream_t st) {
-    const unsigned nwg = (unsigned)(((M + BMT - 1) / BMT) * (N / BNT));
-    gemm_nt_bf16_pf<EPI, BMT, BNT, NS><<<nwg, (BMT / 64) * (BNT / 64) * 64, 0, st>>>(
-        (const unsigned short *)A, lda, (const unsigned short *)B, ldb, bias, (const unsigned short *)U, ldu,
-        (unsigned short *)C0, (unsigned short *)C1, ldc, M, N, K, (unsigned long long *)stamp);
-}
-
 template <int EPI>
 static void gemm_dispatch(int variant, const uint16_t *A, long lda, const uint16_t *B, long ldb, const float *bias,
                           const uint16_t *U, long ldu, uint16_t *C0, uint16_t *C1, long ldc, int M, int N, int K,
@@ -442,9 +264,7 @@ static void gemm_dispatch(int variant, const uint16_t *A, long lda, const uint16
     case 1: gemm_launch<EPI, 1>(A, lda, B, ldb, bias, U, ldu, C0, C1, ldc, M, N, K, stamp, st); break;
     case 2: gemm_launch<EPI, 2>(A, lda, B, ldb, bias, U, ldu, C0, C1, ldc, M, N, K, stamp, st); break;
     case 3: gemm_launch<EPI, 3>(A, lda, B, ldb, bias, U, ldu, C0, C1, ldc, M, N, K, stamp, st); break;
-    case 4: gemm_launch<EPI, 4>(A, lda, B, ldb, bias, U, ldu, C0, C1, ldc, M, N, K, stamp, st); break;
-    case 5: gemm_launch_pf<EPI, 256, 128, 3>(A, lda, B, ldb, bias, U, ldu, C0, C1, ldc, M, N, K, stamp, st); break;
-    default: gemm_launch_pf<EPI, 128, 128, 2>(A, lda, B, ldb, bias, U, ldu, C0, C1, ldc, M, N, K, stamp, st); break;
+    default: gemm_launch<EPI, 4>(A, lda, B, ldb, bias, U, ldu, C0, C1, ldc, M, N, K, stamp, st); break;
     }
 }
 
@@ -453,7 +273,7 @@ extern "C" int irads_gemm_nt_variant(int variant, int epilogue, const uint16_t *
                                      uint16_t *C1, long ldc, int M, int N, int K, void *stream) {
     long long *stamp = (long long *)take_stamp();  // irads_stamp_next's region for this launch, or null
     IRADS_REQUIRE(epilogue >= 0 && epilogue <= 2, "irads_gemm_nt: epilogue %d", epilogue);
-    IRADS_REQUIRE(variant >= 0 && variant <= 6, "irads_gemm_nt: variant %d", variant);
+    IRADS_REQUIRE(variant >= 0 && variant <= 4, "irads_gemm_nt: variant %d", variant);
     IRADS_REQUIRE(variant != 4 || N % 256 == 0, "irads_gemm_nt: the 256 x 256 tiling needs N %% 256 == 0 (N=%d)", N);
     IRADS_REQUIRE(M >= 0 && N > 0 && K > 0 && N % GBN == 0 && K % GBK == 0,
                   "irads_gemm_nt: needs N %% 128 == 0 and K %% 64 == 0 (M=%d N=%d K=%d)", M, N, K);

@@ -71,7 +71,7 @@ def main():
             row["lib_us"] = timed(lambda: F.linear(A, W, bias))
             row["irads_us"] = timed(lambda: gemm(0, A, W, bias32))
             for v in VARIANTS:
-                if v == 4 and Nn % 256:
+                if v >= 4 and Nn % 256:
                     continue
                 row[f"irads_v{v}_us"] = timed(lambda: gemm(0, A, W, bias32, variant=v))
                 assert torch.equal(gemm(0, A, W, bias32, variant=v), mine)
@@ -99,7 +99,7 @@ def main():
             row["lib_us"] = timed(lambda: torch.mm(dY, W))
             row["irads_us"] = timed(lambda: gemm(0, dY, Wt))
             for v in VARIANTS:
-                if v == 4 and K % 256:
+                if v >= 4 and K % 256:
                     continue
                 row[f"irads_v{v}_us"] = timed(lambda: gemm(0, dY, Wt, variant=v))
                 assert torch.equal(gemm(0, dY, Wt, variant=v), mine)

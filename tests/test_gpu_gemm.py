@@ -37,6 +37,8 @@ def _gemm(epi, A, B, bias=None, U=None, C1=None, variant=None):
     return C0
 
 
+N_VARIANTS = 5  # irads_gemm_nt_variant tilings 0-4 (4: 256 x 256, N % 256 == 0)
+
 # (M, N, K): trunk shapes, a ragged M (tiles past M clamped / masked), a single k-step, a long K
 SHAPES = [(16384, 512, 512), (4096, 1024, 4096), (1000, 384, 128), (77, 128, 64), (2048, 2048, 1536)]
 
@@ -54,8 +56,8 @@ def test_gemm_nt_bias_vs_fp32_and_hipblaslt(M, Nn, K):
     # no bias, and every tile variant bit for bit
     nob = _gemm(0, A, W)
     assert _rel(nob, A.float() @ W.float().t()) <= 1.5 * _rel(lib, ref) + 1e-4
-    for v in range(5):
-        if v == 4 and Nn % 256:
+    for v in range(N_VARIANTS):
+        if v >= 4 and Nn % 256:
             continue
         assert torch.equal(_gemm(0, A, W, b16.float(), variant=v), mine), v
 
@@ -80,13 +82,13 @@ def test_gemm_nt_gelu_epilogues_bit_exact(M, Nn, K):
     dx = _gemm(0, dY, Wt)
     du_ref = torch.empty_like(dx)
     N.call("irads_gelu_bwd", N.ptr(U), N.ptr(dx), N.ptr(du_ref), dx.numel(), N.stream())
-    for v in range(5):
-        if not (v == 4 and Nn % 256):
+    for v in range(N_VARIANTS):
+        if not (v >= 4 and Nn % 256):
             g = torch.empty_like(plain)
             u = _gemm(1, A, W, b32, C1=g, variant=v)
             assert torch.equal(u, plain), v
             assert torch.equal(g, g_ref), v
-        if not (v == 4 and K % 256):
+        if not (v >= 4 and K % 256):
             du = _gemm(2, dY, Wt, U=U, variant=v)
             assert torch.equal(du, du_ref), v
 
