@@ -17,6 +17,8 @@
 // atomic scatter of D-wide contiguous segments (Guideline 12: 128-256 B per wave-op).
 // Compiled with -ffp-contract=off: only the explicit fma() calls fuse.
 #include "common.h"
+#include <cstdlib>
+#include <cstring>
 
 namespace irads {
 namespace {
@@ -507,9 +509,8 @@ __global__ void __launch_bounds__(256) msda_bucket_fill(const float *__restrict_
             const int m = (int)((sid / LP) % M);
             const int b = (int)(sid / ((long)LP * M * Q));
             bk[k] = sample_bucket(loc, sid, l, sH, sW, sS, b, m, M, S);
-            // the gather's whole view of the sample in one 16-B record: query, attention weight, location
-            const int q = (int)((sid / ((long)LP * M)) % Q);
-            r[k] = make_float4(__int_as_float(q), aw[sid], loc[2 * sid], loc[2 * sid + 1]);
+            // the walk's whole view of the sample in one 16-B record: sample id, attention weight, location
+            r[k] = make_float4(__int_as_float((int)sid), aw[sid], loc[2 * sid], loc[2 * sid + 1]);
         }
     }
     int slot[kSPT], base[kSPT];
@@ -533,8 +534,10 @@ __global__ void __launch_bounds__(256) msda_bucket_fill(const float *__restrict_
         if (bk[k] >= 0) rec[base[k] + slot[k]] = r[k];
 }
 
-// The fill when the grad_loc / grad_aw pass already ranked every sample in its bucket: a streaming
-// pass (location, rank, bucket offset -> one 16-B record), no atomics.  16 lanes per (b, q, m),
+// The fill when the counting loc/aw pass or msda_count_rank already ranked every sample in its bucket:
+// a streaming pass
+// (location, rank, bucket offset -> one 16-B record (sample id, attention weight, x, y) for the
+// bucket walk), no atomics.  16 lanes per (b, q, m),
 // placed as map_group does, so with M % 8 == 0 XCD x writes only the record ranges of heads x, x + 8, ...
 __global__ void __launch_bounds__(256) msda_bucket_fill_ranked(const float *__restrict__ loc,
                                                                const int64_t *__restrict__ shapes,
@@ -546,14 +549,14 @@ __global__ void __launch_bounds__(256) msda_bucket_fill_ranked(const float *__re
     load_levels(shapes, lsi, L, sH, sW, sS);
     const GroupMap gm = map_group<16>((long)bs * Q, M);
     if (!gm.valid) return;
-    const int m = gm.m, b = (int)(gm.row / Q), q = (int)(gm.row % Q);
+    const int m = gm.m, b = (int)(gm.row / Q);
     const int LP = L * P;
     const long sid0 = (gm.row * M + m) * LP;
     for (int sl = threadIdx.x % 16; sl < LP; sl += 16) {
         const long sid = sid0 + sl;
         const float lx = loc[2 * sid], ly = loc[2 * sid + 1];
         const long bk = bucket_at(lx, ly, sl / P, sH, sW, sS, b, m, M, S);
-        if (bk >= 0) rec[off[bk] + rank[sid]] = make_float4(__int_as_float(q), aw[sid], lx, ly);
+        if (bk >= 0) rec[off[bk] + rank[sid]] = make_float4(__int_as_float((int)sid), aw[sid], lx, ly);
     }
 }
 
@@ -562,7 +565,7 @@ __global__ void __launch_bounds__(256) msda_bucket_fill_ranked(const float *__re
 // round trips that outlasts the whole rest of the launch.  Such levels are split: their cells are
 // written as zeros by msda_gather_gvalue and summed by msda_gather_split, `parts` groups per cell,
 // each walking every parts-th chunk of the records and adding its partial row with float atomics.
-__device__ __forceinline__ int split_parts(int Q, int P, int H, int W) {
+__host__ __device__ __forceinline__ int split_parts(int Q, int P, int H, int W) {
     const long rec4 = 4L * Q * P / ((long)H * W);  // mean records over a cell's 4 buckets
     return rec4 > 128 ? (int)min(32L, (rec4 + 63) / 64) : 1;
 }
@@ -575,7 +578,7 @@ __device__ __forceinline__ int split_parts(int Q, int P, int H, int W) {
 template <int V, int KCM = 4>
 __device__ __forceinline__ void gather_walk(const int *__restrict__ off, const float4 *__restrict__ rec,
                                             const float *__restrict__ gout, int b, int m, int M, int D, int Q,
-                                            long bkrow, int H, int W, int y, int x, int lane, int part,
+                                            int LPM, long bkrow, int H, int W, int y, int x, int lane, int part,
                                             int parts, float4 &acc) {
     int eb[2], ee[2];  // the bounds of both ranges in one round trip
 #pragma unroll
@@ -607,7 +610,7 @@ __device__ __forceinline__ void gather_walk(const int *__restrict__ off, const f
                 if ((unsigned)dy <= 1u && (unsigned)dx <= 1u)
                     wc = dy == 0 ? (dx == 0 ? sp.nw : sp.ne) : (dx == 0 ? sp.sw : sp.se);
                 a = r.y;
-                q = __float_as_int(r.x);
+                q = (int)(((unsigned)__float_as_int(r.x) / (unsigned)LPM) % (unsigned)Q);  // the record's sample id -> query
             }
             // every grad_out row load of the chunk is issued before the first accumulation (lanes past
             // the bucket end and non-corner entries carry w = 0 and load nothing)
@@ -663,7 +666,8 @@ __global__ void __launch_bounds__(256) msda_gather_gvalue(const int64_t *__restr
     const int c = s - sS[l], y = c / W, x = c - y * W;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     if (split_parts(Q, P, H, W) == 1)  // uniform over the group; split levels: zeros, msda_gather_split adds
-        gather_walk<V>(off, rec, gout, b, m, M, D, Q, ((long)b * M + m) * S + sS[l], H, W, y, x, lane, 0, 1, acc);
+        gather_walk<V>(off, rec, gout, b, m, M, D, Q, L * P * M, ((long)b * M + m) * S + sS[l], H, W, y, x, lane, 0, 1,
+                       acc);
     *(float4 *)(gvalue + gid * D + 4 * lane) = acc;
 }
 
@@ -695,8 +699,8 @@ __device__ __forceinline__ void split_round(bool valid, int m, long it, const lo
         const int c = (int)(r % ((long)H * W));
         const int b = (int)(r / ((long)H * W));
         const int y = c / W, x = c - y * W;
-        gather_walk<V>(off, rec, gout, b, m, M, D, Q, ((long)b * M + m) * S + sS[l], H, W, y, x, lane, part, parts,
-                       acc);
+        gather_walk<V>(off, rec, gout, b, m, M, D, Q, L * P * M, ((long)b * M + m) * S + sS[l], H, W, y, x, lane, part,
+                       parts, acc);
         row = (((long)b * S + sS[l] + c) * M + m) * D;
     }
     part_row[gi][lane] = acc;
@@ -758,11 +762,11 @@ __global__ void __launch_bounds__(256) msda_gather_split(const int64_t *__restri
     }
 }
 
-// grad_loc / grad_aw: the forward's 16-B gathers, V lanes per (b, q, m).  With COUNT (V % 4 == 0, so
-// a DPP quad never straddles two groups) the pass also makes the bucket counts of msda_bucket_count
-// from the locations it already holds, and keeps each sample's rank in its bucket (the counter's
-// value before its add, + its rank among the quad lanes of that bucket): the counter round trips
-// overlap the value gathers, and the fill pass after the scan needs no atomics at all.
+// grad_loc / grad_aw by the forward's 16-B gathers, V lanes per (b, q, m): the cell-walk paths (sparse
+// samples, or D = 4, 8).  With COUNT (V % 4 == 0, so a DPP quad never straddles two groups) the pass
+// also makes the bucket counts from the locations it already holds, and keeps each sample's rank in
+// its bucket (the counter's value before its add, + its rank among the quad lanes of that bucket):
+// the counter round trips overlap the value gathers, and the fill after the scan needs no atomics.
 template <int V, bool COUNT>
 __global__ void __launch_bounds__(256) msda_bwd_locaw_vec(const float *__restrict__ value,
                                                           const int64_t *__restrict__ shapes,
@@ -858,11 +862,431 @@ __global__ void __launch_bounds__(256) msda_bwd_locaw_vec(const float *__restric
     }
 }
 
+// ------------------------------------------------------------------ bucket walk (V % 4 == 0)
+// The cell walk above reads every sample's grad_out row once per corner cell (4x) and the
+// grad_loc / grad_aw pass re-gathers all four corners of every sample: ~5.8 GB of L2 gathers per
+// DINO encoder backward.  The bucket walk reads each sample ONCE: one group per bucket (b, m, top-left
+// cell (y, x)) holds the value rows of the bucket's 2 x 2 cells, and for every record of the bucket
+// loads its grad_out row, forms the four corner dot products g_c = grad_out · v_c (shuffle sums over
+// the group), and from them the sample's complete grad_attn = Σ w_c g_c and grad_loc (the bilinear
+// weights' derivatives against the same g_c: the reference's per-channel sums, regrouped), written
+// once per sample; its grad_value contributions w_c · (grad_out · attn) (the reference's per-
+// contribution rounding) go into four register rows, one per cell of the bucket, written as partial
+// rows.  msda_gv_reduce then sums a value cell's four partials (its own bucket's top-left corner, its
+// left neighbour's top-right, upper neighbour's bottom-left, upper-left neighbour's bottom-right)
+// in that fixed order, each over the parts of split buckets in part order.
+//
+// A bucket holds the samples whose clamped top-left corner is (y, x); a sample with x0 = -1 (y0 = -1)
+// has its corner columns (rows) at -1 (outside: value 0, no gradient) and x (y), so its corners map
+// onto the bucket's cells shifted by (oy, ox) = (y0 - y, x0 - x) ∈ {-1, 0}².
+//
+// Work items: per (b, m), the cells of every level, split levels' cells `parts` times (split_parts:
+// parts walk every parts-th chunk of V records); item index ((b·M + m)·NI + first[l] + cell·parts +
+// part) with NI = first[L] (bucket_items).
+// buckets per item: one, whose records touch its 2 x 2 cells (items of two neighbouring buckets over
+// 2 x 3 cells measured slower: 132 VGPRs, 6 dot products per record)
+__host__ __device__ __forceinline__ int item_span(int) { return 1; }
+constexpr int kItemCols = 2, kItemRows = 2 * kItemCols;  // cells per item and partial rows per item
+
+__device__ __forceinline__ void bucket_items(const int *sH, const int *sW, int L, int Q, int P, long *first) {
+    first[0] = 0;
+    for (int l = 0; l < L; ++l) {
+        const int parts = split_parts(Q, P, sH[l], sW[l]), span = item_span(parts);
+        first[l + 1] = first[l] + (long)sH[l] * ((sW[l] + span - 1) / span) * parts;
+    }
+}
+
+// count + rank: 4 lanes per (b, q, m) (a DPP quad; placed as map_group: XCD x serves the bucket
+// counters of heads x, x + 8, ...), each lane LP / 4 samples with all their atomics in flight before
+// any rank is formed; step j takes samples 4j .. 4j + 3 (P consecutive points of one level, often one
+// bucket at the coarse levels), whose quad's first lane of a bucket adds for the quad, and every lane
+// keeps its rank (counter value before the add + rank in the quad).  Samples with no corner inside
+// their level get their grad_loc / grad_attn zeros here (no bucket will write them).
+constexpr int kCountSteps = 8;  // LP <= 32 (DINO: 16)
+__global__ void __launch_bounds__(256) msda_count_rank(const float *__restrict__ loc, const int64_t *__restrict__ shapes,
+                                                       const int64_t *__restrict__ lsi, int bs, int S, int M, int L,
+                                                       int Q, int P, int *__restrict__ cnt, int *__restrict__ rank,
+                                                       float *__restrict__ gloc, float *__restrict__ gaw) {
+    __shared__ int sH[kMaxLevels], sW[kMaxLevels], sS[kMaxLevels];
+    load_levels(shapes, lsi, L, sH, sW, sS);
+    const GroupMap gm = map_group<4>((long)bs * Q, M);
+    if (!gm.valid) return;  // whole quads exit together
+    const int m = gm.m, b = (int)(gm.row / Q);
+    const int LP = L * P, lane = threadIdx.x & 3;
+    const long sid0 = (gm.row * M + m) * LP;
+    for (int j0 = 0; j0 < LP; j0 += 4 * kCountSteps) {  // uniform trip counts: every quad lane takes part
+        long bk[kCountSteps];
+        int got[kCountSteps];
+        QuadAgg qa[kCountSteps];
+#pragma unroll
+        for (int j = 0; j < kCountSteps; ++j) {
+            const int sl = j0 + 4 * j + lane;
+            bk[j] = -1;
+            if (sl < LP) bk[j] = bucket_at(loc[2 * (sid0 + sl)], loc[2 * (sid0 + sl) + 1], sl / P, sH, sW, sS, b, m, M, S);
+        }
+#pragma unroll
+        for (int j = 0; j < kCountSteps; ++j) {
+            qa[j] = quad_agg((int)bk[j]);
+            got[j] = 0;
+            if (bk[j] >= 0 && qa[j].first == lane) got[j] = atomicAdd(cnt + bk[j], qa[j].count);
+        }
+#pragma unroll
+        for (int j = 0; j < kCountSteps; ++j) {
+            const int sl = j0 + 4 * j + lane;
+            const int b0 = quad_bcast<0>(got[j]), b1 = quad_bcast<1>(got[j]), b2 = quad_bcast<2>(got[j]),
+                      b3 = quad_bcast<3>(got[j]);
+            const int f = qa[j].first;
+            if (sl < LP) {
+                const long sid = sid0 + sl;
+                if (bk[j] >= 0) {
+                    rank[sid] = (f == 0 ? b0 : f == 1 ? b1 : f == 2 ? b2 : b3) + qa[j].rank;
+                } else {
+                    gaw[sid] = 0.f;
+                    gloc[2 * sid] = 0.f;
+                    gloc[2 * sid + 1] = 0.f;
+                }
+            }
+        }
+    }
+}
+
+// Count + rank without memory-side atomics (those run at ~20 G/s chip-wide for scattered addresses,
+// ~170 µs at the DINO encoder shape): kCountBlocks workgroups per (b, m) — on one XCD — each take a
+// contiguous range of queries and histogram their samples' buckets in LDS (one int per cell of the
+// head's S cells, ds_add_rtn: the sample's rank within (bucket, workgroup)), then store the histogram
+// as row kb of cntT[b, m][kCountBlocks][S].  msda_count_fold turns each bucket's column into
+// exclusive offsets and its total into cnt[bucket] for the bucket scan; a sample's record lands at
+// off[bucket] + cntT[b, m][kb][cell] + rank (msda_fill_lds: the same workgroups, both terms of
+// their cells staged in LDS).
+constexpr int kCountBlocks = 16;
+constexpr long kCountLdsCells = 38 * 1024;  // S * 4 B of LDS per workgroup (below: the atomic count)
+
+constexpr int kCountThreads = 1024;  // 16 waves: the one workgroup per CU its LDS allows keeps loads in flight
+__global__ void __launch_bounds__(kCountThreads) msda_count_lds(const float *__restrict__ loc, const int64_t *__restrict__ shapes,
+                                                      const int64_t *__restrict__ lsi, int bs, int S, int M, int L,
+                                                      int Q, int P, int *__restrict__ cntB, int *__restrict__ rank,
+                                                      float *__restrict__ gloc, float *__restrict__ gaw) {
+    extern __shared__ int hist[];  // S counters of this (b, m)
+    __shared__ int sH[kMaxLevels], sW[kMaxLevels], sS[kMaxLevels];
+    for (int c = threadIdx.x; c < S; c += kCountThreads) hist[c] = 0;
+    load_levels(shapes, lsi, L, sH, sW, sS);  // its barrier also publishes the zeroed histogram
+    const int lid = (int)xcd_remap(blockIdx.x, gridDim.x);  // the blocks of one (b, m) on one XCD
+    const int bm = lid / kCountBlocks, kb = lid - bm * kCountBlocks;
+    const int b = bm / M, m = bm - b * M;
+    const int LP = L * P, qc = (Q + kCountBlocks - 1) / kCountBlocks;
+    const int q0 = kb * qc, nq = max(0, min(Q, q0 + qc) - q0);
+    const long bk0 = (long)bm * S;  // bucket of cell 0 of this (b, m)
+    for (int i = threadIdx.x; i < nq * LP; i += kCountThreads) {
+        const int q = q0 + i / LP, sl = i - (i / LP) * LP;
+        const long sid = (((long)b * Q + q) * M + m) * LP + sl;
+        const long bk = bucket_at(loc[2 * sid], loc[2 * sid + 1], sl / P, sH, sW, sS, b, m, M, S);
+        if (bk >= 0) {
+            rank[sid] = atomicAdd(&hist[bk - bk0], 1);
+        } else {
+            gaw[sid] = 0.f;
+            gloc[2 * sid] = 0.f;
+            gloc[2 * sid + 1] = 0.f;
+        }
+    }
+    __syncthreads();
+    int *row = cntB + ((long)bm * kCountBlocks + kb) * S;
+    for (int c = threadIdx.x; c < S; c += kCountThreads) row[c] = hist[c];
+}
+
+// per bucket: exclusive offsets over the kCountBlocks workgroups (in place) and the total
+__global__ void __launch_bounds__(256) msda_count_fold(int *__restrict__ cntT, long nb, int S, int *__restrict__ cnt) {
+    const long bk = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (bk >= nb) return;
+    const long bm = bk / S, c = bk - bm * S;
+    int *col = cntT + bm * kCountBlocks * S + c;
+    int v[kCountBlocks];
+#pragma unroll
+    for (int j = 0; j < kCountBlocks; ++j) v[j] = col[(long)j * S];
+    int run = 0;
+#pragma unroll
+    for (int j = 0; j < kCountBlocks; ++j) {
+        col[(long)j * S] = run;
+        run += v[j];
+    }
+    cnt[bk] = run;
+}
+
+// the fill for msda_count_lds's ranks, by the same workgroups over the same samples: the record
+// base of each cell of this (b, m) for this workgroup, off[bucket] + cntT[b, m][kb][cell], staged in
+// LDS (two coalesced reads per cell), so each sample costs one location / rank / weight read and one
+// 16-B record store (sample id, attention weight, x, y)
+__global__ void __launch_bounds__(kCountThreads) msda_fill_lds(const float *__restrict__ loc, const int64_t *__restrict__ shapes,
+                                                               const int64_t *__restrict__ lsi, int bs, int S, int M, int L,
+                                                               int Q, int P, const float *__restrict__ aw,
+                                                               const int *__restrict__ off, const int *__restrict__ cntT,
+                                                               const int *__restrict__ rank, float4 *__restrict__ rec) {
+    extern __shared__ int base[];  // S record bases
+    __shared__ int sH[kMaxLevels], sW[kMaxLevels], sS[kMaxLevels];
+    const int lid = (int)xcd_remap(blockIdx.x, gridDim.x);
+    const int bm = lid / kCountBlocks, kb = lid - bm * kCountBlocks;
+    const int b = bm / M, m = bm - b * M;
+    const long bk0 = (long)bm * S;
+    const int *row = cntT + ((long)bm * kCountBlocks + kb) * S;
+    for (int c = threadIdx.x; c < S; c += kCountThreads) base[c] = off[bk0 + c] + row[c];
+    load_levels(shapes, lsi, L, sH, sW, sS);  // its barrier also publishes base[]
+    const int LP = L * P, qc = (Q + kCountBlocks - 1) / kCountBlocks;
+    const int q0 = kb * qc, nq = max(0, min(Q, q0 + qc) - q0);
+    for (int i = threadIdx.x; i < nq * LP; i += kCountThreads) {
+        const int q = q0 + i / LP, sl = i - (i / LP) * LP;
+        const long sid = (((long)b * Q + q) * M + m) * LP + sl;
+        const float lx = loc[2 * sid], ly = loc[2 * sid + 1];
+        const long bk = bucket_at(lx, ly, sl / P, sH, sW, sS, b, m, M, S);
+        if (bk >= 0) rec[base[bk - bk0] + rank[sid]] = make_float4(__int_as_float((int)sid), aw[sid], lx, ly);
+    }
+}
+
+__device__ __forceinline__ float dot4(float4 a, float4 b) { return a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w; }
+
+// sum over a V-lane group by DPP (no LDS traffic): quad butterflies, then the half-row and row mirrors
+// (lane i of 8 / 16 reads lane 7 - i / 15 - i, the other half); every lane ends with the same sum.
+// V = 32, 64: the shuffle sum.
+template <int V>
+__device__ __forceinline__ float group_sum_dpp(float v) {
+    if constexpr (V > 16) {
+        return group_sum<float, V>(v);
+    } else {
+        auto dpp = [](float x, auto ctrl) {
+            return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), decltype(ctrl)::value, 0xF, 0xF, false));
+        };
+        if constexpr (V >= 2) v += dpp(v, std::integral_constant<int, 0xB1>{});   // quad_perm [1, 0, 3, 2]
+        if constexpr (V >= 4) v += dpp(v, std::integral_constant<int, 0x4E>{});   // quad_perm [2, 3, 0, 1]
+        if constexpr (V >= 8) v += dpp(v, std::integral_constant<int, 0x141>{});  // row_half_mirror
+        if constexpr (V >= 16) v += dpp(v, std::integral_constant<int, 0x140>{}); // row_mirror
+        return v;
+    }
+}
+
+template <int V>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(V <= 16 ? 4 : 1))) msda_bucket_walk(const float *__restrict__ value, const int64_t *__restrict__ shapes,
+                                                        const int64_t *__restrict__ lsi, const float *__restrict__ gout,
+                                                        int bs, int S, int M, int D, int L, int Q, int P,
+                                                        const int *__restrict__ off, const float4 *__restrict__ rec,
+                                                        float *__restrict__ gloc, float *__restrict__ gaw,
+                                                        float4 *__restrict__ part_rows, long NIM) {
+    __shared__ int sH[kMaxLevels], sW[kMaxLevels], sS[kMaxLevels];
+    __shared__ long first[kMaxLevels + 1];
+    // per group, the chunk's records as its lanes need them: (attention weight, the weights onto the
+    // item's six cells, query) — written by the record's lane, read back as broadcasts
+    __shared__ __attribute__((aligned(16))) float bc[256 / V][V][8];
+    load_levels(shapes, lsi, L, sH, sW, sS);
+    if (threadIdx.x == 0) bucket_items(sH, sW, L, Q, P, first);
+    __syncthreads();
+    // groups over bs x NIM items per head (NIM >= NI = first[L], the host's bound: bucket_items_bound)
+    const GroupMap gm = map_group<V>((long)bs * NIM, M);
+    const int lane = threadIdx.x % V;
+    if (!gm.valid) return;  // whole group exits together
+    const int m = gm.m, b = (int)(gm.row / NIM);
+    const long it = gm.row - (long)b * NIM;  // item within (b, m)
+    if (it >= first[L]) return;
+    int l = 0;
+    for (int k = 1; k < L; ++k) l = it >= first[k] ? k : l;
+    const int H = sH[l], W = sW[l], parts = split_parts(Q, P, H, W), span = item_span(parts);
+    const int nx = (W + span - 1) / span;  // items per row of cells
+    const long r = it - first[l];
+    const int part = (int)(r % parts), ci = (int)(r / parts);
+    const int y = ci / nx, x = (ci - y * nx) * span;  // the item's first bucket (y, x)
+    const int nbk = min(span, W - x);                  // its buckets: (y, x) .. (y, x + nbk - 1)
+    const long cs = (long)M * D;
+    // the item's 2 x 3 cells: rows y, y + 1, columns x .. x + 2 (zero outside the level)
+    const float *vb = value + ((long)b * S + sS[l]) * cs + (long)m * D + 4 * lane;
+    const long bk = ((long)b * M + m) * S + sS[l] + (long)y * W + x;
+    const int e1 = off[bk + nbk];
+    const int e0 = off[bk] + part * V;
+    if (e0 >= e1) return;  // uniform over the group: an empty (item, part) has no partials (the reduce skips it)
+    float4 v[2][kItemCols];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < kItemCols; ++j) {
+            v[i][j] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (y + i < H && x + j < W && j <= nbk)  // uniform over the group
+                v[i][j] = *(const float4 *)(vb + ((long)(y + i) * W + x + j) * cs);
+        }
+    float4 acc[2][kItemCols];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < kItemCols; ++j) acc[i][j] = make_float4(0.f, 0.f, 0.f, 0.f);
+    const int LPM = L * P * M;
+    const int step = parts * V;
+    float(*gbc)[8] = bc[threadIdx.x / V];
+    float4 rn = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (e0 + lane < e1) rn = rec[e0 + lane];
+    for (int e = e0; e < e1; e += step) {
+        const float4 rr = rn;  // lane j: record e + j = (sample id, attention weight, x, y)
+        if (e + step + lane < e1) rn = rec[e + step + lane];
+        const bool have = e + lane < e1;
+        // lane j locates its own record: corner (i, j) of the sample (rows y0 + i, columns x0 + j)
+        // lands on the item's cell (i - oy, dx + j - ox), oy / ox = 1 where the clamped corner row /
+        // column is -1, dx = the record's bucket column - x; w[r][c]: the corner weight on cell (r, c)
+        long sid = 0;
+        int q = 0, oy = 0, cx = 0;  // cx = dx - ox: the column of the sample's x0 within the item
+        float a = 0.f;
+        Samp<float> sp{0, 0, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        float w[2][kItemCols];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < kItemCols; ++j) w[i][j] = 0.f;
+        if (have) {
+            sid = (long)(unsigned)__float_as_int(rr.x);
+            q = (int)(((unsigned)sid / (unsigned)LPM) % (unsigned)Q);  // sample ids < 2^31 (gather_ws_layout)
+            a = rr.y;
+            sp = locate(rr.z, rr.w, H, W);
+            oy = sp.y0 < y ? 1 : 0;
+            cx = sp.x0 - x;  // -1 .. nbk - 1
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < kItemCols; ++j) {
+                    const int si = i + oy, sj = j - cx;  // the sample's corner on cell (i, j)
+                    const float wc = si == 0 ? (sj == 0 ? sp.nw : sp.ne) : (sj == 0 ? sp.sw : sp.se);
+                    w[i][j] = (si <= 1 && (unsigned)sj <= 1u) ? wc : 0.f;
+                }
+        }
+        static_assert(kItemCols == 2, "the broadcast slots hold a 2 x 2 block");
+        *(float4 *)gbc[lane] = make_float4(a, w[0][0], w[0][1], w[1][0]);
+        *(float2 *)(gbc[lane] + 4) = make_float2(w[1][1], __int_as_float(q));
+        float mg[2][kItemCols];  // this lane's record: grad_out · the item's cells
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < kItemCols; ++j) mg[i][j] = 0.f;
+        constexpr int KC = V < 4 ? V : 4;
+#pragma unroll
+        for (int k0 = 0; k0 < V; k0 += KC) {
+            if (k0 > 0 && e + k0 >= e1) break;  // uniform: past the range end
+            float4 go[KC];
+#pragma unroll
+            for (int k = 0; k < KC; ++k) {  // every grad_out row of the batch in flight first
+                const int qk = __float_as_int(gbc[k0 + k][5]);
+                go[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (e + k0 + k < e1) go[k] = *(const float4 *)(gout + (((long)b * Q + qk) * M + m) * D + 4 * lane);
+            }
+#pragma unroll
+            for (int k = 0; k < KC; ++k) {
+                if (e + k0 + k >= e1) break;  // uniform over the group
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int j = 0; j < kItemCols; ++j) {
+                        const float d = group_sum_dpp<V>(dot4(go[k], v[i][j]));
+                        if (lane == k0 + k) mg[i][j] = d;
+                    }
+                // grad_value: w_corner · (grad_out · attn) into the cell each corner lands on
+                const float4 r0 = *(const float4 *)gbc[k0 + k];
+                const float ak = r0.x, u[2][kItemCols] = {{r0.y, r0.z}, {r0.w, gbc[k0 + k][4]}};
+                const float4 ga = make_float4(go[k].x * ak, go[k].y * ak, go[k].z * ak, go[k].w * ak);
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int j = 0; j < kItemCols; ++j) {
+                        acc[i][j].x += u[i][j] * ga.x;
+                        acc[i][j].y += u[i][j] * ga.y;
+                        acc[i][j].z += u[i][j] * ga.z;
+                        acc[i][j].w += u[i][j] * ga.w;
+                    }
+            }
+        }
+        if (have) {  // the sample's corners among the item's cells (zero outside), then its gradients
+            float g[2][2];
+#pragma unroll
+            for (int si = 0; si < 2; ++si)
+#pragma unroll
+                for (int sj = 0; sj < 2; ++sj) {
+                    const int i = si - oy, j = cx + sj;  // cell of corner (si, sj)
+                    float gv = 0.f;
+#pragma unroll
+                    for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+                        for (int jj = 0; jj < kItemCols; ++jj) gv = (i == ii && j == jj) ? mg[ii][jj] : gv;
+                    g[si][sj] = gv;
+                }
+            gaw[sid] = sp.nw * g[0][0] + sp.ne * g[0][1] + sp.sw * g[1][0] + sp.se * g[1][1];
+            gloc[2 * sid] = a * ((g[0][1] - g[0][0]) * (1.f - sp.fy) + (g[1][1] - g[1][0]) * sp.fy) * (float)W;
+            gloc[2 * sid + 1] = a * ((g[1][0] - g[0][0]) * (1.f - sp.fx) + (g[1][1] - g[0][1]) * sp.fx) * (float)H;
+        }
+    }
+    // the partial rows of this (item, part): [item][cell (i, j) row-major][V lanes]
+    float4 *pr = part_rows + (((long)b * M + m) * NIM + it) * kItemRows * V + lane;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < kItemCols; ++j) pr[(kItemCols * i + j) * V] = acc[i][j];
+}
+
+// grad_value row of cell (b, s, m): the partials of the items whose 2 x kItemCols cells contain it, in
+// a fixed order (item row y, then y - 1; columns left to right; parts in order)
+template <int V>
+__global__ void __launch_bounds__(256) msda_gv_reduce(const int64_t *__restrict__ shapes, const int64_t *__restrict__ lsi,
+                                                      int bs, int S, int M, int D, int L, int Q, int P,
+                                                      const float4 *__restrict__ part_rows, long NIM,
+                                                      const int *__restrict__ off, float *__restrict__ gvalue) {
+    __shared__ int sH[kMaxLevels], sW[kMaxLevels], sS[kMaxLevels];
+    __shared__ long first[kMaxLevels + 1];
+    load_levels(shapes, lsi, L, sH, sW, sS);
+    if (threadIdx.x == 0) bucket_items(sH, sW, L, Q, P, first);
+    __syncthreads();
+    const GroupMap gm = map_group<V>((long)bs * S, M);
+    const int lane = threadIdx.x % V;
+    if (!gm.valid) return;
+    const int m = gm.m;
+    const int s = (int)(gm.row % S), b = (int)(gm.row / S);
+    const int l = level_of(s, sS, L);
+    const int H = sH[l], W = sW[l], parts = split_parts(Q, P, H, W), span = item_span(parts);
+    const int nx = (W + span - 1) / span;
+    const int c = s - sS[l], y = c / W, x = c - y * W;
+    const float4 *base = part_rows + (((long)b * M + m) * NIM + first[l]) * kItemRows * V + lane;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    const long bkl = ((long)b * M + m) * S + sS[l];  // bucket of cell 0 of this level
+    auto add = [&](int iy, int ix, int cell) {  // item (iy, ix-th of its row), its cell (i, j) row-major
+        const float4 *p = base + (((long)iy * nx + ix) * parts * kItemRows + cell) * V;
+        const long bk = bkl + (long)iy * W + ix * span;
+        const int r0 = off[bk], r1 = off[bk + min(span, W - ix * span)];
+        const int np = min(parts, (r1 - r0 + V - 1) / V);  // parts with records (the walk wrote only those)
+        for (int k0 = 0; k0 < np; k0 += 4) {  // the parts in order, 4 loads in flight
+            float4 t[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) t[k] = k0 + k < np ? p[(long)(k0 + k) * kItemRows * V] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if (k0 + k >= np) break;
+                acc.x += t[k].x;
+                acc.y += t[k].y;
+                acc.z += t[k].z;
+                acc.w += t[k].w;
+            }
+        }
+    };
+    // items covering column x: those starting at x - j for j = 0 .. span (multiples of span)
+    for (int i = 0; i < 2; ++i) {
+        const int iy = y - i;
+        if (iy < 0) break;
+        for (int j = span; j >= 0; --j) {
+            const int x0 = x - j;
+            if (x0 < 0 || x0 % span) continue;
+            add(iy, x0 / span, kItemCols * i + j);
+        }
+    }
+    *(float4 *)(gvalue + (((long)b * S + s) * M + m) * D + 4 * lane) = acc;
+}
+
 struct GatherWs {
     int *cnt, *off, *bsum, *total, *rank;
-    float4 *rec;
+    float4 *rec, *part_rows;  // part_rows: the bucket walk's partial grad_value rows (V % 4 == 0)
+    int *cntb;                // msda_count_lds's per-(bucket, workgroup) counts (V % 4 == 0)
     long nb, n, nblk;
 };
+
+// Bound on the bucket walk's items per (b, m) without the level shapes (device memory): a split
+// level has parts <= rec4 / 64 + 1 with rec4 <= 4·Q·P / (H·W), so parts·H·W <= Q·P / 16 + H·W, and the
+// levels' cells sum to S: items <= S + L·(Q·P / 16 + 1).
+long bucket_items_bound(int S, int L, int Q, int P) { return (long)S + (long)L * ((long)Q * P / 16 + 1); }
 
 // workspace carve-up (256-B aligned pieces); bytes == 0 when the gather path does not apply
 long gather_ws_layout(int bs, int S, int M, int D, int L, int Q, int P, char *base, GatherWs *ws) {
@@ -873,9 +1297,12 @@ long gather_ws_layout(int bs, int S, int M, int D, int L, int Q, int P, char *ba
     const long nblk = (nb + 1023) / 1024;
     if (nblk > 256L * 64) return 0;
     auto al = [](long b) { return (b + 255) / 256 * 256; };
+    // the bucket walk's partial rows (V % 4 == 0): kItemRows rows of D floats per item
+    const long n_part = V % 4 == 0 ? (long)bs * M * bucket_items_bound(S, L, Q, P) * kItemRows * D * 4 : 0;
     const long o_cnt = 0, o_off = o_cnt + al(4 * nb), o_bsum = o_off + al(4 * (nb + 1)),
                o_tot = o_bsum + al(4 * nblk), o_rec = o_tot + 256, o_rank = o_rec + al(16 * n),
-               end = o_rank + al(4 * n);
+               o_part = o_rank + al(4 * n), o_cntb = o_part + al(n_part),
+               end = o_cntb + (V % 4 == 0 ? al(4 * nb * kCountBlocks) : 0);
     if (ws) {
         ws->cnt = (int *)(base + o_cnt);
         ws->off = (int *)(base + o_off);
@@ -883,6 +1310,8 @@ long gather_ws_layout(int bs, int S, int M, int D, int L, int Q, int P, char *ba
         ws->total = (int *)(base + o_tot);
         ws->rec = (float4 *)(base + o_rec);
         ws->rank = (int *)(base + o_rank);
+        ws->part_rows = n_part ? (float4 *)(base + o_part) : nullptr;
+        ws->cntb = V % 4 == 0 ? (int *)(base + o_cntb) : nullptr;
         ws->nb = nb;
         ws->n = n;
         ws->nblk = nblk;
@@ -1029,9 +1458,66 @@ extern "C" int irads_msda_bwd_gather(const float *value, const int64_t *shapes, 
     const int V = D / 4;
     auto g1 = [](long n) { return dim3((unsigned)((n + 255) / 256)); };
     msda_zero_ints<<<g1(ws.nb), 256, 0, st>>>(ws.cnt, ws.nb);
+    auto scans = [&]() {
+        msda_scan_blocks<<<(unsigned)ws.nblk, 256, 0, st>>>(ws.cnt, ws.nb, ws.off, ws.bsum);
+        msda_scan_totals<<<1, 256, 0, st>>>(ws.bsum, (int)ws.nblk, ws.total);
+        msda_scan_add<<<g1(ws.nb), 256, 0, st>>>(ws.off, ws.nb, ws.bsum, ws.total, ws.cnt);
+    };
+    // Dense samples (>= 4 per bucket on average: the DINO encoder, 16): LDS count + rank, scan, fill,
+    // bucket walk (grad_loc / grad_attn per sample, partial grad_value rows per bucket), fixed-order
+    // reduce of the partials.  Sparse ones (the decoder's 2 200 queries over the same 22 223 cells,
+    // 1.6 per bucket): most buckets are empty or hold one record, and the cell walk below is faster.
+    // IRADS_MSDA_WALK=bucket|cell forces either path (tests: both on every shape)
+    const char *force = getenv("IRADS_MSDA_WALK");
+    const bool dense = force && !strcmp(force, "bucket") ? true
+                       : force && !strcmp(force, "cell") ? false
+                                                         : (long)Q * L * P >= 4L * S;
+    if (V % 4 == 0 && dense) {
+        const long nim = bucket_items_bound(S, L, Q, P);
+        const bool lds_count = S <= kCountLdsCells;
+        if (ws.n > 0 && lds_count) {
+            static bool attr = [] {  // > 64 KiB of dynamic LDS
+                return hipFuncSetAttribute((const void *)msda_count_lds, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)(kCountLdsCells * 4)) == hipSuccess;
+            }();
+            (void)attr;
+            msda_count_lds<<<(unsigned)((long)bs * M * kCountBlocks), kCountThreads, (size_t)S * 4, st>>>(
+                loc, shapes, level_start, bs, S, M, L, Q, P, ws.cntb, ws.rank, grad_loc, grad_aw);
+            msda_count_fold<<<g1(ws.nb), 256, 0, st>>>(ws.cntb, ws.nb, S, ws.cnt);
+        } else if (ws.n > 0) {
+            msda_count_rank<<<group_grid((long)bs * Q, M, 4), 256, 0, st>>>(loc, shapes, level_start, bs, S, M, L, Q, P,
+                                                                           ws.cnt, ws.rank, grad_loc, grad_aw);
+        }
+        scans();
+        if (ws.n > 0 && lds_count) {
+            static bool attr = [] {
+                return hipFuncSetAttribute((const void *)msda_fill_lds, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)(kCountLdsCells * 4)) == hipSuccess;
+            }();
+            (void)attr;
+            msda_fill_lds<<<(unsigned)((long)bs * M * kCountBlocks), kCountThreads, (size_t)S * 4, st>>>(
+                loc, shapes, level_start, bs, S, M, L, Q, P, aw, ws.off, ws.cntb, ws.rank, ws.rec);
+        }
+        else if (ws.n > 0)
+            msda_bucket_fill_ranked<<<group_grid((long)bs * Q, M, 16), 256, 0, st>>>(
+                loc, shapes, level_start, bs, S, M, L, Q, P, aw, ws.off, ws.rank, ws.rec);
+#define IRADS_MSDA_W(VV)                                                                                              \
+    case VV:                                                                                                          \
+        msda_bucket_walk<VV><<<group_grid((long)bs * nim, M, VV), 256, 0, st>>>(                                      \
+            value, shapes, level_start, grad_out, bs, S, M, D, L, Q, P, ws.off, ws.rec, grad_loc, grad_aw,            \
+            ws.part_rows, nim);                                                                                       \
+        msda_gv_reduce<VV><<<group_grid((long)bs * S, M, VV), 256, 0, st>>>(shapes, level_start, bs, S, M, D, L, Q, P, \
+                                                                          ws.part_rows, nim, ws.off, grad_value);     \
+        break;
+        switch (V) { IRADS_MSDA_W(4) IRADS_MSDA_W(8) IRADS_MSDA_W(16) IRADS_MSDA_W(32) IRADS_MSDA_W(64) }
+#undef IRADS_MSDA_W
+        return check_launch("irads_msda_bwd_gather");
+    }
+    // Cell walk: grad_loc / grad_attn by the forward's gathers (V % 4 == 0: counting the buckets and
+    // ranking the samples beside them; D = 4, 8: a separate count pass and the atomic fill), scan,
+    // fill, grad_value gathered per cell (msda_gather_gvalue + msda_gather_split)
     auto gs = [](long n) { return dim3((unsigned)((n + 256L * kSPT - 1) / (256L * kSPT))); };
     const dim3 gg = group_grid((long)bs * S, M, V), gq = group_grid((long)bs * Q, M, V);
-    // grad_loc / grad_aw first: for V % 4 == 0 that pass also counts the buckets
 #define IRADS_MSDA_LA(VV, CNT)                                                                                   \
     case VV:                                                                                                     \
         msda_bwd_locaw_vec<VV, CNT><<<gq, 256, 0, st>>>(value, shapes, level_start, loc, aw, grad_out, bs, S, M, \
@@ -1045,9 +1531,7 @@ extern "C" int irads_msda_bwd_gather(const float *value, const int64_t *shapes, 
         }
     }
 #undef IRADS_MSDA_LA
-    msda_scan_blocks<<<(unsigned)ws.nblk, 256, 0, st>>>(ws.cnt, ws.nb, ws.off, ws.bsum);
-    msda_scan_totals<<<1, 256, 0, st>>>(ws.bsum, (int)ws.nblk, ws.total);
-    msda_scan_add<<<g1(ws.nb), 256, 0, st>>>(ws.off, ws.nb, ws.bsum, ws.total, ws.cnt);
+    scans();
     if (ws.n > 0 && V % 4)
         msda_bucket_fill<<<gs(ws.n), 256, 0, st>>>(loc, shapes, level_start, bs, S, M, L, Q, P, aw, ws.off, ws.cnt,
                                                    ws.rec);

@@ -306,15 +306,21 @@ def test_reference_driver_import_surface():
 
 def test_msda_gather_workspace_query(lib):
     """irads_msda_bwd_workspace_bytes is a pure size query (no GPU work): counters (bs*M*S), their
-    exclusive scan, one 16-B record and one int rank per sample; 0 where the gather backward does
-    not apply."""
+    exclusive scan, one 16-B record and one int rank per sample, and for D = 4·V with V % 4 == 0 the
+    bucket walk's per-workgroup counts (16 per bucket) and partial rows (4 rows of D floats per item,
+    items bounded by S + L·(Q·P/16 + 1) per (b, m)); 0 where the gather backward does not apply."""
     q = lib.irads_msda_bwd_workspace_bytes
     q.restype = ctypes.c_long
     bs, S, M, D, L, Q, P = 2, 22223, 8, 32, 4, 22223, 4
     n = q(0, bs, S, M, D, L, Q, P)
-    need = 4 * (2 * bs * M * S) + (16 + 4) * bs * Q * M * L * P
+    items = S + L * (Q * P // 16 + 1)
+    need = 4 * (2 * bs * M * S) + (16 + 4) * bs * Q * M * L * P + 4 * 16 * bs * M * S + 4 * D * 4 * bs * M * items
     assert n >= need
     assert n < need + 8192 + 4 * (bs * M * S // 1024 + 1)
+    # D = 8 (V = 2): the cell walk, no walk pieces
+    n8 = q(0, bs, S, M, 8, L, Q, P)
+    need8 = 4 * (2 * bs * M * S) + (16 + 4) * bs * Q * M * L * P
+    assert need8 <= n8 < need8 + 8192 + 4 * (bs * M * S // 1024 + 1)
     assert q(2, bs, S, M, D, L, Q, P) == 0  # fp64: the scatter kernel
     assert q(0, bs, S, M, 30, L, Q, P) == 0  # D not 4 * 2^k
     assert q(0, bs, S, M, 24, L, Q, P) == 0

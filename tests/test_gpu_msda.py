@@ -191,9 +191,10 @@ def test_fp32_vector_path_bitexact_vs_scalar_path(D):
     torch.testing.assert_close(vec.double(), ref, atol=1e-5, rtol=1e-5)
 
 
+@pytest.mark.parametrize("walk", ["auto", "bucket", "cell"])
 @pytest.mark.parametrize("D,case", [(4, "edges"), (16, "edges"), (32, "edges"), (64, "edges"), (256, "edges"),
                                     (32, "split"), (8, "split")])
-def test_fp32_gather_backward_vs_scatter_and_fp64(D, case):
+def test_fp32_gather_backward_vs_scatter_and_fp64(D, case, walk, monkeypatch):
     """The atomic-free fp32 backward (irads_msda_bwd_gather: samples bucketed by corner cell,
     grad_value gathered per cell and written once) against the atomic-scatter kernel on the same
     fp32 inputs and against the fp64 kernel (itself pinned to the reference above).  Locations
@@ -202,8 +203,12 @@ def test_fp32_gather_backward_vs_scatter_and_fp64(D, case):
     (their gradient rows must come out zero, not stale: grad_value is allocated uninitialised).
     Case "split": coarse levels with hundreds of records per cell, summed by msda_gather_split
     (several groups per cell, partial rows added with float atomics); in "edges" only the 1x1
-    level is split."""
+    level is split.  `walk`: the path the density picks ("edges": 2.7 samples per bucket, the cell
+    walk; "split": 25, the bucket walk), or either one forced (IRADS_MSDA_WALK; D = 4, 8 always take
+    the cell walk)."""
     from irads import native as N
+    if walk != "auto":
+        monkeypatch.setenv("IRADS_MSDA_WALK", walk)
     ops = _ops()
     g = torch.Generator().manual_seed(100 + D)
     lv = [(13, 17), (7, 9), (1, 1), (4, 5)] if case == "edges" else [(13, 17), (6, 5), (2, 3), (1, 1)]
