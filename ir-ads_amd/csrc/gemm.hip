@@ -22,6 +22,9 @@
 // Shapes: K % 64 == 0, N % 128 == 0, lda / ldb / ldc multiples of 8; M free (rows past M clamped on
 // load, masked on store).
 #include "common.h"
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
 
 namespace irads {
 namespace {
@@ -67,6 +70,28 @@ __device__ __forceinline__ gbf16x8 g_frag(const unsigned char *img, int rb, int 
     return *(const gbf16x8 *)(img + row * 128 + ((c ^ (row & 7)) << 4));
 }
 
+// GELU / GELU' by table in the 256 x 256 tiling's epilogues: for every bf16 U whose exponent field is
+// in [kTabE0, kTabE0 + kTabNE) (|U| in [2^-23, 2^9)), bf16(GELU(U)) and the fp32 GELU'(U) are
+// precomputed by gemm_gelu_table_kernel with the epilogue's own g_gelu / g_gelu_grad — so a lookup is
+// bit for bit the formula — and staged in LDS beside the k-step buffers; other U (zero, tiny, huge,
+// Inf / NaN) take the formula.  The erf formula cost ~20 (GELU) / ~27 (GELU') VALU instructions per
+// element, at 2 waves per SIMD the longest phase of a 256 x 256 tile.
+constexpr int kTabE0 = 104, kTabNE = 32, kTabN = 2 * kTabNE * 128;  // entries: sign x exponent x mantissa
+__device__ __forceinline__ int gelu_tab_index(unsigned b, bool &in) {
+    const int ex = (int)((b >> 7) & 0xFF) - kTabE0;
+    in = (unsigned)ex < (unsigned)kTabNE;
+    return (int)((b >> 15) << 12) | (ex << 7) | (int)(b & 0x7F);
+}
+
+__global__ void gemm_gelu_table_kernel(unsigned short *__restrict__ g, float *__restrict__ dg) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= kTabN) return;
+    const unsigned b = ((unsigned)(i >> 12) << 15) | ((unsigned)(((i >> 7) & (kTabNE - 1)) + kTabE0) << 7) | (i & 0x7F);
+    const float u = bf2f((unsigned short)b);
+    g[i] = f2bf(g_gelu(u));
+    dg[i] = g_gelu_grad(u);
+}
+
 // BMT x BNT tile on (BMT / WR) x (BNT / 64) waves, each WR x 64 (WR / 16 x 4 MFMA blocks)
 template <int EPI, int NS, int BMT, int BNT, int WR, bool TR = false>
 __global__ void __launch_bounds__((BMT / WR) * (BNT / 64) * 64) gemm_nt_bf16(const unsigned short *__restrict__ A, long lda,
@@ -74,7 +99,8 @@ __global__ void __launch_bounds__((BMT / WR) * (BNT / 64) * 64) gemm_nt_bf16(con
                                                     const float *__restrict__ bias,
                                                     const unsigned short *__restrict__ U, long ldu,
                                                     unsigned short *__restrict__ C0, unsigned short *__restrict__ C1,
-                                                    long ldc, int M, int N, int K, long long *trace = nullptr) {
+                                                    long ldc, int M, int N, int K, long long *trace = nullptr,
+                                                    const unsigned char *__restrict__ gtab = nullptr) {
     // TR: wave 0 of every workgroup logs wall_clock64() at entry, after each k-step's barrier, after the
     // main loop and at exit into trace[blockIdx.x * (K / 64 + 3) ...] (irads_gemm_nt_trace, A/B only)
     constexpr int NWN = BNT / 64, NW = (BMT / WR) * NWN, MI = WR / 16;
@@ -85,7 +111,20 @@ __global__ void __launch_bounds__((BMT / WR) * (BNT / 64) * 64) gemm_nt_bf16(con
     // exit (bench.py times the window-attention launch before this GEMM up to this GEMM's start)
     unsigned long long *stamp = TR ? nullptr : (unsigned long long *)trace;
     const unsigned long long t_entry = stamp_clock(stamp);
-    __shared__ __attribute__((aligned(16))) unsigned char smem[NS * G_STAGE];  // ONE array (glds wait trap)
+    // the GELU / GELU' table (256 x 256 tiles, gtab given): 16 KiB of bf16 GELU or 32 KiB of fp32 GELU'
+    // after the k-step buffers, in the same array; copied by LDS-DMA, retired by the first k-step's wait
+    constexpr bool TAB = EPI != EPI_BIAS && BMT == 256 && BNT == 256 && NS == 2 && !TR;
+    constexpr int TAB_BYTES = !TAB ? 0 : EPI == EPI_GELU ? kTabN * 2 : kTabN * 4;
+    __shared__ __attribute__((aligned(16))) unsigned char smem[NS * G_STAGE + TAB_BYTES];  // ONE array (glds wait trap)
+    const bool use_tab = TAB && gtab != nullptr;
+    if (use_tab) {
+        const unsigned char *src = gtab + (EPI == EPI_GELU ? 0 : kTabN * 2);  // [kTabN bf16 GELU][kTabN fp32 GELU']
+#pragma unroll
+        for (int c0 = 0; c0 < TAB_BYTES / 16; c0 += NW * 64)
+            __builtin_amdgcn_global_load_lds((g_glb_void *)(src + (c0 + (int)threadIdx.x) * 16),
+                                             (g_lds_void *)(smem + NS * G_STAGE + (c0 + (int)(threadIdx.x & ~63)) * 16),
+                                             16, 0, 0);
+    }
     const int nbn = N / BNT;
     const int lid = xcd_remap(blockIdx.x, gridDim.x);  // the N tiles of an M row-band on one XCD
     const int bm = lid / nbn, bn = lid - bm * nbn;
@@ -214,16 +253,43 @@ __global__ void __launch_bounds__((BMT / WR) * (BNT / 64) * 64) gemm_nt_bf16(con
                 if (m < M) *(gu16x8 *)(C0 + o) = v[it];
             } else if (EPI == EPI_GELU) {
                 gu16x8 g;
+                int ti[8];
+                bool all_in = use_tab;
 #pragma unroll
-                for (int e = 0; e < 8; ++e) g[e] = f2bf(g_gelu(bf2f(v[it][e])));
+                for (int e = 0; e < 8; ++e) {
+                    bool in = false;
+                    ti[e] = gelu_tab_index(v[it][e], in);
+                    all_in = all_in && in;
+                }
+                if (__builtin_amdgcn_ballot_w64(!all_in) == 0) {  // uniform: every lane's 8 values in the table
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) g[e] = ((const unsigned short *)(smem + NS * G_STAGE))[ti[e]];
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) g[e] = f2bf(g_gelu(bf2f(v[it][e])));
+                }
                 if (m < M) {
                     *(gu16x8 *)(C0 + o) = v[it];
                     *(gu16x8 *)(C1 + o) = g;
                 }
             } else {
                 gu16x8 d;
+                int ti[8];
+                bool all_in = use_tab;
 #pragma unroll
-                for (int e = 0; e < 8; ++e) d[e] = f2bf(bf2f(v[it][e]) * g_gelu_grad(bf2f(uq[it][e])));
+                for (int e = 0; e < 8; ++e) {
+                    bool in = false;
+                    ti[e] = gelu_tab_index(uq[it][e], in);
+                    all_in = all_in && in;
+                }
+                if (__builtin_amdgcn_ballot_w64(!all_in) == 0) {  // uniform: every lane's 8 values in the table
+#pragma unroll
+                    for (int e = 0; e < 8; ++e)
+                        d[e] = f2bf(bf2f(v[it][e]) * ((const float *)(smem + NS * G_STAGE))[ti[e]]);
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) d[e] = f2bf(bf2f(v[it][e]) * g_gelu_grad(bf2f(uq[it][e])));
+                }
                 if (m < M) *(gu16x8 *)(C0 + o) = d;
             }
         }
@@ -243,6 +309,39 @@ using namespace irads;
 // variant: 0 = 256 x 128 tiles, 2 buffers; 1 = 256 x 128, 3 buffers (1 workgroup per CU either way);
 // 2 = 128 x 128 tiles on 4 waves, 2 buffers (64 KiB: 2 workgroups per CU); 3 = 128 x 128, 3 buffers;
 // 4 = 256 x 256 tiles on 8 waves of 128 x 64, 2 buffers (128 KiB; N % 256 == 0)
+// The GELU / GELU' tables ([kTabN bf16][kTabN fp32]), built once on the device by the first call that
+// is not inside a stream capture (stream-ordered, then a device sync, so every later stream sees them);
+// null until then (the epilogues then evaluate the formula).  IRADS_GEMM_GELU_TABLE=0 keeps the formula.
+const unsigned char *gelu_tables(hipStream_t st) {
+    static unsigned char *tab = nullptr;
+    static bool failed = false;
+    static std::mutex mu;
+    static const bool off = [] {
+        const char *e = getenv("IRADS_GEMM_GELU_TABLE");
+        return e && !strcmp(e, "0");
+    }();
+    if (off) return nullptr;
+    std::lock_guard<std::mutex> lk(mu);
+    if (!tab && !failed) {
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+        unsigned char *p = nullptr;
+        if (hipMalloc(&p, kTabN * 6) != hipSuccess) {
+            (void)hipGetLastError();
+            failed = true;
+            return nullptr;
+        }
+        gemm_gelu_table_kernel<<<(kTabN + 255) / 256, 256, 0, st>>>((unsigned short *)p, (float *)(p + kTabN * 2));
+        if (hipStreamSynchronize(st) != hipSuccess) {
+            (void)hipGetLastError();
+            failed = true;
+            return nullptr;
+        }
+        tab = p;
+    }
+    return tab;
+}
+
 template <int EPI, int V, bool TR = false>
 static void gemm_launch(const uint16_t *A, long lda, const uint16_t *B, long ldb, const float *bias, const uint16_t *U,
                         long ldu, uint16_t *C0, uint16_t *C1, long ldc, int M, int N, int K, long long *trace,
@@ -250,9 +349,10 @@ static void gemm_launch(const uint16_t *A, long lda, const uint16_t *B, long ldb
     constexpr int BMT = (V < 2 || V == 4) ? 256 : 128, NS = (V & 1) ? 3 : 2, BNT = V == 4 ? 256 : 128;
     constexpr int WR = V == 4 ? 128 : 64;
     const unsigned nwg = (unsigned)(((M + BMT - 1) / BMT) * (N / BNT));
+    const unsigned char *tab = (V == 4 && EPI != EPI_BIAS && !TR) ? gelu_tables(st) : nullptr;
     gemm_nt_bf16<EPI, NS, BMT, BNT, WR, TR><<<nwg, (BMT / WR) * (BNT / 64) * 64, 0, st>>>(
         (const unsigned short *)A, lda, (const unsigned short *)B, ldb, bias, (const unsigned short *)U, ldu,
-        (unsigned short *)C0, (unsigned short *)C1, ldc, M, N, K, trace);
+        (unsigned short *)C0, (unsigned short *)C1, ldc, M, N, K, trace, tab);
 }
 
 template <int EPI>

@@ -93,6 +93,24 @@ def test_gemm_nt_gelu_epilogues_bit_exact(M, Nn, K):
             assert torch.equal(du, du_ref), v
 
 
+def test_gelu_table_covers_every_bf16_u():
+    """The 256 x 256 tiling's GELU' table (gemm.hip gemm_gelu_table_kernel, staged in LDS) against the
+    formula path, bit for bit, on EVERY bf16 value of U (65 536 patterns as a 256 x 256 U: zeros,
+    denormals, the table's exponent range, the values beyond it, Inf and NaN), through EPI_DGELU
+    against the plain GEMM + irads_gelu_bwd."""
+    N = _N()
+    torch.manual_seed(11)
+    dY = torch.randn(256, 64, device=DEV).bfloat16()
+    Wt = (torch.randn(256, 64, device=DEV) * 0.125).bfloat16()
+    U = torch.arange(65536, dtype=torch.int32, device=DEV).to(torch.int16).view(torch.bfloat16).reshape(256, 256)
+    U = U.contiguous()
+    dx = _gemm(0, dY, Wt, variant=4)
+    ref = torch.empty_like(dx)
+    N.call("irads_gelu_bwd", N.ptr(U), N.ptr(dx), N.ptr(ref), dx.numel(), N.stream())
+    du = _gemm(2, dY, Wt, U=U, variant=4)
+    assert torch.equal(du.view(torch.int16), ref.view(torch.int16))
+
+
 def _entry_id(e):
     (d, M, Nn, K), v = e
     return f"{d}-{M}x{Nn}x{K}-v{v}"
