@@ -880,19 +880,101 @@ __global__ void __launch_bounds__(256) msda_bwd_locaw_vec(const float *__restric
 // has its corner columns (rows) at -1 (outside: value 0, no gradient) and x (y), so its corners map
 // onto the bucket's cells shifted by (oy, ox) = (y0 - y, x0 - x) ∈ {-1, 0}².
 //
-// Work items: per (b, m), the cells of every level, split levels' cells `parts` times (split_parts:
-// parts walk every parts-th chunk of V records); item index ((b·M + m)·NI + first[l] + cell·parts +
-// part) with NI = first[L] (bucket_items).
-// buckets per item: one, whose records touch its 2 x 2 cells (items of two neighbouring buckets over
-// 2 x 3 cells measured slower: 132 VGPRs, 6 dot products per record)
-__host__ __device__ __forceinline__ int item_span(int) { return 1; }
-constexpr int kItemCols = 2, kItemRows = 2 * kItemCols;  // cells per item and partial rows per item
+// Work: chunks of G = 256 / V groups (one workgroup) per (b, m, level).  A level whose buckets hold
+// few records (walk_parts == 1) is cut into tiles of TY x TX buckets, one group per bucket; after the
+// walk the workgroup sums, in LDS and in a fixed order, the partial rows its buckets hold for each cell
+// of the (TY + 1) x (TX + 1) cells they touch: a cell whose four buckets all lie in the tile (the
+// (TY - 1) x (TX - 1) interior) is complete and written to grad_value directly; the others (NSLOT per
+// tile) go out as boundary partials that msda_gv_reduce adds to the neighbouring tiles' in a fixed
+// order.  A split level (many records per bucket) gives each bucket pp = walk_parts groups (record
+// chunks part, part + pp, ...), G / pp buckets per workgroup, whose parts are summed in LDS into the
+// bucket's four partial rows (the reduce adds a cell's four: own top-left, left neighbour's
+// top-right, upper neighbour's bottom-left, upper-left neighbour's bottom-right).  The per-bucket
+// partial rows of the previous version (four rows of D floats per (bucket, part): 500 MB per DINO
+// encoder backward written and read back) shrink to the tiles' boundaries.
+constexpr int kItemCols = 2, kItemRows = 2 * kItemCols;  // cells per bucket row and partial rows per bucket
 
-__device__ __forceinline__ void bucket_items(const int *sH, const int *sW, int L, int Q, int P, long *first) {
-    first[0] = 0;
+template <int V>
+struct WalkTile {
+    static constexpr int G = 256 / V;                           // groups per workgroup
+    static constexpr int TX = G >= 16 ? 8 : (G >= 4 ? G / 2 : 1);  // buckets per tile row
+    static constexpr int TY = G / TX;                           // tile rows (>= 2)
+    static constexpr int NSLOT = 2 * (TX + 1) + 2 * (TY - 1);   // boundary cells of the tile's cell region
+};
+
+// boundary slot of region cell (ci, cj), ci in [0, TY], cj in [0, TX], not interior
+__host__ __device__ __forceinline__ int tile_slot(int ci, int cj, int TX, int TY) {
+    return ci == 0 ? cj : ci == TY ? TX + 1 + cj : 2 * (TX + 1) + 2 * (ci - 1) + (cj == TX ? 1 : 0);
+}
+
+__host__ __device__ __forceinline__ int walk_parts(int Q, int P, int H, int W, int G) {
+    const int sp = split_parts(Q, P, H, W);
+    if (sp == 1) return 1;
+    int pp = 2;
+    while (pp < sp && pp < G) pp <<= 1;
+    return pp;
+}
+
+struct WalkLevels {
+    long first[kMaxLevels + 1];  // first group of each level per (b, m); first[L] = groups per (b, m)
+    long pbase[kMaxLevels + 1];  // first partial row of each level per (b, m)
+    int pp[kMaxLevels];          // walk_parts (1: tiled)
+    int ntx[kMaxLevels];         // tiles per row of a tiled level
+};
+
+template <int V>
+__device__ __forceinline__ void walk_levels(const int *sH, const int *sW, int L, int Q, int P, WalkLevels &wl) {
+    using T = WalkTile<V>;
+    wl.first[0] = 0;
+    wl.pbase[0] = 0;
     for (int l = 0; l < L; ++l) {
-        const int parts = split_parts(Q, P, sH[l], sW[l]), span = item_span(parts);
-        first[l + 1] = first[l] + (long)sH[l] * ((sW[l] + span - 1) / span) * parts;
+        const int H = sH[l], W = sW[l], pp = walk_parts(Q, P, H, W, T::G);
+        long groups, prows;
+        wl.pp[l] = pp;
+        if (pp == 1) {
+            const int ntx = (W + T::TX - 1) / T::TX, nty = (H + T::TY - 1) / T::TY;
+            wl.ntx[l] = ntx;
+            groups = (long)ntx * nty * T::G;
+            prows = (long)ntx * nty * T::NSLOT;
+        } else {
+            const int cpw = T::G / pp;
+            wl.ntx[l] = 0;
+            groups = ((long)H * W + cpw - 1) / cpw * T::G;
+            prows = (long)H * W * kItemRows;
+        }
+        wl.first[l + 1] = wl.first[l] + groups;
+        wl.pbase[l + 1] = wl.pbase[l] + prows;
+    }
+}
+
+// the walk's grid: a multiple of 8 (XCD x = blockIdx % 8 serves heads x, x + 8, ...), at most 8192
+// workgroups, each looping over the chunks the device finds (<= `chunks`, a host bound)
+dim3 walk_grid(long chunks) {
+    long g = chunks < 8192 ? chunks : 8192;
+    g = (g + 7) / 8 * 8;
+    return dim3((unsigned)(g < 8 ? 8 : g));
+}
+
+// host bounds without the level shapes (device memory): a level of s = H·W cells has H + W <= s + 1,
+// so a tiled level has <= s / G + (s + 1) / TY + 1 tiles and a split level pp·s <= Q·P / 8 + 2s groups
+template <int V>
+long walk_groups_bound(int S, int L, int Q, int P) {
+    using T = WalkTile<V>;
+    return (long)S * (T::TX + 3) + (long)L * ((long)Q * P / 8 + T::TX + 2 * T::G);
+}
+template <int V>
+long walk_prows_bound(int S, int L) {
+    using T = WalkTile<V>;
+    return ((long)S * T::NSLOT + T::G - 1) / T::G + ((long)(S + L) * T::NSLOT + T::TY - 1) / T::TY +
+           (long)L * T::NSLOT + (long)kItemRows * S;
+}
+long walk_prows_bound_v(int V, int S, int L) {
+    switch (V) {
+        case 4: return walk_prows_bound<4>(S, L);
+        case 8: return walk_prows_bound<8>(S, L);
+        case 16: return walk_prows_bound<16>(S, L);
+        case 32: return walk_prows_bound<32>(S, L);
+        default: return walk_prows_bound<64>(S, L);
     }
 }
 
@@ -1061,176 +1143,254 @@ __device__ __forceinline__ float group_sum_dpp(float v) {
     }
 }
 
+// One workgroup per chunk (b, m, level, tile or bucket range), a grid-stride loop over the chunks
+// (their number is known on the device only); with M % 8 == 0 XCD x takes the chunks of heads
+// x, x + 8, ... (one (image, head) slice of value / grad_out in its L2 at a time).
 template <int V>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(V <= 16 ? 4 : 1))) msda_bucket_walk(const float *__restrict__ value, const int64_t *__restrict__ shapes,
                                                         const int64_t *__restrict__ lsi, const float *__restrict__ gout,
                                                         int bs, int S, int M, int D, int L, int Q, int P,
                                                         const int *__restrict__ off, const float4 *__restrict__ rec,
                                                         float *__restrict__ gloc, float *__restrict__ gaw,
-                                                        float4 *__restrict__ part_rows, long NIM) {
+                                                        float *__restrict__ gvalue, float4 *__restrict__ part_rows,
+                                                        long PST) {
+    using T = WalkTile<V>;
     __shared__ int sH[kMaxLevels], sW[kMaxLevels], sS[kMaxLevels];
-    __shared__ long first[kMaxLevels + 1];
+    __shared__ WalkLevels wl;
     // per group, the chunk's records as its lanes need them: (attention weight, the weights onto the
-    // item's six cells, query) — written by the record's lane, read back as broadcasts
-    __shared__ __attribute__((aligned(16))) float bc[256 / V][V][8];
+    // bucket's four cells, query) — written by the record's lane, read back as broadcasts
+    __shared__ __attribute__((aligned(16))) float bc[T::G][V][8];
+    __shared__ float4 red[T::G][kItemRows][V];  // every group's four partial rows
     load_levels(shapes, lsi, L, sH, sW, sS);
-    if (threadIdx.x == 0) bucket_items(sH, sW, L, Q, P, first);
+    if (threadIdx.x == 0) walk_levels<V>(sH, sW, L, Q, P, wl);
     __syncthreads();
-    // groups over bs x NIM items per head (NIM >= NI = first[L], the host's bound: bucket_items_bound)
-    const GroupMap gm = map_group<V>((long)bs * NIM, M);
-    const int lane = threadIdx.x % V;
-    if (!gm.valid) return;  // whole group exits together
-    const int m = gm.m, b = (int)(gm.row / NIM);
-    const long it = gm.row - (long)b * NIM;  // item within (b, m)
-    if (it >= first[L]) return;
-    int l = 0;
-    for (int k = 1; k < L; ++k) l = it >= first[k] ? k : l;
-    const int H = sH[l], W = sW[l], parts = split_parts(Q, P, H, W), span = item_span(parts);
-    const int nx = (W + span - 1) / span;  // items per row of cells
-    const long r = it - first[l];
-    const int part = (int)(r % parts), ci = (int)(r / parts);
-    const int y = ci / nx, x = (ci - y * nx) * span;  // the item's first bucket (y, x)
-    const int nbk = min(span, W - x);                  // its buckets: (y, x) .. (y, x + nbk - 1)
+    const int gi = threadIdx.x / V, lane = threadIdx.x % V;
+    const long nch = wl.first[L] / T::G;  // chunks per (b, m)
+    long t0, tstep, ntask;
+    const bool by_xcd = M % 8 == 0 && gridDim.x % 8 == 0;
+    if (by_xcd) {
+        t0 = blockIdx.x / 8, tstep = gridDim.x / 8, ntask = (long)(M / 8) * bs * nch;
+    } else {
+        t0 = blockIdx.x, tstep = gridDim.x, ntask = (long)M * bs * nch;
+    }
     const long cs = (long)M * D;
-    // the item's 2 x 3 cells: rows y, y + 1, columns x .. x + 2 (zero outside the level)
-    const float *vb = value + ((long)b * S + sS[l]) * cs + (long)m * D + 4 * lane;
-    const long bk = ((long)b * M + m) * S + sS[l] + (long)y * W + x;
-    const int e1 = off[bk + nbk];
-    const int e0 = off[bk] + part * V;
-    if (e0 >= e1) return;  // uniform over the group: an empty (item, part) has no partials (the reduce skips it)
-    float4 v[2][kItemCols];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < kItemCols; ++j) {
-            v[i][j] = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (y + i < H && x + j < W && j <= nbk)  // uniform over the group
-                v[i][j] = *(const float4 *)(vb + ((long)(y + i) * W + x + j) * cs);
-        }
-    float4 acc[2][kItemCols];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < kItemCols; ++j) acc[i][j] = make_float4(0.f, 0.f, 0.f, 0.f);
     const int LPM = L * P * M;
-    const int step = parts * V;
-    float(*gbc)[8] = bc[threadIdx.x / V];
-    float4 rn = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (e0 + lane < e1) rn = rec[e0 + lane];
-    for (int e = e0; e < e1; e += step) {
-        const float4 rr = rn;  // lane j: record e + j = (sample id, attention weight, x, y)
-        if (e + step + lane < e1) rn = rec[e + step + lane];
-        const bool have = e + lane < e1;
-        // lane j locates its own record: corner (i, j) of the sample (rows y0 + i, columns x0 + j)
-        // lands on the item's cell (i - oy, dx + j - ox), oy / ox = 1 where the clamped corner row /
-        // column is -1, dx = the record's bucket column - x; w[r][c]: the corner weight on cell (r, c)
-        long sid = 0;
-        int q = 0, oy = 0, cx = 0;  // cx = dx - ox: the column of the sample's x0 within the item
-        float a = 0.f;
-        Samp<float> sp{0, 0, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-        float w[2][kItemCols];
+    float(*gbc)[8] = bc[gi];
+    for (long task = t0; task < ntask; task += tstep) {
+        int m, b;
+        long k;
+        if (by_xcd) {
+            const long ml = task / ((long)bs * nch), rem = task - ml * bs * nch;
+            m = (int)(blockIdx.x % 8 + 8 * ml);
+            b = (int)(rem / nch);
+            k = rem - (long)b * nch;
+        } else {
+            m = (int)(task % M);
+            const long rem = task / M;
+            b = (int)(rem / nch);
+            k = rem - (long)b * nch;
+        }
+        const long it = k * T::G;
+        int l = 0;
+        for (int kk = 1; kk < L; ++kk) l = it >= wl.first[kk] ? kk : l;
+        const int H = sH[l], W = sW[l], pp = wl.pp[l];
+        const long kc = (it - wl.first[l]) / T::G;  // chunk within the level
+        int y, x, part, tyi = 0, txi = 0;
+        bool inb;
+        if (pp == 1) {
+            tyi = (int)(kc / wl.ntx[l]);
+            txi = (int)(kc - (long)tyi * wl.ntx[l]);
+            y = tyi * T::TY + gi / T::TX;
+            x = txi * T::TX + gi % T::TX;
+            part = 0;
+            inb = y < H && x < W;
+        } else {
+            const long cell = kc * (T::G / pp) + gi / pp;
+            part = gi % pp;
+            inb = cell < (long)H * W;
+            y = (int)(cell / W);
+            x = (int)(cell - (long)y * W);
+        }
+        float4 acc[2][kItemCols];
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
-            for (int j = 0; j < kItemCols; ++j) w[i][j] = 0.f;
-        if (have) {
-            sid = (long)(unsigned)__float_as_int(rr.x);
-            q = (int)(((unsigned)sid / (unsigned)LPM) % (unsigned)Q);  // sample ids < 2^31 (gather_ws_layout)
-            a = rr.y;
-            sp = locate(rr.z, rr.w, H, W);
-            oy = sp.y0 < y ? 1 : 0;
-            cx = sp.x0 - x;  // -1 .. nbk - 1
+            for (int j = 0; j < kItemCols; ++j) acc[i][j] = make_float4(0.f, 0.f, 0.f, 0.f);
+        int e0 = 0, e1 = 0;
+        if (inb) {  // uniform over the group
+            const long bk = ((long)b * M + m) * S + sS[l] + (long)y * W + x;
+            e1 = off[bk + 1];
+            e0 = off[bk] + part * V;
+        }
+        if (e0 < e1) {  // uniform over the group: the bucket's records, chunks part, part + pp, ...
+            // the bucket's 2 x 2 cells: rows y, y + 1, columns x, x + 1 (zero outside the level)
+            const float *vb = value + ((long)b * S + sS[l]) * cs + (long)m * D + 4 * lane;
+            float4 v[2][kItemCols];
 #pragma unroll
             for (int i = 0; i < 2; ++i)
 #pragma unroll
                 for (int j = 0; j < kItemCols; ++j) {
-                    const int si = i + oy, sj = j - cx;  // the sample's corner on cell (i, j)
-                    const float wc = si == 0 ? (sj == 0 ? sp.nw : sp.ne) : (sj == 0 ? sp.sw : sp.se);
-                    w[i][j] = (si <= 1 && (unsigned)sj <= 1u) ? wc : 0.f;
+                    v[i][j] = make_float4(0.f, 0.f, 0.f, 0.f);
+                    if (y + i < H && x + j < W)  // uniform over the group
+                        v[i][j] = *(const float4 *)(vb + ((long)(y + i) * W + x + j) * cs);
                 }
+            const int step = pp * V;
+            float4 rn = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (e0 + lane < e1) rn = rec[e0 + lane];
+            for (int e = e0; e < e1; e += step) {
+                const float4 rr = rn;  // lane j: record e + j = (sample id, attention weight, x, y)
+                if (e + step + lane < e1) rn = rec[e + step + lane];
+                const bool have = e + lane < e1;
+                // lane j locates its own record: corner (i, j) of the sample (rows y0 + i, columns x0 + j)
+                // lands on the bucket's cell (i - oy, j - ox), oy / ox = 1 where the clamped corner row /
+                // column is -1; w[r][c]: the corner weight on cell (r, c)
+                long sid = 0;
+                int q = 0, oy = 0, cx = 0;  // cx = x0 - x: the column of the sample's x0 within the bucket
+                float a = 0.f;
+                Samp<float> sp{0, 0, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+                float w[2][kItemCols];
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int j = 0; j < kItemCols; ++j) w[i][j] = 0.f;
+                if (have) {
+                    sid = (long)(unsigned)__float_as_int(rr.x);
+                    q = (int)(((unsigned)sid / (unsigned)LPM) % (unsigned)Q);  // sample ids < 2^31 (gather_ws_layout)
+                    a = rr.y;
+                    sp = locate(rr.z, rr.w, H, W);
+                    oy = sp.y0 < y ? 1 : 0;
+                    cx = sp.x0 - x;  // -1 .. 0
+#pragma unroll
+                    for (int i = 0; i < 2; ++i)
+#pragma unroll
+                        for (int j = 0; j < kItemCols; ++j) {
+                            const int si = i + oy, sj = j - cx;  // the sample's corner on cell (i, j)
+                            const float wc = si == 0 ? (sj == 0 ? sp.nw : sp.ne) : (sj == 0 ? sp.sw : sp.se);
+                            w[i][j] = (si <= 1 && (unsigned)sj <= 1u) ? wc : 0.f;
+                        }
+                }
+                static_assert(kItemCols == 2, "the broadcast slots hold a 2 x 2 block");
+                *(float4 *)gbc[lane] = make_float4(a, w[0][0], w[0][1], w[1][0]);
+                *(float2 *)(gbc[lane] + 4) = make_float2(w[1][1], __int_as_float(q));
+                float mg[2][kItemCols];  // this lane's record: grad_out · the bucket's cells
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int j = 0; j < kItemCols; ++j) mg[i][j] = 0.f;
+                constexpr int KC = V < 4 ? V : 4;
+#pragma unroll
+                for (int k0 = 0; k0 < V; k0 += KC) {
+                    if (k0 > 0 && e + k0 >= e1) break;  // uniform: past the range end
+                    float4 go[KC];
+#pragma unroll
+                    for (int kk = 0; kk < KC; ++kk) {  // every grad_out row of the batch in flight first
+                        const int qk = __float_as_int(gbc[k0 + kk][5]);
+                        go[kk] = make_float4(0.f, 0.f, 0.f, 0.f);
+                        if (e + k0 + kk < e1) go[kk] = *(const float4 *)(gout + (((long)b * Q + qk) * M + m) * D + 4 * lane);
+                    }
+#pragma unroll
+                    for (int kk = 0; kk < KC; ++kk) {
+                        if (e + k0 + kk >= e1) break;  // uniform over the group
+#pragma unroll
+                        for (int i = 0; i < 2; ++i)
+#pragma unroll
+                            for (int j = 0; j < kItemCols; ++j) {
+                                const float d = group_sum_dpp<V>(dot4(go[kk], v[i][j]));
+                                if (lane == k0 + kk) mg[i][j] = d;
+                            }
+                        // grad_value: w_corner · (grad_out · attn) into the cell each corner lands on
+                        const float4 r0 = *(const float4 *)gbc[k0 + kk];
+                        const float ak = r0.x, u[2][kItemCols] = {{r0.y, r0.z}, {r0.w, gbc[k0 + kk][4]}};
+                        const float4 ga = make_float4(go[kk].x * ak, go[kk].y * ak, go[kk].z * ak, go[kk].w * ak);
+#pragma unroll
+                        for (int i = 0; i < 2; ++i)
+#pragma unroll
+                            for (int j = 0; j < kItemCols; ++j) {
+                                acc[i][j].x += u[i][j] * ga.x;
+                                acc[i][j].y += u[i][j] * ga.y;
+                                acc[i][j].z += u[i][j] * ga.z;
+                                acc[i][j].w += u[i][j] * ga.w;
+                            }
+                    }
+                }
+                if (have) {  // the sample's corners among the bucket's cells (zero outside), then its gradients
+                    float g[2][2];
+#pragma unroll
+                    for (int si = 0; si < 2; ++si)
+#pragma unroll
+                        for (int sj = 0; sj < 2; ++sj) {
+                            const int i = si - oy, j = cx + sj;  // cell of corner (si, sj)
+                            float gv = 0.f;
+#pragma unroll
+                            for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+                                for (int jj = 0; jj < kItemCols; ++jj) gv = (i == ii && j == jj) ? mg[ii][jj] : gv;
+                            g[si][sj] = gv;
+                        }
+                    gaw[sid] = sp.nw * g[0][0] + sp.ne * g[0][1] + sp.sw * g[1][0] + sp.se * g[1][1];
+                    gloc[2 * sid] = a * ((g[0][1] - g[0][0]) * (1.f - sp.fy) + (g[1][1] - g[1][0]) * sp.fy) * (float)W;
+                    gloc[2 * sid + 1] = a * ((g[1][0] - g[0][0]) * (1.f - sp.fx) + (g[1][1] - g[0][1]) * sp.fx) * (float)H;
+                }
+            }
         }
-        static_assert(kItemCols == 2, "the broadcast slots hold a 2 x 2 block");
-        *(float4 *)gbc[lane] = make_float4(a, w[0][0], w[0][1], w[1][0]);
-        *(float2 *)(gbc[lane] + 4) = make_float2(w[1][1], __int_as_float(q));
-        float mg[2][kItemCols];  // this lane's record: grad_out · the item's cells
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
-            for (int j = 0; j < kItemCols; ++j) mg[i][j] = 0.f;
-        constexpr int KC = V < 4 ? V : 4;
-#pragma unroll
-        for (int k0 = 0; k0 < V; k0 += KC) {
-            if (k0 > 0 && e + k0 >= e1) break;  // uniform: past the range end
-            float4 go[KC];
-#pragma unroll
-            for (int k = 0; k < KC; ++k) {  // every grad_out row of the batch in flight first
-                const int qk = __float_as_int(gbc[k0 + k][5]);
-                go[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-                if (e + k0 + k < e1) go[k] = *(const float4 *)(gout + (((long)b * Q + qk) * M + m) * D + 4 * lane);
+            for (int j = 0; j < kItemCols; ++j) red[gi][kItemCols * i + j][lane] = acc[i][j];
+        __syncthreads();
+        const long pb = (((long)b * M + m) * PST + wl.pbase[l]) * V + lane;
+        if (pp == 1) {
+            // the tile's cell region, each cell summed over the tile's buckets touching it in the fixed
+            // order top-left (own bucket), top-right (left bucket), bottom-left (upper), bottom-right
+            constexpr int RW = T::TX + 1, NR = (T::TY + 1) * RW;
+            for (int rc = gi; rc < NR; rc += T::G) {
+                const int ci = rc / RW, cj = rc - ci * RW;
+                const int yy = tyi * T::TY + ci, xx = txi * T::TX + cj;
+                if (yy >= H || xx >= W) continue;  // uniform over the group
+                float4 sum = make_float4(0.f, 0.f, 0.f, 0.f);
+                auto add = [&](float4 t) { sum.x += t.x, sum.y += t.y, sum.z += t.z, sum.w += t.w; };
+                if (ci < T::TY && cj < T::TX) add(red[ci * T::TX + cj][0][lane]);
+                if (ci < T::TY && cj >= 1) add(red[ci * T::TX + cj - 1][1][lane]);
+                if (ci >= 1 && cj < T::TX) add(red[(ci - 1) * T::TX + cj][2][lane]);
+                if (ci >= 1 && cj >= 1) add(red[(ci - 1) * T::TX + cj - 1][3][lane]);
+                if (ci >= 1 && ci < T::TY && cj >= 1 && cj < T::TX)  // interior: complete
+                    *(float4 *)(gvalue + (((long)b * S + sS[l] + (long)yy * W + xx) * M + m) * D + 4 * lane) = sum;
+                else
+                    part_rows[pb + (kc * T::NSLOT + tile_slot(ci, cj, T::TX, T::TY)) * V] = sum;
             }
-#pragma unroll
-            for (int k = 0; k < KC; ++k) {
-                if (e + k0 + k >= e1) break;  // uniform over the group
-#pragma unroll
-                for (int i = 0; i < 2; ++i)
-#pragma unroll
-                    for (int j = 0; j < kItemCols; ++j) {
-                        const float d = group_sum_dpp<V>(dot4(go[k], v[i][j]));
-                        if (lane == k0 + k) mg[i][j] = d;
-                    }
-                // grad_value: w_corner · (grad_out · attn) into the cell each corner lands on
-                const float4 r0 = *(const float4 *)gbc[k0 + k];
-                const float ak = r0.x, u[2][kItemCols] = {{r0.y, r0.z}, {r0.w, gbc[k0 + k][4]}};
-                const float4 ga = make_float4(go[k].x * ak, go[k].y * ak, go[k].z * ak, go[k].w * ak);
-#pragma unroll
-                for (int i = 0; i < 2; ++i)
-#pragma unroll
-                    for (int j = 0; j < kItemCols; ++j) {
-                        acc[i][j].x += u[i][j] * ga.x;
-                        acc[i][j].y += u[i][j] * ga.y;
-                        acc[i][j].z += u[i][j] * ga.z;
-                        acc[i][j].w += u[i][j] * ga.w;
-                    }
-            }
-        }
-        if (have) {  // the sample's corners among the item's cells (zero outside), then its gradients
-            float g[2][2];
-#pragma unroll
-            for (int si = 0; si < 2; ++si)
-#pragma unroll
-                for (int sj = 0; sj < 2; ++sj) {
-                    const int i = si - oy, j = cx + sj;  // cell of corner (si, sj)
-                    float gv = 0.f;
-#pragma unroll
-                    for (int ii = 0; ii < 2; ++ii)
-#pragma unroll
-                        for (int jj = 0; jj < kItemCols; ++jj) gv = (i == ii && j == jj) ? mg[ii][jj] : gv;
-                    g[si][sj] = gv;
+        } else {
+            // split level: each bucket's parts summed in part order into its four partial rows
+            const int cpw = T::G / pp;
+            for (int rr = gi; rr < cpw * kItemRows; rr += T::G) {
+                const int c = rr / kItemRows, row = rr - c * kItemRows;
+                const long cell = kc * cpw + c;
+                if (cell >= (long)H * W) continue;  // uniform over the group
+                float4 sum = make_float4(0.f, 0.f, 0.f, 0.f);
+                for (int p2 = 0; p2 < pp; ++p2) {
+                    const float4 t = red[c * pp + p2][row][lane];
+                    sum.x += t.x, sum.y += t.y, sum.z += t.z, sum.w += t.w;
                 }
-            gaw[sid] = sp.nw * g[0][0] + sp.ne * g[0][1] + sp.sw * g[1][0] + sp.se * g[1][1];
-            gloc[2 * sid] = a * ((g[0][1] - g[0][0]) * (1.f - sp.fy) + (g[1][1] - g[1][0]) * sp.fy) * (float)W;
-            gloc[2 * sid + 1] = a * ((g[1][0] - g[0][0]) * (1.f - sp.fx) + (g[1][1] - g[0][1]) * sp.fx) * (float)H;
+                part_rows[pb + (cell * kItemRows + row) * V] = sum;
+            }
         }
+        __syncthreads();  // red / bc are reused by the next chunk
     }
-    // the partial rows of this (item, part): [item][cell (i, j) row-major][V lanes]
-    float4 *pr = part_rows + (((long)b * M + m) * NIM + it) * kItemRows * V + lane;
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < kItemCols; ++j) pr[(kItemCols * i + j) * V] = acc[i][j];
 }
 
-// grad_value row of cell (b, s, m): the partials of the items whose 2 x kItemCols cells contain it, in
-// a fixed order (item row y, then y - 1; columns left to right; parts in order)
+// grad_value row of cell (b, s, m) where the walk left partials: a tiled level's boundary cells (the
+// tiles touching the cell in the order own, left, upper, upper-left), a split level's cells (own
+// bucket's top-left, left neighbour's top-right, upper neighbour's bottom-left, upper-left
+// neighbour's bottom-right).  A tiled level's interior cells were written by the walk.
 template <int V>
 __global__ void __launch_bounds__(256) msda_gv_reduce(const int64_t *__restrict__ shapes, const int64_t *__restrict__ lsi,
                                                       int bs, int S, int M, int D, int L, int Q, int P,
-                                                      const float4 *__restrict__ part_rows, long NIM,
-                                                      const int *__restrict__ off, float *__restrict__ gvalue) {
+                                                      const float4 *__restrict__ part_rows, long PST,
+                                                      float *__restrict__ gvalue) {
+    using T = WalkTile<V>;
     __shared__ int sH[kMaxLevels], sW[kMaxLevels], sS[kMaxLevels];
-    __shared__ long first[kMaxLevels + 1];
+    __shared__ WalkLevels wl;
     load_levels(shapes, lsi, L, sH, sW, sS);
-    if (threadIdx.x == 0) bucket_items(sH, sW, L, Q, P, first);
+    if (threadIdx.x == 0) walk_levels<V>(sH, sW, L, Q, P, wl);
     __syncthreads();
     const GroupMap gm = map_group<V>((long)bs * S, M);
     const int lane = threadIdx.x % V;
@@ -1238,40 +1398,28 @@ __global__ void __launch_bounds__(256) msda_gv_reduce(const int64_t *__restrict_
     const int m = gm.m;
     const int s = (int)(gm.row % S), b = (int)(gm.row / S);
     const int l = level_of(s, sS, L);
-    const int H = sH[l], W = sW[l], parts = split_parts(Q, P, H, W), span = item_span(parts);
-    const int nx = (W + span - 1) / span;
+    const int W = sW[l];
     const int c = s - sS[l], y = c / W, x = c - y * W;
-    const float4 *base = part_rows + (((long)b * M + m) * NIM + first[l]) * kItemRows * V + lane;
+    const float4 *base = part_rows + (((long)b * M + m) * PST + wl.pbase[l]) * V + lane;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    const long bkl = ((long)b * M + m) * S + sS[l];  // bucket of cell 0 of this level
-    auto add = [&](int iy, int ix, int cell) {  // item (iy, ix-th of its row), its cell (i, j) row-major
-        const float4 *p = base + (((long)iy * nx + ix) * parts * kItemRows + cell) * V;
-        const long bk = bkl + (long)iy * W + ix * span;
-        const int r0 = off[bk], r1 = off[bk + min(span, W - ix * span)];
-        const int np = min(parts, (r1 - r0 + V - 1) / V);  // parts with records (the walk wrote only those)
-        for (int k0 = 0; k0 < np; k0 += 4) {  // the parts in order, 4 loads in flight
-            float4 t[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) t[k] = k0 + k < np ? p[(long)(k0 + k) * kItemRows * V] : make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                if (k0 + k >= np) break;
-                acc.x += t[k].x;
-                acc.y += t[k].y;
-                acc.z += t[k].z;
-                acc.w += t[k].w;
-            }
-        }
+    auto add = [&](long row) {
+        const float4 t = base[row * V];
+        acc.x += t.x, acc.y += t.y, acc.z += t.z, acc.w += t.w;
     };
-    // items covering column x: those starting at x - j for j = 0 .. span (multiples of span)
-    for (int i = 0; i < 2; ++i) {
-        const int iy = y - i;
-        if (iy < 0) break;
-        for (int j = span; j >= 0; --j) {
-            const int x0 = x - j;
-            if (x0 < 0 || x0 % span) continue;
-            add(iy, x0 / span, kItemCols * i + j);
-        }
+    if (wl.pp[l] == 1) {
+        const int ntx = wl.ntx[l];
+        const int tyi = y / T::TY, ci = y - tyi * T::TY, txi = x / T::TX, cj = x - txi * T::TX;
+        if (ci >= 1 && cj >= 1) return;  // interior of its tile: the walk wrote it
+        const long tile = (long)tyi * ntx + txi;
+        add(tile * T::NSLOT + tile_slot(ci, cj, T::TX, T::TY));
+        if (cj == 0 && txi > 0) add((tile - 1) * T::NSLOT + tile_slot(ci, T::TX, T::TX, T::TY));
+        if (ci == 0 && tyi > 0) add((tile - ntx) * T::NSLOT + tile_slot(T::TY, cj, T::TX, T::TY));
+        if (ci == 0 && cj == 0 && tyi > 0 && txi > 0) add((tile - ntx - 1) * T::NSLOT + tile_slot(T::TY, T::TX, T::TX, T::TY));
+    } else {
+        add((long)c * kItemRows + 0);
+        if (x > 0) add((long)(c - 1) * kItemRows + 1);
+        if (y > 0) add((long)(c - W) * kItemRows + 2);
+        if (x > 0 && y > 0) add((long)(c - W - 1) * kItemRows + 3);
     }
     *(float4 *)(gvalue + (((long)b * S + s) * M + m) * D + 4 * lane) = acc;
 }
@@ -1283,10 +1431,6 @@ struct GatherWs {
     long nb, n, nblk;
 };
 
-// Bound on the bucket walk's items per (b, m) without the level shapes (device memory): a split
-// level has parts <= rec4 / 64 + 1 with rec4 <= 4·Q·P / (H·W), so parts·H·W <= Q·P / 16 + H·W, and the
-// levels' cells sum to S: items <= S + L·(Q·P / 16 + 1).
-long bucket_items_bound(int S, int L, int Q, int P) { return (long)S + (long)L * ((long)Q * P / 16 + 1); }
 
 // workspace carve-up (256-B aligned pieces); bytes == 0 when the gather path does not apply
 long gather_ws_layout(int bs, int S, int M, int D, int L, int Q, int P, char *base, GatherWs *ws) {
@@ -1297,8 +1441,8 @@ long gather_ws_layout(int bs, int S, int M, int D, int L, int Q, int P, char *ba
     const long nblk = (nb + 1023) / 1024;
     if (nblk > 256L * 64) return 0;
     auto al = [](long b) { return (b + 255) / 256 * 256; };
-    // the bucket walk's partial rows (V % 4 == 0): kItemRows rows of D floats per item
-    const long n_part = V % 4 == 0 ? (long)bs * M * bucket_items_bound(S, L, Q, P) * kItemRows * D * 4 : 0;
+    // the bucket walk's partial rows (V % 4 == 0): walk_prows_bound rows of D floats per (b, m)
+    const long n_part = V % 4 == 0 ? (long)bs * M * walk_prows_bound_v(V, S, L) * D * 4 : 0;
     const long o_cnt = 0, o_off = o_cnt + al(4 * nb), o_bsum = o_off + al(4 * (nb + 1)),
                o_tot = o_bsum + al(4 * nblk), o_rec = o_tot + 256, o_rank = o_rec + al(16 * n),
                o_part = o_rank + al(4 * n), o_cntb = o_part + al(n_part),
@@ -1473,7 +1617,6 @@ extern "C" int irads_msda_bwd_gather(const float *value, const int64_t *shapes, 
                        : force && !strcmp(force, "cell") ? false
                                                          : (long)Q * L * P >= 4L * S;
     if (V % 4 == 0 && dense) {
-        const long nim = bucket_items_bound(S, L, Q, P);
         const bool lds_count = S <= kCountLdsCells;
         if (ws.n > 0 && lds_count) {
             static bool attr = [] {  // > 64 KiB of dynamic LDS
@@ -1502,13 +1645,15 @@ extern "C" int irads_msda_bwd_gather(const float *value, const int64_t *shapes, 
             msda_bucket_fill_ranked<<<group_grid((long)bs * Q, M, 16), 256, 0, st>>>(
                 loc, shapes, level_start, bs, S, M, L, Q, P, aw, ws.off, ws.rank, ws.rec);
 #define IRADS_MSDA_W(VV)                                                                                              \
-    case VV:                                                                                                          \
-        msda_bucket_walk<VV><<<group_grid((long)bs * nim, M, VV), 256, 0, st>>>(                                      \
-            value, shapes, level_start, grad_out, bs, S, M, D, L, Q, P, ws.off, ws.rec, grad_loc, grad_aw,            \
-            ws.part_rows, nim);                                                                                       \
+    case VV: {                                                                                                        \
+        const long pst = walk_prows_bound<VV>(S, L);                                                                  \
+        msda_bucket_walk<VV><<<walk_grid((long)bs * M * walk_groups_bound<VV>(S, L, Q, P) / WalkTile<VV>::G), 256, 0, \
+                               st>>>(value, shapes, level_start, grad_out, bs, S, M, D, L, Q, P, ws.off, ws.rec,      \
+                                     grad_loc, grad_aw, grad_value, ws.part_rows, pst);                               \
         msda_gv_reduce<VV><<<group_grid((long)bs * S, M, VV), 256, 0, st>>>(shapes, level_start, bs, S, M, D, L, Q, P, \
-                                                                          ws.part_rows, nim, ws.off, grad_value);     \
-        break;
+                                                                          ws.part_rows, pst, grad_value);             \
+        break;                                                                                                        \
+    }
         switch (V) { IRADS_MSDA_W(4) IRADS_MSDA_W(8) IRADS_MSDA_W(16) IRADS_MSDA_W(32) IRADS_MSDA_W(64) }
 #undef IRADS_MSDA_W
         return check_launch("irads_msda_bwd_gather");

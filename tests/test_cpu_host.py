@@ -307,14 +307,17 @@ def test_reference_driver_import_surface():
 def test_msda_gather_workspace_query(lib):
     """irads_msda_bwd_workspace_bytes is a pure size query (no GPU work): counters (bs*M*S), their
     exclusive scan, one 16-B record and one int rank per sample, and for D = 4·V with V % 4 == 0 the
-    bucket walk's per-workgroup counts (16 per bucket) and partial rows (4 rows of D floats per item,
-    items bounded by S + L·(Q·P/16 + 1) per (b, m)); 0 where the gather backward does not apply."""
+    bucket walk's per-workgroup counts (16 per bucket) and partial rows (D floats each, per (b, m) at
+    most the tiled levels' boundary slots -- NSLOT = 24 per 4 x 8 tile for V = 8, tiles bounded by
+    S/32 + (S + L)/4 + L -- plus 4 rows per cell of the split levels); 0 where the gather backward does
+    not apply."""
     q = lib.irads_msda_bwd_workspace_bytes
     q.restype = ctypes.c_long
     bs, S, M, D, L, Q, P = 2, 22223, 8, 32, 4, 22223, 4
     n = q(0, bs, S, M, D, L, Q, P)
-    items = S + L * (Q * P // 16 + 1)
-    need = 4 * (2 * bs * M * S) + (16 + 4) * bs * Q * M * L * P + 4 * 16 * bs * M * S + 4 * D * 4 * bs * M * items
+    nslot, G, TY = 24, 32, 4
+    prows = -(-S * nslot // G) + -(-(S + L) * nslot // TY) + L * nslot + 4 * S
+    need = 4 * (2 * bs * M * S) + (16 + 4) * bs * Q * M * L * P + 4 * 16 * bs * M * S + 4 * D * bs * M * prows
     assert n >= need
     assert n < need + 8192 + 4 * (bs * M * S // 1024 + 1)
     # D = 8 (V = 2): the cell walk, no walk pieces
