@@ -440,6 +440,14 @@ int irads_wgrad(const uint16_t *A, long lda, const uint16_t *B, long ldb, int K,
  * partial sums several backward kernels leave for the small parameter gradients. */
 int irads_sum_rows(const float *ws, int rows, long count, float *out, void *stream);
 
+/* Greedy non-maximum suppression (vCLR DINO inference: projects/vCLR_deformable_mask/modeling/
+ * dino.py:1245 batched_nms(box, score, label, 0.7) -> detectron2 layers/nms.py ->
+ * torchvision.ops.batched_nms).  boxes: n x 4 fp32 xyxy, 16-B aligned, ALREADY in decreasing score
+ * order (and shifted per label by the caller: torchvision's coordinate trick); keep[i] = 1 when box
+ * i survives: no earlier kept box has IoU > iou_threshold with it, IoU = inter / (area_a + area_b -
+ * inter).  n <= 4096; one workgroup. */
+int irads_nms(const float *boxes, int n, float iou_threshold, unsigned char *keep, void *stream);
+
 /* SegFormer head tail in training mode (segformer.py:22-48: ConvModule BatchNorm2d (batch
  * statistics) + ReLU, then Dropout2d) on the fused map held token-major: x (M x E) bf16, M =
  * B * rows_per_sample.  irads_bnact_stats: per-block partials [block][2][E] of sum (x - x[0]) and

@@ -1,0 +1,442 @@
+"""COCO-style instance evaluation for the vCLR open-world detector, without detectron2 or pycocotools.
+
+The reference evaluates with detectron2's COCOEvaluatorCustom
+(detectron2/detectron2/evaluation/coco_evaluation_custom.py:47-398, configured in
+projects/vCLR_deformable_mask/configs/dino-resnet/deformable_train_voc_eval_nonvoc.py:97-99 with
+max_dets_per_image = [1, 10, 20, 30, 50, 100, 300, 900]), which runs pycocotools' COCOeval through
+COCOevalMaxDets (coco_evaluation_custom.py:641-783: evaluate with the largest maxDets, summarize
+into 23 AP / AR numbers).  pycocotools (2.0.x, the version detectron2 pins) is a third-party
+dependency absent here, so this module restates its published algorithm:
+
+  * ``_prepare``: ground truths ignored when crowd; detections ids 1..N, areas from the box (bbox)
+    or the mask (segm);
+  * ``computeIoU``: detections of an (image, category) by score (stable sort), the first
+    maxDets[-1]; IoU of xywh boxes in float64, or of binary masks; against a crowd ground truth the
+    union is the detection's own area;
+  * ``evaluateImg``: per IoU threshold, detections in score order take the best still-free ground
+    truth with IoU >= min(t, 1 - 1e-10), preferring non-ignored ones (the search stops at the
+    ignored tail once a regular match exists); unmatched detections outside the area range are
+    ignored;
+  * ``accumulate``: per (category, area range, maxDets) the detections of all images by score
+    (stable), cumulative TP / FP, recall = TP / non-ignored GTs, precision made monotone from the
+    right and sampled at 101 recall thresholds (searchsorted, side='left');
+  * ``summarize``: means over the entries > -1, in COCOevalMaxDets' 23-stat layout when 8 maxDets
+    are given, the standard 12-stat layout otherwise.
+
+Masks: ground-truth polygons are filled at pixel centres (even-odd rule) and RLEs decoded, both
+compressed strings and count lists (pycocotools rleFrString / rleDecode); predictions are kept as
+RLE count lists (column-major, as pycocotools encodes).  The polygon fill is NOT pycocotools'
+rleFrPoly rasterizer (which upsamples the outline 5x): boundary pixels can differ, so segm numbers on
+polygon ground truth are parity unpinned; box numbers and RLE ground truth follow the algorithm
+above exactly."""
+import json
+
+import numpy as np
+import torch
+
+MAX_DETS_VCLR = (1, 10, 20, 30, 50, 100, 300, 900)
+AREA_RNG = ((0.0, 1e5 ** 2), (0.0, 32.0 ** 2), (32.0 ** 2, 96.0 ** 2), (96.0 ** 2, 1e5 ** 2))
+AREA_LBL = ("all", "small", "medium", "large")
+
+
+# ----------------------------------------------------------------- masks
+def rle_from_string(s):
+    """pycocotools rleFrString: the compressed counts string -> count list (LEB128-like 5-bit groups,
+    counts after the second stored as differences to the count two places back)."""
+    if isinstance(s, bytes):
+        s = s.decode("ascii")
+    cnts, p = [], 0
+    while p < len(s):
+        x, k, more = 0, 0, True
+        while more:
+            c = ord(s[p]) - 48
+            x |= (c & 0x1F) << (5 * k)
+            more = bool(c & 0x20)
+            p += 1
+            k += 1
+            if not more and (c & 0x10):
+                x |= -1 << (5 * k)
+        if len(cnts) > 2:
+            x += cnts[-2]
+        cnts.append(x)
+    return cnts
+
+
+def rle_decode(rle):
+    """RLE {"size": [h, w], "counts": list or compressed string} -> (h, w) bool mask (column-major runs
+    starting with zeros)."""
+    h, w = rle["size"]
+    counts = rle["counts"]
+    if isinstance(counts, (str, bytes)):
+        counts = rle_from_string(counts)
+    vals = np.zeros(len(counts), dtype=bool)
+    vals[1::2] = True
+    flat = np.repeat(vals, np.asarray(counts, dtype=np.int64))
+    if flat.size != h * w:
+        raise ValueError(f"RLE covers {flat.size} pixels, mask is {h}x{w}")
+    return flat.reshape(w, h).T
+
+
+def rle_encode(mask):
+    """(h, w) bool mask -> {"size": [h, w], "counts": [...]} (uncompressed, column-major)."""
+    mask = np.asarray(mask, dtype=bool)
+    h, w = mask.shape
+    flat = mask.T.reshape(-1)
+    if flat.size == 0:
+        return {"size": [h, w], "counts": [0]}
+    edges = np.flatnonzero(flat[1:] != flat[:-1]) + 1
+    counts = np.diff(np.concatenate([[0], edges, [flat.size]])).tolist()
+    if flat[0]:
+        counts = [0] + counts
+    return {"size": [h, w], "counts": counts}
+
+
+def rle_area(rle):
+    counts = rle["counts"]
+    if isinstance(counts, (str, bytes)):
+        counts = rle_from_string(counts)
+    return int(np.sum(counts[1::2]))
+
+
+def polygons_to_mask(polygons, h, w):
+    """Fill COCO polygons ([[x0, y0, x1, y1, ...], ...], pixel coordinates) at pixel centres, even-odd
+    rule per polygon, union over the polygons."""
+    out = np.zeros((h, w), dtype=bool)
+    ys = np.arange(h, dtype=np.float64) + 0.5
+    xs = np.arange(w, dtype=np.float64) + 0.5
+    for poly in polygons:
+        p = np.asarray(poly, dtype=np.float64).reshape(-1, 2)
+        if len(p) < 3:
+            continue
+        inside = np.zeros((h, w), dtype=bool)
+        x0, y0 = p[:, 0], p[:, 1]
+        x1, y1 = np.roll(x0, -1), np.roll(y0, -1)
+        for ax, ay, bx, by in zip(x0, y0, x1, y1):
+            if ay == by:
+                continue
+            lo, hi = min(ay, by), max(ay, by)
+            rows = (ys >= lo) & (ys < hi)
+            if not rows.any():
+                continue
+            xc = ax + (ys[rows] - ay) * (bx - ax) / (by - ay)  # crossing of each row's centre line
+            inside[rows] ^= xs[None, :] < xc[:, None]
+        out |= inside
+    return out
+
+
+def ann_to_mask(ann, h, w):
+    seg = ann["segmentation"]
+    if isinstance(seg, list):
+        return polygons_to_mask(seg, h, w)
+    if isinstance(seg, dict):
+        return rle_decode(seg)
+    raise ValueError("unsupported segmentation format")
+
+
+# ----------------------------------------------------------------- IoU
+def box_iou_xywh(d, g, iscrowd):
+    """pycocotools bbIou: (D, 4) x (G, 4) xywh in float64; crowd ground truth -> union = det area."""
+    d = np.asarray(d, dtype=np.float64).reshape(-1, 4)
+    g = np.asarray(g, dtype=np.float64).reshape(-1, 4)
+    if len(d) == 0 or len(g) == 0:
+        return np.zeros((len(d), len(g)))
+    w = np.minimum(d[:, None, 0] + d[:, None, 2], g[None, :, 0] + g[None, :, 2]) - np.maximum(d[:, None, 0], g[None, :, 0])
+    h = np.minimum(d[:, None, 1] + d[:, None, 3], g[None, :, 1] + g[None, :, 3]) - np.maximum(d[:, None, 1], g[None, :, 1])
+    inter = np.where((w > 0) & (h > 0), w * h, 0.0)
+    da = (d[:, 2] * d[:, 3])[:, None]
+    ga = (g[:, 2] * g[:, 3])[None, :]
+    crowd = np.asarray(iscrowd, dtype=bool)[None, :]
+    union = np.where(crowd, da, da + ga - inter)
+    return np.where(inter > 0, inter / np.where(union > 0, union, 1.0), 0.0)
+
+
+def mask_iou(dm, gm, iscrowd):
+    """(D, h, w) x (G, h, w) bool masks: intersection counts by one matrix product (exact in fp32
+    below 2^24 pixels); crowd ground truth -> union = det area."""
+    D, G = len(dm), len(gm)
+    if D == 0 or G == 0:
+        return np.zeros((D, G))
+    b = torch.from_numpy(np.asarray(gm, dtype=np.float32).reshape(G, -1))
+    inter = np.zeros((D, G))
+    da = np.zeros((D, 1))
+    for d0 in range(0, D, 64):  # 64 detections' masks at a time
+        a = torch.from_numpy(np.asarray(dm[d0:d0 + 64], dtype=np.float32).reshape(-1, b.shape[1]))
+        inter[d0:d0 + 64] = (a @ b.t()).double().numpy()
+        da[d0:d0 + 64, 0] = a.sum(1).double().numpy()
+    ga = b.sum(1).double().numpy()[None, :]
+    crowd = np.asarray(iscrowd, dtype=bool)[None, :]
+    union = np.where(crowd, da, da + ga - inter)
+    return np.where(inter > 0, inter / np.where(union > 0, union, 1.0), 0.0)
+
+
+class _LazyMasks:
+    """The detections' RLEs decoded slice by slice (mask_iou takes 64 at a time)."""
+
+    def __init__(self, dets):
+        self.dets = dets
+
+    def __len__(self):
+        return len(self.dets)
+
+    def __getitem__(self, sl):
+        return np.stack([rle_decode(d["segmentation"]) for d in self.dets[sl]])
+
+
+# ----------------------------------------------------------------- COCOeval
+class COCOeval:
+    """pycocotools COCOeval (evaluate / accumulate / summarize) over an in-memory ground truth.
+
+    gt: {"images": [{"id", "height", "width"}], "annotations": [{"id", "image_id", "category_id",
+    "bbox" (xywh), "area", "iscrowd", "segmentation"}], "categories": [{"id", ...}]}; dts: result
+    dicts {"image_id", "category_id", "score", "bbox" (xywh) | "segmentation" (RLE)}."""
+
+    def __init__(self, gt, dts, iou_type="bbox", max_dets=(1, 10, 100), use_cats=True, img_ids=None):
+        assert iou_type in ("bbox", "segm")
+        self.iou_type = iou_type
+        self.iou_thrs = np.linspace(0.5, 0.95, int(np.round((0.95 - 0.5) / 0.05)) + 1, endpoint=True)
+        self.rec_thrs = np.linspace(0.0, 1.00, int(np.round((1.00 - 0.0) / 0.01)) + 1, endpoint=True)
+        self.max_dets = sorted(int(m) for m in max_dets)
+        self.use_cats = use_cats
+        self.img_info = {im["id"]: im for im in gt["images"]}
+        self.img_ids = sorted(set(img_ids) if img_ids is not None else self.img_info)
+        self.cat_ids = sorted({c["id"] for c in gt["categories"]})
+        self.gts, self.dts = {}, {}
+        for g in gt["annotations"]:
+            g = dict(g)
+            g["ignore"] = int(g.get("ignore", 0) or g.get("iscrowd", 0))
+            self.gts.setdefault((g["image_id"], g["category_id"]), []).append(g)
+        for i, d in enumerate(dts):
+            d = dict(d)
+            d["id"] = i + 1
+            d["iscrowd"] = 0
+            if iou_type == "bbox":
+                d["area"] = float(d["bbox"][2] * d["bbox"][3])
+            else:
+                d["area"] = float(rle_area(d["segmentation"]))
+            self.dts.setdefault((d["image_id"], d["category_id"]), []).append(d)
+        self._masks = {}
+
+    def _lists(self, img, cat):
+        if self.use_cats:
+            return self.gts.get((img, cat), []), self.dts.get((img, cat), [])
+        gt = [g for c in self.cat_ids for g in self.gts.get((img, c), [])]
+        dt = [d for c in self.cat_ids for d in self.dts.get((img, c), [])]
+        return gt, dt
+
+    def _gt_mask(self, g):
+        key = g["id"]
+        if key not in self._masks:
+            im = self.img_info[g["image_id"]]
+            self._masks[key] = ann_to_mask(g, im["height"], im["width"])
+        return self._masks[key]
+
+    def compute_iou(self, img, cat):
+        gt, dt = self._lists(img, cat)
+        if len(gt) == 0 and len(dt) == 0:
+            return np.zeros((0, 0))
+        order = np.argsort([-d["score"] for d in dt], kind="mergesort")
+        dt = [dt[i] for i in order][: self.max_dets[-1]]
+        crowd = [int(g.get("iscrowd", 0)) for g in gt]
+        if self.iou_type == "bbox":
+            return box_iou_xywh([d["bbox"] for d in dt], [g["bbox"] for g in gt], crowd)
+        return mask_iou(_LazyMasks(dt), [self._gt_mask(g) for g in gt], crowd)
+
+    def evaluate_img(self, img, cat, a_rng, max_det):
+        gt, dt = self._lists(img, cat)
+        if len(gt) == 0 and len(dt) == 0:
+            return None
+        g_ign = np.array([1 if (g["ignore"] or g["area"] < a_rng[0] or g["area"] > a_rng[1]) else 0 for g in gt],
+                         dtype=np.int64)
+        gtind = np.argsort(g_ign, kind="mergesort")
+        gt = [gt[i] for i in gtind]
+        g_ign = g_ign[gtind]
+        dtind = np.argsort([-d["score"] for d in dt], kind="mergesort")
+        dt = [dt[i] for i in dtind[:max_det]]
+        crowd = [int(g.get("iscrowd", 0)) for g in gt]
+        ious = self.ious[img, cat]
+        ious = ious[:, gtind] if ious.size else ious
+        T, G, D = len(self.iou_thrs), len(gt), len(dt)
+        gtm = np.zeros((T, G))
+        dtm = np.zeros((T, D))
+        dt_ig = np.zeros((T, D), dtype=bool)
+        if ious.size and G:
+            # pycocotools' loop per threshold t and detection d (cocoeval.py evaluateImg): over the
+            # ground truths in order (regular first), skip matched non-crowd ones, stop at the ignored
+            # tail once a regular one matched, take any with IoU >= the best so far (initially
+            # min(t, 1 - 1e-10)).  That is: the regular candidates' maximum IoU (the last one on
+            # ties) if any, else the ignored candidates'; all thresholds at once.
+            thr = np.minimum(self.iou_thrs, 1 - 1e-10)[:, None]
+            crowd_a = np.asarray(crowd, dtype=bool)[None, :]
+            reg = (g_ign == 0)[None, :]
+            gt_id = np.array([g["id"] for g in gt], dtype=np.float64)
+            rev = np.arange(G - 1, -1, -1)
+            for di in range(D):
+                row = ious[di][None, :]
+                cand = ((gtm == 0) | crowd_a) & (row >= thr)
+                if not cand.any():
+                    continue
+                creg = cand & reg
+                use = np.where(creg.any(1, keepdims=True), creg, cand & ~reg)
+                score = np.where(use, row, -1.0)
+                m = rev[np.argmax(score[:, rev], axis=1)]  # last index of the maximum
+                ok = use.any(1)
+                t_ok = np.flatnonzero(ok)
+                mm = m[t_ok]
+                dt_ig[t_ok, di] = g_ign[mm] == 1
+                dtm[t_ok, di] = gt_id[mm]
+                gtm[t_ok, mm] = dt[di]["id"]
+        out_rng = np.array([d["area"] < a_rng[0] or d["area"] > a_rng[1] for d in dt], dtype=bool).reshape(1, D)
+        dt_ig = np.logical_or(dt_ig, np.logical_and(dtm == 0, np.repeat(out_rng, T, 0)))
+        return {"dtMatches": dtm, "dtScores": np.array([d["score"] for d in dt]), "gtIgnore": g_ign, "dtIgnore": dt_ig}
+
+    def evaluate(self):
+        cats = self.cat_ids if self.use_cats else [-1]
+        self.ious = {(i, c): self.compute_iou(i, c) for i in self.img_ids for c in cats}
+        self.eval_imgs = [self.evaluate_img(i, c, a, self.max_dets[-1]) for c in cats for a in AREA_RNG
+                          for i in self.img_ids]
+        return self
+
+    def accumulate(self):
+        T, R = len(self.iou_thrs), len(self.rec_thrs)
+        K = len(self.cat_ids) if self.use_cats else 1
+        A, M, I = len(AREA_RNG), len(self.max_dets), len(self.img_ids)
+        precision = -np.ones((T, R, K, A, M))
+        recall = -np.ones((T, K, A, M))
+        for k in range(K):
+            for a in range(A):
+                E = [e for e in self.eval_imgs[k * A * I + a * I: k * A * I + a * I + I] if e is not None]
+                if not E:
+                    continue
+                for m, max_det in enumerate(self.max_dets):
+                    scores = np.concatenate([e["dtScores"][:max_det] for e in E])
+                    inds = np.argsort(-scores, kind="mergesort")
+                    dtm = np.concatenate([e["dtMatches"][:, :max_det] for e in E], axis=1)[:, inds]
+                    dt_ig = np.concatenate([e["dtIgnore"][:, :max_det] for e in E], axis=1)[:, inds]
+                    g_ign = np.concatenate([e["gtIgnore"] for e in E])
+                    npig = np.count_nonzero(g_ign == 0)
+                    if npig == 0:
+                        continue
+                    tps = np.logical_and(dtm, np.logical_not(dt_ig))
+                    fps = np.logical_and(np.logical_not(dtm), np.logical_not(dt_ig))
+                    tp_sum = np.cumsum(tps, axis=1).astype(np.float64)
+                    fp_sum = np.cumsum(fps, axis=1).astype(np.float64)
+                    for t, (tp, fp) in enumerate(zip(tp_sum, fp_sum)):
+                        nd = len(tp)
+                        rc = tp / npig
+                        pr = (tp / (fp + tp + np.spacing(1))).tolist()
+                        recall[t, k, a, m] = rc[-1] if nd else 0
+                        for i in range(nd - 1, 0, -1):
+                            if pr[i] > pr[i - 1]:
+                                pr[i - 1] = pr[i]
+                        q = np.zeros(R)
+                        for ri, pi in enumerate(np.searchsorted(rc, self.rec_thrs, side="left")):
+                            if pi < nd:
+                                q[ri] = pr[pi]
+                        precision[t, :, k, a, m] = q
+        self.precision, self.recall = precision, recall
+        return self
+
+    def _summ(self, ap, iou_thr=None, area="all", max_det=100):
+        a = AREA_LBL.index(area)
+        m = self.max_dets.index(max_det)
+        s = self.precision if ap else self.recall
+        if iou_thr is not None:
+            s = s[np.where(np.isclose(self.iou_thrs, iou_thr))[0]]
+        s = s[:, :, :, a, m] if ap else s[:, :, a, m]
+        v = s[s > -1]
+        return float(np.mean(v)) if v.size else -1.0
+
+    def summarize(self):
+        md = self.max_dets
+        S = self._summ
+        if len(md) >= 8:  # COCOevalMaxDets._summarizeDets (coco_evaluation_custom.py:730-756)
+            stats = [S(1, max_det=md[5]), S(1, 0.5, max_det=md[5]), S(1, 0.75, max_det=md[5]),
+                     S(1, area="small", max_det=md[5]), S(1, area="medium", max_det=md[5]),
+                     S(1, area="large", max_det=md[5])]
+            stats += [S(0, max_det=md[i]) for i in range(8)]
+            for i in (5, 6, 7):
+                stats += [S(0, area=ar, max_det=md[i]) for ar in ("small", "medium", "large")]
+        else:  # pycocotools' standard 12
+            stats = [S(1, max_det=md[-1]), S(1, 0.5, max_det=md[-1]), S(1, 0.75, max_det=md[-1]),
+                     S(1, area="small", max_det=md[-1]), S(1, area="medium", max_det=md[-1]),
+                     S(1, area="large", max_det=md[-1]), S(0, max_det=md[0]), S(0, max_det=md[1]),
+                     S(0, max_det=md[2]), S(0, area="small", max_det=md[-1]),
+                     S(0, area="medium", max_det=md[-1]), S(0, area="large", max_det=md[-1])]
+        self.stats = np.array(stats)
+        return self.stats
+
+
+METRICS_VCLR = ("AP", "AP50", "AP75", "APs", "APm", "APl", "AR1", "AR10", "AR20", "AR30", "AR50", "AR100", "AR300",
+                "AR900", "ARs100", "ARm100", "ARl100", "ARs300", "ARm300", "ARl300", "ARs900", "ARm900", "ARl900")
+
+
+def instances_to_coco_json(instances, img_id, masks=True):
+    """detectron2 instances_to_coco_json (coco_evaluation_custom.py:399-460) for the dict
+    DINO.postprocess returns: xyxy -> xywh boxes, contiguous class ids, masks as RLE."""
+    boxes = instances["pred_boxes"].detach().float().cpu().numpy()
+    if len(boxes) == 0:
+        return []
+    boxes = np.concatenate([boxes[:, :2], boxes[:, 2:] - boxes[:, :2]], 1)
+    scores = instances["scores"].detach().float().cpu().numpy()
+    classes = instances["pred_classes"].detach().cpu().numpy()
+    rles = None
+    if masks and "pred_masks" in instances:
+        rles = [rle_encode(m) for m in instances["pred_masks"].detach().cpu().numpy()]
+    out = []
+    for k in range(len(boxes)):
+        r = {"image_id": img_id, "category_id": int(classes[k]), "bbox": boxes[k].tolist(), "score": float(scores[k])}
+        if rles is not None:
+            r["segmentation"] = rles[k]
+        out.append(r)
+    return out
+
+
+class COCOEvaluatorCustom:
+    """detectron2 COCOEvaluatorCustom (coco_evaluation_custom.py:47-398) on a COCO json loaded in
+    memory: process(inputs, outputs) collects the predictions (contiguous class ids mapped back to the
+    dataset's), evaluate() runs COCOeval per task ("bbox", and "segm" when masks are predicted) with
+    max_dets_per_image and returns {task: {metric: value x 100}} with the reference's metric names
+    (and per-category AP when there is more than one category)."""
+
+    def __init__(self, gt, max_dets_per_image=MAX_DETS_VCLR, contiguous_to_dataset_id=None, tasks=None):
+        if isinstance(gt, str):
+            with open(gt) as fh:
+                gt = json.load(fh)
+        self.gt = gt
+        self.max_dets = list(max_dets_per_image) if max_dets_per_image is not None else [1, 10, 100]
+        assert len(self.max_dets) >= 3, "COCOeval needs at least 3 maxDets"
+        cats = sorted(c["id"] for c in gt["categories"])
+        self.to_dataset = contiguous_to_dataset_id or {i: c for i, c in enumerate(cats)}
+        self.class_names = [c.get("name", str(c["id"])) for c in sorted(gt["categories"], key=lambda c: c["id"])]
+        self.tasks = tasks
+        self.reset()
+
+    def reset(self):
+        self.predictions = []
+
+    def process(self, inputs, outputs):
+        for x, y in zip(inputs, outputs):
+            if "instances" in y:
+                self.predictions.extend(instances_to_coco_json(y["instances"], x["image_id"]))
+
+    def evaluate(self, img_ids=None):
+        preds = [dict(p, category_id=self.to_dataset[p["category_id"]]) for p in self.predictions]
+        tasks = self.tasks or (["bbox", "segm"] if any("segmentation" in p for p in preds) else ["bbox"])
+        metrics = METRICS_VCLR if len(self.max_dets) >= 8 else (
+            "AP", "AP50", "AP75", "APs", "APm", "APl", "AR1", "AR10", "AR100", "ARs", "ARm", "ARl")
+        results = {}
+        for task in tasks:
+            if not preds:
+                results[task] = {m: float("nan") for m in metrics}
+                continue
+            dts = preds if task == "segm" else [{k: v for k, v in p.items() if k != "segmentation"} for p in preds]
+            ev = COCOeval(self.gt, dts, task, self.max_dets, img_ids=img_ids).evaluate().accumulate()
+            stats = ev.summarize()
+            res = {m: float(stats[i] * 100) if stats[i] >= 0 else float("nan") for i, m in enumerate(metrics)}
+            if len(self.class_names) > 1:
+                for k, name in enumerate(self.class_names):
+                    p = ev.precision[:, :, k, 0, -1]
+                    p = p[p > -1]
+                    res["AP-" + name] = float(np.mean(p) * 100) if p.size else float("nan")
+            results[task] = res
+        return results

@@ -34,6 +34,7 @@ SIGNATURES = {
     "irads_dattn_gate_fwd": [_vp] * 4 + [_i] * 3 + [_vp, _vp],
     "irads_dattn_gate_bwd": [_vp] * 5 + [_i] * 3 + [_vp] * 4,
     "irads_sum_rows": [_vp, _i, _l, _vp, _vp],
+    "irads_nms": [_vp, _i, _f, _vp, _vp],
     "irads_dattn_mix_fwd": [_vp] * 3 + [_i] * 3 + [_vp] * 3,
     "irads_dattn_mix_bwd": [_vp] * 5 + [_i] * 3 + [_vp] * 4,
     "irads_dattn_attn_fwd": [_vp] * 8 + [_i] * 9 + [_f, _vp, _vp, _vp],

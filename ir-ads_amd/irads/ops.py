@@ -1213,6 +1213,26 @@ def confusion_update(scores, target, ignore_index, hist):
            N.ptr(hist), N.stream())
 
 
+def batched_nms(boxes, scores, idxs, iou_threshold):
+    """detectron2 layers/nms.py batched_nms (the vCLR inference's dino.py:1245) = torchvision's
+    batched_nms below 20 000 boxes: every box shifted by idxs x (max coordinate + 1) so that boxes of
+    different labels never overlap, then greedy NMS in decreasing score order on the HIP kernel
+    (irads_nms).  Returns the kept indices in decreasing score order (torchvision's order; ties in
+    score keep their input order here).  boxes (n, 4) xyxy, scores (n,), idxs (n,) integer labels."""
+    N.check_device(boxes, "batched_nms boxes")
+    n = boxes.shape[0]
+    if n == 0:
+        return torch.empty((0,), dtype=torch.int64, device=boxes.device)
+    b = boxes.float()
+    offsets = idxs.to(b) * (b.max() + 1)
+    b = b + offsets[:, None]
+    order = torch.sort(scores, descending=True, stable=True).indices
+    b = b[order].contiguous()
+    keep = torch.empty((n,), dtype=torch.uint8, device=boxes.device)
+    N.call("irads_nms", N.ptr(b), n, float(iou_threshold), N.ptr(keep), N.stream())
+    return order[keep.bool()]
+
+
 # ------------------------------------------------------------------ LayerNorm -> bf16 GEMM operand
 LN_ROW_WIDTHS = (2, 3, 4, 6, 8, 12, 16, 24, 32, 48)  # C / 64 the row kernels take
 

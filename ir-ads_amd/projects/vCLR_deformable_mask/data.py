@@ -1,0 +1,325 @@
+"""COCO-format data for the vCLR detector without detectron2.
+
+Reference: configs/dino-resnet/deformable_train_voc_eval_nonvoc.py:27-95 registers the open-world
+COCO jsons (detectron2 register_coco_instances -> data/datasets/coco.py load_coco_json), keeps the
+images with annotations (get_detection_dataset_dicts(filter_empty=True)), and maps them with
+OursDatasetMapper for training (modeling/ours_mapper.py:62-205) and CustominsDetrDatasetMapper
+(ResizeShortestEdge(800, 1333) only) for testing.  Restated here:
+
+  * ``load_coco_json``: images -> dicts {file_name, height, width, image_id, annotations}, each
+    annotation {bbox (xywh, absolute), category_id (contiguous: the dataset's ids in sorted order
+    -> 0..K-1), segmentation, iscrowd}; ``meta`` holds thing_classes and the id map;
+  * transforms (detectron2 data/transforms): RandomFlip (horizontal, p = 0.5), ResizeShortestEdge
+    (a short side drawn from the list, "choice", capped by max_size; output size rounded with
+    int(x + 0.5); PIL bilinear for uint8 images), RandomCrop("absolute_range", (384, 600)), and the
+    strong view's RandomApply(RandomBrightness / RandomContrast / RandomSaturation(0.5, 1.5));
+  * OursDatasetMapper: a random pick between the plain and the crop augmentation lists (p = 1/2),
+    for train2017 images a random pick of the style-transferred / depth-colormap copy (1/3 each,
+    when that file exists), the "image_rgb" copy of the original under the same transforms, the
+    strong view, and the instances: boxes transformed, clipped, masks from the transformed
+    polygons, empty instances dropped (utils.transform_instance_annotations,
+    annotations_to_instances, filter_empty_instances, convert_coco_poly_to_mask).
+
+Random draws go through numpy's and Python's global generators as detectron2's do.  Masks are
+filled at pixel centres (detrex/evaluation/coco.py polygons_to_mask), not with pycocotools'
+rasterizer: boundary pixels may differ from the reference's (parity unpinned)."""
+import copy
+import json
+import os
+import random
+
+import numpy as np
+import torch
+from PIL import Image, ImageOps
+
+from detrex.evaluation.coco import polygons_to_mask, rle_decode
+
+
+# ----------------------------------------------------------------- dataset dicts
+def load_coco_json(json_file, image_root):
+    """detectron2 load_coco_json: (dataset dicts, meta)."""
+    with open(json_file) as fh:
+        js = json.load(fh)
+    cats = sorted(js["categories"], key=lambda c: c["id"])
+    id_map = {c["id"]: i for i, c in enumerate(cats)}
+    anns = {}
+    for a in js["annotations"]:
+        anns.setdefault(a["image_id"], []).append(a)
+    dicts = []
+    for im in sorted(js["images"], key=lambda i: i["id"]):
+        objs = []
+        for a in anns.get(im["id"], []):
+            if a.get("ignore", 0):
+                raise ValueError("annotations with 'ignore' are not supported (detectron2 asserts the same)")
+            obj = {"bbox": list(a["bbox"]), "category_id": id_map[a["category_id"]], "iscrowd": a.get("iscrowd", 0)}
+            seg = a.get("segmentation")
+            if isinstance(seg, list):
+                seg = [p for p in seg if len(p) % 2 == 0 and len(p) >= 6]
+                if not seg:
+                    continue  # detectron2 drops annotations whose polygons are all invalid
+            if seg is not None:
+                obj["segmentation"] = seg
+            objs.append(obj)
+        dicts.append({"file_name": os.path.join(image_root, im["file_name"]), "height": im["height"],
+                      "width": im["width"], "image_id": im["id"], "annotations": objs})
+    meta = {"thing_classes": [c.get("name", str(c["id"])) for c in cats],
+            "thing_dataset_id_to_contiguous_id": id_map, "json": js}
+    return dicts, meta
+
+
+def filter_empty(dicts):
+    """get_detection_dataset_dicts(filter_empty=True): keep images with a non-crowd annotation."""
+    return [d for d in dicts if any(not a.get("iscrowd", 0) for a in d["annotations"])]
+
+
+def read_image(path):
+    """detectron2 utils.read_image(format="RGB"): EXIF orientation applied, HWC uint8."""
+    with Image.open(path) as im:
+        im = ImageOps.exif_transpose(im)
+        return np.asarray(im.convert("RGB"))
+
+
+# ----------------------------------------------------------------- transforms
+class Transform:
+    """One geometric transform: apply_image (HWC uint8), apply_coords ((N, 2) x, y)."""
+
+    def apply_box(self, boxes):
+        """xyxy boxes: transform the four corners, take their bounding box (detectron2 apply_box)."""
+        b = np.asarray(boxes, dtype=np.float32).reshape(-1, 4)
+        corners = b[:, [0, 1, 2, 1, 0, 3, 2, 3]].reshape(-1, 2)
+        c = self.apply_coords(corners).reshape(-1, 4, 2)
+        return np.concatenate([c.min(1), c.max(1)], 1)
+
+
+class HFlip(Transform):
+    def __init__(self, w):
+        self.w = w
+
+    def apply_image(self, img):
+        return np.ascontiguousarray(img[:, ::-1])
+
+    def apply_coords(self, c):
+        c = np.array(c, dtype=np.float32)
+        c[:, 0] = self.w - c[:, 0]
+        return c
+
+
+class Resize(Transform):
+    def __init__(self, h, w, newh, neww):
+        self.h, self.w, self.newh, self.neww = h, w, newh, neww
+
+    def apply_image(self, img):
+        return np.asarray(Image.fromarray(img).resize((self.neww, self.newh), Image.BILINEAR))
+
+    def apply_coords(self, c):
+        c = np.array(c, dtype=np.float32)
+        c[:, 0] *= self.neww * 1.0 / self.w
+        c[:, 1] *= self.newh * 1.0 / self.h
+        return c
+
+
+class Crop(Transform):
+    def __init__(self, x0, y0, w, h):
+        self.x0, self.y0, self.w, self.h = x0, y0, w, h
+
+    def apply_image(self, img):
+        return np.ascontiguousarray(img[self.y0:self.y0 + self.h, self.x0:self.x0 + self.w])
+
+    def apply_coords(self, c):
+        c = np.array(c, dtype=np.float32)
+        c[:, 0] -= self.x0
+        c[:, 1] -= self.y0
+        return c
+
+
+def resize_shortest_edge_shape(h, w, short, max_size):
+    """detectron2 ResizeShortestEdge.get_output_shape."""
+    scale = short * 1.0 / min(h, w)
+    newh, neww = (short, scale * w) if h < w else (scale * h, short)
+    if max(newh, neww) > max_size:
+        scale = max_size * 1.0 / max(newh, neww)
+        newh, neww = newh * scale, neww * scale
+    return int(newh + 0.5), int(neww + 0.5)
+
+
+class RandomFlip:
+    def __init__(self, prob=0.5):
+        self.prob = prob
+
+    def get(self, img):
+        return HFlip(img.shape[1]) if np.random.uniform() < self.prob else None
+
+
+class ResizeShortestEdge:
+    def __init__(self, short_edge_length, max_size=float("inf"), sample_style="range"):
+        self.short = (short_edge_length, short_edge_length) if isinstance(short_edge_length, int) else tuple(
+            short_edge_length)
+        self.max_size, self.choice = max_size, sample_style == "choice"
+
+    def get(self, img):
+        h, w = img.shape[:2]
+        if self.choice:
+            size = int(np.random.choice(self.short))
+        else:
+            size = int(np.random.randint(self.short[0], self.short[1] + 1))
+        if size == 0:
+            return None
+        newh, neww = resize_shortest_edge_shape(h, w, size, self.max_size)
+        return Resize(h, w, newh, neww)
+
+
+class RandomCrop:
+    """crop_type "absolute_range": height and width each drawn in [min(side, lo), min(side, hi)]."""
+
+    def __init__(self, crop_type, crop_size):
+        assert crop_type == "absolute_range"
+        self.lo, self.hi = crop_size
+
+    def get(self, img):
+        h, w = img.shape[:2]
+        ch = int(np.random.randint(min(h, self.lo), min(h, self.hi) + 1))
+        cw = int(np.random.randint(min(w, self.lo), min(w, self.hi) + 1))
+        y0 = int(np.random.randint(h - ch + 1))
+        x0 = int(np.random.randint(w - cw + 1))
+        return Crop(x0, y0, cw, ch)
+
+
+def apply_augmentations(augs, img):
+    """T.apply_transform_gens: each augmentation draws its transform on the current image."""
+    tfs = []
+    for a in augs:
+        t = a.get(img)
+        if t is not None:
+            img = t.apply_image(img)
+            tfs.append(t)
+    return img, tfs
+
+
+def _blend(img, src, src_w, dst_w):
+    out = src_w * src + dst_w * img.astype(np.float32)
+    return np.clip(out, 0, 255).astype(np.uint8)
+
+
+def strong_color(img, lo=0.5, hi=1.5, prob=0.5):
+    """RandomApply(RandomBrightness), RandomApply(RandomContrast), RandomApply(RandomSaturation),
+    each (lo, hi) and p = 0.5 (detectron2 BlendTransform arithmetic)."""
+    if np.random.uniform() < prob:
+        w = np.random.uniform(lo, hi)
+        img = _blend(img, 0.0, 1 - w, w)
+    if np.random.uniform() < prob:
+        w = np.random.uniform(lo, hi)
+        img = _blend(img, img.mean(), 1 - w, w)
+    if np.random.uniform() < prob:
+        w = np.random.uniform(lo, hi)
+        grey = img.dot(np.array([0.299, 0.587, 0.114], dtype=np.float32))[:, :, None]
+        img = _blend(img, grey, 1 - w, w)
+    return img
+
+
+# ----------------------------------------------------------------- mappers
+def _to_chw(img):
+    return torch.as_tensor(np.ascontiguousarray(img.transpose(2, 0, 1)))
+
+
+class TestMapper:
+    """CustominsDetrDatasetMapper(is_train=False): ResizeShortestEdge(800, 1333), annotations dropped."""
+
+    def __init__(self, min_size=800, max_size=1333):
+        self.aug = [ResizeShortestEdge(min_size, max_size)]
+
+    def __call__(self, d):
+        d = copy.deepcopy(d)
+        img = read_image(d["file_name"])
+        if img.shape[:2] != (d["height"], d["width"]):
+            raise ValueError(f"{d['file_name']}: image is {img.shape[:2]}, annotation says {(d['height'], d['width'])}")
+        img, _ = apply_augmentations(self.aug, img)
+        d["image"] = _to_chw(img)
+        d.pop("annotations", None)
+        return d
+
+
+TRAIN_SHORT = (480, 512, 544, 576, 608, 640, 672, 704, 736, 768, 800)
+
+
+class TrainMapper:
+    """OursDatasetMapper (ours_mapper.py:109-205) with the config's augmentation lists
+    (deformable_train_voc_eval_nonvoc.py:33-70)."""
+
+    def __init__(self, mask_on=True):
+        self.augmentation = [RandomFlip(), ResizeShortestEdge(TRAIN_SHORT, 1333, "choice")]
+        self.augmentation_with_crop = [RandomFlip(), ResizeShortestEdge((400, 500, 600), sample_style="choice"),
+                                       RandomCrop("absolute_range", (384, 600)),
+                                       ResizeShortestEdge(TRAIN_SHORT, 1333, "choice")]
+        self.mask_on = mask_on
+
+    @staticmethod
+    def _variant(path):
+        """train2017 images: the style-transferred or depth-colormap copy with probability 1/3 each."""
+        if "train2017" not in path:
+            return path
+        r = random.random() * 3
+        alt = None
+        if r < 1:
+            alt = path.replace("train2017", "style_coco_train2017")
+        elif r > 2:
+            alt = path.replace("train2017", "train2017_depth_cmap").replace(".jpg", ".png")
+        return alt if alt is not None and os.path.exists(alt) else path
+
+    def __call__(self, d):
+        d = copy.deepcopy(d)
+        path = self._variant(d["file_name"])
+        img = read_image(path)
+        if img.shape[:2] != (d["height"], d["width"]):
+            raise ValueError(f"{path}: image is {img.shape[:2]}, annotation says {(d['height'], d['width'])}")
+        augs = self.augmentation if np.random.rand() > 0.5 else self.augmentation_with_crop
+        img, tfs = apply_augmentations(augs, img)
+        rgb = read_image(d["file_name"])
+        for t in tfs:
+            rgb = t.apply_image(rgb)
+        strong = strong_color(img.copy())
+        h, w = img.shape[:2]
+        d["image"], d["image_rgb"], d["image_strong"] = _to_chw(img), _to_chw(rgb), _to_chw(strong)
+        d["padding_mask"] = torch.zeros((h, w), dtype=torch.bool)
+        boxes, classes, masks = [], [], []
+        H0, W0 = d["height"], d["width"]
+        for a in d.pop("annotations"):
+            if a.get("iscrowd", 0):
+                continue
+            x, y, bw, bh = a["bbox"]
+            box = np.array([[x, y, x + bw, y + bh]], dtype=np.float32)
+            for t in tfs:
+                box = t.apply_box(box)
+            box = np.minimum(box[0].clip(min=0), np.array([w, h, w, h], dtype=np.float32))
+            m = None
+            if self.mask_on and "segmentation" in a:
+                seg = a["segmentation"]
+                if isinstance(seg, dict):  # RLE: decode at the original size, transform as an image
+                    mi = rle_decode(seg).astype(np.uint8) * 255
+                    mi = np.repeat(mi[:, :, None], 3, 2)
+                    for t in tfs:
+                        mi = t.apply_image(mi) if not isinstance(t, Resize) else np.asarray(
+                            Image.fromarray(mi).resize((t.neww, t.newh), Image.NEAREST))
+                    m = mi[:, :, 0] > 127
+                else:
+                    polys = []
+                    for p in seg:
+                        c = np.asarray(p, dtype=np.float32).reshape(-1, 2)
+                        for t in tfs:
+                            c = t.apply_coords(c)
+                        polys.append(c.reshape(-1))
+                    m = polygons_to_mask(polys, h, w)
+            if not (box[2] - box[0] > 1e-5 and box[3] - box[1] > 1e-5):
+                continue  # filter_empty_instances: empty box
+            if m is not None and not m.any():
+                continue  # ... and empty mask
+            boxes.append(box)
+            classes.append(a["category_id"])
+            if m is not None:
+                masks.append(m)
+        inst = {"image_size": (h, w),
+                "gt_boxes": torch.as_tensor(np.array(boxes, dtype=np.float32).reshape(-1, 4)),
+                "gt_classes": torch.as_tensor(classes, dtype=torch.int64)}
+        if self.mask_on:
+            inst["gt_masks"] = torch.as_tensor(np.array(masks, dtype=np.uint8).reshape(-1, h, w))
+        d["instances"] = inst
+        return d

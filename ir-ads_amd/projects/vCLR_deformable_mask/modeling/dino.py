@@ -14,7 +14,9 @@ sine position embeddings -> CDN queries -> DINOTransformer on the HIP MSDA kerne
 class / box / ROI / mask heads with the encoder-memory segmentation features -> dn split ->
 DINOCriterion.  Without a teacher state or a consistency criterion the forward is
 forward_student on the normalised images, as the reference's is when ``siamese_outputs`` is None
-(dino.py:914).  Not built: NMS post-processing to detectron2 Instances (evaluation only).
+(dino.py:914).  In eval mode the forward returns the reference's post-processed detections
+(``postprocess``: mask-weighted scores, the 300 best (query, class) pairs, batched NMS at 0.7 on
+the HIP kernel, boxes and masks at the input's original size), one {"instances": dict} per image.
 
 Inputs: ``batched_inputs`` as detectron2 passes them: dicts with "image" (3, H, W) unnormalised,
 "image_rgb" (the weak view, same size) and, in training, "instances" with ``image_size``,
@@ -31,7 +33,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from detrex.layers import MLP
-from detrex.layers.box_ops import box_xyxy_to_cxcywh
+from detrex.layers.box_ops import box_cxcywh_to_xyxy, box_xyxy_to_cxcywh
 from detrex.modeling import ema
 from detrex.utils import inverse_sigmoid
 
@@ -197,7 +199,8 @@ class DINO(nn.Module):
         images, sizes = self.preprocess_image(batched_inputs)
         B, _, H, W = images.shape
         if not self.training:
-            return self.forward_student(batched_inputs, images, images.new_zeros(B, H, W))
+            output = self.forward_student(batched_inputs, images, images.new_zeros(B, H, W))
+            return self.postprocess(output, batched_inputs, sizes)
         img_masks = images.new_ones(B, H, W)
         for i, x in enumerate(batched_inputs):
             ih, iw = self._image_size(x)
@@ -309,6 +312,45 @@ class DINO(nn.Module):
             if k in self.criterion.weight_dict:
                 loss_dict[k] = loss_dict[k] * self.criterion.weight_dict[k]
         return loss_dict
+
+    # ---------------------------------------------------------------- inference (dino.py:923-947)
+    def postprocess(self, output, batched_inputs, image_sizes, topk=300, nms_threshold=0.7):
+        """The reference's eval branch: score = σ⁻¹(√(σ(logit) · mask score)), the mask score being the
+        mean σ(mask logit) over the mask's positive pixels (dino.py:928-929); per image the ``topk``
+        best (query, class) pairs, batched NMS at ``nms_threshold`` (nms_inference, dino.py:1204-1256);
+        boxes to input pixels, then to the original (height, width), clipped, empty boxes dropped
+        (detector_postprocess, dino.py:41-105); masks bilinearly resized to (height, width) and
+        thresholded at 0 (dino.py:938-945).  Returns [{"instances": {"image_size", "pred_boxes" (xyxy),
+        "scores", "pred_classes", "pred_masks" (bool)}}]."""
+        from irads import ops  # the HIP NMS
+        box_cls, box_pred, mask_pred = output["pred_logits"], output["pred_boxes"], output["pred_masks"]
+        pos = mask_pred > 0
+        mask_score = (pos * mask_pred.sigmoid()).sum((2, 3)) / (pos.sum((2, 3)) + 1e-10)
+        avg_score = inverse_sigmoid(torch.sqrt(box_cls.sigmoid() * mask_score.unsqueeze(-1)))
+        bs, nq, nc = avg_score.shape
+        prob = avg_score.sigmoid().view(bs, nq * nc)
+        idx = torch.arange(nq * nc, device=prob.device)
+        query, label = torch.div(idx, nc, rounding_mode="floor"), idx % nc
+        boxes = box_cxcywh_to_xyxy(box_pred)
+        results = []
+        for i in range(bs):
+            pre = prob[i].topk(min(topk, nq * nc)).indices
+            box, score, lab, msk = boxes[i][query[pre]], prob[i][pre], label[pre], mask_pred[i][query[pre]]
+            keep = ops.batched_nms(box, score, lab, nms_threshold)
+            h_in, w_in = image_sizes[i]
+            box = box[keep] * box.new_tensor([w_in, h_in, w_in, h_in])
+            score, lab, msk = score[keep], lab[keep], msk[keep]
+            x = batched_inputs[i]
+            height, width = int(x.get("height", h_in)), int(x.get("width", w_in))
+            pm = F.interpolate(msk.unsqueeze(1), (height, width), mode="bilinear", align_corners=False)[:, 0] > 0
+            sx, sy = width / w_in, height / h_in
+            box = box * box.new_tensor([sx, sy, sx, sy])
+            box = torch.stack([box[:, 0].clamp(0, width), box[:, 1].clamp(0, height),
+                               box[:, 2].clamp(0, width), box[:, 3].clamp(0, height)], 1)
+            ok = (box[:, 2] - box[:, 0] > 0) & (box[:, 3] - box[:, 1] > 0)
+            results.append({"instances": {"image_size": (height, width), "pred_boxes": box[ok], "scores": score[ok],
+                                          "pred_classes": lab[ok], "pred_masks": pm[ok]}})
+        return results
 
     @staticmethod
     def _set_aux_loss(cls, crd, roi, qry, msk):

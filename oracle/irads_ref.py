@@ -12,6 +12,8 @@ file:line it restates.  mmcv/mmengine/timm building blocks are restated per
 SURVEY.md Appendix B (their arithmetic is plain PyTorch: parity unpinned beyond that).
 """
 import math
+
+import numpy as np
 from typing import List
 
 import torch
@@ -575,6 +577,41 @@ def lightsb_em(x, n_steps, noise, r, S_log_diag, log_alpha_raw, epsilon):
         t = t + dt
         traj.append(x)
     return torch.stack(traj, 1)
+
+
+# ----------------------------------------------------------------- detection post-processing
+def nms_ref(boxes, scores, iou_threshold):
+    """Greedy NMS as torchvision.ops.nms computes it on the CPU (torchvision is a third-party
+    dependency of detectron2, absent here; vCLR calls it through detectron2 batched_nms,
+    projects/vCLR_deformable_mask/modeling/dino.py:1245): boxes in decreasing score order (stable
+    here), box j suppressed when a kept earlier box i has IoU(i, j) > threshold, IoU = inter /
+    (area_i + area_j - inter) in fp32 without fused multiply-adds.  Returns kept indices."""
+    b = np.asarray(boxes, dtype=np.float32)
+    order = np.argsort(-np.asarray(scores, dtype=np.float64), kind="stable")
+    b = b[order]
+    n = len(b)
+    area = (b[:, 2] - b[:, 0]) * (b[:, 3] - b[:, 1])
+    supp = np.zeros(n, dtype=bool)
+    keep = []
+    for i in range(n):
+        if supp[i]:
+            continue
+        keep.append(order[i])
+        w = np.maximum(np.minimum(b[i, 2], b[i + 1:, 2]) - np.maximum(b[i, 0], b[i + 1:, 0]), np.float32(0))
+        h = np.maximum(np.minimum(b[i, 3], b[i + 1:, 3]) - np.maximum(b[i, 1], b[i + 1:, 1]), np.float32(0))
+        inter = (w * h).astype(np.float32)
+        iou = inter / ((area[i] + area[i + 1:]).astype(np.float32) - inter)
+        supp[i + 1:] |= iou > np.float32(iou_threshold)
+    return np.asarray(keep, dtype=np.int64)
+
+
+def batched_nms_ref(boxes, scores, idxs, iou_threshold):
+    """torchvision batched_nms's coordinate trick (offset = label x (max coordinate + 1), fp32) then nms_ref."""
+    b = np.asarray(boxes, dtype=np.float32)
+    if len(b) == 0:
+        return np.zeros((0,), dtype=np.int64)
+    off = np.asarray(idxs).astype(np.float32) * (b.max() + np.float32(1))
+    return nms_ref(b + off[:, None], scores, iou_threshold)
 
 
 # ----------------------------------------------------------------- metrics
