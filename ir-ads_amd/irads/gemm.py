@@ -8,15 +8,17 @@ operands once Wᵀ is kept beside W (made once per weight version).
 
 Which kernel serves a shape is a table, not a heuristic: scripts/gemm_tune.py times both on the
 shapes of BASELINE.json's C2 and C4 steps (interleaved rounds in one process) and writes
-tuned/irads_gemm_select_mi355x.json, the (direction, M, N, K) keys where irads_gemm_nt won by
-≥ 5 %, each with the tiling that won (variant 2: 128 x 128 tiles, 2 workgroups per CU; 4: 256 x 256
+tuned/irads_gemm_select_mi355x.json, the (direction, M, N, K) keys where irads_gemm_nt measured
+within 5 % of hipBLASLt or faster (in the step it gains on the library: the in-step A/B of this rule
+against "5 % faster" read 0.1 ms per C2 step better), each with the tiling that won (variant 2: 128 x 128 tiles, 2 workgroups per CU; 4: 256 x 256
 tiles on 8 waves, N % 256 == 0).  Directions: "fwd" (y = x Wᵀ + b), "bwd" (dX = dY W), and the FFN's fused pairs
 "fwd_gelu" (fc1 with the erf GELU in the epilogue, against the better GEMM + gelu pass) and
 "bwd_dgelu" (fc2's dX with GELU' applied in the epilogue, against GEMM + gelu_bwd pass).  A
 shape not in the table, or one the kernel cannot take (N % 128, K % 64, an operand not 16-byte aligned
 or with a leading dimension not a multiple of 8), goes to hipBLASLt.  IRADS_GEMM=off sends every shape
 to hipBLASLt, IRADS_GEMM=all every shape the kernel takes to irads_gemm_nt (A/B and tests), on the
-tiling IRADS_GEMM_VARIANT names (default 2; variant 4 where N % 256 == 0, else 2).
+tiling IRADS_GEMM_VARIANT names (default 2; variant 4 where N % 256 == 0, else 2); IRADS_GEMM_SELECT
+names another table file (A/B of a re-tune).
 """
 import json
 import os
@@ -40,7 +42,7 @@ def _selected():
     global _table
     if _table is None:
         try:
-            with open(_TABLE_PATH) as fh:
+            with open(os.environ.get("IRADS_GEMM_SELECT", _TABLE_PATH)) as fh:
                 _table = {tuple(k[:4]): (k[4] if len(k) > 4 else DEFAULT_VARIANT) for k in json.load(fh)["irads"]}
         except FileNotFoundError:
             _table = {}
