@@ -579,6 +579,48 @@ def lightsb_em(x, n_steps, noise, r, S_log_diag, log_alpha_raw, epsilon):
     return torch.stack(traj, 1)
 
 
+def lightsb_full_S(U, S_log_diag):
+    """sb.py:47-48: S = (U * exp(s)[:, None, :]) @ Uᵀ (U orthogonal, however parametrised)."""
+    return (U * torch.exp(S_log_diag)[:, None, :]) @ U.permute(0, 2, 1)
+
+
+def lightsb_full_log_C(x, r, S_log_diag, U, log_alpha_raw, epsilon):
+    """sb.py:206-224, is_diagonal=False, dense: xᵀSx by matrix products."""
+    S = lightsb_full_S(U, S_log_diag)
+    x_S_x = (x[:, None, None, :] @ (S[None, :, :, :] @ x[:, None, :, None]))[:, :, 0, 0]
+    x_r = (x[:, None, :] * r[None, :, :]).sum(dim=-1)
+    return torch.logsumexp((x_S_x + 2 * x_r) / (2 * epsilon) + log_alpha_raw[None, :] / epsilon, dim=-1)
+
+
+def lightsb_full_drift(x, t, r, S_log_diag, U, log_alpha_raw, epsilon):
+    """sb.py:106-161, is_diagonal=False, as written: dense S, A (rows x K x D x D), their inverses
+    through the rotation, the log-partition and its gradient by autograd."""
+    x = x.clone().requires_grad_(True)
+    S_diagonal = torch.exp(S_log_diag)
+    A_diagonal = (t / (epsilon * (1 - t)))[:, None, None] + 1 / (epsilon * S_diagonal)[None, :, :]
+    S_log_det = torch.sum(S_log_diag, dim=-1)
+    A_log_det = torch.sum(torch.log(A_diagonal), dim=-1)
+    log_alpha = log_alpha_raw / epsilon
+    S_inv = (U * (1 / S_diagonal[:, None, :])) @ U.permute(0, 2, 1)
+    A_inv = (U[None] * (1 / A_diagonal[:, :, None, :])) @ U.permute(0, 2, 1)[None]
+    c = ((1 / (epsilon * (1 - t)))[:, None] * x)[:, None, :] + (S_inv @ (r[:, :, None]))[None, :, :, 0] / epsilon
+    c_A_inv_c = (c[:, :, None, :] @ A_inv @ c[:, :, :, None])[:, :, 0, 0]
+    r_S_inv_r = (r[:, None, :] @ S_inv @ r[:, :, None])[None, :, 0, 0]
+    exp_arg = log_alpha[None, :] - 0.5 * S_log_det[None, :] - 0.5 * A_log_det - 0.5 * r_S_inv_r / epsilon + 0.5 * c_A_inv_c
+    lse = torch.logsumexp(exp_arg, dim=-1)
+    g = torch.autograd.grad(lse, x, grad_outputs=torch.ones_like(lse))[0]
+    return (-x / (1 - t[:, None]) + epsilon * g).detach()
+
+
+def lightsb_full_log_potential(x, r, S_log_diag, U, log_alpha_raw, epsilon):
+    """sb.py:183-204, is_diagonal=False: the MultivariateNormal mixture's log-density + logsumexp(log α)."""
+    from torch.distributions import Categorical, MixtureSameFamily, MultivariateNormal
+    log_alpha = log_alpha_raw / epsilon
+    S = lightsb_full_S(U, S_log_diag)
+    gmm = MixtureSameFamily(Categorical(logits=log_alpha), MultivariateNormal(loc=r, covariance_matrix=epsilon * S))
+    return gmm.log_prob(x) + torch.logsumexp(log_alpha, dim=-1)
+
+
 # ----------------------------------------------------------------- detection post-processing
 def nms_ref(boxes, scores, iou_threshold):
     """Greedy NMS as torchvision.ops.nms computes it on the CPU (torchvision is a third-party

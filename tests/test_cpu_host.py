@@ -135,9 +135,9 @@ def test_unsupported_configs_raise():
     from semseg.models.backbones.swin import DAttentionMM, WindowMSA
     with pytest.raises(NotImplementedError):
         DAttentionMM(16, n_heads=2, dwc_pe=True, level=0)
-    with pytest.raises(NotImplementedError):
-        from modules.sb import LightSB
-        LightSB(is_diagonal=False)
+    from modules.sb import LightSB
+    with pytest.raises(RuntimeError):  # the full-covariance path exists (GPU only, like the kernels)
+        LightSB(dim=8, n_potentials=2, is_diagonal=False).get_log_C(torch.randn(3, 8))
     w = WindowMSA(96, 4, (12, 12))  # head_dim 24
     with pytest.raises((NotImplementedError, RuntimeError)):
         w(torch.randn(1, 144, 96))
