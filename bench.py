@@ -455,6 +455,7 @@ def main():
         wl["hw"] = (args.size, args.size)
     args.batch = wl["batch"]
     model, opt, sched, loss_fn = build(device, world, local_rank, 100000, graph=graph, wl=wl)
+    grad_exchange_fallback = None
     model.train()
     batch = synthetic_batch(args.batch, wl["hw"], device, 3407 + rank, wl["n_cls"])
 
@@ -470,8 +471,32 @@ def main():
         if world > 1:  # DDP's construction broadcast (the graph path has no DDP wrapper)
             from irads.graph_step import broadcast_module
             broadcast_module(model)
-        runner = GraphedTrainStep(model.parameters(), lambda: fwd_bwd(model, loss_fn, batch), opt, world=world,
-                                  warmup=max(args.warmup, 1), before_capture=arm_stamps)
+
+        def make_runner(comm):
+            return GraphedTrainStep(model.parameters(), lambda: fwd_bwd(model, loss_fn, batch), opt, world=world,
+                                    warmup=max(args.warmup, 1), before_capture=arm_stamps, comm=comm)
+        comm = os.environ.get("IRADS_GRAD_EXCHANGE") or None  # overlap | split (default: overlap on RCCL)
+        if world == 1:
+            runner = make_runner(comm)
+        else:
+            # The bucketed all-reduces captured inside the graph ("overlap") are the fast path; should
+            # their capture fail on ANY rank, every rank rebuilds with the all-reduce outside the graph
+            # ("split"), agreed before any replay (a replay of captured collectives on some ranks only
+            # would hang), and the line says so.
+            try:
+                runner, err = make_runner(comm), ""
+            except Exception as e:  # noqa: BLE001 - reported, never hidden
+                runner, err = None, repr(e)[:300]
+            from irads.graph_step import quiesce_process_groups
+            quiesce_process_groups()
+            ok = torch.tensor([0.0 if err else 1.0], device=device)
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+            if float(ok.item()) < 1.0:
+                grad_exchange_fallback = err or "another rank's capture failed"
+                _progress(f"captured gradient exchange failed ({grad_exchange_fallback}); using the split exchange")
+                runner = None
+                torch.cuda.synchronize()
+                runner = make_runner("split")
         ops.STAMPS.disarm()
 
         def step():
@@ -536,6 +561,7 @@ def main():
                                       "with the backward, inside the graph", "split": "one flat all-reduce between "
                                       "backward and optimizer graphs"}[runner.comm] if graph else
                                      ("DDP buckets" if world > 1 else "none (1 rank)")),
+                   **({"grad_exchange_fallback": grad_exchange_fallback} if grad_exchange_fallback else {}),
                    "gemm_selection": "TunableOp table irads/tuned" if tuned else "hipBLASLt heuristic",
                    "miopen": "deterministic solvers" if args.deterministic else "benchmark (fastest) solvers"},
         "loss": round(loss_val, 5),
