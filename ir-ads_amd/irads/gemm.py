@@ -9,8 +9,9 @@ operands once Wᵀ is kept beside W (made once per weight version).
 Which kernel serves a shape is a table, not a heuristic: scripts/gemm_tune.py times both on the
 shapes of BASELINE.json's C2 and C4 steps (interleaved rounds in one process) and writes
 tuned/irads_gemm_select_mi355x.json, the (direction, M, N, K) keys where irads_gemm_nt measured
-within 5 % of hipBLASLt or faster (in the step it gains on the library: the in-step A/B of this rule
-against "5 % faster" read 0.1 ms per C2 step better), each with the tiling that won (variant 2: 128 x 128 tiles, 2 workgroups per CU; 4: 256 x 256
+within 5 % of hipBLASLt or faster for the C2 shapes (in that step it gains on the library: 0.1 ms per
+step better than a "5 % faster" rule), at least 5 % faster for the C3 / C4 shapes (there the looser
+rule measured slower), each with the tiling that won (variant 2: 128 x 128 tiles, 2 workgroups per CU; 4: 256 x 256
 tiles on 8 waves, N % 256 == 0).  Directions: "fwd" (y = x Wᵀ + b), "bwd" (dX = dY W), and the FFN's fused pairs
 "fwd_gelu" (fc1 with the erf GELU in the epilogue, against the better GEMM + gelu pass) and
 "bwd_dgelu" (fc2's dX with GELU' applied in the epilogue, against GEMM + gelu_bwd pass).  A

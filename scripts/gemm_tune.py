@@ -45,10 +45,11 @@ def rel(a, b):
     return float((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-30))
 
 
-# irads_gemm_nt wins a shape when its median is within WIN of the library arm's: in the step it runs
-# faster than in this isolated timing (hipBLASLt's picks lose more to cold caches), and the 1.05 bound
-# measured 0.1 ms per C2 step better than 0.95 (profiles/r05_bench_le105_*.json)
-WIN = 1.05
+# irads_gemm_nt wins a shape when its median is within WIN[cfg] of the library arm's.  In the C2 step
+# it runs faster than in this isolated timing, and the 1.05 bound measured 0.1 ms per C2 step better
+# than 0.95 (profiles/r05_bench_le105_*.json); for the C3 / C4 shapes the same bound measured 0.18 /
+# 0.07 ms per step slower (profiles/r05_bench_ab_c3_*.json, _c4_*), so they keep 0.95.
+WIN = {"c2": 1.05, "c3": 0.95, "c4": 0.95}
 # irads_gemm_nt_variant tilings tried per shape (4 only where N % 256 == 0); IRADS_TUNE_VARIANTS=0,1,2,3,4
 VARIANTS = tuple(int(v) for v in os.environ.get("IRADS_TUNE_VARIANTS", "2,4").split(","))
 
@@ -114,7 +115,7 @@ def fused_rows(cfg, M, C, C4, A, W1, b16, b32):
                 ts[j].append(timed(a))
         med = [statistics.median(t) for t in ts]
         jb = 2 + min(range(len(vs)), key=lambda j: med[2 + j])
-        win = med[jb] <= WIN * min(med[0], med[1]) and e[jb] <= 2e-2
+        win = med[jb] <= WIN[cfg] * min(med[0], med[1]) and e[jb] <= 2e-2
         row = {"cfg": cfg, "op": "fc1+gelu" if d == "fwd_gelu" else "fc2+dgelu", "dir": d, "M": M, "N": C4, "K": C,
                "lib_plus_pass_us": round(med[0], 2), "irads_plus_pass_us": round(med[1], 2),
                **{f"fused_v{v}_us": round(med[2 + j], 2) for j, v in enumerate(vs)},
@@ -163,7 +164,7 @@ def main():
                         ts[j].append(timed(a))
                 med = [statistics.median(t) for t in ts]
                 jb = 1 + min(range(len(vs)), key=lambda j: med[1 + j])
-                win = med[jb] <= WIN * med[0] and e[jb] <= 1.5 * e[0] + 1e-4
+                win = med[jb] <= WIN[cfg] * med[0] and e[jb] <= 1.5 * e[0] + 1e-4
                 row = {"cfg": cfg, "op": op, "dir": d, "M": key[1], "N": key[2], "K": key[3], "lib_us": round(med[0], 2),
                        **{f"irads_v{v}_us": round(med[1 + j], 2) for j, v in enumerate(vs)}, "variant": vs[jb - 1],
                        "err_lib": round(e[0], 6), "err_irads": round(e[jb], 6), "irads": win}
@@ -179,7 +180,7 @@ def main():
             torch.cuda.empty_cache()
     os.makedirs(os.path.dirname(out_path) or ".", exist_ok=True)
     with open(out_path, "w") as fh:
-        json.dump({"device": torch.cuda.get_device_name(0), "rule": f"median irads <= {WIN} x median hipBLASLt",
+        json.dump({"device": torch.cuda.get_device_name(0), "rule": f"median irads <= WIN[cfg] x median hipBLASLt, WIN = {WIN}",
                    "irads": keys, "measured": rows}, fh, indent=1)
     print(json.dumps({"irads_shapes": len(keys), "of": len(rows)}))
 
