@@ -10,7 +10,7 @@
 // output and runs it on a handful of workgroups (8 x 128 output = one tile), so these were
 // ~6 ms of the 60 ms step.  This kernel splits K instead:
 //
-//   * grid = output tiles x K-splits (~2048 workgroups); a workgroup streams its K-range once,
+//   * grid = output tiles x K-splits (target_workgroups(): 512); a workgroup streams its K-range once,
 //     both operands staged through LDS, v_mfma_f32_16x16x32_bf16 accumulating in registers;
 //   * both MFMA operands want 8 consecutive k per lane at a fixed column, i.e. the transpose
 //     of the row-major HBM layout: tiles are stored in LDS as 16-column blocks of 32-byte rows
@@ -22,6 +22,7 @@
 //   * up to 4 problems of one shape go in one launch pair (the rgb / dte Adapters' D_fc1 and
 //     D_fc2 gradients of a block), which also lets each split cover more rows.
 // The problem is HBM-bound (A and B are each read once: 2(m+n)K bytes for 2mnK flops).
+#include <cstdlib>
 #include <type_traits>
 
 #include "common.h"
@@ -274,14 +275,27 @@ int launch_partial(const WProbs &probs, int count, int K, int m, int n, int nspl
 
 int tile_i(int m) { return m <= 16 ? 16 : (m <= 32 ? 32 : (m <= 64 ? 64 : 128)); }
 
-// K-splits: enough workgroups to fill the chip (~1024 over the batch).  A single problem
+// K-splits: enough workgroups to fill the chip (target_workgroups over the batch).  A single problem
 // takes splits of >= 64 rows (latency-bound: parallelism first).  A batch (the Adapters'
 // skinny (R, C) gradients) covers at least max(256, 4mn/(m+n)) rows per split so that the
 // fp32 partials stay below ~half of the bf16 operand bytes (partials: 4mn per split;
 // operands: 2(m+n) per row) - measured faster for those shapes.
+// Workgroups a launch aims for: 512 (two per CU) measured 26.30 ms per C2 step against 26.35 at
+// 1024 and 26.71 at 256 (profiles/r05_bench_wg_*.json): half the splits halve the fp32 partials the
+// reduce reads back, and two workgroups per CU still keep HBM busy.  IRADS_WGRAD_WGS overrides (A/B).
+long target_workgroups() {
+    static const long t = [] {
+        const char *e = getenv("IRADS_WGRAD_WGS");
+        const long v = e ? atol(e) : 0;
+        return v > 0 ? v : 512L;
+    }();
+    return t;
+}
+
 void plan(int count, int K, int m, int n, long *nsplit_out, long *chunk_out) {
     const long tiles = (long)((m + tile_i(m) - 1) / tile_i(m)) * ((n + 127) / 128);
-    long nsplit = (1024 + tiles * count - 1) / (tiles * count);
+    const long T = target_workgroups();
+    long nsplit = (T + tiles * count - 1) / (tiles * count);
     long rows = 64;
     if (count > 1) {
         rows = 4L * m * n / (m + n);
