@@ -1081,6 +1081,15 @@ int pp_slots() {
     return n;
 }
 
+long bwd_target() {  // persistent backward workgroups per launch; IRADS_WINATTN_BWD_WGS overrides (A/B)
+    static const long t = [] {
+        const char *e = getenv("IRADS_WINATTN_BWD_WGS");
+        const long v = e ? atol(e) : 0;
+        return v > 0 ? v : 256L;
+    }();
+    return t;
+}
+
 int chunk_windows(int total_windows, int nH, long target = 256) {  // target: persistent workgroups
     long cw = ((long)total_windows * nH + target - 1) / target;
     return (int)(cw < 1 ? 1 : cw);
@@ -1186,7 +1195,7 @@ extern "C" int irads_winattn_bwd(int dtype, const void *qkv, const float *qkv_bi
     } else {
         IRADS_REQUIRE(bias_quads, "irads_winattn_bwd: bf16 needs bias_quads (irads_winattn_bias_quads)");
         IRADS_REQUIRE(scale > 0.f, "irads_winattn_bwd: scale must be positive (%g)", scale);
-        const int cw = chunk_windows(B * g.nW, nH);
+        const int cw = chunk_windows(B * g.nW, nH, bwd_target());
         const unsigned nwg = (unsigned)(((B * g.nW + cw - 1) / cw) * nH);
 #define IRADS_WB(M, X)                                                                                            \
     winattn_bwd_bf16<M, X><<<nwg, 576, 0, st>>>((const unsigned short *)qkv, qkv_bias, bias_quads, mask, g, cw,   \
