@@ -320,6 +320,6 @@ class TrainMapper:
                 "gt_boxes": torch.as_tensor(np.array(boxes, dtype=np.float32).reshape(-1, 4)),
                 "gt_classes": torch.as_tensor(classes, dtype=torch.int64)}
         if self.mask_on:
-            inst["gt_masks"] = torch.as_tensor(np.array(masks, dtype=np.uint8).reshape(-1, h, w))
+            inst["gt_masks"] = torch.as_tensor(np.array(masks, dtype=bool).reshape(-1, h, w))  # bool, as convert_coco_poly_to_mask
         d["instances"] = inst
         return d

@@ -53,7 +53,6 @@ def main():
     if args.limit:
         dicts = dicts[:args.limit]
     model = build_model(num_classes=len(meta["thing_classes"]), num_queries=args.num_queries, consistency=False)
-    model.select_box_nums_for_evaluation = 900
     if args.weights:
         model.load_state_dict(torch.load(args.weights, map_location="cpu", weights_only=True))
     model = model.cuda()

@@ -138,3 +138,48 @@ def test_eval_driver_end_to_end(tmp_path):
             v = task[m]
             assert np.isnan(v) or 0.0 <= v <= 100.0
     assert model.training  # evaluate() restores the mode it found
+
+
+def test_train_mapper_feeds_the_training_step(tmp_path):
+    """COCO json -> data.TrainMapper (OursDatasetMapper's augmentations, instances with bool masks) ->
+    train_net.run_step (EMA teacher, strong view, DINO + consistency criteria, clip, AdamW, EMA update)
+    on a reduced model: finite losses, the weights and the EMA state move."""
+    from PIL import Image
+    from projects.vCLR_deformable_mask import train_net
+    from projects.vCLR_deformable_mask.configs.dino_r50 import build_model
+    from projects.vCLR_deformable_mask.data import TrainMapper, filter_empty, load_coco_json
+    g = np.random.default_rng(1)
+    ims, anns = [], []
+    for i, (hh, ww) in enumerate([(120, 160), (100, 150)]):
+        Image.fromarray(g.integers(0, 255, (hh, ww, 3), dtype=np.uint8)).save(tmp_path / f"{i}.png")
+        ims.append({"id": i + 1, "file_name": f"{i}.png", "height": hh, "width": ww})
+        for k in range(4):
+            x, y = float(g.integers(0, ww - 40)), float(g.integers(0, hh - 40))
+            anns.append({"id": len(anns) + 1, "image_id": i + 1, "category_id": 7, "bbox": [x, y, 35.0, 30.0],
+                         "area": 1050.0, "iscrowd": 0,
+                         "segmentation": [[x, y, x + 35, y, x + 35, y + 30, x, y + 30]]})
+    (tmp_path / "ann.json").write_text(json.dumps({"images": ims, "annotations": anns,
+                                                   "categories": [{"id": 7, "name": "object"}]}))
+    dicts, meta = load_coco_json(str(tmp_path / "ann.json"), str(tmp_path))
+    dicts = filter_empty(dicts)
+    np.random.seed(0)
+    import random
+    random.seed(0)
+    batched = [TrainMapper()(d) for d in dicts]
+    for b in batched:
+        inst = b["instances"]
+        assert inst["gt_masks"].dtype == torch.bool and inst["gt_boxes"].shape[0] >= 1
+        assert tuple(b["image"].shape[1:]) == tuple(inst["image_size"]) == tuple(b["image_rgb"].shape[1:])
+    torch.manual_seed(0)
+    model = build_model(num_classes=1, num_queries=30, enc_layers=1, dec_layers=1, dn_number=4).to(DEV).train()
+    updater = train_net.build_ema(model, decay=0.999)
+    opt = torch.optim.AdamW([p for p in model.parameters() if p.requires_grad], lr=1e-4, weight_decay=1e-4)
+    w0 = model.class_embed[0].weight.detach().clone()
+    ema0 = {k: v.detach().clone() for k, v in updater.state.state.items()} if hasattr(updater.state, "state") else None
+    for _ in range(2):
+        total, losses = train_net.run_step(model, opt, batched, {"max_norm": 0.1, "norm_type": 2}, updater)
+        assert torch.isfinite(total) and all(torch.isfinite(v) for v in losses.values())
+    assert "loss_sim" in losses  # the consistency criterion ran against the EMA teacher
+    assert not torch.equal(model.class_embed[0].weight, w0)
+    if ema0 is not None:
+        assert any(not torch.equal(updater.state.state[k], ema0[k]) for k in ema0)
