@@ -337,6 +337,11 @@ int irads_gelu_bwd(const uint16_t *u, const uint16_t *dg, uint16_t *du, long n, 
 int irads_relu_dropout_fwd(const uint16_t *a, uint16_t *r, long n, float p, uint64_t seed, const uint64_t *seed_dev,
                            void *stream);
 int irads_relu_dropout_bwd(const uint16_t *r, const uint16_t *dr, uint16_t *da, long n, float p, void *stream);
+/* DropPath factors of one Swin stage (common.py DropPath, bf16): out[slot][s] = floor(bf16(keep[slot] +
+ * U)) / keep (the fp32 inv[slot]) for keep[slot] < 1, else 1; U a multiple of 2^-8 in [0, 1) drawn
+ * from *seed_dev ^ salt and the element index. n_slots = 2 x blocks (attention, FFN), S samples. */
+int irads_droppath_scales(const uint64_t *seed_dev, uint64_t salt, const double *keep, const float *inv,
+                          int n_slots, int S, float *out, void *stream);
 
 /* MAPA prompt residual + stream concatenation (MPGBlock.forward, swin.py:1045-1068, and the stage
  * loop's x_rgb + f_rgb / x_dte + f_dte, :1455-1460):
@@ -464,6 +469,18 @@ int irads_bnact_bwd(const uint16_t *dy, const uint16_t *x, long M, int E, long r
                     const float *invstd, const float *weight, const float *bias, const uint16_t *mask,
                     float *partials, const float *mean_d, const float *mean_dxhat, uint16_t *dx, void *stream);
 long irads_bnact_partials(long M, int E);
+/* irads_bnact_finalize: from sums (2E floats: the stats partials added, irads_sum_rows) and x's row 0,
+ * mean = x[0] + S1/M, var = max(S2/M - (S1/M)^2, 0), invstd = rsqrt(var + eps), and (when
+ * running_mean / running_var are given) the BatchNorm running update with momentum (unbiased
+ * var · M/(M-1)) and num_batches_tracked += 1 (may be NULL) — the host expressions of
+ * BNActFn.forward in one launch.  irads_bnact_bwd_sums: pass 2 with the raw sums of pass 1
+ * (sum d, sum d * xhat; 2E floats), divided by M in the kernel. */
+int irads_bnact_finalize(const float *sums, const uint16_t *x, long M, int E, float eps, double momentum,
+                         float *mean, float *invstd, float *running_mean, float *running_var,
+                         int64_t *num_batches_tracked, void *stream);
+int irads_bnact_bwd_sums(const uint16_t *dy, const uint16_t *x, long M, int E, long rows_per_sample, const float *mean,
+                         const float *invstd, const float *weight, const float *bias, const uint16_t *mask,
+                         const float *sums, uint16_t *dx, void *stream);
 
 /* Metrics.update (semseg/metrics.py:58-69): hist ((C+1) x C int64, accumulated) += the
  * confusion of target (row; C = valid targets outside [0, C)) and arg-max over the C scores

@@ -165,7 +165,8 @@ __global__ __launch_bounds__(256) void bnact_bwd2_kernel(const u16 *__restrict__
                                                          const float *__restrict__ invstd,
                                                          const float *__restrict__ w, const float *__restrict__ b,
                                                          const u16 *__restrict__ mask, const float *__restrict__ md,
-                                                         const float *__restrict__ mdx, u16 *__restrict__ dx) {
+                                                         const float *__restrict__ mdx, float inv_m,
+                                                         u16 *__restrict__ dx) {
     const Lay l = lay(E);
     if (!l.act) return;
     Chan ch;
@@ -174,8 +175,9 @@ __global__ __launch_bounds__(256) void bnact_bwd2_kernel(const u16 *__restrict__
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
         a[j] = ch.w[j] * ch.inv[j];
-        c1[j] = md[l.c0 + j];
-        c2[j] = mdx[l.c0 + j];
+        // mean(d), mean(d xhat): given, or the raw sums (md = sums[0:E], mdx = sums[E:2E]) x (1/M)
+        c1[j] = inv_m > 0.f ? md[l.c0 + j] * inv_m : md[l.c0 + j];
+        c2[j] = inv_m > 0.f ? mdx[l.c0 + j] * inv_m : mdx[l.c0 + j];
     }
     for (long r = (long)blockIdx.x * l.rpi + l.rl; r < M; r += (long)gridDim.x * l.rpi) {
         float v[8], g[8], mk[8] = {1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f}, o[8];
@@ -191,6 +193,33 @@ __global__ __launch_bounds__(256) void bnact_bwd2_kernel(const u16 *__restrict__
         }
         *reinterpret_cast<u32x4 *>(dx + r * E + l.c0) = pack8(o);
     }
+}
+
+// Batch statistics from the summed partials (sums[c] = sum (x - s), sums[E + c] = sum (x - s)^2, s = row
+// 0 of x) and the running-statistics update, in one launch: torch's expressions of the host code
+// this replaces (BNActFn.forward), op by op, each rounded to fp32 as those element kernels round:
+//   m1 = S1 * (1/M); mean = s + m1; var = max(S2 * (1/M) - m1 * m1, 0); invstd = rsqrt(var + eps)
+//   running_mean = running_mean * (1 - mom) + mom * mean        (add_(.., alpha=mom): one fma)
+//   running_var  = running_var * (1 - mom) + mom * (var * M / (M - 1));  num_batches_tracked += 1
+__global__ __launch_bounds__(256) void bnact_finalize_kernel(const float *__restrict__ sums, const u16 *__restrict__ x,
+                                                             int E, float inv_m, float eps, float keep, float mom,
+                                                             float unbias, float *__restrict__ mean,
+                                                             float *__restrict__ invstd, float *__restrict__ rmean,
+                                                             float *__restrict__ rvar, long long *__restrict__ nbt) {
+#pragma clang fp contract(off)
+    for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < E; c += gridDim.x * blockDim.x) {
+        const float m1 = sums[c] * inv_m;
+        const float mu = bf2f(x[c]) + m1;
+        float var = sums[E + c] * inv_m - m1 * m1;
+        var = var < 0.f ? 0.f : var;  // clamp_min(0): a NaN stays NaN
+        mean[c] = mu;
+        invstd[c] = rsqrtf(var + eps);
+        if (rmean) {
+            rmean[c] = fmaf(mom, mu, rmean[c] * keep);
+            rvar[c] = fmaf(mom, var * unbias, rvar[c] * keep);
+        }
+    }
+    if (nbt && blockIdx.x == 0 && threadIdx.x == 0) nbt[0] = nbt[0] + 1;
 }
 
 int bn_blocks(long M, int E) {
@@ -243,6 +272,33 @@ extern "C" int irads_bnact_bwd(const uint16_t *dy, const uint16_t *x, long M, in
     }
     IRADS_REQUIRE(mean_d && mean_dxhat, "irads_bnact_bwd: pass 2 needs mean_d, mean_dxhat");
     hipLaunchKernelGGL(bnact_bwd2_kernel, dim3(bn_blocks(M, E)), dim3(256), 0, st, dy, x, M, E, rows_per_sample, mean,
-                       invstd, weight, bias, mask, mean_d, mean_dxhat, dx);
+                       invstd, weight, bias, mask, mean_d, mean_dxhat, 0.f, dx);
     return check_launch("irads_bnact_bwd pass 2");
+}
+
+extern "C" int irads_bnact_bwd_sums(const uint16_t *dy, const uint16_t *x, long M, int E, long rows_per_sample,
+                                    const float *mean, const float *invstd, const float *weight, const float *bias,
+                                    const uint16_t *mask, const float *sums, uint16_t *dx, void *stream) {
+    IRADS_BN_CHECK("irads_bnact_bwd_sums");
+    IRADS_REQUIRE(dy && x && mean && invstd && weight && bias && sums && dx && rows_per_sample > 0,
+                  "irads_bnact_bwd_sums: bad argument");
+    const float inv_m = 1.0f / (float)M;  // torch's division by the scalar M: a multiply by its fp32 reciprocal
+    hipLaunchKernelGGL(bnact_bwd2_kernel, dim3(bn_blocks(M, E)), dim3(256), 0, (hipStream_t)stream, dy, x, M, E,
+                       rows_per_sample, mean, invstd, weight, bias, mask, sums, sums + E, inv_m, dx);
+    return check_launch("irads_bnact_bwd_sums");
+}
+
+extern "C" int irads_bnact_finalize(const float *sums, const uint16_t *x, long M, int E, float eps, double momentum,
+                                    float *mean, float *invstd, float *running_mean, float *running_var,
+                                    int64_t *num_batches_tracked, void *stream) {
+    IRADS_BN_CHECK("irads_bnact_finalize");
+    IRADS_REQUIRE(sums && x && mean && invstd, "irads_bnact_finalize: null pointer");
+    IRADS_REQUIRE((running_mean != nullptr) == (running_var != nullptr), "irads_bnact_finalize: running stats pair");
+    const float inv_m = 1.0f / (float)M;
+    const float keep = (float)(1.0 - momentum), mom = (float)momentum;
+    const float unbias = (float)((double)M / (double)(M - 1));
+    hipLaunchKernelGGL(bnact_finalize_kernel, dim3((E + 255) / 256), dim3(256), 0, (hipStream_t)stream, sums, x, E,
+                       inv_m, eps, keep, mom, unbias, mean, invstd, running_mean, running_var,
+                       reinterpret_cast<long long *>(num_batches_tracked));
+    return check_launch("irads_bnact_finalize");
 }

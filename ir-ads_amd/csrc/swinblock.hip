@@ -362,6 +362,29 @@ int resln_bwd_vpt(const u16 *dy, const float *x, const float *mean, const float 
     return IRADS_EINVAL;
 }
 
+// DropPath factors of a whole stage in one launch (semseg/models/layers/common.py DropPath in bf16 under
+// autocast: x.div(keep) * floor(keep + U), U ~ torch.rand in bf16 — 8 random bits, multiples of 2^-8):
+// out[slot][s] = floor(bf16(keep[slot] + U)) * inv[slot] for an active slot (keep < 1), 1 otherwise.
+// U is drawn from the stage's device seed (the Adapter dropout's, ^ salt), so a captured graph draws
+// fresh factors on every replay; the keep + U sum is formed in fp64 and rounded fp32 -> bf16 like
+// torch's (u.double() + keep).to(bfloat16).
+__global__ __launch_bounds__(256) void droppath_kernel(const unsigned long long *__restrict__ seed_dev,
+                                                       unsigned long long salt, const double *__restrict__ keep,
+                                                       const float *__restrict__ inv, int n_slots, int S,
+                                                       float *__restrict__ out) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n_slots * S) return;
+    const int slot = i / S;
+    const double k = keep[slot];
+    if (!(k < 1.0)) {
+        out[i] = 1.f;
+        return;
+    }
+    const float u = floorf(uniform01(*seed_dev ^ salt, (unsigned long long)i) * 256.f) * (1.f / 256.f);
+    const float t = bf2f(f2bf((float)((double)u + k)));
+    out[i] = floorf(t) * inv[slot];
+}
+
 }  // namespace
 }  // namespace irads
 
@@ -451,4 +474,14 @@ extern "C" int irads_relu_dropout_bwd(const uint16_t *r, const uint16_t *dr, uin
                                       void *stream) {
     IRADS_REQUIRE(r && dr && da && p >= 0.f && p < 1.f, "irads_relu_dropout_bwd: bad arguments");
     return elem_launch(3, r, dr, da, n, p, p > 0.f ? 1.f / (1.f - p) : 1.f, 0, stream);
+}
+
+extern "C" int irads_droppath_scales(const uint64_t *seed_dev, uint64_t salt, const double *keep, const float *inv,
+                                     int n_slots, int S, float *out, void *stream) {
+    IRADS_REQUIRE(seed_dev && keep && inv && out && n_slots >= 1 && S >= 1, "irads_droppath_scales: bad arguments");
+    const int n = n_slots * S;
+    hipLaunchKernelGGL(droppath_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                       reinterpret_cast<const unsigned long long *>(seed_dev), (unsigned long long)salt, keep, inv,
+                       n_slots, S, out);
+    return check_launch("irads_droppath_scales");
 }

@@ -60,12 +60,15 @@ SIGNATURES = {
     "irads_gelu_bwd": [_vp, _vp, _vp, _l, _vp],
     "irads_relu_dropout_fwd": [_vp, _vp, _l, _f, _u64, _vp, _vp],
     "irads_relu_dropout_bwd": [_vp, _vp, _vp, _l, _f, _vp],
+    "irads_droppath_scales": [_vp, _u64, _vp, _vp, _i, _i, _vp, _vp],
     "irads_wgrad_batched": [_i, _vp, _i, _i, _i, _f, _i, _vp, _vp],
     "irads_dattn_offset_fwd": [_vp] * 7 + [_i] * 8 + [_f] + [_vp] * 3,
     "irads_dattn_offset_bwd": [_vp] * 7 + [_i] * 8 + [_f] + [_vp] * 8,
     "irads_bnact_stats": [_vp, _l, _i, _vp, _vp],
     "irads_bnact_fwd": [_vp, _l, _i, _l] + [_vp] * 7,
     "irads_bnact_bwd": [_vp, _vp, _l, _i, _l] + [_vp] * 10,
+    "irads_bnact_bwd_sums": [_vp, _vp, _l, _i, _l] + [_vp] * 8,
+    "irads_bnact_finalize": [_vp, _vp, _l, _i, _f, _d] + [_vp] * 6,
     "irads_mpg_fwd": [_vp] * 7 + [_l, _i, _vp, _vp],
     "irads_mpg_fwd_bf16": [_vp] * 7 + [_l, _i, _vp, _vp],
     "irads_ln_bf16_fwd": [_vp] * 3 + [_l, _i, _f] + [_vp] * 4,

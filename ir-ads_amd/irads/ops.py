@@ -971,18 +971,20 @@ class BNActFn(torch.autograd.Function):
         n_part = N.load().irads_bnact_partials(M, E)
         parts = torch.empty((n_part,), device=x.device, dtype=torch.float32)
         N.call("irads_bnact_stats", N.ptr(xb), M, E, N.ptr(parts), N.stream())
-        s = sum_rows(parts, 2 * E).view(2, E)
-        shift = xb.view(M, E)[0].float()
-        m1 = s[0] / M
-        mean = shift + m1
-        var = (s[1] / M - m1 * m1).clamp_min(0.)
-        invstd = torch.rsqrt(var + bn.eps)
-        if bn.track_running_stats and bn.running_mean is not None:
-            with torch.no_grad():
-                mom = bn.momentum
-                bn.running_mean.mul_(1 - mom).add_(mean, alpha=mom)
-                bn.running_var.mul_(1 - mom).add_(var * (M / (M - 1)), alpha=mom)
-                bn.num_batches_tracked.add_(1)
+        s = sum_rows(parts, 2 * E)
+        # batch mean / invstd and the running-statistics update in one launch (the host expressions
+        # s[0] / M + x[0], clamp_min(s[1] / M - m1²), rsqrt(var + eps), running_*.mul_(1 - mom).add_(..,
+        # alpha=mom), num_batches_tracked += 1, op for op; tests/test_gpu_seghead.py pins them bitwise)
+        mean = torch.empty((E,), device=x.device, dtype=torch.float32)
+        invstd = torch.empty_like(mean)
+        track = bn.track_running_stats and bn.running_mean is not None
+        rm = rv = nbt = None
+        if track:
+            rm = N.check(bn.running_mean, "bn running_mean", torch.float32)
+            rv = N.check(bn.running_var, "bn running_var", torch.float32)
+            nbt = bn.num_batches_tracked
+        N.call("irads_bnact_finalize", N.ptr(s), N.ptr(xb), M, E, float(bn.eps), float(bn.momentum), N.ptr(mean),
+               N.ptr(invstd), N.ptr(rm), N.ptr(rv), N.ptr(nbt), N.stream())
         y = torch.empty_like(xb)
         N.call("irads_bnact_fwd", N.ptr(xb), M, E, L, N.ptr(mean), N.ptr(invstd), N.ptr(w), N.ptr(b), N.ptr(mask),
                N.ptr(y), N.stream())
@@ -999,11 +1001,11 @@ class BNActFn(torch.autograd.Function):
         parts = torch.empty((N.load().irads_bnact_partials(M, E),), device=g.device, dtype=torch.float32)
         N.call("irads_bnact_bwd", N.ptr(g), N.ptr(xb), M, E, L, N.ptr(mean), N.ptr(invstd), N.ptr(w), N.ptr(b),
                N.ptr(mask), N.ptr(parts), None, None, None, N.stream())
-        s = sum_rows(parts, 2 * E).view(2, E)  # (sum d, sum d * xhat)
-        md, mdx = s[0] / M, s[1] / M
+        s = sum_rows(parts, 2 * E)  # (sum d, sum d * xhat), divided by M inside pass 2
         dx = torch.empty_like(xb)
-        N.call("irads_bnact_bwd", N.ptr(g), N.ptr(xb), M, E, L, N.ptr(mean), N.ptr(invstd), N.ptr(w), N.ptr(b),
-               N.ptr(mask), None, N.ptr(md), N.ptr(mdx), N.ptr(dx), N.stream())
+        N.call("irads_bnact_bwd_sums", N.ptr(g), N.ptr(xb), M, E, L, N.ptr(mean), N.ptr(invstd), N.ptr(w), N.ptr(b),
+               N.ptr(mask), N.ptr(s), N.ptr(dx), N.stream())
+        s = s.view(2, E)
         return dx, s[1], s[0], None, None
 
 

@@ -85,10 +85,14 @@ def adapter_params(seq):
     return ps
 
 
-def _droppath_scales(seq, S, device):
+_DP_SALT = 0xD1B54A32D192ED03  # the DropPath stream of a stage's seed (the Adapters' use _salt)
+
+
+def _droppath_scales(seq, S, device, seed=None):
     """(n_blocks, 2, S) fp32 per-sample factors s = mask ? fp32(1/keep) : 0 for the attention
-    and FFN DropPaths (common.py DropPath: x.div(keep) * floor(keep + U), U in x.dtype), or
-    None when no DropPath is active."""
+    and FFN DropPaths (common.py DropPath: x.div(keep) * floor(keep + U), U in x.dtype), 1 for a
+    branch without one, or None when no DropPath is active.  `seed`: int64 device tensor (the
+    stage's Adapter-dropout seed), drawn here when None."""
     ps = []
     for blk in seq.blocks:
         pa = blk.attn.drop.p if (blk.training and getattr(blk.attn.drop, "p", 0)) else 0.
@@ -100,14 +104,17 @@ def _droppath_scales(seq, S, device):
     if cache is None or cache[0] != (tuple(ps), device):
         keep = torch.tensor([[1. - a, 1. - b] for a, b in ps], dtype=torch.float64)
         inv = (1.0 / keep.float()).float()  # the fp32 reciprocal torch's div-by-scalar multiplies by
-        active = torch.tensor([[a > 0, b > 0] for a, b in ps])
-        cache = ((tuple(ps), device), keep.to(device)[..., None], inv.to(device)[..., None], active.to(device)[..., None])
+        cache = ((tuple(ps), device), keep.to(device).contiguous(), inv.to(device).contiguous())
         seq.__dict__["_dp_cache"] = cache
-    _, keep, inv, active = cache
-    u = torch.rand((len(ps), 2, S), device=device, dtype=_BF16)
-    mask = (u.double() + keep).to(_BF16).floor()  # keep + U in bf16, as the reference's bf16 DropPath
-    s = mask.float() * inv
-    return torch.where(active, s, torch.ones_like(s))
+    _, keep, inv = cache
+    if seed is None:
+        seed = torch.randint(0, 2 ** 62, (1,), device=device, dtype=torch.int64)
+    # floor(bf16(keep + U)) / keep per (block, branch, sample), 1 where the branch has no DropPath:
+    # one launch (irads_droppath_scales) for what torch ran as rand, casts, add, floor, mul, where
+    out = torch.empty((len(ps), 2, S), device=device, dtype=torch.float32)
+    N.call("irads_droppath_scales", N.ptr(seed), _DP_SALT, N.ptr(keep), N.ptr(inv), 2 * len(ps), S, N.ptr(out),
+           N.stream())
+    return out
 
 
 def _resln_fwd(x, M, C, rps, add1=None, add1_scale=None, add2=None, add2_mult=0.5, norm=None, x_out=False,
@@ -192,11 +199,12 @@ class SwinStageFn(torch.autograd.Function):
         nb = len(blocks)
         dev = x.device
         x = x.contiguous().view(M, C)
-        dp = _droppath_scales(seq, S, dev)
         # the Adapter's F.dropout(p=0.1, training=self.training) (swin.py:496)
         p_drop = ADAPTER_DROPOUT if blocks[0].MLP_RGB_Adapter.training else 0.
-        # dropout seed drawn on the device by torch's generator: graph-capturable, fresh per replay
+        # dropout seed drawn on the device by torch's generator: graph-capturable, fresh per replay;
+        # the stage's DropPath factors draw from the same seed (another salt)
         seed = torch.randint(0, 2 ** 62, (1,), device=dev, dtype=torch.int64) if p_drop > 0 else None
+        dp = _droppath_scales(seq, S, dev, seed)
         # all adapter weights of the stage cast to bf16 in two launches (autocast casts each per
         # call), grouped as (2nb, R, C) D_fc1 weights, (2nb, C, R) D_fc2 weights and the biases
         aw = _adapter_weights(aparams, nb)

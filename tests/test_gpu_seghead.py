@@ -295,6 +295,57 @@ def test_head_bnact_tail_matches_module_path(E):
     assert 0.2 < (per_chan > 0).float().mean().item() < 0.8
 
 
+@pytest.mark.parametrize("E,M", [(256, 2 * 64 * 64), (512, 2 * 128 * 128), (768, 77)])
+def test_bnact_finalize_and_sums_pass_match_torch_expressions(E, M):
+    """irads_bnact_finalize (batch mean / invstd + running-statistics update in one launch) and
+    irads_bnact_bwd_sums (pass 2 from the raw sums) bit for bit (invstd within 1 ulp) against the
+    torch expressions they replace: m1 = S1 / M, mean = x[0] + m1, var = (S2 / M - m1²).clamp_min(0), rsqrt(var + eps),
+    running_*.mul_(1 - mom).add_(.., alpha=mom), num_batches_tracked += 1; md, mdx = S / M."""
+    from irads import native as N
+    torch.manual_seed(E + M)
+    x = torch.randn(M, E, device=DEV).bfloat16()
+    sums = torch.randn(2 * E, device=DEV) * 50
+    sums[E:] = sums[E:].abs() * 20
+    sums[E + 3] = 0.0  # a channel whose variance formula goes negative -> clamped to 0
+    bn = torch.nn.BatchNorm2d(E).to(DEV)
+    bn.running_mean.normal_()
+    bn.running_var.uniform_(0.5, 2.0)
+    rm, rv, nbt = bn.running_mean.clone(), bn.running_var.clone(), bn.num_batches_tracked.clone()
+    s = sums.view(2, E)
+    m1 = s[0] / M
+    mean_ref = x[0].float() + m1
+    var = (s[1] / M - m1 * m1).clamp_min(0.)
+    inv_ref = torch.rsqrt(var + bn.eps)
+    mom = bn.momentum
+    rm.mul_(1 - mom).add_(mean_ref, alpha=mom)
+    rv.mul_(1 - mom).add_(var * (M / (M - 1)), alpha=mom)
+    nbt.add_(1)
+    mean = torch.empty(E, device=DEV)
+    inv = torch.empty(E, device=DEV)
+    N.call("irads_bnact_finalize", N.ptr(sums), N.ptr(x), M, E, float(bn.eps), float(mom), N.ptr(mean), N.ptr(inv),
+           N.ptr(bn.running_mean), N.ptr(bn.running_var), N.ptr(bn.num_batches_tracked), N.stream())
+    assert torch.equal(mean, mean_ref)
+    # the variance is bit-exact (running_var carries it); rsqrt is the device library's, within an ulp
+    # of torch's rsqrt kernel (the two builds lower it differently)
+    ulp = (inv_ref.view(torch.int32) - inv.view(torch.int32)).abs()
+    assert int(ulp.max()) <= 1, int(ulp.max())
+    assert torch.equal(bn.running_mean, rm) and torch.equal(bn.running_var, rv)
+    assert int(bn.num_batches_tracked) == int(nbt)
+    # pass 2 from the raw sums against pass 2 from torch's S / M
+    L = M // 2 if M % 2 == 0 else M
+    w = torch.randn(E, device=DEV)
+    b = torch.randn(E, device=DEV)
+    dy = torch.randn(M, E, device=DEV).bfloat16()
+    dsum = torch.randn(2 * E, device=DEV) * 30
+    md, mdx = dsum[:E] / M, dsum[E:] / M
+    dx0, dx1 = torch.empty_like(x), torch.empty_like(x)
+    N.call("irads_bnact_bwd", N.ptr(dy), N.ptr(x), M, E, L, N.ptr(mean), N.ptr(inv), N.ptr(w), N.ptr(b), None, None,
+           N.ptr(md), N.ptr(mdx), N.ptr(dx0), N.stream())
+    N.call("irads_bnact_bwd_sums", N.ptr(dy), N.ptr(x), M, E, L, N.ptr(mean), N.ptr(inv), N.ptr(w), N.ptr(b), None,
+           N.ptr(dsum), N.ptr(dx1), N.stream())
+    assert torch.equal(dx0, dx1)
+
+
 RESIZE_CE_CASES = [
     # (B, C, h, w, H, W): x4 like the CMNeXt heads, ragged widths (segments of 32 low-res columns
     # with a partial last one), non-integer ratios, one-column / one-row maps

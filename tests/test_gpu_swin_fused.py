@@ -220,6 +220,18 @@ def test_fused_stage_droppath_semantics():
     assert ok.all()
     frac = (s != 0).float().mean(-1)
     assert ((frac - keep[..., 0]).abs() < 0.25).all()
+    # one launch per stage (irads_droppath_scales): keep + U, U on the 2^-8 grid, rounded to bf16 ->
+    # P(kept) = P(bf16(keep + U) >= 1), counted over the 256 values of U; fresh factors per seed
+    big = torch.stack([SF._droppath_scales(seq, 8192, torch.device(DEV)) for _ in range(4)])
+    for k, (kp, slot) in enumerate([(0.8, 0), (0.7, 1)]):
+        u = torch.arange(256, dtype=torch.float64) / 256
+        p_keep = ((u + kp).float().bfloat16().float().floor() >= 1).double().mean().item()
+        got = (big[:, slot] != 0).double().mean().item()
+        assert abs(got - p_keep) < 0.01, (kp, got, p_keep)
+    assert not torch.equal(big[0], big[1])
+    seq.blocks[0].attn.drop.p = 0.0  # a branch without DropPath: factor 1
+    s1 = SF._droppath_scales(seq, 64, torch.device(DEV))
+    assert torch.equal(s1[0, 0], torch.ones(64, device=DEV))
 
 
 @pytest.mark.parametrize("K,m,n", [(131072, 8, 128), (8192, 512, 32), (1000, 16, 24), (300, 64, 256), (77, 128, 136),
